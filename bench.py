@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""MGMC V-cycle benchmark (BASELINE.json metric): samples/s of the 3D 512^3 shifted-Laplace
+7-level V-cycle, one independent chain per GPU, plus the fine-smoother HBM roofline and the CPU
+oracle baseline.
+
+  python bench.py --gpus N --steps K --warmup W
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+One process per GPU (RANK / LOCAL_RANK / WORLD_SIZE from the environment).  Each rank runs an
+independent chain (Philox key = (seed, chain = rank)); the only collective is the final all-gather
+of the per-chain QoI moments (RCCL, backend "nccl").  A step is one MGMC V-cycle; the K timed steps
+are bracketed by barrier + device synchronisation on both sides and the max over ranks is used.
+
+Rank 0 prints ONE JSON line.  Field notes:
+  value      = chains x K / max-over-ranks time (whole job, samples/s)
+  roofline   = fine-level (level 0) Gibbs sweep: algorithmic 24 B/unknown (read x, read f,
+               write x) x N0 / average sweep time, measured with HIP events on the library's
+               stream around the fine pre/post-sampler graph segments inside the timed region
+  cpu_baseline = the CPU oracle (oracle/refcpu.cpp, FAITHFUL mode = the reference algorithm,
+               1 thread) timed on a bounded sample of the same workload on rank 0 at N=1
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Load the HIP library (ROCm 7.2 runtime) before torch so one runtime serves the process.
+import multigridmc_amd as mg  # noqa: E402
+
+mg.load_library()
+
+METRIC = "MGMC V-cycle samples/sec + fine-smoother HBM GB/s, 512³ lattice, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+SEED = 5418513         # driver_mgmc.cc:448
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--n", type=int, default=512, help="cells per direction (3D)")
+    ap.add_argument("--nlevel", type=int, default=7)
+    ap.add_argument("--cpu-samples", type=int, default=2, help="V-cycles timed for the CPU baseline (0 = skip)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--plain", action="store_true", help="time the single-graph loop instead of the segmented one")
+    return ap.parse_args()
+
+
+def cpu_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model
+
+
+def cpu_baseline(n, nlevel, nsamples):
+    """FAITHFUL oracle (reference algorithm: lexicographic SOR Gibbs sweeps, mt19937_64 +
+    normal_distribution, CSR operators) on the same 512^3 hierarchy, 1 thread."""
+    from tests import oracle_lib as O
+    p = mg.MultigridParameters(nlevel=nlevel, smoother="SOR", coarse_solver="SSOR", npresmooth=1, npostsmooth=1,
+                               ncoarsesmooth=1, omega=1.0, cycle=1, coarse_scaling=1.0)
+    t0 = time.perf_counter()
+    o = O.Oracle.fd((n, n, n), p, kappa_sq=25.0, mode=O.FAITHFUL, seed=SEED, galerkin=1)
+    setup = time.perf_counter() - t0
+    secs = o.time_samples(nsamples)
+    del o
+    return {
+        "value": nsamples / secs,
+        "unit": "samples/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{nsamples} V-cycles of the same 3D {n}^3 {nlevel}-level hierarchy after a {setup:.0f} s setup "
+                  f"(oracle/refcpu.cpp FAITHFUL mode: lexicographic SOR Gibbs, mt19937_64, CSR; g++ -O2, 1 thread); "
+                  f"{secs:.1f} s timed; host CPU: {cpu_info()}",
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    import torch
+    import torch.distributed as dist
+    dist_on = world > 1
+    if dist_on:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+
+    n, nlevel = args.n, args.nlevel
+    lat = mg.Lattice3d(n, n, n)
+    op = mg.ShiftedLaplaceFDOperator(lat, kappa_sq=1.0 / 0.2 ** 2)  # Lambda = 0.2 (parameters_template.cfg)
+    params = mg.MultigridParameters(nlevel=nlevel, smoother="SOR", coarse_solver="SSOR", npresmooth=1, npostsmooth=1,
+                                    ncoarsesmooth=1, omega=1.0, cycle=1, coarse_scaling=1.0)
+    sampler = mg.MultigridMCSampler(op, SEED, params, device=local_rank, chain_id=rank)
+    qoi = mg.measurement_vector_index(lat, [0.5, 0.5, 0.5])
+    n0 = lat.Nvertex
+
+    def barrier():
+        if dist_on:
+            dist.barrier(device_ids=[local_rank])
+
+    # warmup (prior: f = 0, x0 = 0 -- driver_mgmc.cc:61-69 with mean_x_exact = xbar = 0)
+    sampler.sample(args.warmup, qoi)
+    sampler.reset_moments()
+    sampler.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if args.plain:
+        sampler.sample_async(args.steps, qoi)
+        sampler.synchronize()
+        fine_ms, nfine = float("nan"), 0
+    else:
+        _, fine_ms, nfine = sampler.sample_timed(args.steps, qoi)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist_on:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    from multigridmc_amd.distributed import pooled_statistics
+    stats = pooled_statistics(tuple(sampler.qoi_moments()), device="cuda" if dist_on else None)
+
+    if rank == 0:
+        value = world * args.steps / elapsed
+        roof = None
+        if nfine > 0:
+            t_sweep = fine_ms / nfine * 1e-3
+            bytes_sweep = 24.0 * n0
+            achieved = bytes_sweep / t_sweep / 1e9
+            traffic = None
+            if os.path.exists(args.traffic_file):
+                try:
+                    tj = json.load(open(args.traffic_file))
+                    if tj.get("n") == n:
+                        traffic = tj.get("fine_sweep_hbm_bytes_per_launch")
+                except (OSError, ValueError):
+                    traffic = None
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": "fine-level multicolour Gibbs sweep (k_sweep_rb, red+black passes)",
+                    "bytes_per_launch": bytes_sweep, "avg_launch_ms": round(t_sweep * 1e3, 4)}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline and args.cpu_samples > 0:
+            cpu = cpu_baseline(n, nlevel, args.cpu_samples)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: prior (f = 0), x0 = 0, Philox4x32-10 counter-based Gaussian noise",
+            "config": {"workload": f"3D {n}^3 shifted-Laplace FD prior (kappa^2 = 25), {nlevel}-level V-cycle, "
+                                   f"SOR Gibbs 1/1, SSOR coarse 1, omega 1, one independent chain per GPU",
+                       "lattice": [n, n, n], "unknowns": n0, "nlevel": nlevel, "chains": world,
+                       "parallelism": f"chains{world} (independent MCMC chains, 1 per GPU)"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "qoi": {"index": qoi, "samples": stats["n"], "mean": stats["mean"], "variance": stats["variance"],
+                    "chains": stats["chains"]},
+        }
+        print(json.dumps(line), flush=True)
+    sampler.close()
+    if dist_on:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

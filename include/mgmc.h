@@ -1,0 +1,167 @@
+/*
+ * mgmc.h -- C-ABI boundary of the MI355X-native Multigrid Monte Carlo (MGMC) sampler.
+ *
+ * This is the drop-in boundary for the reference's `driver_mgmc` hot path
+ * (nilsfriess/MultigridMC, all citations relative to its src/ directory):
+ *
+ *   Sampler::apply(f, x)                     sampler/sampler.hh:41           -> mgmc_apply / mgmc_sample
+ *   Sampler::fix_rhs(f)                      sampler/sampler.hh:56           -> mgmc_set_rhs
+ *   MultigridMCSampler ctor                  sampler/multigridmc_sampler.cc:8-100 -> mgmc_create
+ *   MultigridMCSampler::sample(level)        sampler/multigridmc_sampler.cc:103-130 (one V/W-cycle per sample)
+ *   SORSampler::apply                        sampler/sor_sampler.cc:37-59    -> mgmc_sor_sampler_apply
+ *   SORSmoother::apply_sparse                smoother/sor_smoother.cc:56-78  -> mgmc_smoother_apply
+ *   LinearOperator::apply                    linear_operator/linear_operator.hh:66-76 -> mgmc_operator_apply
+ *   IntergridOperator::restrict              intergrid/intergrid_operator.hh:74-88    -> mgmc_restrict
+ *   IntergridOperator::prolongate_add        intergrid/intergrid_operator.hh:106-120  -> mgmc_prolongate_add
+ *   LinearOperator::coarsen (Galerkin RAP)   linear_operator/linear_operator.cc:10-23 -> mgmc_describe (stencils)
+ *   measure_sampling_time QoI loop           driver_mgmc.cc:66-94            -> mgmc_sample + mgmc_qoi_moments
+ *
+ * Every function returns MGMC_OK (0) or a negative MGMC_E* code; the text of the last
+ * error is available from mgmc_last_error(handle) (or mgmc_last_error(NULL) for errors
+ * raised before a handle exists).  The reference prints and exit(-1)s instead
+ * (e.g. sampler/multigridmc_sampler.cc:47-49); the C++ wrapper in mgmc_sampler.hh restores
+ * that behaviour at the driver level.
+ *
+ * Vectors crossing this boundary as host pointers use the reference's layout: one double per
+ * interior lattice vertex, numbered lexicographically with x fastest
+ * (lattice/lattice3d.hh:126-135, lattice/lattice2d.hh:95-103).  Device-resident state uses
+ * a padded zero-halo layout ("Data layout in HBM") and never leaves HBM unless a
+ * get/apply call asks for it.
+ */
+#ifndef MGMC_H
+#define MGMC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGMC_ABI_VERSION 1
+
+/* error codes */
+#define MGMC_OK 0
+#define MGMC_E_INVALID -1   /* invalid argument / configuration           */
+#define MGMC_E_HIP -2       /* HIP runtime error (incl. no device)        */
+#define MGMC_E_NOMEM -3     /* device allocation failed                   */
+#define MGMC_E_UNSUPPORTED -4 /* feature not (yet) on the device path     */
+
+/* smoother kinds (parameters.hh:145-174 MultigridParameters::smoother) */
+#define MGMC_SMOOTHER_SOR 0   /* forward SOR pre-sampler, backward SOR post-sampler */
+#define MGMC_SMOOTHER_SSOR 1  /* SSOR (forward+backward) pre- and post-sampler      */
+
+/* coarse solvers (MultigridParameters::coarse_solver) */
+#define MGMC_COARSE_SSOR 0
+#define MGMC_COARSE_CHOLESKY 1 /* not on the device path yet -> MGMC_E_UNSUPPORTED */
+
+/* sweep directions (smoother/sor_smoother.hh:14-18) */
+#define MGMC_FORWARD 1
+#define MGMC_BACKWARD 2
+
+/* Plain-old-data configuration; mirrors the MultigridParameters / LatticeParameters /
+ * ConstantCorrelationLengthModelParameters fields of auxilliary/parameters.hh that reach the
+ * hot path.  The fine operator is ShiftedLaplaceFDOperator with constant kappa^2 = 1/Lambda^2
+ * (linear_operator/shiftedlaplace_fd_operator.cc:9-57, correlationlength_model.hh:45-66). */
+typedef struct mgmc_config {
+    int dim;            /* 2 or 3 */
+    int nx, ny, nz;     /* cells per direction (nz ignored for dim=2) */
+    int nlevel;         /* number of multigrid levels (>=1) */
+    int cycle;          /* 1 = V-cycle, 2 = W-cycle, ... (applies below level 0) */
+    int npresmooth;
+    int npostsmooth;
+    int ncoarsesmooth;
+    int smoother;       /* MGMC_SMOOTHER_* */
+    int coarse_solver;  /* MGMC_COARSE_* */
+    int verbose;
+    double omega;          /* overrelaxation factor of the Gibbs samplers */
+    double coarse_scaling; /* factor on the prolongated coarse correction */
+    double kappa_sq;       /* 1/Lambda^2 */
+} mgmc_config;
+
+/* Host-side description of one multigrid level (no device needed). */
+typedef struct mgmc_level_desc {
+    int nx, ny, nz;       /* cells per direction on this level (nz = 0 for 2D) */
+    int npoints;          /* stencil points: 5/7 (fine FD) or 9/27 (Galerkin) */
+    int ncolours;         /* colours of the Gibbs sweep: 2 (fine) or 2^dim */
+    int pad_;
+    uint64_t ndof;        /* number of interior unknowns */
+    /* stencil coefficients indexed by offset (dz+1)*9 + (dy+1)*3 + (dx+1) (3D) or
+     * (dy+1)*3 + (dx+1) (2D); entries outside the stencil are 0 */
+    double stencil[27];
+} mgmc_level_desc;
+
+typedef struct mgmc_handle mgmc_handle;
+
+/* ---- host-only helpers (no GPU touched) ---- */
+int mgmc_abi_version(void);
+/* Validate cfg and fill out[0..nlevel-1] with the level hierarchy and Galerkin stencils. */
+int mgmc_describe(const mgmc_config* cfg, mgmc_level_desc* out, int max_levels);
+const char* mgmc_last_error(const mgmc_handle* h);
+
+/* ---- lifetime ---- */
+int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chain_id, mgmc_handle** out);
+int mgmc_destroy(mgmc_handle* h);
+int mgmc_level_desc_get(const mgmc_handle* h, int level, mgmc_level_desc* out);
+
+/* ---- Sampler interface (host buffers, reference layout) ---- */
+int mgmc_set_rhs(mgmc_handle* h, const double* f, size_t n);       /* fix_rhs: f stays in HBM */
+int mgmc_set_state(mgmc_handle* h, const double* x, size_t n);
+int mgmc_get_state(mgmc_handle* h, double* x, size_t n);
+/* Sampler::apply(f, x): upload f and x, run one MGMC cycle, download x (PCIe inclusive). */
+int mgmc_apply(mgmc_handle* h, const double* f, double* x, size_t n);
+
+/* ---- device-resident sampling loop (the hot path) ----
+ * Run nsteps MGMC cycles on the device-resident state.  After every cycle the QoI
+ * z = x[qoi_index] (reference index, radius-0 measurement vector,
+ * linear_operator/measured_operator.cc:74-91) is appended to a device time series and folded
+ * into device-side running moments.  If qoi_out != NULL the nsteps values are copied back. */
+int mgmc_sample(mgmc_handle* h, int nsteps, int64_t qoi_index, double* qoi_out);
+/* Enqueue nsteps cycles on the handle's stream without synchronising or copying back. */
+int mgmc_sample_async(mgmc_handle* h, int nsteps, int64_t qoi_index);
+int mgmc_synchronize(mgmc_handle* h);
+/* out[0] = n, out[1] = mean, out[2] = M2 (sum of squared deviations) of the recorded QoI */
+int mgmc_qoi_moments(mgmc_handle* h, double out[3]);
+int mgmc_reset_moments(mgmc_handle* h);
+int mgmc_set_sample_index(mgmc_handle* h, uint64_t index);
+int mgmc_get_sample_index(mgmc_handle* h, uint64_t* index);
+/* HIP stream (hipStream_t) the handle enqueues on */
+int mgmc_get_stream(mgmc_handle* h, void** stream);
+
+/* ---- component entry points (host buffers, reference layout) used by the parity tests ---- */
+/* y = A_level x  (LinearOperator::apply) */
+int mgmc_operator_apply(mgmc_handle* h, int level, const double* x, double* y);
+/* deterministic multicolour SOR sweeps (SORSmoother::apply, no noise) */
+int mgmc_smoother_apply(mgmc_handle* h, int level, int direction, int nsweeps,
+                        const double* b, double* x);
+/* one noisy multicolour SOR Gibbs sweep with explicit RNG counter (SORSampler::apply, nsmooth=1) */
+int mgmc_sor_sampler_apply(mgmc_handle* h, int level, int direction, uint32_t sweep_tag,
+                           uint64_t sample_index, const double* f, double* x);
+/* coarse = R r  (restrict, level -> level+1) */
+int mgmc_restrict(mgmc_handle* h, int level, const double* r, double* rc);
+/* x += alpha * P xc  (prolongate_add, level+1 -> level) */
+int mgmc_prolongate_add(mgmc_handle* h, int level, double alpha, const double* xc, double* x);
+/* fc = R (f - A x)  (fused residual + restriction of multigridmc_sampler.cc:118-120) */
+int mgmc_residual_restrict(mgmc_handle* h, int level, const double* f, const double* x, double* fc);
+/* n standard normals of pair ids [pair0, pair0+n/2) for (sweep_tag, sample_index):
+ * out[2p] = cos branch, out[2p+1] = sin branch of the Box-Muller pair p */
+int mgmc_normals(mgmc_handle* h, uint64_t pair0, size_t n, uint32_t sweep_tag, uint64_t sample_index,
+                 double* out);
+
+/* ---- timing hooks for the roofline measurement (bench.py) ----
+ * Run `nsweeps` noisy fine-level (level 0) Gibbs sweeps on the device state, bracketed by
+ * HIP events recorded on the handle's own stream; *ms = elapsed milliseconds. */
+int mgmc_time_fine_sweeps(mgmc_handle* h, int nsweeps, float* ms);
+/* Same as mgmc_sample_async + synchronize, but each cycle is replayed as four graph segments
+ * [fine pre-sampler | coarse-grid correction | fine post-sampler | QoI] with HIP events recorded
+ * between them on the handle's stream.  *total_ms = first-to-last event time of the nsteps
+ * cycles, *fine_ms = summed time of the fine-level (level 0) pre- and post-sampler segments,
+ * *nfine = number of fine-level sweeps they contain. */
+int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* fine_ms,
+                      int* nfine);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MGMC_H */

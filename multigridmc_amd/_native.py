@@ -1,0 +1,117 @@
+"""ctypes binding of the C-ABI in include/mgmc.h (libmgmc_hip.so, built in-tree for gfx950).
+
+There is no CPU fallback: if the HIP library is missing or cannot be loaded, importing the
+device path raises.  The CPU oracle under oracle/ is test infrastructure and is never used here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_uint32, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmgmc_hip.so")
+
+MGMC_OK = 0
+MGMC_E_INVALID = -1
+MGMC_E_HIP = -2
+MGMC_E_NOMEM = -3
+MGMC_E_UNSUPPORTED = -4
+
+SMOOTHER_SOR = 0
+SMOOTHER_SSOR = 1
+COARSE_SSOR = 0
+COARSE_CHOLESKY = 1
+FORWARD = 1
+BACKWARD = 2
+
+
+class MgmcConfig(ctypes.Structure):
+    _fields_ = [
+        ("dim", c_int), ("nx", c_int), ("ny", c_int), ("nz", c_int),
+        ("nlevel", c_int), ("cycle", c_int),
+        ("npresmooth", c_int), ("npostsmooth", c_int), ("ncoarsesmooth", c_int),
+        ("smoother", c_int), ("coarse_solver", c_int), ("verbose", c_int),
+        ("omega", c_double), ("coarse_scaling", c_double), ("kappa_sq", c_double),
+    ]
+
+
+class MgmcLevelDesc(ctypes.Structure):
+    _fields_ = [
+        ("nx", c_int), ("ny", c_int), ("nz", c_int),
+        ("npoints", c_int), ("ncolours", c_int), ("pad_", c_int),
+        ("ndof", c_uint64),
+        ("stencil", c_double * 27),
+    ]
+
+
+class MgmcError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"mgmc error {code}: {message}")
+        self.code = code
+
+
+# (name, restype, argtypes) -- every symbol declared in include/mgmc.h
+_DP = POINTER(c_double)
+_H = c_void_p
+SIGNATURES = [
+    ("mgmc_abi_version", c_int, []),
+    ("mgmc_describe", c_int, [POINTER(MgmcConfig), POINTER(MgmcLevelDesc), c_int]),
+    ("mgmc_last_error", c_char_p, [_H]),
+    ("mgmc_create", c_int, [POINTER(MgmcConfig), c_int, c_uint64, c_uint64, POINTER(c_void_p)]),
+    ("mgmc_destroy", c_int, [_H]),
+    ("mgmc_level_desc_get", c_int, [_H, c_int, POINTER(MgmcLevelDesc)]),
+    ("mgmc_set_rhs", c_int, [_H, _DP, c_size_t]),
+    ("mgmc_set_state", c_int, [_H, _DP, c_size_t]),
+    ("mgmc_get_state", c_int, [_H, _DP, c_size_t]),
+    ("mgmc_apply", c_int, [_H, _DP, _DP, c_size_t]),
+    ("mgmc_sample", c_int, [_H, c_int, c_int64, _DP]),
+    ("mgmc_sample_async", c_int, [_H, c_int, c_int64]),
+    ("mgmc_synchronize", c_int, [_H]),
+    ("mgmc_qoi_moments", c_int, [_H, _DP]),
+    ("mgmc_reset_moments", c_int, [_H]),
+    ("mgmc_set_sample_index", c_int, [_H, c_uint64]),
+    ("mgmc_get_sample_index", c_int, [_H, POINTER(c_uint64)]),
+    ("mgmc_get_stream", c_int, [_H, POINTER(c_void_p)]),
+    ("mgmc_operator_apply", c_int, [_H, c_int, _DP, _DP]),
+    ("mgmc_smoother_apply", c_int, [_H, c_int, c_int, c_int, _DP, _DP]),
+    ("mgmc_sor_sampler_apply", c_int, [_H, c_int, c_int, c_uint32, c_uint64, _DP, _DP]),
+    ("mgmc_restrict", c_int, [_H, c_int, _DP, _DP]),
+    ("mgmc_prolongate_add", c_int, [_H, c_int, c_double, _DP, _DP]),
+    ("mgmc_residual_restrict", c_int, [_H, c_int, _DP, _DP, _DP]),
+    ("mgmc_normals", c_int, [_H, c_uint64, c_size_t, c_uint32, c_uint64, _DP]),
+    ("mgmc_time_fine_sweeps", c_int, [_H, c_int, POINTER(c_float)]),
+    ("mgmc_sample_timed", c_int, [_H, c_int, c_int64, _DP, _DP, POINTER(c_int)]),
+]
+
+_lib = None
+
+
+def load_library(path: str | None = None) -> ctypes.CDLL:
+    """Load libmgmc_hip.so and bind every C-ABI symbol; raises if the library is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(
+            f"{p} not found: the HIP extension is not built (run `python -c 'import __graft_entry__ as g; g.build()'`)")
+    lib = ctypes.CDLL(p)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def last_error(handle=None) -> str:
+    msg = load_library().mgmc_last_error(handle)
+    return msg.decode() if msg else ""
+
+
+def check(code: int, handle=None) -> int:
+    if code < 0:
+        raise MgmcError(code, last_error(handle))
+    return code

@@ -1,0 +1,833 @@
+// mgmc_capi.hip -- C-ABI implementation of include/mgmc.h on gfx950.
+//
+// One handle = one MCMC chain on one GPU.  All per-level state (x_l, f_l) stays resident in HBM
+// across calls (the reference keeps it in `mutable` per-level vectors,
+// sampler/multigridmc_sampler.hh:66-72).  One sample = one MGMC cycle
+// (sampler/multigridmc_sampler.cc:103-138) = a fixed sequence of kernel launches, captured once
+// into a hipGraph and replayed; the RNG counter (sample index) is read from device memory so
+// the frozen graph produces fresh noise on every replay.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mgmc.h"
+#include "mgmc_hierarchy.hpp"
+#include "mgmc_kernels.hpp"
+
+using namespace mgmc;
+
+namespace {
+
+std::mutex g_err_mutex;
+std::string g_last_error;
+
+void set_global_error(const std::string& s) {
+    std::lock_guard<std::mutex> lock(g_err_mutex);
+    g_last_error = s;
+}
+
+enum OpKind { OP_SWEEP = 0, OP_RESIDUAL_RESTRICT = 1, OP_PROLONGATE = 2, OP_COARSE_LDS = 3, OP_QOI = 4 };
+
+struct Op {
+    OpKind kind;
+    int level;
+    int direction;  // MGMC_FORWARD / MGMC_BACKWARD for sweeps
+    uint32_t tag;   // first sweep tag
+    int nsweeps;    // OP_COARSE_LDS
+};
+
+struct Level {
+    LevelSpec spec;
+    Layout L;
+    StencilArg S;
+    double* x = nullptr;
+    double* f = nullptr;
+    double* scratch[3] = {nullptr, nullptr, nullptr};
+    size_t lds_bytes = 0;  // >0 if the whole-level LDS kernel can hold x and f
+};
+
+}  // namespace
+
+struct mgmc_handle {
+    mgmc_config cfg;
+    int device = 0;
+    uint64_t seed = 0, chain = 0;
+    RngKey key;
+    std::vector<Level> levels;
+    hipStream_t stream = nullptr;
+    uint64_t* ctrl = nullptr;       // [0] sample index [1] series length [2] qoi index [3] scratch sample
+    double* mom = nullptr;          // running (n, mean, M2)
+    double* series = nullptr;
+    uint64_t series_cap = 0;
+    double* lex_tmp = nullptr;      // staging buffer in reference layout (device)
+    size_t lex_cap = 0;
+    std::vector<Op> ops;            // one sample
+    size_t seg_end_pre = 0, seg_begin_post = 0, seg_end_post = 0;  // fine-sweep segments
+    hipGraphExec_t graph_all = nullptr;
+    hipGraphExec_t graph_seg[4] = {nullptr, nullptr, nullptr, nullptr};
+    int64_t qoi_store_index = -1;
+    std::string last_error;
+};
+
+#define HIPCHK(h, call)                                                                              \
+    do {                                                                                             \
+        hipError_t e_ = (call);                                                                      \
+        if (e_ != hipSuccess) {                                                                      \
+            std::string m_ = std::string("HIP error ") + hipGetErrorString(e_) + " at " #call;       \
+            if (h) (h)->last_error = m_;                                                             \
+            set_global_error(m_);                                                                    \
+            return MGMC_E_HIP;                                                                       \
+        }                                                                                            \
+    } while (0)
+
+static int fail(mgmc_handle* h, int code, const std::string& msg) {
+    if (h) h->last_error = msg;
+    set_global_error(msg);
+    return code;
+}
+
+// ------------------------------------------------------------------------------------------
+// launch helpers
+// ------------------------------------------------------------------------------------------
+namespace {
+
+dim3 grid3(int nthreads_x, int nrows_y, int nz_blocks, dim3 block) {
+    return dim3((unsigned)((nthreads_x + block.x - 1) / block.x), (unsigned)((nrows_y + block.y - 1) / block.y),
+                (unsigned)std::max(nz_blocks, 1));
+}
+
+GibbsArg make_gibbs(const mgmc_handle* h, const Level& lv, uint32_t tag, int colour, const uint64_t* sample) {
+    GibbsArg g;
+    g.omega = h->cfg.omega;
+    const double diag = lv.spec.diag();
+    g.sd = sqrt(diag * (2. - h->cfg.omega) / h->cfg.omega);  // sor_sampler.cc:26
+    g.key = h->key;
+    g.tag = tag;
+    g.colour = colour;
+    g.sample = sample;
+    return g;
+}
+
+template <int DIM, int NPTS, bool NOISE>
+void launch_sweep_t(const Level& lv, double* x, const double* f, const GibbsArg& g0, int direction,
+                    hipStream_t s) {
+    const Layout& L = lv.L;
+    const int nc = lv.spec.ncolours;
+    dim3 block(64, 4, 1);
+    for (int cc = 0; cc < nc; ++cc) {
+        GibbsArg g = g0;
+        g.colour = (direction == MGMC_FORWARD) ? cc : nc - 1 - cc;
+        if (NPTS == 5 || NPTS == 7) {
+            dim3 grid = grid3(L.nx / 2, L.ny - 1, DIM == 3 ? L.nz - 1 : 1, block);
+            hipLaunchKernelGGL((k_sweep_rb<DIM, NPTS, NOISE>), grid, block, 0, s, L, x, f, lv.S, g);
+        } else {
+            dim3 grid = grid3(L.nx / 2, L.ny / 2, DIM == 3 ? L.nz / 2 : 1, block);
+            hipLaunchKernelGGL((k_sweep_mc<DIM, NPTS, NOISE>), grid, block, 0, s, L, x, f, lv.S, g);
+        }
+    }
+}
+
+void launch_sweep(const Level& lv, double* x, const double* f, const GibbsArg& g, int direction, bool noise,
+                  hipStream_t s) {
+    const int dim = lv.spec.dim, np = lv.spec.npoints;
+#define DISPATCH(D, P)                                                       \
+    if (dim == D && np == P) {                                               \
+        if (noise)                                                           \
+            launch_sweep_t<D, P, true>(lv, x, f, g, direction, s);           \
+        else                                                                 \
+            launch_sweep_t<D, P, false>(lv, x, f, g, direction, s);          \
+        return;                                                              \
+    }
+    DISPATCH(3, 7) DISPATCH(3, 27) DISPATCH(2, 5) DISPATCH(2, 9)
+#undef DISPATCH
+}
+
+void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStream_t s) {
+    const int dim = lv.spec.dim, np = lv.spec.npoints, nc = lv.spec.ncolours;
+    dim3 block(1024), grid(1);
+    if (dim == 3 && np == 27)
+        hipLaunchKernelGGL((k_coarse_ssor_lds<3, 27>), grid, block, lv.lds_bytes, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc);
+    else if (dim == 3 && np == 7)
+        hipLaunchKernelGGL((k_coarse_ssor_lds<3, 7>), grid, block, lv.lds_bytes, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc);
+    else if (dim == 2 && np == 9)
+        hipLaunchKernelGGL((k_coarse_ssor_lds<2, 9>), grid, block, lv.lds_bytes, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc);
+    else
+        hipLaunchKernelGGL((k_coarse_ssor_lds<2, 5>), grid, block, lv.lds_bytes, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc);
+}
+
+void launch_residual_restrict(const Level& lf, const Level& lc, const double* x, const double* f, double* fc,
+                              double* xc, int zero_xc, hipStream_t s) {
+    dim3 block(64, 4, 1);
+    dim3 grid = grid3(lc.L.nx - 1, lc.L.ny - 1, lf.spec.dim == 3 ? lc.L.nz - 1 : 1, block);
+    const int dim = lf.spec.dim, np = lf.spec.npoints;
+    if (dim == 3 && np == 7)
+        hipLaunchKernelGGL((k_residual_restrict<3, 7>), grid, block, 0, s, lf.L, lc.L, x, f, fc, xc, lf.S, zero_xc);
+    else if (dim == 3)
+        hipLaunchKernelGGL((k_residual_restrict<3, 27>), grid, block, 0, s, lf.L, lc.L, x, f, fc, xc, lf.S, zero_xc);
+    else if (np == 5)
+        hipLaunchKernelGGL((k_residual_restrict<2, 5>), grid, block, 0, s, lf.L, lc.L, x, f, fc, xc, lf.S, zero_xc);
+    else
+        hipLaunchKernelGGL((k_residual_restrict<2, 9>), grid, block, 0, s, lf.L, lc.L, x, f, fc, xc, lf.S, zero_xc);
+}
+
+void launch_prolongate(const Level& lf, const Level& lc, double* x, const double* xc, double alpha, hipStream_t s) {
+    dim3 block(64, 4, 1);
+    dim3 grid = grid3(lf.L.nx - 1, lf.L.ny - 1, lf.spec.dim == 3 ? lf.L.nz - 1 : 1, block);
+    if (lf.spec.dim == 3)
+        hipLaunchKernelGGL((k_prolongate_add<3>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha);
+    else
+        hipLaunchKernelGGL((k_prolongate_add<2>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha);
+}
+
+void launch_pack(const Level& lv, const double* lex, double* pad, bool pack, hipStream_t s) {
+    dim3 block(64, 4, 1);
+    dim3 grid = grid3(lv.L.nx - 1, lv.L.ny - 1, lv.spec.dim == 3 ? lv.L.nz - 1 : 1, block);
+    if (lv.spec.dim == 3) {
+        if (pack)
+            hipLaunchKernelGGL((k_pack<3>), grid, block, 0, s, lv.L, lex, pad);
+        else
+            hipLaunchKernelGGL((k_unpack<3>), grid, block, 0, s, lv.L, (const double*)pad, (double*)lex);
+    } else {
+        if (pack)
+            hipLaunchKernelGGL((k_pack<2>), grid, block, 0, s, lv.L, lex, pad);
+        else
+            hipLaunchKernelGGL((k_unpack<2>), grid, block, 0, s, lv.L, (const double*)pad, (double*)lex);
+    }
+}
+
+// ---- the op sequence of one sample (multigridmc_sampler.cc:103-138) ----
+void build_ops_level(mgmc_handle* h, int level, uint32_t& tag) {
+    const mgmc_config& c = h->cfg;
+    const int nlevel = (int)h->levels.size();
+    if (level == nlevel - 1) {
+        // coarse sampler: SSORSampler(ncoarsesmooth) = ncoarsesmooth x (fwd SOR sampler, bwd SOR sampler)
+        const Level& lv = h->levels[level];
+        if (lv.lds_bytes > 0) {
+            h->ops.push_back({OP_COARSE_LDS, level, MGMC_FORWARD, tag, 2 * c.ncoarsesmooth});
+            tag += 2 * c.ncoarsesmooth;
+        } else {
+            for (int t = 0; t < c.ncoarsesmooth; ++t) {
+                h->ops.push_back({OP_SWEEP, level, MGMC_FORWARD, tag++, 1});
+                h->ops.push_back({OP_SWEEP, level, MGMC_BACKWARD, tag++, 1});
+            }
+        }
+        return;
+    }
+    const int cycle_ = (level > 0) ? c.cycle : 1;
+    for (int jc = 0; jc < cycle_; ++jc) {
+        // presampler
+        for (int t = 0; t < c.npresmooth; ++t) {
+            if (c.smoother == MGMC_SMOOTHER_SOR) {
+                h->ops.push_back({OP_SWEEP, level, MGMC_FORWARD, tag++, 1});
+            } else {
+                h->ops.push_back({OP_SWEEP, level, MGMC_FORWARD, tag++, 1});
+                h->ops.push_back({OP_SWEEP, level, MGMC_BACKWARD, tag++, 1});
+            }
+        }
+        if (level == 0) h->seg_end_pre = h->ops.size();
+        h->ops.push_back({OP_RESIDUAL_RESTRICT, level, 0, 0, 0});
+        build_ops_level(h, level + 1, tag);
+        h->ops.push_back({OP_PROLONGATE, level, 0, 0, 0});
+        if (level == 0) h->seg_begin_post = h->ops.size();
+        for (int t = 0; t < c.npostsmooth; ++t) {
+            if (c.smoother == MGMC_SMOOTHER_SOR) {
+                h->ops.push_back({OP_SWEEP, level, MGMC_BACKWARD, tag++, 1});
+            } else {
+                h->ops.push_back({OP_SWEEP, level, MGMC_FORWARD, tag++, 1});
+                h->ops.push_back({OP_SWEEP, level, MGMC_BACKWARD, tag++, 1});
+            }
+        }
+        if (level == 0) h->seg_end_post = h->ops.size();
+    }
+}
+
+void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
+    const uint64_t* sample = h->ctrl;  // ctrl[0]
+    for (size_t q = begin; q < end; ++q) {
+        const Op& op = h->ops[q];
+        Level& lv = h->levels[op.level];
+        switch (op.kind) {
+            case OP_SWEEP: {
+                GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
+                launch_sweep(lv, lv.x, lv.f, g, op.direction, true, s);
+                break;
+            }
+            case OP_COARSE_LDS: {
+                GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
+                launch_coarse_lds(lv, g, op.nsweeps, s);
+                break;
+            }
+            case OP_RESIDUAL_RESTRICT: {
+                Level& lc = h->levels[op.level + 1];
+                launch_residual_restrict(lv, lc, lv.x, lv.f, lc.f, lc.x, 1, s);
+                break;
+            }
+            case OP_PROLONGATE: {
+                Level& lc = h->levels[op.level + 1];
+                launch_prolongate(lv, lc, lv.x, lc.x, h->cfg.coarse_scaling, s);
+                break;
+            }
+            case OP_QOI: {
+                hipLaunchKernelGGL(k_qoi_record, dim3(1), dim3(64), 0, s, (const double*)h->levels[0].x, h->ctrl,
+                                   h->series, h->series_cap, h->mom);
+                break;
+            }
+        }
+    }
+}
+
+int capture(mgmc_handle* h, size_t begin, size_t end, hipGraphExec_t* out) {
+    hipGraph_t g = nullptr;
+    HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    enqueue_ops(h, begin, end, h->stream);
+    HIPCHK(h, hipStreamEndCapture(h->stream, &g));
+    HIPCHK(h, hipGraphInstantiate(out, g, nullptr, nullptr, 0));
+    HIPCHK(h, hipGraphDestroy(g));
+    return MGMC_OK;
+}
+
+void destroy_graphs(mgmc_handle* h) {
+    if (h->graph_all) hipGraphExecDestroy(h->graph_all);
+    h->graph_all = nullptr;
+    for (auto& g : h->graph_seg) {
+        if (g) hipGraphExecDestroy(g);
+        g = nullptr;
+    }
+}
+
+// (re)capture the graphs; they embed series/series_cap, so recapture when those change
+int build_graphs(mgmc_handle* h) {
+    destroy_graphs(h);
+    int rc = capture(h, 0, h->ops.size(), &h->graph_all);
+    if (rc) return rc;
+    if (h->levels.size() > 1) {
+        const size_t n = h->ops.size();
+        const size_t b[5] = {0, h->seg_end_pre, h->seg_begin_post, h->seg_end_post, n};
+        for (int s = 0; s < 4; ++s) {
+            rc = capture(h, b[s], b[s + 1], &h->graph_seg[s]);
+            if (rc) return rc;
+        }
+    }
+    return MGMC_OK;
+}
+
+int ensure_series(mgmc_handle* h, uint64_t needed) {
+    if (needed <= h->series_cap) return MGMC_OK;
+    uint64_t cap = std::max<uint64_t>(needed, 2 * h->series_cap);
+    double* p = nullptr;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMalloc(&p, cap * sizeof(double)));
+    if (h->series) HIPCHK(h, hipFree(h->series));
+    h->series = p;
+    h->series_cap = cap;
+    return build_graphs(h);
+}
+
+int ensure_lex(mgmc_handle* h, size_t n) {
+    if (n <= h->lex_cap) return MGMC_OK;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (h->lex_tmp) HIPCHK(h, hipFree(h->lex_tmp));
+    HIPCHK(h, hipMalloc(&h->lex_tmp, n * sizeof(double)));
+    h->lex_cap = n;
+    return MGMC_OK;
+}
+
+int ensure_scratch(mgmc_handle* h, int level) {
+    Level& lv = h->levels[level];
+    for (auto& p : lv.scratch) {
+        if (!p) {
+            HIPCHK(h, hipMalloc(&p, lv.L.nstore * sizeof(double)));
+            HIPCHK(h, hipMemsetAsync(p, 0, lv.L.nstore * sizeof(double), h->stream));
+        }
+    }
+    return MGMC_OK;
+}
+
+// host (reference layout) -> padded device buffer
+int upload(mgmc_handle* h, int level, const double* host, double* pad) {
+    Level& lv = h->levels[level];
+    int rc = ensure_lex(h, lv.spec.ndof);
+    if (rc) return rc;
+    HIPCHK(h, hipMemcpyAsync(h->lex_tmp, host, lv.spec.ndof * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    launch_pack(lv, h->lex_tmp, pad, true, h->stream);
+    HIPCHK(h, hipGetLastError());
+    return MGMC_OK;
+}
+
+int download(mgmc_handle* h, int level, const double* pad, double* host) {
+    Level& lv = h->levels[level];
+    int rc = ensure_lex(h, lv.spec.ndof);
+    if (rc) return rc;
+    launch_pack(lv, h->lex_tmp, const_cast<double*>(pad), false, h->stream);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipMemcpyAsync(host, h->lex_tmp, lv.spec.ndof * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return MGMC_OK;
+}
+
+int check_level(mgmc_handle* h, int level, bool need_coarser) {
+    if (!h) return fail(nullptr, MGMC_E_INVALID, "null handle");
+    if (level < 0 || level >= (int)h->levels.size()) return fail(h, MGMC_E_INVALID, "level out of range");
+    if (need_coarser && level + 1 >= (int)h->levels.size())
+        return fail(h, MGMC_E_INVALID, "level has no coarser level");
+    return MGMC_OK;
+}
+
+void fill_desc(const LevelSpec& s, mgmc_level_desc* d) {
+    memset(d, 0, sizeof(*d));
+    d->nx = s.n[0];
+    d->ny = s.n[1];
+    d->nz = s.dim == 3 ? s.n[2] : 0;
+    d->npoints = s.npoints;
+    d->ncolours = s.ncolours;
+    d->ndof = s.ndof;
+    memcpy(d->stencil, s.st, sizeof(d->stencil));
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+extern "C" {
+
+int mgmc_abi_version(void) { return MGMC_ABI_VERSION; }
+
+const char* mgmc_last_error(const mgmc_handle* h) {
+    if (h) return h->last_error.c_str();
+    std::lock_guard<std::mutex> lock(g_err_mutex);
+    static thread_local std::string copy;
+    copy = g_last_error;
+    return copy.c_str();
+}
+
+int mgmc_describe(const mgmc_config* cfg, mgmc_level_desc* out, int max_levels) {
+    if (!cfg) return fail(nullptr, MGMC_E_INVALID, "null config");
+    const std::string err = validate_config(*cfg);
+    if (!err.empty()) return fail(nullptr, MGMC_E_INVALID, err);
+    const std::vector<LevelSpec> lv = build_hierarchy(*cfg);
+    if (out) {
+        for (int l = 0; l < (int)lv.size() && l < max_levels; ++l) fill_desc(lv[l], &out[l]);
+    }
+    return (int)lv.size();
+}
+
+int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chain_id, mgmc_handle** out) {
+    if (!cfg || !out) return fail(nullptr, MGMC_E_INVALID, "null argument");
+    *out = nullptr;
+    const std::string err = validate_config(*cfg);
+    if (!err.empty()) return fail(nullptr, MGMC_E_INVALID, err);
+    if (cfg->coarse_solver == MGMC_COARSE_CHOLESKY)
+        return fail(nullptr, MGMC_E_UNSUPPORTED, "coarse_solver=Cholesky is not on the device path yet");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(nullptr, MGMC_E_HIP, "no HIP device");
+    if (device < 0 || device >= ndev) return fail(nullptr, MGMC_E_INVALID, "device index out of range");
+    mgmc_handle* h = new mgmc_handle();
+    h->cfg = *cfg;
+    h->device = device;
+    h->seed = seed;
+    h->chain = chain_id;
+    h->key = make_key(seed, chain_id);
+    if (hipSetDevice(device) != hipSuccess) {
+        delete h;
+        return fail(nullptr, MGMC_E_HIP, "hipSetDevice failed");
+    }
+    int rc = MGMC_OK;
+    auto bail = [&](int code) {
+        set_global_error(h->last_error);
+        mgmc_destroy(h);
+        return code;
+    };
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        h->last_error = "hipStreamCreate failed";
+        return bail(MGMC_E_HIP);
+    }
+    const std::vector<LevelSpec> specs = build_hierarchy(*cfg);
+    size_t lds_limit = 150 * 1024;
+    for (size_t l = 0; l < specs.size(); ++l) {
+        Level lv;
+        lv.spec = specs[l];
+        lv.L = make_layout(cfg->dim, specs[l].n);
+        memcpy(lv.S.a, specs[l].st, sizeof(lv.S.a));
+        const size_t bytes = lv.L.nstore * sizeof(double);
+        if (hipMalloc(&lv.x, bytes) != hipSuccess || hipMalloc(&lv.f, bytes) != hipSuccess) {
+            h->levels.push_back(lv);
+            h->last_error = "device allocation failed";
+            return bail(MGMC_E_NOMEM);
+        }
+        hipMemsetAsync(lv.x, 0, bytes, h->stream);
+        hipMemsetAsync(lv.f, 0, bytes, h->stream);
+        if (l + 1 == specs.size() && 2 * bytes <= lds_limit) lv.lds_bytes = 2 * bytes;
+        h->levels.push_back(lv);
+    }
+    if (hipMalloc(&h->ctrl, 8 * sizeof(uint64_t)) != hipSuccess || hipMalloc(&h->mom, 4 * sizeof(double)) != hipSuccess) {
+        h->last_error = "device allocation failed";
+        return bail(MGMC_E_NOMEM);
+    }
+    uint64_t ctrl0[8] = {0, 0, (uint64_t)(int64_t)-1, 0, 0, 0, 0, 0};
+    hipMemcpyAsync(h->ctrl, ctrl0, sizeof(ctrl0), hipMemcpyHostToDevice, h->stream);
+    hipMemsetAsync(h->mom, 0, 4 * sizeof(double), h->stream);
+    // op sequence of one sample
+    uint32_t tag = 0;
+    build_ops_level(h, 0, tag);
+    h->ops.push_back({OP_QOI, 0, 0, 0, 0});
+    if (specs.size() == 1) {
+        h->seg_end_pre = h->seg_begin_post = h->seg_end_post = 0;
+    }
+    if ((rc = ensure_series(h, 1024)) != MGMC_OK) return bail(rc);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) {
+        h->last_error = "stream sync failed after setup";
+        return bail(MGMC_E_HIP);
+    }
+    if (cfg->verbose > 0) {
+        printf("Setting up Multilevel MC sampler (HIP, device %d)\n", device);
+        for (size_t l = 0; l < specs.size(); ++l)
+            printf("  level %zu lattice : %dd lattice, %d x %d x %d cells, %llu unknowns, %d-point stencil\n", l,
+                   cfg->dim, specs[l].n[0], specs[l].n[1], specs[l].n[2], (unsigned long long)specs[l].ndof,
+                   specs[l].npoints);
+    }
+    *out = h;
+    return MGMC_OK;
+}
+
+int mgmc_destroy(mgmc_handle* h) {
+    if (!h) return MGMC_OK;
+    hipSetDevice(h->device);
+    if (h->stream) hipStreamSynchronize(h->stream);
+    destroy_graphs(h);
+    for (auto& lv : h->levels) {
+        if (lv.x) hipFree(lv.x);
+        if (lv.f) hipFree(lv.f);
+        for (auto p : lv.scratch)
+            if (p) hipFree(p);
+    }
+    if (h->ctrl) hipFree(h->ctrl);
+    if (h->mom) hipFree(h->mom);
+    if (h->series) hipFree(h->series);
+    if (h->lex_tmp) hipFree(h->lex_tmp);
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;
+    return MGMC_OK;
+}
+
+int mgmc_level_desc_get(const mgmc_handle* h, int level, mgmc_level_desc* out) {
+    if (!h || !out) return fail(nullptr, MGMC_E_INVALID, "null argument");
+    if (level < 0 || level >= (int)h->levels.size()) return fail(nullptr, MGMC_E_INVALID, "level out of range");
+    fill_desc(h->levels[level].spec, out);
+    return MGMC_OK;
+}
+
+int mgmc_set_rhs(mgmc_handle* h, const double* f, size_t n) {
+    if (!h || !f) return fail(h, MGMC_E_INVALID, "null argument");
+    if (n != h->levels[0].spec.ndof) return fail(h, MGMC_E_INVALID, "rhs size mismatch");
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc = upload(h, 0, f, h->levels[0].f);
+    if (rc) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return MGMC_OK;
+}
+
+int mgmc_set_state(mgmc_handle* h, const double* x, size_t n) {
+    if (!h || !x) return fail(h, MGMC_E_INVALID, "null argument");
+    if (n != h->levels[0].spec.ndof) return fail(h, MGMC_E_INVALID, "state size mismatch");
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc = upload(h, 0, x, h->levels[0].x);
+    if (rc) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return MGMC_OK;
+}
+
+int mgmc_get_state(mgmc_handle* h, double* x, size_t n) {
+    if (!h || !x) return fail(h, MGMC_E_INVALID, "null argument");
+    if (n != h->levels[0].spec.ndof) return fail(h, MGMC_E_INVALID, "state size mismatch");
+    HIPCHK(h, hipSetDevice(h->device));
+    return download(h, 0, h->levels[0].x, x);
+}
+
+static int set_qoi(mgmc_handle* h, int64_t qoi_index) {
+    int64_t store = -1;
+    if (qoi_index >= 0) {
+        const Level& lv = h->levels[0];
+        if ((uint64_t)qoi_index >= lv.spec.ndof) return fail(h, MGMC_E_INVALID, "qoi index out of range");
+        const int nxi = lv.L.nx - 1, nyi = lv.L.ny - 1;
+        const int i = (int)(qoi_index % nxi) + 1;
+        const int j = (int)((qoi_index / nxi) % nyi) + 1;
+        const int k = lv.spec.dim == 3 ? (int)(qoi_index / ((int64_t)nxi * nyi)) + 1 : 0;
+        store = lv.L.at(i, j, k);
+    }
+    if (store != h->qoi_store_index) {
+        HIPCHK(h, hipMemcpyAsync(h->ctrl + 2, &store, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->qoi_store_index = store;
+    }
+    return MGMC_OK;
+}
+
+int mgmc_apply(mgmc_handle* h, const double* f, double* x, size_t n) {
+    if (!h || !f || !x) return fail(h, MGMC_E_INVALID, "null argument");
+    int rc = mgmc_set_rhs(h, f, n);
+    if (rc) return rc;
+    if ((rc = mgmc_set_state(h, x, n))) return rc;
+    if ((rc = set_qoi(h, -1))) return rc;
+    HIPCHK(h, hipGraphLaunch(h->graph_all, h->stream));
+    return mgmc_get_state(h, x, n);
+}
+
+int mgmc_sample_async(mgmc_handle* h, int nsteps, int64_t qoi_index) {
+    if (!h || nsteps < 0) return fail(h, MGMC_E_INVALID, "invalid argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc = set_qoi(h, qoi_index);
+    if (rc) return rc;
+    // series restarts at 0 for each call
+    HIPCHK(h, hipMemsetAsync(h->ctrl + 1, 0, sizeof(uint64_t), h->stream));
+    if ((rc = ensure_series(h, (uint64_t)std::max(nsteps, 1)))) return rc;
+    for (int s = 0; s < nsteps; ++s) HIPCHK(h, hipGraphLaunch(h->graph_all, h->stream));
+    return MGMC_OK;
+}
+
+int mgmc_synchronize(mgmc_handle* h) {
+    if (!h) return fail(nullptr, MGMC_E_INVALID, "null handle");
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return MGMC_OK;
+}
+
+int mgmc_sample(mgmc_handle* h, int nsteps, int64_t qoi_index, double* qoi_out) {
+    int rc = mgmc_sample_async(h, nsteps, qoi_index);
+    if (rc) return rc;
+    if (qoi_out && nsteps > 0 && qoi_index >= 0)
+        HIPCHK(h, hipMemcpyAsync(qoi_out, h->series, nsteps * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return MGMC_OK;
+}
+
+int mgmc_qoi_moments(mgmc_handle* h, double out[3]) {
+    if (!h || !out) return fail(h, MGMC_E_INVALID, "null argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    double m[4];
+    HIPCHK(h, hipMemcpyAsync(m, h->mom, sizeof(m), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    out[0] = m[0];
+    out[1] = m[1];
+    out[2] = m[2];
+    return MGMC_OK;
+}
+
+int mgmc_reset_moments(mgmc_handle* h) {
+    if (!h) return fail(nullptr, MGMC_E_INVALID, "null handle");
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipMemsetAsync(h->mom, 0, 4 * sizeof(double), h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return MGMC_OK;
+}
+
+int mgmc_set_sample_index(mgmc_handle* h, uint64_t index) {
+    if (!h) return fail(nullptr, MGMC_E_INVALID, "null handle");
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipMemcpyAsync(h->ctrl, &index, sizeof(index), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return MGMC_OK;
+}
+
+int mgmc_get_sample_index(mgmc_handle* h, uint64_t* index) {
+    if (!h || !index) return fail(h, MGMC_E_INVALID, "null argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipMemcpyAsync(index, h->ctrl, sizeof(uint64_t), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return MGMC_OK;
+}
+
+int mgmc_get_stream(mgmc_handle* h, void** stream) {
+    if (!h || !stream) return fail(h, MGMC_E_INVALID, "null argument");
+    *stream = (void*)h->stream;
+    return MGMC_OK;
+}
+
+// ---------------- component entry points ----------------
+
+int mgmc_operator_apply(mgmc_handle* h, int level, const double* x, double* y) {
+    int rc = check_level(h, level, false);
+    if (rc) return rc;
+    if (!x || !y) return fail(h, MGMC_E_INVALID, "null argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    if ((rc = ensure_scratch(h, level))) return rc;
+    Level& lv = h->levels[level];
+    if ((rc = upload(h, level, x, lv.scratch[0]))) return rc;
+    dim3 block(64, 4, 1);
+    dim3 grid = grid3(lv.L.nx - 1, lv.L.ny - 1, lv.spec.dim == 3 ? lv.L.nz - 1 : 1, block);
+    const int dim = lv.spec.dim, np = lv.spec.npoints;
+    const double* xs = lv.scratch[0];
+    double* ys = lv.scratch[1];
+    if (dim == 3 && np == 7)
+        hipLaunchKernelGGL((k_operator_apply<3, 7>), grid, block, 0, h->stream, lv.L, xs, ys, lv.S);
+    else if (dim == 3)
+        hipLaunchKernelGGL((k_operator_apply<3, 27>), grid, block, 0, h->stream, lv.L, xs, ys, lv.S);
+    else if (np == 5)
+        hipLaunchKernelGGL((k_operator_apply<2, 5>), grid, block, 0, h->stream, lv.L, xs, ys, lv.S);
+    else
+        hipLaunchKernelGGL((k_operator_apply<2, 9>), grid, block, 0, h->stream, lv.L, xs, ys, lv.S);
+    HIPCHK(h, hipGetLastError());
+    return download(h, level, ys, y);
+}
+
+static int sweep_component(mgmc_handle* h, int level, int direction, int nsweeps, bool noise, uint32_t tag,
+                           uint64_t sample, const double* b, double* x) {
+    int rc = check_level(h, level, false);
+    if (rc) return rc;
+    if (!b || !x) return fail(h, MGMC_E_INVALID, "null argument");
+    if (direction != MGMC_FORWARD && direction != MGMC_BACKWARD) return fail(h, MGMC_E_INVALID, "invalid direction");
+    HIPCHK(h, hipSetDevice(h->device));
+    if ((rc = ensure_scratch(h, level))) return rc;
+    Level& lv = h->levels[level];
+    if ((rc = upload(h, level, b, lv.scratch[0]))) return rc;
+    if ((rc = upload(h, level, x, lv.scratch[1]))) return rc;
+    HIPCHK(h, hipMemcpyAsync(h->ctrl + 3, &sample, sizeof(sample), hipMemcpyHostToDevice, h->stream));
+    for (int s = 0; s < nsweeps; ++s) {
+        GibbsArg g = make_gibbs(h, lv, tag + (uint32_t)s, 0, h->ctrl + 3);
+        launch_sweep(lv, lv.scratch[1], lv.scratch[0], g, direction, noise, h->stream);
+    }
+    HIPCHK(h, hipGetLastError());
+    return download(h, level, lv.scratch[1], x);
+}
+
+int mgmc_smoother_apply(mgmc_handle* h, int level, int direction, int nsweeps, const double* b, double* x) {
+    return sweep_component(h, level, direction, nsweeps, false, 0, 0, b, x);
+}
+
+int mgmc_sor_sampler_apply(mgmc_handle* h, int level, int direction, uint32_t sweep_tag, uint64_t sample_index,
+                           const double* f, double* x) {
+    return sweep_component(h, level, direction, 1, true, sweep_tag, sample_index, f, x);
+}
+
+int mgmc_restrict(mgmc_handle* h, int level, const double* r, double* rc_out) {
+    int rc = check_level(h, level, true);
+    if (rc) return rc;
+    if (!r || !rc_out) return fail(h, MGMC_E_INVALID, "null argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    if ((rc = ensure_scratch(h, level)) || (rc = ensure_scratch(h, level + 1))) return rc;
+    Level& lf = h->levels[level];
+    Level& lc = h->levels[level + 1];
+    if ((rc = upload(h, level, r, lf.scratch[0]))) return rc;
+    dim3 block(64, 4, 1);
+    dim3 grid = grid3(lc.L.nx - 1, lc.L.ny - 1, lf.spec.dim == 3 ? lc.L.nz - 1 : 1, block);
+    if (lf.spec.dim == 3)
+        hipLaunchKernelGGL((k_restrict<3>), grid, block, 0, h->stream, lf.L, lc.L, (const double*)lf.scratch[0],
+                           lc.scratch[0]);
+    else
+        hipLaunchKernelGGL((k_restrict<2>), grid, block, 0, h->stream, lf.L, lc.L, (const double*)lf.scratch[0],
+                           lc.scratch[0]);
+    HIPCHK(h, hipGetLastError());
+    return download(h, level + 1, lc.scratch[0], rc_out);
+}
+
+int mgmc_prolongate_add(mgmc_handle* h, int level, double alpha, const double* xc, double* x) {
+    int rc = check_level(h, level, true);
+    if (rc) return rc;
+    if (!xc || !x) return fail(h, MGMC_E_INVALID, "null argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    if ((rc = ensure_scratch(h, level)) || (rc = ensure_scratch(h, level + 1))) return rc;
+    Level& lf = h->levels[level];
+    Level& lc = h->levels[level + 1];
+    if ((rc = upload(h, level + 1, xc, lc.scratch[0]))) return rc;
+    if ((rc = upload(h, level, x, lf.scratch[0]))) return rc;
+    launch_prolongate(lf, lc, lf.scratch[0], lc.scratch[0], alpha, h->stream);
+    HIPCHK(h, hipGetLastError());
+    return download(h, level, lf.scratch[0], x);
+}
+
+int mgmc_residual_restrict(mgmc_handle* h, int level, const double* f, const double* x, double* fc) {
+    int rc = check_level(h, level, true);
+    if (rc) return rc;
+    if (!f || !x || !fc) return fail(h, MGMC_E_INVALID, "null argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    if ((rc = ensure_scratch(h, level)) || (rc = ensure_scratch(h, level + 1))) return rc;
+    Level& lf = h->levels[level];
+    Level& lc = h->levels[level + 1];
+    if ((rc = upload(h, level, f, lf.scratch[0]))) return rc;
+    if ((rc = upload(h, level, x, lf.scratch[1]))) return rc;
+    launch_residual_restrict(lf, lc, lf.scratch[1], lf.scratch[0], lc.scratch[0], lc.scratch[1], 1, h->stream);
+    HIPCHK(h, hipGetLastError());
+    return download(h, level + 1, lc.scratch[0], fc);
+}
+
+int mgmc_normals(mgmc_handle* h, uint64_t pair0, size_t n, uint32_t sweep_tag, uint64_t sample_index, double* out) {
+    if (!h || !out) return fail(h, MGMC_E_INVALID, "null argument");
+    if (n % 2) return fail(h, MGMC_E_INVALID, "n must be even");
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc = ensure_lex(h, std::max<size_t>(n, 1));
+    if (rc) return rc;
+    const uint64_t npairs = n / 2;
+    if (npairs) {
+        hipLaunchKernelGGL(k_normals, dim3((unsigned)((npairs + 255) / 256)), dim3(256), 0, h->stream, h->key, pair0,
+                           npairs, sweep_tag, sample_index, h->lex_tmp);
+        HIPCHK(h, hipGetLastError());
+        HIPCHK(h, hipMemcpyAsync(out, h->lex_tmp, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return MGMC_OK;
+}
+
+int mgmc_time_fine_sweeps(mgmc_handle* h, int nsweeps, float* ms) {
+    if (!h || !ms || nsweeps < 1) return fail(h, MGMC_E_INVALID, "invalid argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    Level& lv = h->levels[0];
+    hipEvent_t e0, e1;
+    HIPCHK(h, hipEventCreate(&e0));
+    HIPCHK(h, hipEventCreate(&e1));
+    HIPCHK(h, hipEventRecord(e0, h->stream));
+    for (int s = 0; s < nsweeps; ++s) {
+        GibbsArg g = make_gibbs(h, lv, 0x80000000u + (uint32_t)s, 0, h->ctrl);
+        launch_sweep(lv, lv.x, lv.f, g, MGMC_FORWARD, true, h->stream);
+    }
+    HIPCHK(h, hipEventRecord(e1, h->stream));
+    HIPCHK(h, hipEventSynchronize(e1));
+    HIPCHK(h, hipEventElapsedTime(ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    return MGMC_OK;
+}
+
+int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* fine_ms,
+                      int* nfine) {
+    if (!h || nsteps < 1 || !total_ms || !fine_ms || !nfine) return fail(h, MGMC_E_INVALID, "invalid argument");
+    if (h->levels.size() < 2) return fail(h, MGMC_E_UNSUPPORTED, "timed sampling needs nlevel >= 2");
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc = set_qoi(h, qoi_index);
+    if (rc) return rc;
+    HIPCHK(h, hipMemsetAsync(h->ctrl + 1, 0, sizeof(uint64_t), h->stream));
+    if ((rc = ensure_series(h, (uint64_t)nsteps))) return rc;
+    std::vector<hipEvent_t> ev(4 * (size_t)nsteps + 1);
+    for (auto& e : ev) HIPCHK(h, hipEventCreate(&e));
+    for (int s = 0; s < nsteps; ++s) {
+        for (int g = 0; g < 4; ++g) {
+            HIPCHK(h, hipEventRecord(ev[4 * s + g], h->stream));
+            HIPCHK(h, hipGraphLaunch(h->graph_seg[g], h->stream));
+        }
+    }
+    HIPCHK(h, hipEventRecord(ev[4 * nsteps], h->stream));
+    HIPCHK(h, hipEventSynchronize(ev[4 * nsteps]));
+    float t = 0.f;
+    double fine = 0.0;
+    for (int s = 0; s < nsteps; ++s) {
+        HIPCHK(h, hipEventElapsedTime(&t, ev[4 * s], ev[4 * s + 1]));
+        fine += t;
+        HIPCHK(h, hipEventElapsedTime(&t, ev[4 * s + 2], ev[4 * s + 3]));
+        fine += t;
+    }
+    HIPCHK(h, hipEventElapsedTime(&t, ev[0], ev[4 * nsteps]));
+    *total_ms = t;
+    *fine_ms = fine;
+    int cnt = 0;
+    for (size_t q = 0; q < h->ops.size(); ++q)
+        if (h->ops[q].kind == OP_SWEEP && h->ops[q].level == 0) ++cnt;
+    *nfine = cnt * nsteps;
+    for (auto& e : ev) hipEventDestroy(e);
+    return MGMC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,357 @@
+// mgmc_kernels.hpp -- HIP kernels of the MGMC V-cycle for gfx950 (CDNA4).
+//
+// Data layout in HBM (every level): the (n+1)^d lattice vertices INCLUDING the Dirichlet
+// boundary are stored, boundary values are zero and never written, so every stencil is
+// branch-free.  Vertex (i,j,k), 0 <= i <= nx, sits at  k*sp + j*sx + i + off  with off = 7
+// (interior i=1 is 64-byte aligned) and sx a multiple of 8 doubles.
+//
+// Per-point arithmetic is the reference's expression tree, evaluated in the same order
+// (compiled with -ffp-contract=off):
+//   * Gibbs/SOR update  x += omega * (c - sum_k a_k x_k) / a_c,  c = sqrt(a_c(2-w)/w)*xi + f,
+//     the sum running over the row in ascending column order starting from 0.0
+//     (smoother/sor_smoother.cc:66-76, sampler/sor_sampler.cc:42-46);
+//   * residual  r = f - A x  with A x accumulated in ascending column order
+//     (linear_operator/linear_operator.hh:66-76, Eigen ColMajor SpMV);
+//   * restriction  sum_sigma w_sigma r(2i+sigma), sigma with x fastest
+//     (intergrid/intergrid_operator.hh:74-88, intergrid_operator_linear.cc:13-29);
+//   * prolongate-add  x += (alpha*w) * xc  in ascending coarse index
+//     (intergrid/intergrid_operator.hh:106-120) -- evaluated in gather form, which visits the
+//     coarse contributions of a fine vertex in exactly the scatter order of the reference.
+// What differs from the reference is the visiting order of the Gibbs updates (multicolour
+// instead of lexicographic) and the noise stream (Philox, see philox_normal.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "philox_normal.h"
+
+namespace mgmc {
+
+struct Layout {
+    int dim;
+    int nx, ny, nz;  // cells
+    int off;
+    int pad_;
+    long long sx, sp, nstore;
+    __host__ __device__ long long at(int i, int j, int k) const {
+        return (long long)k * sp + (long long)j * sx + (long long)i + off;
+    }
+};
+
+inline Layout make_layout(int dim, const int n[3]) {
+    Layout L;
+    L.dim = dim;
+    L.nx = n[0];
+    L.ny = n[1];
+    L.nz = dim == 3 ? n[2] : 0;
+    L.off = 7;
+    L.pad_ = 0;
+    L.sx = ((long long)L.nx + 8 + 7) / 8 * 8;
+    L.sp = L.sx * (L.ny + 1);
+    L.nstore = (dim == 3 ? L.sp * (L.nz + 1) : L.sp) + 64;
+    return L;
+}
+
+struct StencilArg {
+    double a[27];
+};
+
+struct GibbsArg {
+    double omega;
+    double sd;  // sqrt(diag*(2-omega)/omega)
+    RngKey key;
+    uint32_t tag;
+    int colour;
+    const uint64_t* sample;  // device word holding the sample index
+};
+
+// ascending-column-order row sum  sum_k a_k x_k  starting from 0.0
+template <int DIM, int NPTS>
+__device__ __forceinline__ double stencil_sum(const double* __restrict__ x, long long p, const Layout& L,
+                                              const StencilArg& S) {
+    double res = 0.0;
+    if (NPTS == 7) {
+        res += S.a[4] * x[p - L.sp];
+        res += S.a[10] * x[p - L.sx];
+        res += S.a[12] * x[p - 1];
+        res += S.a[13] * x[p];
+        res += S.a[14] * x[p + 1];
+        res += S.a[16] * x[p + L.sx];
+        res += S.a[22] * x[p + L.sp];
+    } else if (NPTS == 5) {
+        res += S.a[1] * x[p - L.sx];
+        res += S.a[3] * x[p - 1];
+        res += S.a[4] * x[p];
+        res += S.a[5] * x[p + 1];
+        res += S.a[7] * x[p + L.sx];
+    } else if (NPTS == 27) {
+#pragma unroll
+        for (int dz = -1; dz <= 1; ++dz)
+#pragma unroll
+            for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                for (int dx = -1; dx <= 1; ++dx)
+                    res += S.a[(dz + 1) * 9 + (dy + 1) * 3 + (dx + 1)] * x[p + dz * L.sp + dy * L.sx + dx];
+    } else {  // 9
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) res += S.a[(dy + 1) * 3 + (dx + 1)] * x[p + dy * L.sx + dx];
+    }
+    return res;
+}
+
+template <int DIM>
+__device__ __forceinline__ double centre(const StencilArg& S) {
+    return DIM == 3 ? S.a[13] : S.a[4];
+}
+
+// Philox pair id of vertex (i,j,k) and whether it takes the cos branch
+template <int DIM>
+__device__ __forceinline__ uint32_t pair_id(const Layout& L, int i, int j, int k) {
+    const uint64_t row = (DIM == 3) ? (uint64_t)(k - 1) * (uint64_t)(L.ny - 1) + (uint64_t)(j - 1) : (uint64_t)(j - 1);
+    return (uint32_t)(row * (uint64_t)(L.nx / 2) + (uint64_t)((i - 1) >> 1));
+}
+
+template <int DIM, int NPTS, bool NOISE>
+__device__ __forceinline__ void gibbs_point(double* __restrict__ x, const double* __restrict__ f, long long p,
+                                            const Layout& L, const StencilArg& S, const GibbsArg& G, uint64_t sample,
+                                            int i, int j, int k) {
+    const double res = stencil_sum<DIM, NPTS>(x, p, L, S);
+    double c = f[p];
+    if (NOISE) {
+        const double xi = point_normal(G.key, pair_id<DIM>(L, i, j, k), (i & 1) != 0, G.tag, sample);
+        c = G.sd * xi + f[p];
+    }
+    x[p] += G.omega * (c - res) / centre<DIM>(S);
+}
+
+// ---- red-black sweep pass of the fine 5/7-point level: vertices with (i+j+k)&1 == colour ----
+template <int DIM, int NPTS, bool NOISE>
+__global__ void __launch_bounds__(256) k_sweep_rb(Layout L, double* __restrict__ x, const double* __restrict__ f,
+                                                  StencilArg S, GibbsArg G) {
+    const int tx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = blockIdx.y * blockDim.y + threadIdx.y + 1;
+    const int k = (DIM == 3) ? (int)blockIdx.z + 1 : 0;
+    if (j > L.ny - 1) return;
+    const int i = 1 + (((1 + j + k) ^ G.colour) & 1) + 2 * tx;
+    if (i > L.nx - 1) return;
+    const uint64_t sample = NOISE ? *G.sample : 0;
+    gibbs_point<DIM, NPTS, NOISE>(x, f, L.at(i, j, k), L, S, G, sample, i, j, k);
+}
+
+// ---- 2^d-colour sweep pass of a Galerkin 9/27-point level: colour bit d = parity of coord d ----
+template <int DIM, int NPTS, bool NOISE>
+__global__ void __launch_bounds__(256) k_sweep_mc(Layout L, double* __restrict__ x, const double* __restrict__ f,
+                                                  StencilArg S, GibbsArg G) {
+    const int i = 2 - (G.colour & 1) + 2 * (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int j = 2 - ((G.colour >> 1) & 1) + 2 * (int)(blockIdx.y * blockDim.y + threadIdx.y);
+    const int k = (DIM == 3) ? 2 - ((G.colour >> 2) & 1) + 2 * (int)blockIdx.z : 0;
+    if (i > L.nx - 1 || j > L.ny - 1) return;
+    if (DIM == 3 && k > L.nz - 1) return;
+    const uint64_t sample = NOISE ? *G.sample : 0;
+    gibbs_point<DIM, NPTS, NOISE>(x, f, L.at(i, j, k), L, S, G, sample, i, j, k);
+}
+
+// colour of a vertex under the scheme used for a level with NPTS points
+template <int DIM, int NPTS>
+__device__ __forceinline__ int colour_of(int i, int j, int k) {
+    if (NPTS == 7 || NPTS == 5) return (i + j + k) & 1;
+    return (i & 1) | ((j & 1) << 1) | ((k & 1) << 2);
+}
+
+// ---- whole coarse-level SSOR sampler in one workgroup, state in LDS ----
+// nsweeps sweeps alternating forward/backward (SSORSampler::apply, ssor_sampler.cc:9-15),
+// sweep s uses tag0 + s.
+template <int DIM, int NPTS>
+__global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __restrict__ xg,
+                                                          const double* __restrict__ fg, StencilArg S, GibbsArg G,
+                                                          int nsweeps, int ncolours) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* xs = smem;
+    double* fs = smem + L.nstore;
+    for (long long q = threadIdx.x; q < L.nstore; q += blockDim.x) {
+        xs[q] = xg[q];
+        fs[q] = fg[q];
+    }
+    __syncthreads();
+    const uint64_t sample = *G.sample;
+    const int nxi = L.nx - 1, nyi = L.ny - 1;
+    const long long ndof = (long long)nxi * nyi * (DIM == 3 ? (L.nz - 1) : 1);
+    GibbsArg g = G;
+    for (int s = 0; s < nsweeps; ++s) {
+        g.tag = G.tag + (uint32_t)s;
+        const bool backward = (s & 1) != 0;
+        for (int cc = 0; cc < ncolours; ++cc) {
+            const int colour = backward ? ncolours - 1 - cc : cc;
+            for (long long q = threadIdx.x; q < ndof; q += blockDim.x) {
+                const int i = (int)(q % nxi) + 1;
+                const int j = (int)((q / nxi) % nyi) + 1;
+                const int k = (DIM == 3) ? (int)(q / ((long long)nxi * nyi)) + 1 : 0;
+                if (colour_of<DIM, NPTS>(i, j, k) != colour) continue;
+                gibbs_point<DIM, NPTS, true>(xs, fs, L.at(i, j, k), L, S, g, sample, i, j, k);
+            }
+            __syncthreads();
+        }
+    }
+    for (long long q = threadIdx.x; q < L.nstore; q += blockDim.x) xg[q] = xs[q];
+}
+
+// ---- fused residual + restriction: fc = R (f - A x), xc = 0 (multigridmc_sampler.cc:118-122) ----
+__device__ __forceinline__ double w1(int s) { return s == 0 ? 1.0 : 0.5; }
+
+template <int DIM, int NPTS>
+__global__ void __launch_bounds__(256) k_residual_restrict(Layout Lf, Layout Lc, const double* __restrict__ xf,
+                                                           const double* __restrict__ ff, double* __restrict__ fc,
+                                                           double* __restrict__ xc, StencilArg S, int zero_xc) {
+    const int I = blockIdx.x * blockDim.x + threadIdx.x + 1;
+    const int J = blockIdx.y * blockDim.y + threadIdx.y + 1;
+    const int K = (DIM == 3) ? (int)blockIdx.z + 1 : 0;
+    if (I > Lc.nx - 1 || J > Lc.ny - 1) return;
+    const long long pf = Lf.at(2 * I, 2 * J, 2 * K);
+    double result = 0.0;
+    const int zr = (DIM == 3) ? 1 : 0;
+#pragma unroll
+    for (int sz = -zr; sz <= zr; ++sz)
+#pragma unroll
+        for (int sy = -1; sy <= 1; ++sy)
+#pragma unroll
+            for (int sx = -1; sx <= 1; ++sx) {
+                const long long q = pf + sz * Lf.sp + sy * Lf.sx + sx;
+                const double y = stencil_sum<DIM, NPTS>(xf, q, Lf, S);
+                const double r = ff[q] - y;
+                double w = 1.0;
+                w *= w1(sx);
+                w *= w1(sy);
+                if (DIM == 3) w *= w1(sz);
+                result += w * r;
+            }
+    const long long pc = Lc.at(I, J, K);
+    fc[pc] = result;
+    if (zero_xc) xc[pc] = 0.0;
+}
+
+// ---- restriction only (tests): rc = R r ----
+template <int DIM>
+__global__ void __launch_bounds__(256) k_restrict(Layout Lf, Layout Lc, const double* __restrict__ r,
+                                                  double* __restrict__ rc) {
+    const int I = blockIdx.x * blockDim.x + threadIdx.x + 1;
+    const int J = blockIdx.y * blockDim.y + threadIdx.y + 1;
+    const int K = (DIM == 3) ? (int)blockIdx.z + 1 : 0;
+    if (I > Lc.nx - 1 || J > Lc.ny - 1) return;
+    const long long pf = Lf.at(2 * I, 2 * J, 2 * K);
+    double result = 0.0;
+    const int zr = (DIM == 3) ? 1 : 0;
+    for (int sz = -zr; sz <= zr; ++sz)
+        for (int sy = -1; sy <= 1; ++sy)
+            for (int sx = -1; sx <= 1; ++sx) {
+                double w = 1.0;
+                w *= w1(sx);
+                w *= w1(sy);
+                if (DIM == 3) w *= w1(sz);
+                result += w * r[pf + sz * Lf.sp + sy * Lf.sx + sx];
+            }
+    rc[Lc.at(I, J, K)] = result;
+}
+
+// ---- prolongate-add in gather form: x += alpha * P xc ----
+template <int DIM>
+__global__ void __launch_bounds__(256) k_prolongate_add(Layout Lf, Layout Lc, double* __restrict__ x,
+                                                        const double* __restrict__ xc, double alpha) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x + 1;
+    const int j = blockIdx.y * blockDim.y + threadIdx.y + 1;
+    const int k = (DIM == 3) ? (int)blockIdx.z + 1 : 0;
+    if (i > Lf.nx - 1 || j > Lf.ny - 1) return;
+    const long long p = Lf.at(i, j, k);
+    double v = x[p];
+    // coarse coordinates contributing along each axis, ascending
+    const int i0 = i >> 1, j0 = j >> 1, k0 = k >> 1;
+    const int ni = (i & 1) ? 2 : 1, nj = (j & 1) ? 2 : 1, nk = (DIM == 3 && (k & 1)) ? 2 : 1;
+    for (int a = 0; a < nk; ++a) {
+        const int kk = k0 + a;
+        if (DIM == 3 && (kk < 1 || kk > Lc.nz - 1)) continue;
+        for (int b = 0; b < nj; ++b) {
+            const int jj = j0 + b;
+            if (jj < 1 || jj > Lc.ny - 1) continue;
+            for (int c = 0; c < ni; ++c) {
+                const int ii = i0 + c;
+                if (ii < 1 || ii > Lc.nx - 1) continue;
+                double w = 1.0;
+                w *= w1(i - 2 * ii);
+                w *= w1(j - 2 * jj);
+                if (DIM == 3) w *= w1(k - 2 * kk);
+                v += alpha * w * xc[Lc.at(ii, jj, DIM == 3 ? kk : 0)];
+            }
+        }
+    }
+    x[p] = v;
+}
+
+// ---- y = A x (tests, LinearOperator::apply) ----
+template <int DIM, int NPTS>
+__global__ void __launch_bounds__(256) k_operator_apply(Layout L, const double* __restrict__ x, double* __restrict__ y,
+                                                        StencilArg S) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x + 1;
+    const int j = blockIdx.y * blockDim.y + threadIdx.y + 1;
+    const int k = (DIM == 3) ? (int)blockIdx.z + 1 : 0;
+    if (i > L.nx - 1 || j > L.ny - 1) return;
+    const long long p = L.at(i, j, k);
+    y[p] = stencil_sum<DIM, NPTS>(x, p, L, S);
+}
+
+// ---- reference (lexicographic interior) layout <-> padded layout ----
+template <int DIM>
+__global__ void __launch_bounds__(256) k_pack(Layout L, const double* __restrict__ lex, double* __restrict__ pad) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x + 1;
+    const int j = blockIdx.y * blockDim.y + threadIdx.y + 1;
+    const int k = (DIM == 3) ? (int)blockIdx.z + 1 : 0;
+    if (i > L.nx - 1 || j > L.ny - 1) return;
+    const long long row = (DIM == 3) ? (long long)(k - 1) * (L.ny - 1) + (j - 1) : (long long)(j - 1);
+    pad[L.at(i, j, k)] = lex[row * (L.nx - 1) + (i - 1)];
+}
+
+template <int DIM>
+__global__ void __launch_bounds__(256) k_unpack(Layout L, const double* __restrict__ pad, double* __restrict__ lex) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x + 1;
+    const int j = blockIdx.y * blockDim.y + threadIdx.y + 1;
+    const int k = (DIM == 3) ? (int)blockIdx.z + 1 : 0;
+    if (i > L.nx - 1 || j > L.ny - 1) return;
+    const long long row = (DIM == 3) ? (long long)(k - 1) * (L.ny - 1) + (j - 1) : (long long)(j - 1);
+    lex[row * (L.nx - 1) + (i - 1)] = pad[L.at(i, j, k)];
+}
+
+// ---- QoI record + running moments; advances the sample index (driver_mgmc.cc:72-78, :86-94) ----
+// ctrl[0] = sample index, ctrl[1] = series length, ctrl[2] = QoI storage index (int64, <0 = off)
+__global__ void k_qoi_record(const double* __restrict__ x, uint64_t* ctrl, double* series, uint64_t capacity,
+                             double* mom) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const long long q = (long long)ctrl[2];
+    if (q >= 0) {
+        const double z = x[q];
+        const uint64_t n = ctrl[1];
+        if (n < capacity) series[n] = z;
+        ctrl[1] = n + 1;
+        const double cnt = mom[0] + 1.0;
+        const double delta = z - mom[1];
+        const double mean = mom[1] + delta / cnt;
+        mom[2] = mom[2] + delta * (z - mean);
+        mom[1] = mean;
+        mom[0] = cnt;
+    }
+    ctrl[0] = ctrl[0] + 1;
+}
+
+// ---- normals for the RNG parity test ----
+__global__ void k_normals(RngKey key, uint64_t pair0, uint64_t npairs, uint32_t tag, uint64_t sample,
+                          double* __restrict__ out) {
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= npairs) return;
+    const Philox4 r = philox4x32_10((uint32_t)(pair0 + q), tag, (uint32_t)sample, (uint32_t)(sample >> 32), key.k0,
+                                    key.k1);
+    double z0, z1;
+    normal_pair(r, &z0, &z1);
+    out[2 * q] = z0;
+    out[2 * q + 1] = z1;
+}
+
+}  // namespace mgmc

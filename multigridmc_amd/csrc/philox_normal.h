@@ -1,0 +1,162 @@
+// philox_normal.h -- counter-based Gaussian noise for the multicolour Gibbs sweeps.
+//
+// The reference draws its noise from one shared std::mt19937_64 through a
+// std::normal_distribution per sampler object (sampler/sampler.hh:31-34, :69-71;
+// sampler/sor_sampler.cc:42-46).  That stream is inherently sequential, so the device path
+// replaces it with a counter-based generator: every normal is a pure function of
+//   key     = (lo32(seed), lo32(chain) ^ hi32(seed))
+//   counter = (pair id, sweep tag, lo32(sample), hi32(sample))
+// (Philox4x32-10, Salmon et al. SC'11) followed by a Box-Muller transform whose log / sin / cos
+// are evaluated with a fixed sequence of IEEE-754 double operations (explicit fma, correctly
+// rounded div/sqrt).  The same bits therefore come out of gfx950 and of a host compiler with
+// -ffp-contract=off, which is what lets the CPU oracle replay the device chain exactly.
+//
+// Pair id: points (i, i+1) with i odd share one Philox call (cos branch for i odd, sin branch
+// for i even), pair = row * (nx/2) + (i-1)/2 with row the lexicographic index of (j,k).
+#pragma once
+#include <math.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define MGMC_HD __host__ __device__ inline __attribute__((always_inline))
+#else
+#define MGMC_HD static inline
+#endif
+
+namespace mgmc {
+
+struct Philox4 {
+    uint32_t v[4];
+};
+
+MGMC_HD Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)M0 * c0;
+        const uint64_t p1 = (uint64_t)M1 * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n1 = (uint32_t)p1;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        const uint32_t n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += W0; k1 += W1;
+    }
+    Philox4 out;
+    out.v[0] = c0; out.v[1] = c1; out.v[2] = c2; out.v[3] = c3;
+    return out;
+}
+
+MGMC_HD double as_double(uint64_t b) {
+    union { uint64_t u; double d; } c;
+    c.u = b;
+    return c.d;
+}
+MGMC_HD uint64_t as_bits(double d) {
+    union { uint64_t u; double d; } c;
+    c.d = d;
+    return c.u;
+}
+
+// 53-bit integer from two 32-bit words
+MGMC_HD uint64_t bits53(uint32_t a, uint32_t b) {
+    return ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+}
+
+// natural log of u in [2^-53, 1]; |rel err| ~ 1e-16
+MGMC_HD double log_unit(double u) {
+    const uint64_t b = as_bits(u);
+    int e = (int)((b >> 52) & 0x7ff) - 1023;
+    double m = as_double((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull);  // [1,2)
+    const bool big = m > 1.4142135623730951;
+    m = big ? m * 0.5 : m;
+    e = big ? e + 1 : e;
+    const double s = (m - 1.0) / (m + 1.0);  // |s| <= 0.1716
+    const double s2 = s * s;
+    double p = 1.0 / 23.0;
+    p = fma(p, s2, 1.0 / 21.0);
+    p = fma(p, s2, 1.0 / 19.0);
+    p = fma(p, s2, 1.0 / 17.0);
+    p = fma(p, s2, 1.0 / 15.0);
+    p = fma(p, s2, 1.0 / 13.0);
+    p = fma(p, s2, 1.0 / 11.0);
+    p = fma(p, s2, 1.0 / 9.0);
+    p = fma(p, s2, 1.0 / 7.0);
+    p = fma(p, s2, 1.0 / 5.0);
+    p = fma(p, s2, 1.0 / 3.0);
+    const double s3p = (s * s2) * p;            // s^3 * (1/3 + s^2/5 + ...)
+    const double logm = fma(2.0, s, 2.0 * s3p); // 2 atanh(s)
+    const double de = (double)e;
+    const double LN2_HI = 6.93147180369123816490e-01;  // 0x3fe62e42fee00000
+    const double LN2_LO = 1.90821492927058770002e-10;  // 0x3dea39ef35793c76
+    return fma(de, LN2_HI, fma(de, LN2_LO, logm));
+}
+
+// (cos(2 pi t), sin(2 pi t)) for t in [0,1)
+MGMC_HD void sincos_2pi(double t, double* c_out, double* s_out) {
+    const int q = (int)(t * 4.0 + 0.5);          // 0..4
+    const double r = t - (double)q * 0.25;         // exact, |r| <= 1/8
+    const double th = r * 6.28318530717958647692;  // |th| <= pi/4
+    const double t2 = th * th;
+    // sin(th) = th * (1 - t2/3! + t2^2/5! - ...) up to th^17
+    double ps = -1.0 / 355687428096000.0;   // -1/17!
+    ps = fma(ps, t2, 1.0 / 1307674368000.0);  // 1/15!
+    ps = fma(ps, t2, -1.0 / 6227020800.0);    // -1/13!
+    ps = fma(ps, t2, 1.0 / 39916800.0);       // 1/11!
+    ps = fma(ps, t2, -1.0 / 362880.0);        // -1/9!
+    ps = fma(ps, t2, 1.0 / 5040.0);           // 1/7!
+    ps = fma(ps, t2, -1.0 / 120.0);           // -1/5!
+    ps = fma(ps, t2, 1.0 / 6.0);              // 1/3!  (sign folded below)
+    const double sn = fma(-(th * t2), ps, th);
+    // cos(th) = 1 - t2/2 + ... up to th^16
+    double pc = 1.0 / 20922789888000.0;        // 1/16!
+    pc = fma(pc, t2, -1.0 / 87178291200.0);    // -1/14!
+    pc = fma(pc, t2, 1.0 / 479001600.0);       // 1/12!
+    pc = fma(pc, t2, -1.0 / 3628800.0);        // -1/10!
+    pc = fma(pc, t2, 1.0 / 40320.0);           // 1/8!
+    pc = fma(pc, t2, -1.0 / 720.0);            // -1/6!
+    pc = fma(pc, t2, 1.0 / 24.0);              // 1/4!
+    pc = fma(pc, t2, -0.5);                    // -1/2!
+    const double cs = fma(pc, t2, 1.0);
+    const int qq = q & 3;
+    double c, s;
+    if (qq == 0) { c = cs; s = sn; }
+    else if (qq == 1) { c = -sn; s = cs; }
+    else if (qq == 2) { c = -cs; s = -sn; }
+    else { c = sn; s = -cs; }
+    *c_out = c;
+    *s_out = s;
+}
+
+// Box-Muller pair from one Philox block: (z_cos, z_sin)
+MGMC_HD void normal_pair(const Philox4& r, double* z0, double* z1) {
+    const double u1 = ((double)bits53(r.v[0], r.v[1]) + 1.0) * 0x1p-53;  // (0,1]
+    const double u2 = (double)bits53(r.v[2], r.v[3]) * 0x1p-53;          // [0,1)
+    const double rad = sqrt(-2.0 * log_unit(u1));
+    double c, s;
+    sincos_2pi(u2, &c, &s);
+    *z0 = rad * c;
+    *z1 = rad * s;
+}
+
+struct RngKey {
+    uint32_t k0, k1;
+};
+
+MGMC_HD RngKey make_key(uint64_t seed, uint64_t chain) {
+    RngKey k;
+    k.k0 = (uint32_t)seed;
+    k.k1 = (uint32_t)chain ^ (uint32_t)(seed >> 32);
+    return k;
+}
+
+// one normal for the point whose pair id is `pair`; cos_branch selects the first of the two
+MGMC_HD double point_normal(RngKey key, uint32_t pair, bool cos_branch, uint32_t tag, uint64_t sample) {
+    const Philox4 r = philox4x32_10(pair, tag, (uint32_t)sample, (uint32_t)(sample >> 32), key.k0, key.k1);
+    double z0, z1;
+    normal_pair(r, &z0, &z1);
+    return cos_branch ? z0 : z1;
+}
+
+}  // namespace mgmc

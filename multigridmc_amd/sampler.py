@@ -1,0 +1,345 @@
+"""Host-side mirror of the reference's Sampler / Smoother / LinearOperator interfaces, backed by
+the HIP C-ABI (include/mgmc.h).
+
+Reference interface shapes (nilsfriess/MultigridMC, src/):
+  Lattice2d / Lattice3d ............ lattice/lattice2d.hh, lattice/lattice3d.hh
+  ShiftedLaplaceFDOperator ......... linear_operator/shiftedlaplace_fd_operator.{hh,cc}
+  MeasuredOperator.measurement_vector (radius 0) .. linear_operator/measured_operator.cc:69-91
+  MultigridMCSampler(op, rng, params).apply(f, x) .. sampler/multigridmc_sampler.{hh,cc}
+  SORSampler.apply(f, x) ........... sampler/sor_sampler.cc:37-59
+  SORSmoother.apply(b, x) .......... smoother/sor_smoother.cc:41-78
+  LinearOperator.apply(x, y) ....... linear_operator/linear_operator.hh:66-76
+
+Differences, by design: the reference passes a `std::mt19937_64&`; the device samplers take an
+integer seed and a chain id instead (the counter-based noise stream, DESIGN.md "Noise").  Vectors
+are numpy float64 arrays in the reference's lexicographic interior-vertex order.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native
+from ._native import FORWARD, BACKWARD, MgmcConfig, MgmcLevelDesc, check, load_library
+from .parameters import MultigridParameters
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _as_f64(a, n: int, name: str) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if a.shape != (n,):
+        raise ValueError(f"{name} must have shape ({n},), got {a.shape}")
+    return a
+
+
+class Lattice:
+    """Structured lattice with n cells per direction and (n-1)^d interior vertices."""
+
+    def __init__(self, *n: int):
+        if len(n) not in (2, 3):
+            raise ValueError("only 2D and 3D lattices are on the device path")
+        self.shape = tuple(int(v) for v in n)
+        self.dim = len(n)
+        self.Nvertex = int(np.prod([v - 1 for v in self.shape]))
+
+    def vertexidx_euclidean2linear(self, idx) -> int:
+        ell = 0
+        for d in reversed(range(self.dim)):
+            if not (0 < idx[d] < self.shape[d]):
+                raise IndexError("vertex is not interior")
+            ell = ell * (self.shape[d] - 1) + (idx[d] - 1)
+        return ell
+
+    def vertexidx_linear2euclidean(self, ell: int):
+        out = []
+        for d in range(self.dim):
+            out.append(ell % (self.shape[d] - 1) + 1)
+            ell //= self.shape[d] - 1
+        return tuple(out)
+
+    def vertex_coordinates(self, ell: int):
+        idx = self.vertexidx_linear2euclidean(ell)
+        return tuple(float(idx[d]) * (1.0 / float(self.shape[d])) for d in range(self.dim))
+
+    def get_coarse_lattice(self) -> "Lattice":
+        if any(v % 2 for v in self.shape):
+            raise ValueError(f"cannot coarsen lattice of size {self.shape} [one of the extents is odd]")
+        if any(v // 2 <= 1 for v in self.shape):
+            raise ValueError(f"cannot coarsen lattice of size {self.shape} "
+                             "[resulting lattice would have no interior vertices]")
+        return Lattice(*[v // 2 for v in self.shape])
+
+    def get_info(self) -> str:
+        return f"{self.dim}d lattice, {' x '.join(str(v) for v in self.shape)} points, {self.Nvertex} unknowns"
+
+
+def Lattice2d(nx: int, ny: int) -> Lattice:
+    return Lattice(nx, ny)
+
+
+def Lattice3d(nx: int, ny: int, nz: int) -> Lattice:
+    return Lattice(nx, ny, nz)
+
+
+class ShiftedLaplaceFDOperator:
+    """Fine-level precision operator: FD shifted Laplacian with constant kappa^2.
+
+    The device path consumes the operator's data (the stencil), not its methods, because the
+    reference's LinearOperator::apply is not virtual (linear_operator.hh:66)."""
+
+    def __init__(self, lattice: Lattice, kappa_sq: float):
+        self.lattice = lattice
+        self.kappa_sq = float(kappa_sq)
+
+    def get_lattice(self) -> Lattice:
+        return self.lattice
+
+    def get_ndof(self) -> int:
+        return self.lattice.Nvertex
+
+    def get_m_lowrank(self) -> int:
+        return 0
+
+
+def measurement_vector_index(lattice: Lattice, x0, radius: float = 0.0) -> int:
+    """Index of the radius-0 measurement vector (measured_operator.cc:74-91): the interior vertex
+    nearest to x0.  The distance is separable, so the nearest vertex is found per direction;
+    ties go to the lower index, as the reference's strict '<' keeps the first minimum."""
+    if radius >= 1e-12:
+        raise NotImplementedError("measurement radius > 0 (quadrature) is not on the device path")
+    idx = []
+    for d in range(lattice.dim):
+        n = lattice.shape[d]
+        coords = np.arange(1, n, dtype=np.float64) * (1.0 / float(n))
+        idx.append(int(np.argmin(np.abs(coords - float(x0[d])))) + 1)
+    return lattice.vertexidx_euclidean2linear(idx)
+
+
+def make_config(linear_operator: ShiftedLaplaceFDOperator, params: MultigridParameters) -> MgmcConfig:
+    lat = linear_operator.get_lattice()
+    smoother = {"SOR": _native.SMOOTHER_SOR, "SSOR": _native.SMOOTHER_SSOR}.get(params.smoother)
+    if smoother is None:
+        raise ValueError(f"ERROR: invalid sampler '{params.smoother}'")
+    coarse = {"SSOR": _native.COARSE_SSOR, "Cholesky": _native.COARSE_CHOLESKY}.get(params.coarse_solver)
+    if coarse is None:
+        raise ValueError(f"ERROR: multigrid coarse sampler '{params.coarse_solver}'")
+    c = MgmcConfig()
+    c.dim = lat.dim
+    c.nx, c.ny = lat.shape[0], lat.shape[1]
+    c.nz = lat.shape[2] if lat.dim == 3 else 0
+    c.nlevel = params.nlevel
+    c.cycle = params.cycle
+    c.npresmooth = params.npresmooth
+    c.npostsmooth = params.npostsmooth
+    c.ncoarsesmooth = params.ncoarsesmooth
+    c.smoother = smoother
+    c.coarse_solver = coarse
+    c.verbose = params.verbose
+    c.omega = params.omega
+    c.coarse_scaling = params.coarse_scaling
+    c.kappa_sq = linear_operator.kappa_sq
+    return c
+
+
+def describe(config: MgmcConfig) -> list:
+    """Host-only: level hierarchy and Galerkin stencils (no GPU touched)."""
+    lib = load_library()
+    n = check(lib.mgmc_describe(ctypes.byref(config), None, 0))
+    out = (MgmcLevelDesc * n)()
+    check(lib.mgmc_describe(ctypes.byref(config), out, n))
+    levels = []
+    for d in out:
+        levels.append({
+            "shape": (d.nx, d.ny) if config.dim == 2 else (d.nx, d.ny, d.nz),
+            "npoints": d.npoints, "ncolours": d.ncolours, "ndof": int(d.ndof),
+            "stencil": np.array(d.stencil[:], dtype=np.float64),
+        })
+    return levels
+
+
+class MultigridMCSampler:
+    """Device MGMC sampler with the reference's Sampler interface (sampler/sampler.hh:23-72).
+
+    apply(f, x) performs one MGMC cycle (multigridmc_sampler.cc:133-138) with x in/out.  The chain
+    state and the right hand side stay resident in HBM between calls; apply() moves both across
+    PCIe (like the reference's by-reference vectors), sample() runs the device-resident loop."""
+
+    def __init__(self, linear_operator: ShiftedLaplaceFDOperator, seed: int, params: MultigridParameters,
+                 device: int = 0, chain_id: int = 0):
+        self.linear_operator = linear_operator
+        self.params = params
+        self.config = make_config(linear_operator, params)
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        check(self.lib.mgmc_create(ctypes.byref(self.config), int(device), int(seed) & (2**64 - 1),
+                                   int(chain_id) & (2**64 - 1), ctypes.byref(h)))
+        self.handle = h
+        self.ndof = linear_operator.get_ndof()
+        self.nlevel = params.nlevel
+        self._fixed_rhs = None
+
+    # -- lifetime --
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.mgmc_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, code):
+        return check(code, self.handle)
+
+    # -- Sampler interface --
+    def get_linear_operator(self):
+        return self.linear_operator
+
+    def fix_rhs(self, f):
+        f = _as_f64(f, self.ndof, "f")
+        self._chk(self.lib.mgmc_set_rhs(self.handle, _dp(f), self.ndof))
+        self._fixed_rhs = f
+
+    def unfix_rhs(self):
+        self._fixed_rhs = None
+
+    def apply(self, f, x: np.ndarray):
+        """Draw a new sample x (in/out), one MGMC cycle."""
+        f = _as_f64(f, self.ndof, "f")
+        if not (isinstance(x, np.ndarray) and x.dtype == np.float64 and x.flags.c_contiguous and x.shape == (self.ndof,)):
+            raise ValueError("x must be a contiguous float64 array of length ndof")
+        self._chk(self.lib.mgmc_apply(self.handle, _dp(f), _dp(x), self.ndof))
+
+    # -- device-resident chain (driver_mgmc.cc:66-94) --
+    def set_state(self, x):
+        x = _as_f64(x, self.ndof, "x")
+        self._chk(self.lib.mgmc_set_state(self.handle, _dp(x), self.ndof))
+
+    def get_state(self) -> np.ndarray:
+        x = np.empty(self.ndof)
+        self._chk(self.lib.mgmc_get_state(self.handle, _dp(x), self.ndof))
+        return x
+
+    def sample(self, nsteps: int, qoi_index: int = -1) -> np.ndarray:
+        out = np.empty(max(nsteps, 0))
+        self._chk(self.lib.mgmc_sample(self.handle, int(nsteps), int(qoi_index), _dp(out) if qoi_index >= 0 else None))
+        return out
+
+    def sample_async(self, nsteps: int, qoi_index: int = -1):
+        self._chk(self.lib.mgmc_sample_async(self.handle, int(nsteps), int(qoi_index)))
+
+    def synchronize(self):
+        self._chk(self.lib.mgmc_synchronize(self.handle))
+
+    def sample_timed(self, nsteps: int, qoi_index: int = -1):
+        tot = ctypes.c_double()
+        fine = ctypes.c_double()
+        nfine = ctypes.c_int()
+        self._chk(self.lib.mgmc_sample_timed(self.handle, int(nsteps), int(qoi_index), ctypes.byref(tot),
+                                             ctypes.byref(fine), ctypes.byref(nfine)))
+        return tot.value, fine.value, nfine.value
+
+    def qoi_moments(self):
+        out = np.zeros(3)
+        self._chk(self.lib.mgmc_qoi_moments(self.handle, _dp(out)))
+        return out
+
+    def reset_moments(self):
+        self._chk(self.lib.mgmc_reset_moments(self.handle))
+
+    def set_sample_index(self, index: int):
+        self._chk(self.lib.mgmc_set_sample_index(self.handle, int(index)))
+
+    def get_sample_index(self) -> int:
+        v = ctypes.c_uint64()
+        self._chk(self.lib.mgmc_get_sample_index(self.handle, ctypes.byref(v)))
+        return v.value
+
+    def level_desc(self, level: int) -> dict:
+        d = MgmcLevelDesc()
+        self._chk(self.lib.mgmc_level_desc_get(self.handle, int(level), ctypes.byref(d)))
+        return {"shape": (d.nx, d.ny, d.nz)[: self.config.dim], "npoints": d.npoints, "ncolours": d.ncolours,
+                "ndof": int(d.ndof), "stencil": np.array(d.stencil[:])}
+
+    # -- component operations (reference layout host vectors) --
+    def operator_apply(self, level: int, x) -> np.ndarray:
+        n = self.level_desc(level)["ndof"]
+        x = _as_f64(x, n, "x")
+        y = np.empty(n)
+        self._chk(self.lib.mgmc_operator_apply(self.handle, level, _dp(x), _dp(y)))
+        return y
+
+    def smoother_apply(self, level: int, direction: int, nsweeps: int, b, x) -> np.ndarray:
+        n = self.level_desc(level)["ndof"]
+        b = _as_f64(b, n, "b")
+        out = _as_f64(x, n, "x").copy()
+        self._chk(self.lib.mgmc_smoother_apply(self.handle, level, direction, nsweeps, _dp(b), _dp(out)))
+        return out
+
+    def sor_sampler_apply(self, level: int, direction: int, tag: int, sample_index: int, f, x) -> np.ndarray:
+        n = self.level_desc(level)["ndof"]
+        f = _as_f64(f, n, "f")
+        out = _as_f64(x, n, "x").copy()
+        self._chk(self.lib.mgmc_sor_sampler_apply(self.handle, level, direction, tag, sample_index, _dp(f), _dp(out)))
+        return out
+
+    def restrict(self, level: int, r) -> np.ndarray:
+        n = self.level_desc(level)["ndof"]
+        nc = self.level_desc(level + 1)["ndof"]
+        r = _as_f64(r, n, "r")
+        out = np.empty(nc)
+        self._chk(self.lib.mgmc_restrict(self.handle, level, _dp(r), _dp(out)))
+        return out
+
+    def prolongate_add(self, level: int, alpha: float, xc, x) -> np.ndarray:
+        n = self.level_desc(level)["ndof"]
+        nc = self.level_desc(level + 1)["ndof"]
+        xc = _as_f64(xc, nc, "xc")
+        out = _as_f64(x, n, "x").copy()
+        self._chk(self.lib.mgmc_prolongate_add(self.handle, level, float(alpha), _dp(xc), _dp(out)))
+        return out
+
+    def residual_restrict(self, level: int, f, x) -> np.ndarray:
+        n = self.level_desc(level)["ndof"]
+        nc = self.level_desc(level + 1)["ndof"]
+        f = _as_f64(f, n, "f")
+        x = _as_f64(x, n, "x")
+        out = np.empty(nc)
+        self._chk(self.lib.mgmc_residual_restrict(self.handle, level, _dp(f), _dp(x), _dp(out)))
+        return out
+
+    def normals(self, pair0: int, n: int, tag: int, sample_index: int) -> np.ndarray:
+        out = np.empty(n)
+        self._chk(self.lib.mgmc_normals(self.handle, int(pair0), int(n), int(tag), int(sample_index), _dp(out)))
+        return out
+
+    def time_fine_sweeps(self, nsweeps: int) -> float:
+        ms = ctypes.c_float()
+        self._chk(self.lib.mgmc_time_fine_sweeps(self.handle, int(nsweeps), ctypes.byref(ms)))
+        return ms.value
+
+
+class HipMulticolourSORSmoother:
+    """Smoother interface (smoother/smoother.hh:15-34): deterministic multicolour SOR sweep on a
+    level of a device hierarchy (the level-0 operator for a one-level sampler)."""
+
+    def __init__(self, sampler: MultigridMCSampler, level: int, direction: int, nsmooth: int = 1):
+        self.sampler = sampler
+        self.level = level
+        self.direction = direction
+        self.nsmooth = nsmooth
+
+    def apply(self, b, x: np.ndarray):
+        x[:] = self.sampler.smoother_apply(self.level, self.direction, self.nsmooth, b, x)
+
+
+__all__ = [
+    "Lattice", "Lattice2d", "Lattice3d", "ShiftedLaplaceFDOperator", "MultigridMCSampler",
+    "HipMulticolourSORSmoother", "measurement_vector_index", "make_config", "describe", "FORWARD", "BACKWARD",
+]

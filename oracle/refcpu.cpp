@@ -1,0 +1,960 @@
+// oracle/refcpu.cpp -- CPU restatement of the reference MGMC hot path (TEST INFRASTRUCTURE).
+//
+// This file is the parity oracle and the CPU baseline.  Only tests/, __graft_entry__.smoke()
+// and bench.py's cpu_baseline leg may load it; the product (multigridmc_amd) never does.
+//
+// It restates nilsfriess/MultigridMC (citations relative to the reference's src/) with plain
+// std:: containers instead of Eigen (absent in this image, so the reference itself cannot be
+// compiled here -- see DESIGN.md "Oracle"):
+//   Lattice index maps ............ lattice/lattice{1,2,3}d.hh
+//   FD shifted-Laplace assembly ... linear_operator/shiftedlaplace_fd_operator.cc:9-57
+//   intergrid colidx / weights .... intergrid/intergrid_operator.cc:8-20, intergrid_operator_linear.cc:8-30
+//   restrict / prolongate_add ..... intergrid/intergrid_operator.hh:74-120, to_sparse :123-144
+//   Galerkin coarsening ........... linear_operator/linear_operator.cc:10-23 (R*A*R^T, SpGEMM)
+//   LinearOperator::apply ......... linear_operator/linear_operator.hh:66-76
+//   SORSmoother::apply_sparse ..... smoother/sor_smoother.cc:56-78
+//   SORSampler / SSORSampler ...... sampler/sor_sampler.cc:9-59, sampler/ssor_sampler.cc:9-15
+//   DenseCholeskySampler .......... sampler/cholesky_sampler.{hh,cc} (dense LLT, no permutation)
+//   MultigridMCSampler ............ sampler/multigridmc_sampler.cc:8-138
+//   RNG plumbing .................. one shared std::mt19937_64, one std::normal_distribution<double>
+//                                   per sampler object (sampler/sampler.hh:31-34, :69-71)
+//
+// Two modes:
+//   FAITHFUL (0): the reference algorithm -- lexicographic forward / reverse sweeps, libstdc++
+//                 mt19937_64 + normal_distribution (Marsaglia polar) in the reference's
+//                 construction and call order.  Tier T1 of the parity contract.
+//   MULTICOLOUR (1): identical per-point arithmetic, but the Gibbs updates visit the vertices
+//                 colour by colour (red-black on the fine FD level, 2^d colours on Galerkin
+//                 levels) and the noise is the counter-based Philox4x32-10 / Box-Muller stream
+//                 keyed by (seed, chain, pair, sweep tag, sample).  This replays the device
+//                 chain; it is written independently of multigridmc_amd/csrc.  Tier T2.
+//
+// Build: oracle/Makefile (g++ -O2 -ffp-contract=off, shared library + cpu baseline binary).
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <array>
+#include <chrono>
+#include <memory>
+#include <random>
+#include <string>
+#include <vector>
+
+namespace orc {
+
+// =============================================================================================
+// Lattice (lattice/lattice1d.hh, lattice2d.hh, lattice3d.hh): n cells -> (n-1)^d interior
+// vertices, vertex 0 at Euclidean (1,1,1), lexicographic with x fastest.
+// =============================================================================================
+struct Lattice {
+    int dim = 0;
+    int n[3] = {0, 0, 0};
+    int64_t nvertex() const {
+        int64_t v = 1;
+        for (int d = 0; d < dim; ++d) v *= (n[d] - 1);
+        return v;
+    }
+    void lin2euc(int64_t ell, int idx[3]) const {
+        idx[0] = idx[1] = idx[2] = 0;
+        const int64_t a = n[0] - 1;
+        if (dim == 1) {
+            idx[0] = (int)ell + 1;
+        } else if (dim == 2) {
+            idx[0] = (int)(ell % a) + 1;
+            idx[1] = (int)(ell / a) + 1;
+        } else {
+            const int64_t b = n[1] - 1;
+            idx[0] = (int)((ell % (a * b)) % a) + 1;
+            idx[1] = (int)((ell % (a * b)) / a) + 1;
+            idx[2] = (int)(ell / (a * b)) + 1;
+        }
+    }
+    int64_t euc2lin(const int idx[3]) const {
+        if (dim == 1) return idx[0] - 1;
+        if (dim == 2) return (int64_t)(idx[1] - 1) * (n[0] - 1) + (idx[0] - 1);
+        return ((int64_t)(idx[2] - 1) * (n[1] - 1) + (idx[1] - 1)) * (n[0] - 1) + (idx[0] - 1);
+    }
+    bool interior(const int idx[3]) const {
+        for (int d = 0; d < dim; ++d)
+            if (idx[d] <= 0 || idx[d] >= n[d]) return false;
+        return true;
+    }
+    // shifted_vertex_is_internal_vertex
+    bool shifted(int64_t ell, const int s[3], int64_t& out) const {
+        int idx[3];
+        lin2euc(ell, idx);
+        for (int d = 0; d < dim; ++d) idx[d] += s[d];
+        if (!interior(idx)) return false;
+        out = euc2lin(idx);
+        return true;
+    }
+    // lattice3d.hh:227-234 etc: index on the next-finer lattice (2n cells)
+    int64_t fine_vertex_idx(int64_t ell) const {
+        int idx[3];
+        lin2euc(ell, idx);
+        Lattice f = *this;
+        for (int d = 0; d < dim; ++d) {
+            f.n[d] = 2 * n[d];
+            idx[d] *= 2;
+        }
+        return f.euc2lin(idx);
+    }
+    Lattice coarse() const {
+        Lattice c = *this;
+        for (int d = 0; d < dim; ++d) c.n[d] = n[d] / 2;
+        return c;
+    }
+};
+
+// =============================================================================================
+// CSR matrix (rows sorted by column, as Eigen's compressed storage after setFromTriplets)
+// =============================================================================================
+struct CSR {
+    int64_t nrow = 0, ncol = 0;
+    std::vector<int64_t> rowptr;
+    std::vector<int32_t> col;
+    std::vector<double> val;
+    double diag(int64_t r) const {
+        for (int64_t q = rowptr[r]; q < rowptr[r + 1]; ++q)
+            if (col[q] == r) return val[q];
+        return 0.0;
+    }
+};
+
+// y = A x with Eigen's ColMajor accumulation order: y_i = ((0 + a_i,j1 x_j1) + a_i,j2 x_j2) ...
+// with j ascending (A symmetric, so the row-wise ascending sum is the same sequence)
+static void spmv(const CSR& A, const double* x, double* y) {
+    for (int64_t r = 0; r < A.nrow; ++r) {
+        double s = 0.0;
+        for (int64_t q = A.rowptr[r]; q < A.rowptr[r + 1]; ++q) s += A.val[q] * x[A.col[q]];
+        y[r] = s;
+    }
+}
+
+// C = A * B (Gustavson, dense accumulator, sorted output)
+static CSR spgemm(const CSR& A, const CSR& B) {
+    CSR C;
+    C.nrow = A.nrow;
+    C.ncol = B.ncol;
+    C.rowptr.assign(A.nrow + 1, 0);
+    std::vector<double> acc(B.ncol, 0.0);
+    std::vector<char> used(B.ncol, 0);
+    std::vector<int32_t> cols;
+    for (int64_t r = 0; r < A.nrow; ++r) {
+        cols.clear();
+        for (int64_t q = A.rowptr[r]; q < A.rowptr[r + 1]; ++q) {
+            const int32_t k = A.col[q];
+            const double a = A.val[q];
+            for (int64_t t = B.rowptr[k]; t < B.rowptr[k + 1]; ++t) {
+                const int32_t c = B.col[t];
+                if (!used[c]) {
+                    used[c] = 1;
+                    acc[c] = a * B.val[t];
+                    cols.push_back(c);
+                } else {
+                    acc[c] += a * B.val[t];
+                }
+            }
+        }
+        std::sort(cols.begin(), cols.end());
+        for (int32_t c : cols) {
+            C.col.push_back(c);
+            C.val.push_back(acc[c]);
+            used[c] = 0;
+        }
+        C.rowptr[r + 1] = (int64_t)C.col.size();
+    }
+    return C;
+}
+
+static CSR transpose(const CSR& A) {
+    CSR T;
+    T.nrow = A.ncol;
+    T.ncol = A.nrow;
+    T.rowptr.assign(A.ncol + 1, 0);
+    for (int32_t c : A.col) T.rowptr[c + 1]++;
+    for (int64_t r = 0; r < T.nrow; ++r) T.rowptr[r + 1] += T.rowptr[r];
+    T.col.resize(A.col.size());
+    T.val.resize(A.val.size());
+    std::vector<int64_t> pos(T.rowptr.begin(), T.rowptr.end() - 1);
+    for (int64_t r = 0; r < A.nrow; ++r)
+        for (int64_t q = A.rowptr[r]; q < A.rowptr[r + 1]; ++q) {
+            const int64_t p = pos[A.col[q]]++;
+            T.col[p] = (int32_t)r;
+            T.val[p] = A.val[q];
+        }
+    return T;
+}
+
+// =============================================================================================
+// Fine operator: ShiftedLaplaceFDOperator with constant kappa^2 (shiftedlaplace_fd_operator.cc)
+// =============================================================================================
+static CSR fd_operator(const Lattice& lat, double kappa_sq) {
+    const int dim = lat.dim;
+    double hinv2[3] = {0, 0, 0};
+    double cell_volume = 1.0;
+    for (int d = 0; d < dim; ++d) {
+        const double h = 1. / double(lat.n[d]);
+        hinv2[d] = 1. / (h * h);
+        cell_volume *= h;
+    }
+    CSR A;
+    const int64_t nrow = lat.nvertex();
+    A.nrow = A.ncol = nrow;
+    A.rowptr.assign(nrow + 1, 0);
+    A.col.reserve((size_t)nrow * (2 * dim + 1));
+    A.val.reserve((size_t)nrow * (2 * dim + 1));
+    std::vector<std::pair<int64_t, double>> row;
+    for (int64_t ell = 0; ell < nrow; ++ell) {
+        row.clear();
+        double diagonal = cell_volume * kappa_sq;
+        for (int d = 0; d < dim; ++d) {
+            for (int j = 0; j < 2; ++j) {
+                int s[3] = {0, 0, 0};
+                s[d] = 2 * j - 1;
+                int64_t e;
+                if (lat.shifted(ell, s, e)) row.push_back({e, -cell_volume * hinv2[d]});
+            }
+            diagonal += 2. * cell_volume * hinv2[d];
+        }
+        row.push_back({ell, diagonal});
+        std::sort(row.begin(), row.end(), [](const std::pair<int64_t, double>& a, const std::pair<int64_t, double>& b) {
+            return a.first < b.first;
+        });
+        for (auto& e : row) {
+            A.col.push_back((int32_t)e.first);
+            A.val.push_back(e.second);
+        }
+        A.rowptr[ell + 1] = (int64_t)A.col.size();
+    }
+    return A;
+}
+
+// =============================================================================================
+// IntergridOperatorLinear
+// =============================================================================================
+struct Intergrid {
+    Lattice fine, coarse;
+    int stencil_size = 0;
+    std::vector<double> matrix;
+    std::vector<int64_t> colidx;
+    explicit Intergrid(const Lattice& lat) : fine(lat), coarse(lat.coarse()) {
+        const int dim = lat.dim;
+        stencil_size = (int)lround(pow(3, dim));
+        const double stencil1d[3] = {0.5, 1.0, 0.5};
+        const int shift1d[3] = {-1, 0, +1};
+        std::vector<std::array<int, 3>> shift;
+        for (int j = 0; j < stencil_size; ++j) {
+            double m = 1.0;
+            std::array<int, 3> s = {0, 0, 0};
+            int mu = j;
+            for (int d = 0; d < dim; ++d) {
+                m *= stencil1d[mu % 3];
+                s[d] = shift1d[mu % 3];
+                mu /= 3;
+            }
+            matrix.push_back(m);
+            shift.push_back(s);
+        }
+        const int64_t nc = coarse.nvertex();
+        colidx.resize((size_t)nc * stencil_size);
+        for (int64_t ec = 0; ec < nc; ++ec) {
+            int idx[3];
+            coarse.lin2euc(ec, idx);
+            for (int d = 0; d < dim; ++d) idx[d] *= 2;
+            const int64_t ell = fine.euc2lin(idx);
+            for (int j = 0; j < stencil_size; ++j) {
+                int64_t e = -1;
+                if (!fine.shifted(ell, shift[j].data(), e)) {
+                    fprintf(stderr, "oracle: intergrid shift left the lattice\n");
+                    abort();
+                }
+                colidx[(size_t)ec * stencil_size + j] = e;
+            }
+        }
+    }
+    void restrict_(const double* x, double* xc) const {
+        const int64_t nc = coarse.nvertex();
+        for (int64_t ec = 0; ec < nc; ++ec) {
+            double result = 0;
+            for (int k = 0; k < stencil_size; ++k) result += matrix[k] * x[colidx[(size_t)ec * stencil_size + k]];
+            xc[ec] = result;
+        }
+    }
+    void prolongate_add(double alpha, const double* xc, double* x) const {
+        const int64_t nc = coarse.nvertex();
+        for (int64_t ec = 0; ec < nc; ++ec) {
+            const double v = xc[ec];
+            for (int k = 0; k < stencil_size; ++k) x[colidx[(size_t)ec * stencil_size + k]] += alpha * matrix[k] * v;
+        }
+    }
+    CSR to_sparse() const {
+        CSR R;
+        R.nrow = coarse.nvertex();
+        R.ncol = fine.nvertex();
+        R.rowptr.assign(R.nrow + 1, 0);
+        std::vector<std::pair<int64_t, double>> row;
+        for (int64_t ec = 0; ec < R.nrow; ++ec) {
+            row.clear();
+            for (int k = 0; k < stencil_size; ++k) row.push_back({colidx[(size_t)ec * stencil_size + k], matrix[k]});
+            std::sort(row.begin(), row.end(),
+                      [](const std::pair<int64_t, double>& a, const std::pair<int64_t, double>& b) { return a.first < b.first; });
+            for (auto& e : row) {
+                R.col.push_back((int32_t)e.first);
+                R.val.push_back(e.second);
+            }
+            R.rowptr[ec + 1] = (int64_t)R.col.size();
+        }
+        return R;
+    }
+};
+
+static CSR galerkin_spgemm(const CSR& A, const Intergrid& ig) {
+    const CSR R = ig.to_sparse();
+    const CSR P = transpose(R);
+    const CSR RA = spgemm(R, A);
+    return spgemm(RA, P);
+}
+
+// Galerkin coarse operator built row-by-row from the interior row of an R*A*R^T product
+// evaluated on a small lattice (8 cells per direction).  Because the fine operator has constant
+// coefficients and every row of the product is formed from the same terms in the same order,
+// that row equals every row of the full product (Dirichlet truncation only drops entries);
+// this is what makes the 512^3 hierarchy buildable on a CPU in seconds.
+static CSR stencil_csr(const Lattice& lat, const double st[27]);
+static void stencil_of_interior_row(const CSR& A, const Lattice& lat, double st[27]);
+
+static CSR galerkin_stencil_mode(const CSR& A_small_src, const Lattice& small, const Lattice& coarse_big,
+                                 double st_out[27]) {
+    Intergrid ig(small);
+    const CSR Ac = galerkin_spgemm(A_small_src, ig);
+    stencil_of_interior_row(Ac, ig.coarse, st_out);
+    return stencil_csr(coarse_big, st_out);
+}
+
+static inline int sidx(int dim, int dx, int dy, int dz) {
+    if (dim == 3) return (dz + 1) * 9 + (dy + 1) * 3 + (dx + 1);
+    if (dim == 2) return (dy + 1) * 3 + (dx + 1);
+    return dx + 1;
+}
+
+static CSR stencil_csr(const Lattice& lat, const double st[27]) {
+    CSR A;
+    const int64_t nrow = lat.nvertex();
+    const int dim = lat.dim;
+    A.nrow = A.ncol = nrow;
+    A.rowptr.assign(nrow + 1, 0);
+    const int zr = dim == 3 ? 1 : 0, yr = dim >= 2 ? 1 : 0;
+    for (int64_t ell = 0; ell < nrow; ++ell) {
+        for (int dz = -zr; dz <= zr; ++dz)
+            for (int dy = -yr; dy <= yr; ++dy)
+                for (int dx = -1; dx <= 1; ++dx) {
+                    const double v = st[sidx(dim, dx, dy, dz)];
+                    if (v == 0.0) continue;
+                    int s[3] = {dx, dy, dz};
+                    int64_t e;
+                    if (lat.shifted(ell, s, e)) {
+                        A.col.push_back((int32_t)e);
+                        A.val.push_back(v);
+                    }
+                }
+        A.rowptr[ell + 1] = (int64_t)A.col.size();
+    }
+    return A;
+}
+
+static void stencil_of_interior_row(const CSR& A, const Lattice& lat, double st[27]) {
+    for (int k = 0; k < 27; ++k) st[k] = 0.0;
+    int idx[3] = {2, 2, 2};
+    const int64_t r = lat.euc2lin(idx);
+    int ci[3];
+    for (int64_t q = A.rowptr[r]; q < A.rowptr[r + 1]; ++q) {
+        lat.lin2euc(A.col[q], ci);
+        const int dx = ci[0] - idx[0];
+        const int dy = lat.dim >= 2 ? ci[1] - idx[1] : 0;
+        const int dz = lat.dim == 3 ? ci[2] - idx[2] : 0;
+        st[sidx(lat.dim, dx, dy, dz)] = A.val[q];
+    }
+}
+
+// =============================================================================================
+// Philox4x32-10 + Box-Muller (multicolour mode); same definition as the device path
+// (DESIGN.md "Noise"), written independently.
+// =============================================================================================
+static inline void philox10(uint32_t ctr[4], uint32_t key0, uint32_t key1) {
+    for (int round = 0; round < 10; ++round) {
+        const uint64_t prod0 = (uint64_t)0xD2511F53u * (uint64_t)ctr[0];
+        const uint64_t prod1 = (uint64_t)0xCD9E8D57u * (uint64_t)ctr[2];
+        const uint32_t out0 = (uint32_t)(prod1 >> 32) ^ ctr[1] ^ key0;
+        const uint32_t out2 = (uint32_t)(prod0 >> 32) ^ ctr[3] ^ key1;
+        ctr[0] = out0;
+        ctr[1] = (uint32_t)prod1;
+        ctr[2] = out2;
+        ctr[3] = (uint32_t)prod0;
+        key0 += 0x9E3779B9u;
+        key1 += 0xBB67AE85u;
+    }
+}
+
+static inline double bits_to_double(uint64_t b) {
+    double d;
+    memcpy(&d, &b, 8);
+    return d;
+}
+static inline uint64_t double_to_bits(double d) {
+    uint64_t b;
+    memcpy(&b, &d, 8);
+    return b;
+}
+
+static double ln_unit(double u) {
+    const uint64_t b = double_to_bits(u);
+    int e = (int)((b >> 52) & 0x7ff) - 1023;
+    double m = bits_to_double((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+    if (m > 1.4142135623730951) {
+        m = m * 0.5;
+        e = e + 1;
+    }
+    const double s = (m - 1.0) / (m + 1.0);
+    const double s2 = s * s;
+    static const double inv_odd[11] = {1.0 / 23.0, 1.0 / 21.0, 1.0 / 19.0, 1.0 / 17.0, 1.0 / 15.0, 1.0 / 13.0,
+                                       1.0 / 11.0, 1.0 / 9.0,  1.0 / 7.0,  1.0 / 5.0,  1.0 / 3.0};
+    double p = inv_odd[0];
+    for (int q = 1; q < 11; ++q) p = fma(p, s2, inv_odd[q]);
+    const double logm = fma(2.0, s, 2.0 * ((s * s2) * p));
+    const double de = (double)e;
+    return fma(de, 6.93147180369123816490e-01, fma(de, 1.90821492927058770002e-10, logm));
+}
+
+static void cos_sin_2pi(double t, double& c, double& s) {
+    const int q = (int)(t * 4.0 + 0.5);
+    const double r = t - (double)q * 0.25;
+    const double th = r * 6.28318530717958647692;
+    const double t2 = th * th;
+    static const double sc[8] = {-1.0 / 355687428096000.0, 1.0 / 1307674368000.0, -1.0 / 6227020800.0,
+                                 1.0 / 39916800.0,         -1.0 / 362880.0,      1.0 / 5040.0,
+                                 -1.0 / 120.0,             1.0 / 6.0};
+    double ps = sc[0];
+    for (int k = 1; k < 8; ++k) ps = fma(ps, t2, sc[k]);
+    const double sn = fma(-(th * t2), ps, th);
+    static const double cc[8] = {1.0 / 20922789888000.0, -1.0 / 87178291200.0, 1.0 / 479001600.0,
+                                 -1.0 / 3628800.0,       1.0 / 40320.0,        -1.0 / 720.0,
+                                 1.0 / 24.0,             -0.5};
+    double pc = cc[0];
+    for (int k = 1; k < 8; ++k) pc = fma(pc, t2, cc[k]);
+    const double cs = fma(pc, t2, 1.0);
+    switch (q & 3) {
+        case 0: c = cs; s = sn; break;
+        case 1: c = -sn; s = cs; break;
+        case 2: c = -cs; s = -sn; break;
+        default: c = sn; s = -cs; break;
+    }
+}
+
+static void philox_normals(uint64_t seed, uint64_t chain, uint32_t pair, uint32_t tag, uint64_t sample, double& z0,
+                           double& z1) {
+    uint32_t ctr[4] = {pair, tag, (uint32_t)sample, (uint32_t)(sample >> 32)};
+    philox10(ctr, (uint32_t)seed, (uint32_t)chain ^ (uint32_t)(seed >> 32));
+    const uint64_t m1 = ((uint64_t)(ctr[0] >> 5) << 26) | (uint64_t)(ctr[1] >> 6);
+    const uint64_t m2 = ((uint64_t)(ctr[2] >> 5) << 26) | (uint64_t)(ctr[3] >> 6);
+    const double u1 = ((double)m1 + 1.0) * 0x1p-53;
+    const double u2 = (double)m2 * 0x1p-53;
+    const double rad = sqrt(-2.0 * ln_unit(u1));
+    double c, s;
+    cos_sin_2pi(u2, c, s);
+    z0 = rad * c;
+    z1 = rad * s;
+}
+
+// =============================================================================================
+// Samplers
+// =============================================================================================
+enum Mode { FAITHFUL = 0, MULTICOLOUR = 1 };
+enum Direction { FORWARD = 1, BACKWARD = 2 };
+
+struct Level {
+    Lattice lat;
+    CSR A;
+    int ncolours = 2;  // multicolour scheme: 2 (FD level) or 2^d (Galerkin level)
+    std::vector<int> colour;  // per row
+    std::vector<uint32_t> pair;
+    std::vector<char> cos_branch;
+};
+
+struct Ctx {
+    Mode mode = FAITHFUL;
+    std::mt19937_64 rng;
+    uint64_t seed = 0, chain = 0;
+    uint64_t sample = 0;  // multicolour: sample index of the current cycle
+    uint32_t tag = 0;     // multicolour: running sweep tag within the current cycle
+};
+
+static void init_colouring(Level& L, bool fd_level) {
+    const int64_t n = L.lat.nvertex();
+    L.colour.resize(n);
+    L.pair.resize(n);
+    L.cos_branch.resize(n);
+    const int dim = L.lat.dim;
+    L.ncolours = fd_level ? 2 : (1 << dim);
+    int idx[3];
+    for (int64_t e = 0; e < n; ++e) {
+        L.lat.lin2euc(e, idx);
+        if (fd_level)
+            L.colour[e] = (idx[0] + idx[1] + idx[2]) & 1;
+        else
+            L.colour[e] = (idx[0] & 1) | ((idx[1] & 1) << 1) | ((idx[2] & 1) << 2);
+        uint64_t row = 0;
+        if (dim == 2) row = (uint64_t)(idx[1] - 1);
+        if (dim == 3) row = (uint64_t)(idx[2] - 1) * (uint64_t)(L.lat.n[1] - 1) + (uint64_t)(idx[1] - 1);
+        L.pair[e] = (uint32_t)(row * (uint64_t)(L.lat.n[0] / 2) + (uint64_t)((idx[0] - 1) >> 1));
+        L.cos_branch[e] = (idx[0] & 1) ? 1 : 0;
+    }
+}
+
+// one SOR update of row ell (sor_smoother.cc:70-75)
+static inline void sor_row(const CSR& A, const double* diag, double omega, const double* b, double* x, int64_t ell) {
+    double residual = 0.0;
+    for (int64_t k = A.rowptr[ell]; k < A.rowptr[ell + 1]; ++k) residual += A.val[k] * x[A.col[k]];
+    x[ell] += omega * (b[ell] - residual) / diag[ell];
+}
+
+struct SORSmoother {
+    const Level* L;
+    double omega;
+    Direction direction;
+    std::vector<double> diag;
+    SORSmoother(const Level* L_, double omega_, Direction d) : L(L_), omega(omega_), direction(d) {
+        diag.resize(L->A.nrow);
+        for (int64_t r = 0; r < L->A.nrow; ++r) diag[r] = L->A.diag(r);
+    }
+    void apply(Mode mode, const double* b, double* x) const {
+        const int64_t nrow = L->A.nrow;
+        if (mode == FAITHFUL) {
+            for (int64_t e_ = 0; e_ < nrow; ++e_) {
+                const int64_t ell = (direction == FORWARD) ? e_ : nrow - 1 - e_;
+                sor_row(L->A, diag.data(), omega, b, x, ell);
+            }
+        } else {
+            const int nc = L->ncolours;
+            for (int cc = 0; cc < nc; ++cc) {
+                const int colour = (direction == FORWARD) ? cc : nc - 1 - cc;
+                for (int64_t ell = 0; ell < nrow; ++ell)
+                    if (L->colour[ell] == colour) sor_row(L->A, diag.data(), omega, b, x, ell);
+            }
+        }
+    }
+};
+
+struct Sampler {
+    Ctx* ctx;
+    mutable std::normal_distribution<double> normal_dist{0.0, 1.0};
+    explicit Sampler(Ctx* c) : ctx(c) {}
+    virtual ~Sampler() {}
+    virtual void apply(const double* f, double* x) = 0;
+};
+
+struct SORSampler : Sampler {
+    const Level* L;
+    double omega;
+    Direction direction;
+    unsigned nsmooth;
+    std::vector<double> c_rhs;
+    std::vector<double> sqrt_precision_diag;
+    SORSmoother smoother;
+    SORSampler(Ctx* c, const Level* L_, double omega_, unsigned nsmooth_, Direction d)
+        : Sampler(c), L(L_), omega(omega_), direction(d), nsmooth(nsmooth_), smoother(L_, omega_, d) {
+        const int64_t nrow = L->A.nrow;
+        c_rhs.resize(nrow);
+        sqrt_precision_diag.resize(nrow);
+        for (int64_t ell = 0; ell < nrow; ++ell)
+            sqrt_precision_diag[ell] = sqrt(smoother.diag[ell] * (2. - omega) / omega);
+    }
+    void apply(const double* f, double* x) override {
+        const int64_t n = (int64_t)c_rhs.size();
+        for (unsigned k = 0; k < nsmooth; ++k) {
+            if (ctx->mode == FAITHFUL) {
+                for (int64_t ell = 0; ell < n; ++ell) {
+                    const double tmp = sqrt_precision_diag[ell];
+                    c_rhs[ell] = tmp * normal_dist(ctx->rng) + f[ell];
+                }
+            } else {
+                const uint32_t tag = ctx->tag++;
+                for (int64_t ell = 0; ell < n; ++ell) {
+                    double z0, z1;
+                    philox_normals(ctx->seed, ctx->chain, L->pair[ell], tag, ctx->sample, z0, z1);
+                    const double xi = L->cos_branch[ell] ? z0 : z1;
+                    c_rhs[ell] = sqrt_precision_diag[ell] * xi + f[ell];
+                }
+            }
+            smoother.apply(ctx->mode, c_rhs.data(), x);
+        }
+    }
+};
+
+struct SSORSampler : Sampler {
+    unsigned nsmooth;
+    SORSampler fwd, bwd;
+    SSORSampler(Ctx* c, const Level* L, double omega, unsigned nsmooth_)
+        : Sampler(c), nsmooth(nsmooth_), fwd(c, L, omega, 1, FORWARD), bwd(c, L, omega, 1, BACKWARD) {}
+    void apply(const double* f, double* x) override {
+        for (unsigned k = 0; k < nsmooth; ++k) {
+            fwd.apply(f, x);
+            bwd.apply(f, x);
+        }
+    }
+};
+
+// DenseCholeskySampler (cholesky_sampler.hh:50-66, EigenDenseLLT): A = L L^T,
+// x = L^{-T}(xi + L^{-1} f)
+struct DenseCholeskySampler : Sampler {
+    int64_t n;
+    std::vector<double> Lmat;  // row-major lower factor
+    std::vector<double> xi, g;
+    DenseCholeskySampler(Ctx* c, const Level* L) : Sampler(c) {
+        n = L->A.nrow;
+        Lmat.assign((size_t)n * n, 0.0);
+        for (int64_t r = 0; r < n; ++r)
+            for (int64_t q = L->A.rowptr[r]; q < L->A.rowptr[r + 1]; ++q) Lmat[(size_t)r * n + L->A.col[q]] = L->A.val[q];
+        for (int64_t j = 0; j < n; ++j) {
+            double d = Lmat[(size_t)j * n + j];
+            for (int64_t k = 0; k < j; ++k) d -= Lmat[(size_t)j * n + k] * Lmat[(size_t)j * n + k];
+            d = sqrt(d);
+            Lmat[(size_t)j * n + j] = d;
+            for (int64_t i = j + 1; i < n; ++i) {
+                double s = Lmat[(size_t)i * n + j];
+                for (int64_t k = 0; k < j; ++k) s -= Lmat[(size_t)i * n + k] * Lmat[(size_t)j * n + k];
+                Lmat[(size_t)i * n + j] = s / d;
+            }
+            for (int64_t k = j + 1; k < n; ++k) Lmat[(size_t)j * n + k] = 0.0;
+        }
+        xi.resize(n);
+        g.resize(n);
+    }
+    void apply(const double* f, double* x) override {
+        for (int64_t ell = 0; ell < n; ++ell) xi[ell] = normal_dist(ctx->rng);
+        for (int64_t i = 0; i < n; ++i) {  // L g = f
+            double s = f[i];
+            for (int64_t k = 0; k < i; ++k) s -= Lmat[(size_t)i * n + k] * g[k];
+            g[i] = s / Lmat[(size_t)i * n + i];
+        }
+        for (int64_t i = n - 1; i >= 0; --i) {  // L^T x = xi + g
+            double s = xi[i] + g[i];
+            for (int64_t k = i + 1; k < n; ++k) s -= Lmat[(size_t)k * n + i] * x[k];
+            x[i] = s / Lmat[(size_t)i * n + i];
+        }
+    }
+};
+
+struct Params {
+    int dim, nx, ny, nz;
+    int nlevel, cycle, npresmooth, npostsmooth, ncoarsesmooth;
+    int smoother;       // 0 SOR, 1 SSOR
+    int coarse_solver;  // 0 SSOR, 1 Cholesky (dense)
+    int galerkin;       // 0 = full SpGEMM, 1 = stencil rows from a small SpGEMM
+    double omega, coarse_scaling, kappa_sq;
+};
+
+struct MGMC : Sampler {
+    Params p;
+    std::vector<std::unique_ptr<Level>> levels;
+    std::vector<std::unique_ptr<Sampler>> pre, post;
+    std::vector<std::unique_ptr<Intergrid>> ig;
+    std::unique_ptr<Sampler> coarse;
+    std::vector<std::vector<double>> x_ell, f_ell, r_ell;
+
+    MGMC(Ctx* c, const Params& p_, const Lattice& lat, CSR A0, const double* override_st /* nlevel*27 or null */)
+        : Sampler(c), p(p_) {
+        Lattice lattice = lat;
+        CSR A = std::move(A0);
+        double fine_st[27];
+        bool have_small_src = false;
+        CSR small_src;
+        Lattice small;
+        for (int level = 0; level < p.nlevel; ++level) {
+            std::unique_ptr<Level> L(new Level());
+            L->lat = lattice;
+            L->A = A;
+            if (lattice.dim >= 2) init_colouring(*L, level == 0);
+            x_ell.emplace_back(L->A.nrow, 0.0);
+            f_ell.emplace_back(L->A.nrow, 0.0);
+            r_ell.emplace_back(L->A.nrow, 0.0);
+            Level* Lp = L.get();
+            levels.push_back(std::move(L));
+            // samplers in the reference's construction order (multigridmc_sampler.cc:86-89)
+            if (p.smoother == 0) {
+                pre.emplace_back(new SORSampler(c, Lp, p.omega, p.npresmooth, FORWARD));
+                post.emplace_back(new SORSampler(c, Lp, p.omega, p.npostsmooth, BACKWARD));
+            } else {
+                pre.emplace_back(new SSORSampler(c, Lp, p.omega, p.npresmooth));
+                post.emplace_back(new SSORSampler(c, Lp, p.omega, p.npostsmooth));
+            }
+            if (level < p.nlevel - 1) {
+                ig.emplace_back(new Intergrid(lattice));
+                const Lattice cl = lattice.coarse();
+                if (override_st) {
+                    A = stencil_csr(cl, override_st + 27 * (level + 1));
+                } else if (p.galerkin == 1 && lattice.dim >= 2) {
+                    // stencil mode: level stencil -> small lattice -> SpGEMM -> interior row
+                    if (!have_small_src) {
+                        // the level's own (constant) stencil, placed on an 8^d lattice
+                        small = lattice;
+                        for (int d = 0; d < lattice.dim; ++d) small.n[d] = 8;
+                        stencil_of_interior_row(Lp->A, lattice, fine_st);
+                        small_src = stencil_csr(small, fine_st);
+                        have_small_src = true;
+                    }
+                    A = galerkin_stencil_mode(small_src, small, cl, fine_st);
+                    small_src = stencil_csr(small, fine_st);
+                } else {
+                    A = galerkin_spgemm(Lp->A, *ig.back());
+                }
+                lattice = cl;
+            }
+        }
+        if (p.coarse_solver == 1)
+            coarse.reset(new DenseCholeskySampler(c, levels.back().get()));
+        else
+            coarse.reset(new SSORSampler(c, levels.back().get(), p.omega, p.ncoarsesmooth));
+    }
+
+    void sample(int level) {
+        if (level == p.nlevel - 1) {
+            coarse->apply(f_ell[level].data(), x_ell[level].data());
+            return;
+        }
+        const int cycle_ = (level > 0) ? p.cycle : 1;
+        for (int j = 0; j < cycle_; ++j) {
+            pre[level]->apply(f_ell[level].data(), x_ell[level].data());
+            spmv(levels[level]->A, x_ell[level].data(), r_ell[level].data());
+            for (size_t q = 0; q < r_ell[level].size(); ++q) r_ell[level][q] = f_ell[level][q] - r_ell[level][q];
+            ig[level]->restrict_(r_ell[level].data(), f_ell[level + 1].data());
+            std::fill(x_ell[level + 1].begin(), x_ell[level + 1].end(), 0.0);
+            sample(level + 1);
+            ig[level]->prolongate_add(p.coarse_scaling, x_ell[level + 1].data(), x_ell[level].data());
+            post[level]->apply(f_ell[level].data(), x_ell[level].data());
+        }
+    }
+
+    void apply(const double* f, double* x) override {
+        std::copy(f, f + f_ell[0].size(), f_ell[0].begin());
+        std::copy(x, x + x_ell[0].size(), x_ell[0].begin());
+        ctx->tag = 0;
+        sample(0);
+        ctx->sample++;
+        std::copy(x_ell[0].begin(), x_ell[0].end(), x);
+    }
+};
+
+}  // namespace orc
+
+// =============================================================================================
+// C API for the tests (ctypes) and the CPU baseline
+// =============================================================================================
+using namespace orc;
+
+struct orc_handle {
+    Ctx ctx;
+    std::unique_ptr<MGMC> mg;
+    std::vector<double> f, x;  // fixed rhs and chain state (measure_sampling_time)
+};
+
+extern "C" {
+
+typedef struct orc_params {
+    int dim, nx, ny, nz;
+    int nlevel, cycle, npresmooth, npostsmooth, ncoarsesmooth;
+    int smoother, coarse_solver, galerkin;
+    double omega, coarse_scaling, kappa_sq;
+} orc_params;
+
+static Params to_params(const orc_params* q) {
+    Params p;
+    p.dim = q->dim; p.nx = q->nx; p.ny = q->ny; p.nz = q->nz;
+    p.nlevel = q->nlevel; p.cycle = q->cycle; p.npresmooth = q->npresmooth; p.npostsmooth = q->npostsmooth;
+    p.ncoarsesmooth = q->ncoarsesmooth; p.smoother = q->smoother; p.coarse_solver = q->coarse_solver;
+    p.galerkin = q->galerkin; p.omega = q->omega; p.coarse_scaling = q->coarse_scaling; p.kappa_sq = q->kappa_sq;
+    return p;
+}
+
+static Lattice make_lattice(const orc_params* q) {
+    Lattice lat;
+    lat.dim = q->dim;
+    lat.n[0] = q->nx;
+    lat.n[1] = q->dim >= 2 ? q->ny : 0;
+    lat.n[2] = q->dim == 3 ? q->nz : 0;
+    return lat;
+}
+
+// FD shifted-Laplace prior on a 2D/3D lattice; override_st (nlevel*27) replaces the Galerkin
+// stencils of levels >= 1 (multicolour replay of a device hierarchy), may be NULL.
+orc_handle* orc_create_fd(const orc_params* q, int mode, uint64_t seed, uint64_t chain, const double* override_st) {
+    orc_handle* h = new orc_handle();
+    h->ctx.mode = (Mode)mode;
+    h->ctx.rng.seed(seed);
+    h->ctx.seed = seed;
+    h->ctx.chain = chain;
+    const Lattice lat = make_lattice(q);
+    CSR A = fd_operator(lat, q->kappa_sq);
+    h->mg.reset(new MGMC(&h->ctx, to_params(q), lat, std::move(A), override_st));
+    h->f.assign(h->mg->x_ell[0].size(), 0.0);
+    h->x.assign(h->mg->x_ell[0].size(), 0.0);
+    return h;
+}
+
+// Generic fine operator given as CSR on a 1D/2D/3D lattice (e.g. test_sampler.hh TestOperator1d)
+orc_handle* orc_create_csr(const orc_params* q, int mode, uint64_t seed, int64_t nrow, const int64_t* rowptr,
+                           const int32_t* col, const double* val) {
+    orc_handle* h = new orc_handle();
+    h->ctx.mode = (Mode)mode;
+    h->ctx.rng.seed(seed);
+    h->ctx.seed = seed;
+    CSR A;
+    A.nrow = A.ncol = nrow;
+    A.rowptr.assign(rowptr, rowptr + nrow + 1);
+    A.col.assign(col, col + rowptr[nrow]);
+    A.val.assign(val, val + rowptr[nrow]);
+    Params p = to_params(q);
+    p.galerkin = 0;
+    h->mg.reset(new MGMC(&h->ctx, p, make_lattice(q), std::move(A), nullptr));
+    h->f.assign(nrow, 0.0);
+    h->x.assign(nrow, 0.0);
+    return h;
+}
+
+void orc_destroy(orc_handle* h) { delete h; }
+
+int64_t orc_ndof(orc_handle* h, int level) { return h->mg->levels[level]->A.nrow; }
+int orc_nlevel(orc_handle* h) { return (int)h->mg->levels.size(); }
+int64_t orc_nnz(orc_handle* h, int level) { return (int64_t)h->mg->levels[level]->A.col.size(); }
+
+void orc_get_csr(orc_handle* h, int level, int64_t* rowptr, int32_t* col, double* val) {
+    const CSR& A = h->mg->levels[level]->A;
+    memcpy(rowptr, A.rowptr.data(), (A.nrow + 1) * sizeof(int64_t));
+    memcpy(col, A.col.data(), A.col.size() * sizeof(int32_t));
+    memcpy(val, A.val.data(), A.val.size() * sizeof(double));
+}
+
+void orc_set_rhs(orc_handle* h, const double* f) { std::copy(f, f + h->f.size(), h->f.begin()); }
+void orc_set_state(orc_handle* h, const double* x) { std::copy(x, x + h->x.size(), h->x.begin()); }
+void orc_get_state(orc_handle* h, double* x) { std::copy(h->x.begin(), h->x.end(), x); }
+void orc_set_sample_index(orc_handle* h, uint64_t s) { h->ctx.sample = s; }
+
+// Sampler::apply(f, x)
+void orc_apply(orc_handle* h, const double* f, double* x) { h->mg->apply(f, x); }
+
+// measure_sampling_time loop (driver_mgmc.cc:66-78): nsteps applications on the fixed rhs,
+// qoi_out[k] = x[qoi] after step k (qoi < 0 / qoi_out == NULL: no recording)
+void orc_sample(orc_handle* h, int nsteps, int64_t qoi, double* qoi_out) {
+    for (int k = 0; k < nsteps; ++k) {
+        h->mg->apply(h->f.data(), h->x.data());
+        if (qoi_out && qoi >= 0) qoi_out[k] = h->x[qoi];
+    }
+}
+
+// wall-clock of nsteps applications (std::chrono::steady_clock), seconds
+double orc_time_samples(orc_handle* h, int nsteps) {
+    const auto t0 = std::chrono::steady_clock::now();
+    orc_sample(h, nsteps, -1, nullptr);
+    const auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// sampler/test_sampler.hh:113-153 mean_covariance_error loop: nwarmup applications, then running
+// estimators Ex += (x - Ex)/(k+1), Exx += (x x^T - Exx)/(k+1) over nsamples applications (x starts at 0)
+void orc_mean_cov(orc_handle* h, const double* f, int nwarmup, int64_t nsamples, double* Ex, double* Exx) {
+    const int64_t n = (int64_t)h->x.size();
+    std::vector<double> x(n, 0.0);
+    for (int k = 0; k < nwarmup; ++k) h->mg->apply(f, x.data());
+    for (int64_t q = 0; q < n; ++q) Ex[q] = 0.0;
+    for (int64_t q = 0; q < n * n; ++q) Exx[q] = 0.0;
+    for (int64_t k = 0; k < nsamples; ++k) {
+        h->mg->apply(f, x.data());
+        const double w = 1. / (k + 1);
+        for (int64_t i = 0; i < n; ++i) {
+            Ex[i] += w * (x[i] - Ex[i]);
+            for (int64_t j = 0; j < n; ++j) Exx[i * n + j] += w * (x[i] * x[j] - Exx[i * n + j]);
+        }
+    }
+}
+
+void orc_operator_apply(orc_handle* h, int level, const double* x, double* y) { spmv(h->mg->levels[level]->A, x, y); }
+
+void orc_smoother_apply(orc_handle* h, int level, int direction, int nsweeps, const double* b, double* x) {
+    SORSmoother s(h->mg->levels[level].get(), h->mg->p.omega, (Direction)direction);
+    for (int k = 0; k < nsweeps; ++k) s.apply(h->ctx.mode, b, x);
+}
+
+// one noisy sweep with explicit (tag, sample) in multicolour mode (SORSampler, nsmooth = 1)
+void orc_sor_sampler_apply(orc_handle* h, int level, int direction, uint32_t tag, uint64_t sample, const double* f,
+                           double* x) {
+    SORSampler s(&h->ctx, h->mg->levels[level].get(), h->mg->p.omega, 1, (Direction)direction);
+    const uint32_t save_tag = h->ctx.tag;
+    const uint64_t save_sample = h->ctx.sample;
+    h->ctx.tag = tag;
+    h->ctx.sample = sample;
+    s.apply(f, x);
+    h->ctx.tag = save_tag;
+    h->ctx.sample = save_sample;
+}
+
+void orc_restrict(orc_handle* h, int level, const double* r, double* rc) { h->mg->ig[level]->restrict_(r, rc); }
+void orc_prolongate_add(orc_handle* h, int level, double alpha, const double* xc, double* x) {
+    h->mg->ig[level]->prolongate_add(alpha, xc, x);
+}
+// R (f - A x), multigridmc_sampler.cc:118-120
+void orc_residual_restrict(orc_handle* h, int level, const double* f, const double* x, double* fc) {
+    const CSR& A = h->mg->levels[level]->A;
+    std::vector<double> r(A.nrow);
+    spmv(A, x, r.data());
+    for (int64_t q = 0; q < A.nrow; ++q) r[q] = f[q] - r[q];
+    h->mg->ig[level]->restrict_(r.data(), fc);
+}
+
+void orc_philox_normals(uint64_t seed, uint64_t chain, uint64_t pair0, int64_t n, uint32_t tag, uint64_t sample,
+                        double* out) {
+    for (int64_t q = 0; q < n / 2; ++q) philox_normals(seed, chain, (uint32_t)(pair0 + q), tag, sample, out[2 * q], out[2 * q + 1]);
+}
+
+void orc_philox_raw(const uint32_t ctr_in[4], uint32_t k0, uint32_t k1, uint32_t out[4]) {
+    uint32_t c[4] = {ctr_in[0], ctr_in[1], ctr_in[2], ctr_in[3]};
+    philox10(c, k0, k1);
+    memcpy(out, c, sizeof(c));
+}
+
+double orc_ln_unit(double u) { return ln_unit(u); }
+void orc_cos_sin_2pi(double t, double* c, double* s) { cos_sin_2pi(t, *c, *s); }
+
+// first n values of std::normal_distribution<double>(0,1) on std::mt19937_64(seed)
+void orc_mt_normals(uint64_t seed, int64_t n, double* out) {
+    std::mt19937_64 rng(seed);
+    std::normal_distribution<double> nd(0.0, 1.0);
+    for (int64_t q = 0; q < n; ++q) out[q] = nd(rng);
+}
+
+// ---- lattice known answers (lattice/test_lattice.hh) ----
+static Lattice lat_of(int dim, const int* n) {
+    Lattice l;
+    l.dim = dim;
+    for (int d = 0; d < dim; ++d) l.n[d] = n[d];
+    return l;
+}
+int64_t orc_lattice_fine_vertex_idx(int dim, const int* n, int64_t ell) { return lat_of(dim, n).fine_vertex_idx(ell); }
+void orc_lattice_lin2euc(int dim, const int* n, int64_t ell, int* idx) { lat_of(dim, n).lin2euc(ell, idx); }
+int64_t orc_lattice_euc2lin(int dim, const int* n, const int* idx) {
+    int i3[3] = {idx[0], dim >= 2 ? idx[1] : 0, dim == 3 ? idx[2] : 0};
+    return lat_of(dim, n).euc2lin(i3);
+}
+int64_t orc_lattice_shift(int dim, const int* n, int64_t ell, const int* shift) {
+    int s[3] = {shift[0], dim >= 2 ? shift[1] : 0, dim == 3 ? shift[2] : 0};
+    // shift_vertexidx (lattice*d.hh) does not range-check (asserts only): plain index arithmetic
+    const Lattice l = lat_of(dim, n);
+    int idx[3];
+    l.lin2euc(ell, idx);
+    for (int d = 0; d < dim; ++d) idx[d] += s[d];
+    return l.euc2lin(idx);
+}
+
+}  // extern "C"

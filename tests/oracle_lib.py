@@ -1,0 +1,249 @@
+"""ctypes wrapper of the CPU oracle (oracle/refcpu.cpp -> oracle/build/liboracle.so).
+
+TEST INFRASTRUCTURE: used only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, as the checker / CPU baseline -- never by the product path."""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_int, c_int32, c_int64, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+
+FAITHFUL = 0
+MULTICOLOUR = 1
+
+
+class OrcParams(ctypes.Structure):
+    _fields_ = [
+        ("dim", c_int), ("nx", c_int), ("ny", c_int), ("nz", c_int),
+        ("nlevel", c_int), ("cycle", c_int), ("npresmooth", c_int), ("npostsmooth", c_int),
+        ("ncoarsesmooth", c_int), ("smoother", c_int), ("coarse_solver", c_int), ("galerkin", c_int),
+        ("omega", c_double), ("coarse_scaling", c_double), ("kappa_sq", c_double),
+    ]
+
+
+_DP = POINTER(c_double)
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            import subprocess
+            subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True)
+        L = ctypes.CDLL(LIB)
+        sigs = {
+            "orc_create_fd": (c_void_p, [POINTER(OrcParams), c_int, c_uint64, c_uint64, _DP]),
+            "orc_create_csr": (c_void_p, [POINTER(OrcParams), c_int, c_uint64, c_int64, POINTER(c_int64),
+                                          POINTER(c_int32), _DP]),
+            "orc_destroy": (None, [c_void_p]),
+            "orc_ndof": (c_int64, [c_void_p, c_int]),
+            "orc_nlevel": (c_int, [c_void_p]),
+            "orc_nnz": (c_int64, [c_void_p, c_int]),
+            "orc_get_csr": (None, [c_void_p, c_int, POINTER(c_int64), POINTER(c_int32), _DP]),
+            "orc_set_rhs": (None, [c_void_p, _DP]),
+            "orc_set_state": (None, [c_void_p, _DP]),
+            "orc_get_state": (None, [c_void_p, _DP]),
+            "orc_set_sample_index": (None, [c_void_p, c_uint64]),
+            "orc_apply": (None, [c_void_p, _DP, _DP]),
+            "orc_sample": (None, [c_void_p, c_int, c_int64, _DP]),
+            "orc_time_samples": (c_double, [c_void_p, c_int]),
+            "orc_operator_apply": (None, [c_void_p, c_int, _DP, _DP]),
+            "orc_mean_cov": (None, [c_void_p, _DP, c_int, c_int64, _DP, _DP]),
+            "orc_smoother_apply": (None, [c_void_p, c_int, c_int, c_int, _DP, _DP]),
+            "orc_sor_sampler_apply": (None, [c_void_p, c_int, c_int, c_uint32, c_uint64, _DP, _DP]),
+            "orc_restrict": (None, [c_void_p, c_int, _DP, _DP]),
+            "orc_prolongate_add": (None, [c_void_p, c_int, c_double, _DP, _DP]),
+            "orc_residual_restrict": (None, [c_void_p, c_int, _DP, _DP, _DP]),
+            "orc_philox_normals": (None, [c_uint64, c_uint64, c_uint64, c_int64, c_uint32, c_uint64, _DP]),
+            "orc_philox_raw": (None, [POINTER(c_uint32), c_uint32, c_uint32, POINTER(c_uint32)]),
+            "orc_ln_unit": (c_double, [c_double]),
+            "orc_cos_sin_2pi": (None, [c_double, _DP, _DP]),
+            "orc_mt_normals": (None, [c_uint64, c_int64, _DP]),
+            "orc_lattice_fine_vertex_idx": (c_int64, [c_int, POINTER(c_int), c_int64]),
+            "orc_lattice_lin2euc": (None, [c_int, POINTER(c_int), c_int64, POINTER(c_int)]),
+            "orc_lattice_euc2lin": (c_int64, [c_int, POINTER(c_int), POINTER(c_int)]),
+            "orc_lattice_shift": (c_int64, [c_int, POINTER(c_int), c_int64, POINTER(c_int)]),
+        }
+        for name, (res, args) in sigs.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def dp(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(_DP)
+
+
+def ivec(v):
+    arr = (c_int * len(v))(*v)
+    return arr
+
+
+def params_struct(shape, mg, kappa_sq: float, galerkin: int = 0) -> OrcParams:
+    p = OrcParams()
+    p.dim = len(shape)
+    p.nx = shape[0]
+    p.ny = shape[1] if len(shape) > 1 else 0
+    p.nz = shape[2] if len(shape) > 2 else 0
+    p.nlevel = mg.nlevel
+    p.cycle = mg.cycle
+    p.npresmooth = mg.npresmooth
+    p.npostsmooth = mg.npostsmooth
+    p.ncoarsesmooth = mg.ncoarsesmooth
+    p.smoother = {"SOR": 0, "SSOR": 1}[mg.smoother]
+    p.coarse_solver = {"SSOR": 0, "Cholesky": 1}[mg.coarse_solver]
+    p.galerkin = galerkin
+    p.omega = mg.omega
+    p.coarse_scaling = mg.coarse_scaling
+    p.kappa_sq = kappa_sq
+    return p
+
+
+class Oracle:
+    """One oracle MGMC chain (FAITHFUL = reference algorithm, MULTICOLOUR = device replay)."""
+
+    def __init__(self, handle, params):
+        self.h = handle
+        self.params = params
+        self.L = lib()
+
+    @classmethod
+    def fd(cls, shape, mg, kappa_sq, mode=FAITHFUL, seed=5418513, chain=0, galerkin=0, override_stencils=None):
+        p = params_struct(shape, mg, kappa_sq, galerkin)
+        st = None
+        if override_stencils is not None:
+            override_stencils = np.ascontiguousarray(override_stencils, dtype=np.float64)
+            st = dp(override_stencils)
+        h = lib().orc_create_fd(ctypes.byref(p), mode, seed, chain, st)
+        return cls(h, p)
+
+    @classmethod
+    def csr(cls, shape, mg, rowptr, col, val, mode=FAITHFUL, seed=0):
+        p = params_struct(shape, mg, 0.0)
+        rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+        col = np.ascontiguousarray(col, dtype=np.int32)
+        val = np.ascontiguousarray(val, dtype=np.float64)
+        h = lib().orc_create_csr(ctypes.byref(p), mode, seed, len(rowptr) - 1,
+                                 rowptr.ctypes.data_as(POINTER(c_int64)), col.ctypes.data_as(POINTER(c_int32)),
+                                 dp(val))
+        return cls(h, p)
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.L.orc_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def ndof(self, level=0):
+        return int(self.L.orc_ndof(self.h, level))
+
+    def csr_matrix(self, level=0):
+        import scipy.sparse as sp
+        n = self.ndof(level)
+        nnz = int(self.L.orc_nnz(self.h, level))
+        rowptr = np.empty(n + 1, dtype=np.int64)
+        col = np.empty(nnz, dtype=np.int32)
+        val = np.empty(nnz)
+        self.L.orc_get_csr(self.h, level, rowptr.ctypes.data_as(POINTER(c_int64)),
+                           col.ctypes.data_as(POINTER(c_int32)), dp(val))
+        return sp.csr_matrix((val, col, rowptr), shape=(n, n))
+
+    def apply(self, f, x):
+        f = np.ascontiguousarray(f, dtype=np.float64)
+        self.L.orc_apply(self.h, dp(f), dp(x))
+
+    def set_rhs(self, f):
+        f = np.ascontiguousarray(f, dtype=np.float64)
+        self.L.orc_set_rhs(self.h, dp(f))
+
+    def set_state(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        self.L.orc_set_state(self.h, dp(x))
+
+    def get_state(self):
+        x = np.empty(self.ndof())
+        self.L.orc_get_state(self.h, dp(x))
+        return x
+
+    def sample(self, nsteps, qoi=-1):
+        out = np.empty(max(nsteps, 0))
+        self.L.orc_sample(self.h, nsteps, qoi, dp(out) if qoi >= 0 else None)
+        return out
+
+    def time_samples(self, nsteps):
+        return float(self.L.orc_time_samples(self.h, nsteps))
+
+    def mean_cov(self, f, nwarmup, nsamples):
+        f = np.ascontiguousarray(f, dtype=np.float64)
+        n = self.ndof()
+        ex = np.empty(n)
+        exx = np.empty((n, n))
+        self.L.orc_mean_cov(self.h, dp(f), nwarmup, nsamples, dp(ex), dp(exx))
+        return ex, exx - np.outer(ex, ex)
+
+    def operator_apply(self, level, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.empty(self.ndof(level))
+        self.L.orc_operator_apply(self.h, level, dp(x), dp(y))
+        return y
+
+    def smoother_apply(self, level, direction, nsweeps, b, x):
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        out = np.ascontiguousarray(x, dtype=np.float64).copy()
+        self.L.orc_smoother_apply(self.h, level, direction, nsweeps, dp(b), dp(out))
+        return out
+
+    def sor_sampler_apply(self, level, direction, tag, sample, f, x):
+        f = np.ascontiguousarray(f, dtype=np.float64)
+        out = np.ascontiguousarray(x, dtype=np.float64).copy()
+        self.L.orc_sor_sampler_apply(self.h, level, direction, tag, sample, dp(f), dp(out))
+        return out
+
+    def restrict(self, level, r):
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        out = np.empty(self.ndof(level + 1))
+        self.L.orc_restrict(self.h, level, dp(r), dp(out))
+        return out
+
+    def prolongate_add(self, level, alpha, xc, x):
+        xc = np.ascontiguousarray(xc, dtype=np.float64)
+        out = np.ascontiguousarray(x, dtype=np.float64).copy()
+        self.L.orc_prolongate_add(self.h, level, alpha, dp(xc), dp(out))
+        return out
+
+    def residual_restrict(self, level, f, x):
+        f = np.ascontiguousarray(f, dtype=np.float64)
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        out = np.empty(self.ndof(level + 1))
+        self.L.orc_residual_restrict(self.h, level, dp(f), dp(x), dp(out))
+        return out
+
+
+def philox_normals(seed, chain, pair0, n, tag, sample):
+    out = np.empty(n)
+    lib().orc_philox_normals(seed, chain, pair0, n, tag, sample, dp(out))
+    return out
+
+
+def philox_raw(ctr, key):
+    c = (c_uint32 * 4)(*ctr)
+    o = (c_uint32 * 4)()
+    lib().orc_philox_raw(c, key[0], key[1], o)
+    return list(o)
+
+
+def mt_normals(seed, n):
+    out = np.empty(n)
+    lib().orc_mt_normals(seed, n, dp(out))
+    return out

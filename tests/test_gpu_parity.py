@@ -1,0 +1,258 @@
+"""GPU parity tests (-m gpu): the HIP path through the C-ABI against the CPU oracle.
+
+Tiers (DESIGN.md "Parity contract"):
+  T2  bitwise: every kernel (operator, restriction, prolongation, fused residual+restriction,
+      deterministic and noisy multicolour sweeps, Philox normals) and whole MGMC cycles equal the
+      oracle's MULTICOLOUR replay on the same (seed, chain, tag, sample) -- compared with
+      np.array_equal (exact, signed zeros equal).  Component kernels are also compared with the
+      FAITHFUL oracle's CSR arithmetic (reference expression order).
+  T3  statistical: the device chain's mean / covariance against the dense exact Q^-1, and the QoI
+      variance against the exact (A^-1)_cc -- tolerances stated in each test.
+  Size-independent properties at the benchmark sizes (256^3, 512^3): smoother fixed point,
+  determinism, chain independence, finiteness.
+"""
+import numpy as np
+import pytest
+import scipy.sparse.linalg as spla
+
+import multigridmc_amd as mg
+from tests import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+SEED = 5418513
+
+
+def make(shape, kappa_sq=25.0, chain=0, **kw):
+    p = mg.MultigridParameters(**{"nlevel": 3, "smoother": "SOR", "coarse_solver": "SSOR", **kw})
+    lat = mg.Lattice(*shape)
+    s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, kappa_sq), SEED, p, device=0, chain_id=chain)
+    return s, p, lat
+
+
+def oracle_for(sampler, p, lat, kappa_sq=25.0, mode=O.MULTICOLOUR, chain=0):
+    st = np.concatenate([sampler.level_desc(level)["stencil"] for level in range(p.nlevel)])
+    return O.Oracle.fd(lat.shape, p, kappa_sq, mode=mode, seed=SEED, chain=chain, override_stencils=st)
+
+
+CONFIGS = {
+    "2d64_template_W": ((64, 64), dict(nlevel=4, cycle=2)),
+    "2d_aniso_ssor": ((32, 64), dict(nlevel=3, smoother="SSOR", npresmooth=2, npostsmooth=1, ncoarsesmooth=2,
+                                     omega=0.8, coarse_scaling=1.1)),
+    "3d16": ((16, 16, 16), dict(nlevel=3)),
+    "3d_aniso": ((32, 16, 16), dict(nlevel=2, ncoarsesmooth=3)),
+    "3d64_4lvl": ((64, 64, 64), dict(nlevel=4, omega=1.2)),
+    "2d16_1lvl": ((16, 16), dict(nlevel=1, ncoarsesmooth=2)),
+    "3d8_1lvl": ((8, 8, 8), dict(nlevel=1)),
+    "2d256_global_coarse": ((256, 256), dict(nlevel=2)),
+    "3d32_W_ssor": ((32, 32, 32), dict(nlevel=3, cycle=2, smoother="SSOR")),
+}
+
+
+def test_normals_bitwise(hip_device):
+    s, p, lat = make((16, 16))
+    for chain in (0, 7):
+        s2 = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), SEED, p, chain_id=chain)
+        for pair0, tag, sample in [(0, 0, 0), (12345, 3, 1), (2 ** 31 + 5, 17, 2 ** 33 + 9)]:
+            d = s2.normals(pair0, 20000, tag, sample)
+            o = O.philox_normals(SEED, chain, pair0, 20000, tag, sample)
+            assert np.array_equal(d, o), f"chain {chain} pair0 {pair0}: max diff {np.max(np.abs(d - o))}"
+        s2.close()
+    s.close()
+
+
+@pytest.mark.parametrize("name", ["2d64_template_W", "3d16", "3d_aniso", "2d_aniso_ssor"])
+def test_component_kernels_bitwise(hip_device, name):
+    shape, kw = CONFIGS[name]
+    s, p, lat = make(shape, **kw)
+    faithful = O.Oracle.fd(lat.shape, p, 25.0, mode=O.FAITHFUL, seed=SEED)
+    rng = np.random.default_rng(42)
+    for level in range(p.nlevel):
+        n = s.level_desc(level)["ndof"]
+        assert n == faithful.ndof(level)
+        x = rng.standard_normal(n)
+        f = rng.standard_normal(n)
+        assert np.array_equal(s.operator_apply(level, x), faithful.operator_apply(level, x))
+        if level + 1 < p.nlevel:
+            nc = s.level_desc(level + 1)["ndof"]
+            xc = rng.standard_normal(nc)
+            assert np.array_equal(s.restrict(level, f), faithful.restrict(level, f))
+            assert np.array_equal(s.prolongate_add(level, 1.3, xc, x), faithful.prolongate_add(level, 1.3, xc, x))
+            assert np.array_equal(s.residual_restrict(level, f, x), faithful.residual_restrict(level, f, x))
+    s.close()
+
+
+@pytest.mark.parametrize("name", ["2d64_template_W", "3d16", "3d_aniso", "2d_aniso_ssor", "3d64_4lvl"])
+def test_multicolour_sweeps_bitwise(hip_device, name):
+    shape, kw = CONFIGS[name]
+    s, p, lat = make(shape, **kw)
+    mc = oracle_for(s, p, lat)
+    rng = np.random.default_rng(7)
+    for level in range(p.nlevel):
+        n = s.level_desc(level)["ndof"]
+        b = rng.standard_normal(n)
+        x = rng.standard_normal(n)
+        for direction in (mg.FORWARD, mg.BACKWARD):
+            d = s.smoother_apply(level, direction, 2, b, x)
+            o = mc.smoother_apply(level, direction, 2, b, x)
+            assert np.array_equal(d, o), f"level {level} dir {direction} smoother"
+            d = s.sor_sampler_apply(level, direction, 5 + level, 77, b, x)
+            o = mc.sor_sampler_apply(level, direction, 5 + level, 77, b, x)
+            assert np.array_equal(d, o), f"level {level} dir {direction} sampler"
+    s.close()
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_mgmc_cycles_bitwise(hip_device, name):
+    """Whole MGMC cycles: Sampler::apply and the device-resident QoI loop equal the oracle's
+    multicolour replay exactly."""
+    shape, kw = CONFIGS[name]
+    s, p, lat = make(shape, **kw)
+    mc = oracle_for(s, p, lat)
+    rng = np.random.default_rng(11)
+    f = rng.standard_normal(lat.Nvertex)
+    x_dev = np.zeros(lat.Nvertex)
+    x_orc = np.zeros(lat.Nvertex)
+    for _ in range(2):
+        s.apply(f, x_dev)
+        mc.apply(f, x_orc)
+        assert np.array_equal(x_dev, x_orc)
+    # device-resident chain with QoI series (measure_sampling_time)
+    qoi = mg.measurement_vector_index(lat, [0.5] * lat.dim)
+    s.fix_rhs(f)
+    s.set_state(x_dev)
+    mc.set_rhs(f)
+    mc.set_state(x_orc)
+    z_dev = s.sample(6, qoi)
+    z_orc = mc.sample(6, qoi)
+    assert np.array_equal(z_dev, z_orc)
+    assert np.array_equal(s.get_state(), mc.get_state())
+    assert s.get_sample_index() == 8
+    n, mean, m2 = s.qoi_moments()
+    assert n == 6 and mean == pytest.approx(z_dev.mean(), rel=1e-12, abs=1e-300)
+    s.close()
+
+
+def test_mgmc_seed_chain_independence(hip_device):
+    a, p, lat = make((32, 32, 32))
+    b, _, _ = make((32, 32, 32))
+    c, _, _ = make((32, 32, 32), chain=1)
+    q = mg.measurement_vector_index(lat, [0.5, 0.5, 0.5])
+    za, zb, zc = a.sample(50, q), b.sample(50, q), c.sample(50, q)
+    assert np.array_equal(za, zb)
+    assert not np.array_equal(za, zc)
+    assert abs(np.corrcoef(za, zc)[0, 1]) < 0.5
+    for s in (a, b, c):
+        s.close()
+
+
+def _mean_cov(s, f, nsamples, nwarmup=200):
+    n = s.ndof
+    s.fix_rhs(f)
+    s.set_state(np.zeros(n))
+    s.sample(nwarmup)
+    ex = np.zeros(n)
+    exx = np.zeros((n, n))
+    for k in range(nsamples):
+        s.sample(1)
+        x = s.get_state()
+        ex += (x - ex) / (k + 1)
+        exx += (np.outer(x, x) - exx) / (k + 1)
+    return ex, exx - np.outer(ex, ex)
+
+
+@pytest.mark.parametrize("shape,kw,nsamples,tol", [
+    ((8, 8), dict(nlevel=3, ncoarsesmooth=2), 40000, 0.02),
+    ((8, 8), dict(nlevel=3, smoother="SSOR", cycle=2), 40000, 0.02),
+    ((8, 8, 8), dict(nlevel=2, ncoarsesmooth=2), 20000, 0.03),
+])
+def test_mgmc_statistics_vs_exact_covariance(hip_device, shape, kw, nsamples, tol):
+    """sampler/test_sampler.hh:113-153 on the device chain: sample mean and covariance against the
+    exact Q^-1 f and Q^-1 (infinity norm), relative to max|Q^-1|; tol stated per case."""
+    s, p, lat = make(shape, kappa_sq=4.0, **kw)
+    orc = O.Oracle.fd(lat.shape, p, 4.0, mode=O.FAITHFUL)
+    Q = orc.csr_matrix(0).toarray()
+    mu = np.random.default_rng(1342517).random(lat.Nvertex)
+    ex, cov = _mean_cov(s, Q @ mu, nsamples)
+    Qinv = np.linalg.inv(Q)
+    scale = np.max(np.abs(Qinv))
+    assert np.max(np.abs(ex - mu)) < 2 * tol * scale
+    assert np.max(np.abs(cov - Qinv)) < tol * scale
+    s.close()
+
+
+def _iact(z):
+    z = z - z.mean()
+    var = z.var()
+    tau = 1.0
+    for t in range(1, len(z) // 10):
+        rho = np.dot(z[:-t], z[t:]) / ((len(z) - t) * var)
+        if rho < 0.05:
+            break
+        tau += 2 * rho
+    return tau
+
+
+@pytest.mark.parametrize("shape,nlevel,nsamples", [((64, 64), 4, 20000), ((32, 32, 32), 4, 10000)])
+def test_qoi_variance_vs_exact(hip_device, shape, nlevel, nsamples):
+    """driver_mgmc.cc:86-104: prior (f = 0): E[z] = 0, Var[z] = (A^-1)_cc.  Tolerance: 5 sigma of the
+    Monte Carlo error with the integrated autocorrelation time (Var of a variance estimate ~ 2 var^2)."""
+    s, p, lat = make(shape, nlevel=nlevel)
+    orc = O.Oracle.fd(lat.shape, p, 25.0, mode=O.FAITHFUL)
+    A = orc.csr_matrix(0).tocsc()
+    q = mg.measurement_vector_index(lat, [0.5] * lat.dim)
+    e = np.zeros(lat.Nvertex)
+    e[q] = 1.0
+    var_exact = spla.spsolve(A, e)[q]
+    s.sample(100, q)
+    z = s.sample(nsamples, q)
+    tau = _iact(z)
+    n_eff = nsamples / tau
+    assert abs(z.mean()) < 5 * np.sqrt(var_exact / n_eff)
+    assert abs(z.var() - var_exact) < 5 * var_exact * np.sqrt(2.0 / n_eff)
+    n, mean, m2 = s.qoi_moments()
+    assert n == nsamples + 100
+    s.close()
+
+
+@pytest.mark.parametrize("n", [256, 512])
+def test_fine_smoother_fixed_point_at_scale(hip_device, n):
+    """smoother/test_smoother.hh:90-101 at the benchmark sizes: a forward+backward deterministic
+    sweep leaves the exact solution of A x = b invariant (relative 1e-12)."""
+    s, p, lat = make((n, n, n), nlevel=2)
+    x_exact = np.random.default_rng(1).standard_normal(lat.Nvertex)
+    b = s.operator_apply(0, x_exact)
+    x = s.smoother_apply(0, mg.FORWARD, 1, b, x_exact)
+    x = s.smoother_apply(0, mg.BACKWARD, 1, b, x)
+    assert np.linalg.norm(x - x_exact) / np.linalg.norm(x_exact) < 1e-12
+    s.close()
+
+
+def test_benchmark_hierarchy_cycles_finite_and_deterministic(hip_device):
+    """3D 512^3 7-level V-cycle (BASELINE config 4, one chain): cycles stay finite, the state moves,
+    and a second handle with the same (seed, chain) reproduces the QoI series bit for bit."""
+    shape = (512, 512, 512)
+    q = mg.measurement_vector_index(mg.Lattice(*shape), [0.5, 0.5, 0.5])
+    a, p, lat = make(shape, nlevel=7)
+    za = a.sample(4, q)
+    assert np.all(np.isfinite(za)) and np.all(za != 0)
+    x = a.get_state()
+    assert np.all(np.isfinite(x)) and np.std(x) > 0
+    a.close()
+    b, _, _ = make(shape, nlevel=7)
+    zb = b.sample(4, q)
+    assert np.array_equal(za, zb)
+    b.close()
+
+
+def test_invalid_level_and_sizes_raise(hip_device):
+    s, p, lat = make((16, 16))
+    with pytest.raises(mg.MgmcError):
+        s.operator_apply(5, np.zeros(10))
+    with pytest.raises(ValueError):
+        s.apply(np.zeros(3), np.zeros(3))
+    with pytest.raises(mg.MgmcError):
+        s.sample(3, lat.Nvertex + 5)
+    s.close()
+    with pytest.raises(mg.MgmcError):
+        make((16, 16), coarse_solver="Cholesky")

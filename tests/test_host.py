@@ -1,0 +1,192 @@
+"""Host-side logic and the C-ABI boundary without a GPU: library loads and exports every symbol of
+include/mgmc.h, configuration validation, Galerkin stencils vs the oracle's SpGEMM, the
+libconfig-subset parser, QoI indexing, and the rank-order moment merge (gloo, world_size 2)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import multigridmc_amd as mg
+from multigridmc_amd import _native
+from multigridmc_amd.distributed import merge_moments, moments_of
+from tests import oracle_lib as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def header_symbols():
+    text = open(os.path.join(ROOT, "include", "mgmc.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mgmc_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = mg.load_library()
+    syms = header_symbols()
+    assert len(syms) >= 25
+    bound = {name for name, _, _ in _native.SIGNATURES}
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in include/mgmc.h but not exported"
+        assert s in bound, f"{s} not bound in multigridmc_amd/_native.py"
+    assert lib.mgmc_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_native.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def _cfg(shape=(16, 16, 16), **kw):
+    p = mg.MultigridParameters(**{"nlevel": 3, **kw})
+    return mg.make_config(mg.ShiftedLaplaceFDOperator(mg.Lattice(*shape), 25.0), p)
+
+
+@pytest.mark.parametrize("shape,nlevel,msg", [
+    ((15, 16, 16), 2, "one of the extents is odd"),
+    ((8, 8, 8), 4, "no interior vertices"),
+    ((6, 6), 2, None),
+])
+def test_describe_validation(shape, nlevel, msg):
+    lib = mg.load_library()
+    c = _cfg(shape, nlevel=nlevel)
+    rc = lib.mgmc_describe(ctypes.byref(c), None, 0)
+    if msg is None:
+        assert rc == nlevel
+    else:
+        assert rc == _native.MGMC_E_INVALID
+        assert msg in _native.last_error()
+
+
+def test_invalid_parameters_rejected():
+    lib = mg.load_library()
+    for field, value in [("omega", 2.5), ("cycle", 0), ("smoother", 7), ("dim", 4)]:
+        c = _cfg()
+        setattr(c, field, value)
+        assert lib.mgmc_describe(ctypes.byref(c), None, 0) == _native.MGMC_E_INVALID
+    with pytest.raises(ValueError):
+        mg.make_config(mg.ShiftedLaplaceFDOperator(mg.Lattice(8, 8), 1.0), mg.MultigridParameters(smoother="Jacobi"))
+
+
+def test_create_without_gpu_fails_loudly():
+    """On a host without a HIP device the product path must raise, never fall back to the CPU."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    n = ctypes.c_int(0)
+    if hip.hipGetDeviceCount(ctypes.byref(n)) == 0 and n.value > 0:
+        pytest.skip("a HIP device is present (covered by the gpu tests)")
+    lat = mg.Lattice3d(8, 8, 8)
+    with pytest.raises(mg.MgmcError):
+        mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 1, mg.MultigridParameters(nlevel=2))
+
+
+@pytest.mark.parametrize("shape", [(16, 16), (64, 32), (16, 16, 16), (32, 16, 16), (64, 64, 64)])
+def test_stencils_match_oracle_spgemm_bitwise(shape):
+    nlevel = 3
+    c = _cfg(shape, nlevel=nlevel)
+    levels = mg.describe(c)
+    o = O.Oracle.fd(shape, mg.MultigridParameters(nlevel=nlevel), 25.0, galerkin=0 if np.prod(shape) < 70000 else 1)
+    for lev, d in enumerate(levels):
+        A = o.csr_matrix(lev)
+        lat = mg.Lattice(*d["shape"])
+        assert A.shape[0] == d["ndof"] == lat.Nvertex
+        assert d["npoints"] == (2 * lat.dim + 1 if lev == 0 else 3 ** lat.dim)
+        assert d["ncolours"] == (2 if lev == 0 else 2 ** lat.dim)
+        # interior row (2,2[,2]) of the oracle matrix vs the device stencil
+        r = lat.vertexidx_euclidean2linear([2] * lat.dim)
+        row = A.getrow(r)
+        got = {}
+        for col, v in zip(row.indices, row.data):
+            idx = lat.vertexidx_linear2euclidean(int(col))
+            k = sum((idx[dd] - 2 + 1) * 3 ** dd for dd in range(lat.dim))
+            got[k] = v
+        for k in range(3 ** lat.dim):
+            assert d["stencil"][k] == got.get(k, 0.0), f"level {lev} offset {k}"
+
+
+def test_parameters_template_parses():
+    from multigridmc_amd.parameters import (ConstantCorrelationLengthModelParameters, GeneralParameters,
+                                            LatticeParameters, MeasurementParameters, MultigridParameters,
+                                            SamplingParameters, read_config)
+    cfg = read_config(os.path.join(GOLDEN, "parameters_template.cfg"))
+    g = GeneralParameters.from_config(cfg)
+    assert g.dim == 2 and g.operator_name == "posterior" and g.do_multigridmc
+    lat = LatticeParameters.from_config(cfg)
+    assert (lat.nx, lat.ny, lat.nz) == (32, 32, 32)
+    m = MultigridParameters.from_config(cfg)
+    assert (m.smoother, m.coarse_solver, m.nlevel, m.cycle, m.omega) == ("SOR", "SSOR", 4, 2, 1.0)
+    s = SamplingParameters.from_config(cfg)
+    assert (s.nsamples, s.nwarmup, s.nstepsconvergence, s.nsamplesconvergence) == (10000, 1000, 16, 1000)
+    assert ConstantCorrelationLengthModelParameters.from_config(cfg).kappa_sq == pytest.approx(25.0)
+    meas = MeasurementParameters.from_config(cfg, base_dir=GOLDEN)
+    assert meas.dim == 2 and meas.n == 8 and len(meas.measurement_locations) == 8
+    assert meas.measurement_locations[0] == [0.29024507839949776, 0.4429559665392171]
+    assert meas.variance[7] == 1.864273250664901e-06
+
+
+def test_measurement_vector_index():
+    """radius-0 QoI (measured_operator.cc:74-91): 2D 64^2 [0.5,0.5] -> (32,32); 3D 512^3 -> (256,256,256)."""
+    lat = mg.Lattice2d(64, 64)
+    assert lat.vertexidx_linear2euclidean(mg.measurement_vector_index(lat, [0.5, 0.5])) == (32, 32)
+    lat3 = mg.Lattice3d(512, 512, 512)
+    assert lat3.vertexidx_linear2euclidean(mg.measurement_vector_index(lat3, [0.5, 0.5, 0.5])) == (256, 256, 256)
+    # brute force on a small lattice, reference loop semantics (first strict minimum)
+    lat = mg.Lattice2d(8, 6)
+    x0 = (0.37, 0.61)
+    best, dmin = 0, 2.0
+    for ell in range(lat.Nvertex):
+        c = lat.vertex_coordinates(ell)
+        dist = np.sqrt(sum((c[d] - x0[d]) ** 2 for d in range(2)))
+        if dist < dmin:
+            best, dmin = ell, dist
+    assert mg.measurement_vector_index(lat, x0) == best
+
+
+def test_merge_moments_matches_pooled():
+    rng = np.random.default_rng(3)
+    chunks = [rng.standard_normal(n) + k for k, n in enumerate([10, 1, 57, 0, 300])]
+    parts = [moments_of(c) for c in chunks]
+    n, mean, m2 = merge_moments(parts)
+    allv = np.concatenate(chunks)
+    assert n == allv.size
+    assert mean == pytest.approx(allv.mean(), rel=1e-13)
+    assert m2 / n == pytest.approx(allv.var(), rel=1e-12)
+
+
+def _gloo_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from multigridmc_amd.distributed import moments_of, pooled_statistics
+    series = np.random.default_rng(100 + rank).standard_normal(1000 + 10 * rank) * (1 + rank)
+    stats = pooled_statistics(moments_of(series))
+    q.put((rank, stats))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_pooled_statistics_gloo_world2():
+    import socket
+
+    import torch.multiprocessing as tmp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    allv = np.concatenate([np.random.default_rng(100 + r).standard_normal(1000 + 10 * r) * (1 + r) for r in range(2)])
+    for r in range(2):
+        assert res[r]["chains"] == 2
+        assert res[r]["n"] == allv.size
+        assert res[r]["mean"] == pytest.approx(allv.mean(), rel=1e-12)
+        assert res[r]["variance"] == pytest.approx(allv.var(), rel=1e-12)
