@@ -7,9 +7,13 @@ oracle baseline.
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 One process per GPU (RANK / LOCAL_RANK / WORLD_SIZE from the environment).  Each rank runs an
-independent chain (Philox key = (seed, chain = rank)); the only collective is the final all-gather
-of the per-chain QoI moments (RCCL, backend "nccl").  A step is one MGMC V-cycle; the K timed steps
-are bracketed by barrier + device synchronisation on both sides and the max over ranks is used.
+independent chain (Philox key = (seed, chain = rank)).  The device-side collectives (barrier,
+max-over-ranks time, the final all-gather of the per-chain QoI moments) run on an RCCL
+communicator owned by the C-ABI library on the sampler's own HIP stream; torch.distributed (gloo,
+CPU) only ships the RCCL unique id.  torch.cuda is never initialised: the library and torch bundle
+different HIP runtimes, and the library's stream synchronisation replaces torch.cuda.synchronize().
+A step is one MGMC V-cycle; the K timed steps are bracketed by barrier + device synchronisation on
+both sides and the max over ranks is used.
 
 Rank 0 prints ONE JSON line.  Field notes:
   value      = chains x K / max-over-ranks time (whole job, samples/s)
@@ -93,12 +97,6 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    import torch
-    import torch.distributed as dist
-    dist_on = world > 1
-    if dist_on:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
 
     n, nlevel = args.n, args.nlevel
     lat = mg.Lattice3d(n, n, n)
@@ -109,17 +107,19 @@ def main():
     qoi = mg.measurement_vector_index(lat, [0.5, 0.5, 0.5])
     n0 = lat.Nvertex
 
-    def barrier():
-        if dist_on:
-            dist.barrier(device_ids=[local_rank])
+    if world > 1:
+        # host rendezvous only (gloo, CPU): ship rank 0's RCCL id; every device-side collective
+        # (barrier, max-time, QoI all-gather) then runs on RCCL inside the library
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        obj = [mg.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        sampler.comm_init(world, rank, obj[0])
 
     # warmup (prior: f = 0, x0 = 0 -- driver_mgmc.cc:61-69 with mean_x_exact = xbar = 0)
     sampler.sample(args.warmup, qoi)
     sampler.reset_moments()
-    sampler.synchronize()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
+    sampler.comm_barrier()  # RCCL barrier + device synchronisation
     t0 = time.perf_counter()
     if args.plain:
         sampler.sample_async(args.steps, qoi)
@@ -127,17 +127,14 @@ def main():
         fine_ms, nfine = float("nan"), 0
     else:
         _, fine_ms, nfine = sampler.sample_timed(args.steps, qoi)
-    torch.cuda.synchronize()
+    sampler.synchronize()
     t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
-    if dist_on:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    sampler.comm_barrier()
+    elapsed = sampler.comm_allreduce_max(t1 - t0)
 
-    from multigridmc_amd.distributed import pooled_statistics
-    stats = pooled_statistics(tuple(sampler.qoi_moments()), device="cuda" if dist_on else None)
+    from multigridmc_amd.distributed import merge_moments
+    parts = sampler.comm_allgather_moments(world)
+    nq, mean, m2 = merge_moments([tuple(r) for r in parts])
 
     if rank == 0:
         value = world * args.steps / elapsed
@@ -156,7 +153,7 @@ def main():
                     traffic = None
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "fine-level multicolour Gibbs sweep (k_sweep_rb, red+black passes)",
+                    "kernel": "fine-level (level 0) multicolour Gibbs sweep",
                     "bytes_per_launch": bytes_sweep, "avg_launch_ms": round(t_sweep * 1e3, 4)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.cpu_samples > 0:
@@ -177,16 +174,17 @@ def main():
             "config": {"workload": f"3D {n}^3 shifted-Laplace FD prior (kappa^2 = 25), {nlevel}-level V-cycle, "
                                    f"SOR Gibbs 1/1, SSOR coarse 1, omega 1, one independent chain per GPU",
                        "lattice": [n, n, n], "unknowns": n0, "nlevel": nlevel, "chains": world,
-                       "parallelism": f"chains{world} (independent MCMC chains, 1 per GPU)"},
+                       "parallelism": f"chains{world} (independent MCMC chains, 1 per GPU; RCCL all-gather of QoI moments)"},
             "roofline": roof,
             "cpu_baseline": cpu,
-            "qoi": {"index": qoi, "samples": stats["n"], "mean": stats["mean"], "variance": stats["variance"],
-                    "chains": stats["chains"]},
+            "qoi": {"index": qoi, "samples": nq, "mean": mean, "variance": m2 / nq if nq else None, "chains": len(parts)},
         }
         print(json.dumps(line), flush=True)
-    sampler.close()
-    if dist_on:
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
         dist.destroy_process_group()
+    sampler.close()
 
 
 if __name__ == "__main__":

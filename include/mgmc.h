@@ -160,6 +160,20 @@ int mgmc_time_fine_sweeps(mgmc_handle* h, int nsweeps, float* ms);
 int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* fine_ms,
                       int* nfine);
 
+/* ---- multi-GPU: one chain per rank, RCCL over xGMI for the final QoI reduction ----
+ * (the reference is single-process; this is the only collective of the path) */
+#define MGMC_UNIQUE_ID_BYTES 128
+/* rank 0 creates the id and ships it to the other ranks (any host channel) */
+int mgmc_comm_unique_id(unsigned char out[MGMC_UNIQUE_ID_BYTES]);
+int mgmc_comm_init(mgmc_handle* h, int nranks, int rank, const unsigned char id[MGMC_UNIQUE_ID_BYTES]);
+/* all ranks: out[3*r .. 3*r+2] = (n, mean, M2) of rank r's device-side QoI moments */
+int mgmc_comm_allgather_moments(mgmc_handle* h, double* out);
+/* all ranks: *value <- max over ranks (used for the max-over-ranks benchmark time) */
+int mgmc_comm_allreduce_max(mgmc_handle* h, double* value);
+/* device-side barrier over the communicator, followed by a stream synchronisation */
+int mgmc_comm_barrier(mgmc_handle* h);
+int mgmc_comm_destroy(mgmc_handle* h);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,6 +16,7 @@ from .sampler import (  # noqa: F401
     Lattice3d,
     MultigridMCSampler,
     ShiftedLaplaceFDOperator,
+    comm_unique_id,
     describe,
     make_config,
     measurement_vector_index,

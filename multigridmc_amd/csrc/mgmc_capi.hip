@@ -7,6 +7,7 @@
 // into a hipGraph and replayed; the RNG counter (sample index) is read from device memory so
 // the frozen graph produces fresh noise on every replay.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -72,6 +73,9 @@ struct mgmc_handle {
     hipGraphExec_t graph_seg[4] = {nullptr, nullptr, nullptr, nullptr};
     int64_t qoi_store_index = -1;
     std::string last_error;
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    double* comm_buf = nullptr;  // device scratch for collectives
 };
 
 #define HIPCHK(h, call)                                                                              \
@@ -506,6 +510,8 @@ int mgmc_destroy(mgmc_handle* h) {
         for (auto p : lv.scratch)
             if (p) hipFree(p);
     }
+    if (h->comm) ncclCommDestroy(h->comm);
+    if (h->comm_buf) hipFree(h->comm_buf);
     if (h->ctrl) hipFree(h->ctrl);
     if (h->mom) hipFree(h->mom);
     if (h->series) hipFree(h->series);
@@ -827,6 +833,79 @@ int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* tot
         if (h->ops[q].kind == OP_SWEEP && h->ops[q].level == 0) ++cnt;
     *nfine = cnt * nsteps;
     for (auto& e : ev) hipEventDestroy(e);
+    return MGMC_OK;
+}
+
+#define NCCLCHK(h, call)                                                                     \
+    do {                                                                                     \
+        ncclResult_t r_ = (call);                                                            \
+        if (r_ != ncclSuccess)                                                               \
+            return fail(h, MGMC_E_HIP, std::string("RCCL error ") + ncclGetErrorString(r_) + " at " #call); \
+    } while (0)
+
+int mgmc_comm_unique_id(unsigned char out[MGMC_UNIQUE_ID_BYTES]) {
+    if (!out) return fail(nullptr, MGMC_E_INVALID, "null argument");
+    ncclUniqueId id;
+    NCCLCHK(nullptr, ncclGetUniqueId(&id));
+    memcpy(out, id.internal, MGMC_UNIQUE_ID_BYTES);
+    return MGMC_OK;
+}
+
+int mgmc_comm_init(mgmc_handle* h, int nranks, int rank, const unsigned char id_bytes[MGMC_UNIQUE_ID_BYTES]) {
+    if (!h || !id_bytes || nranks < 1 || rank < 0 || rank >= nranks) return fail(h, MGMC_E_INVALID, "invalid argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->comm) {
+        ncclCommDestroy(h->comm);
+        h->comm = nullptr;
+    }
+    ncclUniqueId id;
+    memcpy(id.internal, id_bytes, MGMC_UNIQUE_ID_BYTES);
+    NCCLCHK(h, ncclCommInitRank(&h->comm, nranks, id, rank));
+    h->nranks = nranks;
+    h->rank = rank;
+    if (h->comm_buf) HIPCHK(h, hipFree(h->comm_buf));
+    HIPCHK(h, hipMalloc(&h->comm_buf, (size_t)(4 * nranks + 4) * sizeof(double)));
+    return MGMC_OK;
+}
+
+int mgmc_comm_allgather_moments(mgmc_handle* h, double* out) {
+    if (!h || !out) return fail(h, MGMC_E_INVALID, "null argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    if (!h->comm) return mgmc_qoi_moments(h, out);  // single chain
+    double* send = h->comm_buf + 4 * h->nranks;
+    HIPCHK(h, hipMemcpyAsync(send, h->mom, 3 * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    NCCLCHK(h, ncclAllGather(send, h->comm_buf, 3, ncclDouble, h->comm, h->stream));
+    HIPCHK(h, hipMemcpyAsync(out, h->comm_buf, 3 * h->nranks * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return MGMC_OK;
+}
+
+int mgmc_comm_allreduce_max(mgmc_handle* h, double* value) {
+    if (!h || !value) return fail(h, MGMC_E_INVALID, "null argument");
+    if (!h->comm) return MGMC_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipMemcpyAsync(h->comm_buf, value, sizeof(double), hipMemcpyHostToDevice, h->stream));
+    NCCLCHK(h, ncclAllReduce(h->comm_buf, h->comm_buf, 1, ncclDouble, ncclMax, h->comm, h->stream));
+    HIPCHK(h, hipMemcpyAsync(value, h->comm_buf, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return MGMC_OK;
+}
+
+int mgmc_comm_barrier(mgmc_handle* h) {
+    if (!h) return fail(nullptr, MGMC_E_INVALID, "null handle");
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->comm) NCCLCHK(h, ncclAllReduce(h->comm_buf, h->comm_buf, 1, ncclDouble, ncclSum, h->comm, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipDeviceSynchronize());
+    return MGMC_OK;
+}
+
+int mgmc_comm_destroy(mgmc_handle* h) {
+    if (!h) return fail(nullptr, MGMC_E_INVALID, "null handle");
+    if (h->comm) ncclCommDestroy(h->comm);
+    h->comm = nullptr;
+    h->nranks = 1;
+    h->rank = 0;
     return MGMC_OK;
 }
 

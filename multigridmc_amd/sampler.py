@@ -319,10 +319,36 @@ class MultigridMCSampler:
         self._chk(self.lib.mgmc_normals(self.handle, int(pair0), int(n), int(tag), int(sample_index), _dp(out)))
         return out
 
+    # -- multi-GPU chains: RCCL communicator owned by the handle --
+    def comm_init(self, nranks: int, rank: int, unique_id: bytes):
+        if len(unique_id) != 128:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        self._chk(self.lib.mgmc_comm_init(self.handle, int(nranks), int(rank), unique_id))
+
+    def comm_allgather_moments(self, nranks: int) -> np.ndarray:
+        out = np.zeros(3 * max(nranks, 1))
+        self._chk(self.lib.mgmc_comm_allgather_moments(self.handle, _dp(out)))
+        return out.reshape(-1, 3)
+
+    def comm_allreduce_max(self, value: float) -> float:
+        v = ctypes.c_double(value)
+        self._chk(self.lib.mgmc_comm_allreduce_max(self.handle, ctypes.byref(v)))
+        return v.value
+
+    def comm_barrier(self):
+        self._chk(self.lib.mgmc_comm_barrier(self.handle))
+
     def time_fine_sweeps(self, nsweeps: int) -> float:
         ms = ctypes.c_float()
         self._chk(self.lib.mgmc_time_fine_sweeps(self.handle, int(nsweeps), ctypes.byref(ms)))
         return ms.value
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id (rank 0), to be shipped to the other ranks over any host channel."""
+    buf = ctypes.create_string_buffer(128)
+    check(load_library().mgmc_comm_unique_id(buf))
+    return buf.raw
 
 
 class HipMulticolourSORSmoother:
@@ -341,5 +367,5 @@ class HipMulticolourSORSmoother:
 
 __all__ = [
     "Lattice", "Lattice2d", "Lattice3d", "ShiftedLaplaceFDOperator", "MultigridMCSampler",
-    "HipMulticolourSORSmoother", "measurement_vector_index", "make_config", "describe", "FORWARD", "BACKWARD",
+    "HipMulticolourSORSmoother", "measurement_vector_index", "comm_unique_id", "make_config", "describe", "FORWARD", "BACKWARD",
 ]
