@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--n", type=int, default=512, help="cells per direction (3D)")
     ap.add_argument("--nlevel", type=int, default=7)
-    ap.add_argument("--cpu-samples", type=int, default=2, help="V-cycles timed for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-samples", type=int, default=1, help="V-cycles timed for the CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--plain", action="store_true", help="time the single-graph loop instead of the segmented one")

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -19,6 +20,7 @@
 #include "../../include/mgmc.h"
 #include "mgmc_hierarchy.hpp"
 #include "mgmc_kernels.hpp"
+#include "mgmc_zsweep.hpp"
 
 using namespace mgmc;
 
@@ -32,7 +34,7 @@ void set_global_error(const std::string& s) {
     g_last_error = s;
 }
 
-enum OpKind { OP_SWEEP = 0, OP_RESIDUAL_RESTRICT = 1, OP_PROLONGATE = 2, OP_COARSE_LDS = 3, OP_QOI = 4 };
+enum OpKind { OP_SWEEP = 0, OP_RESIDUAL_RESTRICT = 1, OP_PROLONGATE = 2, OP_COARSE_LDS = 3, OP_QOI = 4, OP_COPY = 5 };
 
 struct Op {
     OpKind kind;
@@ -40,16 +42,24 @@ struct Op {
     int direction;  // MGMC_FORWARD / MGMC_BACKWARD for sweeps
     uint32_t tag;   // first sweep tag
     int nsweeps;    // OP_COARSE_LDS
+    int src = 0;    // buffer index read (x[src]); z-sweeps write x[1-src]
+    int prolong = 0;  // z-sweep with fused prolongate-add of the coarser level's x
 };
+
+// z-marching sweep tile shape (mgmc_zsweep.hpp)
+constexpr int ZS_XP = 64, ZS_TY = 6, ZS_NT = 256, ZS_TZ = 32;
 
 struct Level {
     LevelSpec spec;
     Layout L;
     StencilArg S;
-    double* x = nullptr;
+    double* x = nullptr;      // canonical state buffer
+    double* x2 = nullptr;     // ping-pong partner (z-sweep levels only)
     double* f = nullptr;
     double* scratch[3] = {nullptr, nullptr, nullptr};
     size_t lds_bytes = 0;  // >0 if the whole-level LDS kernel can hold x and f
+    bool zsweep = false;   // fused z-marching red-black sweep available
+    double* buf(int i) const { return i == 0 ? x : x2; }
 };
 
 }  // namespace
@@ -151,6 +161,32 @@ void launch_sweep(const Level& lv, double* x, const double* f, const GibbsArg& g
 #undef DISPATCH
 }
 
+void launch_zsweep(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g0,
+                   int direction, const Level* coarse, const double* xc, double alpha, hipStream_t s) {
+    ZSweepArgs a;
+    a.L = lv.L;
+    a.xin = xin;
+    a.xout = xout;
+    a.f = f;
+    a.xc = xc;
+    a.Lc = coarse ? coarse->L : lv.L;
+    a.alpha = alpha;
+    a.S = lv.S;
+    a.G = g0;
+    a.G.colour = (direction == MGMC_FORWARD) ? 0 : 1;
+    a.tz = ZS_TZ;
+    a.ntx = (lv.L.nx / 2) / ZS_XP;
+    a.nty = (lv.L.ny - 1 + ZS_TY - 1) / ZS_TY;
+    a.ntz = (lv.L.nz - 1 + ZS_TZ - 1) / ZS_TZ;
+    const int ntiles = a.ntx * a.nty * a.ntz;
+    const int nb = (ntiles + 7) / 8 * 8;
+    const size_t lds = zsweep_lds_bytes(ZS_XP, ZS_TY);
+    if (coarse)
+        hipLaunchKernelGGL((k_zsweep_rb7<ZS_XP, ZS_TY, ZS_NT, true>), dim3(nb), dim3(ZS_NT), lds, s, a);
+    else
+        hipLaunchKernelGGL((k_zsweep_rb7<ZS_XP, ZS_TY, ZS_NT, false>), dim3(nb), dim3(ZS_NT), lds, s, a);
+}
+
 void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStream_t s) {
     const int dim = lv.spec.dim, np = lv.spec.npoints, nc = lv.spec.ncolours;
     dim3 block(1024), grid(1);
@@ -205,9 +241,27 @@ void launch_pack(const Level& lv, const double* lex, double* pad, bool pack, hip
 }
 
 // ---- the op sequence of one sample (multigridmc_sampler.cc:103-138) ----
-void build_ops_level(mgmc_handle* h, int level, uint32_t& tag) {
+// cur[l] tracks which buffer holds x_l while the ops are generated (z-sweeps ping-pong).
+void push_sweep(mgmc_handle* h, std::vector<int>& cur, int level, int direction, uint32_t& tag, int& pending_prolong) {
+    Op op{OP_SWEEP, level, direction, tag++, 1};
+    const Level& lv = h->levels[level];
+    if (lv.zsweep) {
+        op.src = cur[level];
+        op.prolong = pending_prolong;
+        pending_prolong = 0;
+        cur[level] = 1 - cur[level];
+    } else if (pending_prolong) {
+        h->ops.push_back({OP_PROLONGATE, level, 0, 0, 0});
+        h->ops.back().src = cur[level];
+        pending_prolong = 0;
+    }
+    h->ops.push_back(op);
+}
+
+void build_ops_level(mgmc_handle* h, int level, uint32_t& tag, std::vector<int>& cur) {
     const mgmc_config& c = h->cfg;
     const int nlevel = (int)h->levels.size();
+    int none = 0;
     if (level == nlevel - 1) {
         // coarse sampler: SSORSampler(ncoarsesmooth) = ncoarsesmooth x (fwd SOR sampler, bwd SOR sampler)
         const Level& lv = h->levels[level];
@@ -216,8 +270,10 @@ void build_ops_level(mgmc_handle* h, int level, uint32_t& tag) {
             tag += 2 * c.ncoarsesmooth;
         } else {
             for (int t = 0; t < c.ncoarsesmooth; ++t) {
-                h->ops.push_back({OP_SWEEP, level, MGMC_FORWARD, tag++, 1});
-                h->ops.push_back({OP_SWEEP, level, MGMC_BACKWARD, tag++, 1});
+                Op fw{OP_SWEEP, level, MGMC_FORWARD, tag++, 1};
+                Op bw{OP_SWEEP, level, MGMC_BACKWARD, tag++, 1};
+                h->ops.push_back(fw);
+                h->ops.push_back(bw);
             }
         }
         return;
@@ -226,25 +282,34 @@ void build_ops_level(mgmc_handle* h, int level, uint32_t& tag) {
     for (int jc = 0; jc < cycle_; ++jc) {
         // presampler
         for (int t = 0; t < c.npresmooth; ++t) {
-            if (c.smoother == MGMC_SMOOTHER_SOR) {
-                h->ops.push_back({OP_SWEEP, level, MGMC_FORWARD, tag++, 1});
-            } else {
-                h->ops.push_back({OP_SWEEP, level, MGMC_FORWARD, tag++, 1});
-                h->ops.push_back({OP_SWEEP, level, MGMC_BACKWARD, tag++, 1});
-            }
+            push_sweep(h, cur, level, MGMC_FORWARD, tag, none);
+            if (c.smoother == MGMC_SMOOTHER_SSOR) push_sweep(h, cur, level, MGMC_BACKWARD, tag, none);
         }
         if (level == 0) h->seg_end_pre = h->ops.size();
-        h->ops.push_back({OP_RESIDUAL_RESTRICT, level, 0, 0, 0});
-        build_ops_level(h, level + 1, tag);
-        h->ops.push_back({OP_PROLONGATE, level, 0, 0, 0});
+        Op rr{OP_RESIDUAL_RESTRICT, level, 0, 0, 0};
+        rr.src = cur[level];
+        h->ops.push_back(rr);
+        cur[level + 1] = 0;  // residual_restrict zeroes x_{l+1} (buffer 0)
+        build_ops_level(h, level + 1, tag, cur);
+        if (cur[level + 1] != 0) {  // bring x_{l+1} back to its canonical buffer
+            Op cp{OP_COPY, level + 1, 0, 0, 0};
+            cp.src = cur[level + 1];
+            h->ops.push_back(cp);
+            cur[level + 1] = 0;
+        }
+        int pending_prolong = 1;
         if (level == 0) h->seg_begin_post = h->ops.size();
         for (int t = 0; t < c.npostsmooth; ++t) {
             if (c.smoother == MGMC_SMOOTHER_SOR) {
-                h->ops.push_back({OP_SWEEP, level, MGMC_BACKWARD, tag++, 1});
+                push_sweep(h, cur, level, MGMC_BACKWARD, tag, pending_prolong);
             } else {
-                h->ops.push_back({OP_SWEEP, level, MGMC_FORWARD, tag++, 1});
-                h->ops.push_back({OP_SWEEP, level, MGMC_BACKWARD, tag++, 1});
+                push_sweep(h, cur, level, MGMC_FORWARD, tag, pending_prolong);
+                push_sweep(h, cur, level, MGMC_BACKWARD, tag, pending_prolong);
             }
+        }
+        if (pending_prolong) {  // npostsmooth == 0
+            h->ops.push_back({OP_PROLONGATE, level, 0, 0, 0});
+            h->ops.back().src = cur[level];
         }
         if (level == 0) h->seg_end_post = h->ops.size();
     }
@@ -258,7 +323,13 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
         switch (op.kind) {
             case OP_SWEEP: {
                 GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
-                launch_sweep(lv, lv.x, lv.f, g, op.direction, true, s);
+                if (lv.zsweep) {
+                    const Level* lc = op.prolong ? &h->levels[op.level + 1] : nullptr;
+                    launch_zsweep(lv, lv.buf(op.src), lv.buf(1 - op.src), lv.f, g, op.direction, lc,
+                                  lc ? lc->x : nullptr, h->cfg.coarse_scaling, s);
+                } else {
+                    launch_sweep(lv, lv.x, lv.f, g, op.direction, true, s);
+                }
                 break;
             }
             case OP_COARSE_LDS: {
@@ -268,12 +339,16 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
             }
             case OP_RESIDUAL_RESTRICT: {
                 Level& lc = h->levels[op.level + 1];
-                launch_residual_restrict(lv, lc, lv.x, lv.f, lc.f, lc.x, 1, s);
+                launch_residual_restrict(lv, lc, lv.buf(op.src), lv.f, lc.f, lc.x, 1, s);
                 break;
             }
             case OP_PROLONGATE: {
                 Level& lc = h->levels[op.level + 1];
-                launch_prolongate(lv, lc, lv.x, lc.x, h->cfg.coarse_scaling, s);
+                launch_prolongate(lv, lc, lv.buf(op.src), lc.x, h->cfg.coarse_scaling, s);
+                break;
+            }
+            case OP_COPY: {
+                hipMemcpyAsync(lv.x, lv.buf(op.src), lv.L.nstore * sizeof(double), hipMemcpyDeviceToDevice, s);
                 break;
             }
             case OP_QOI: {
@@ -466,6 +541,17 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         }
         hipMemsetAsync(lv.x, 0, bytes, h->stream);
         hipMemsetAsync(lv.f, 0, bytes, h->stream);
+        // fused z-marching sweep: fine 3D 7-point levels whose row splits into 64-pair tiles
+        lv.zsweep = cfg->dim == 3 && lv.spec.npoints == 7 && l + 1 < specs.size() && (lv.L.nx % (2 * ZS_XP)) == 0 &&
+                    getenv("MGMC_NO_ZSWEEP") == nullptr;
+        if (lv.zsweep) {
+            if (hipMalloc(&lv.x2, bytes) != hipSuccess) {
+                h->levels.push_back(lv);
+                h->last_error = "device allocation failed";
+                return bail(MGMC_E_NOMEM);
+            }
+            hipMemsetAsync(lv.x2, 0, bytes, h->stream);
+        }
         if (l + 1 == specs.size() && 2 * bytes <= lds_limit) lv.lds_bytes = 2 * bytes;
         h->levels.push_back(lv);
     }
@@ -478,7 +564,14 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     hipMemsetAsync(h->mom, 0, 4 * sizeof(double), h->stream);
     // op sequence of one sample
     uint32_t tag = 0;
-    build_ops_level(h, 0, tag);
+    std::vector<int> cur(specs.size(), 0);
+    build_ops_level(h, 0, tag, cur);
+    if (cur[0] != 0) {
+        Op cp{OP_COPY, 0, 0, 0, 0};
+        cp.src = cur[0];
+        h->ops.push_back(cp);
+        h->seg_end_post = h->ops.size();
+    }
     h->ops.push_back({OP_QOI, 0, 0, 0, 0});
     if (specs.size() == 1) {
         h->seg_end_pre = h->seg_begin_post = h->seg_end_post = 0;
@@ -506,6 +599,7 @@ int mgmc_destroy(mgmc_handle* h) {
     destroy_graphs(h);
     for (auto& lv : h->levels) {
         if (lv.x) hipFree(lv.x);
+        if (lv.x2) hipFree(lv.x2);
         if (lv.f) hipFree(lv.f);
         for (auto p : lv.scratch)
             if (p) hipFree(p);
@@ -693,12 +787,19 @@ static int sweep_component(mgmc_handle* h, int level, int direction, int nsweeps
     if ((rc = upload(h, level, b, lv.scratch[0]))) return rc;
     if ((rc = upload(h, level, x, lv.scratch[1]))) return rc;
     HIPCHK(h, hipMemcpyAsync(h->ctrl + 3, &sample, sizeof(sample), hipMemcpyHostToDevice, h->stream));
+    int cur = 1;
     for (int s = 0; s < nsweeps; ++s) {
         GibbsArg g = make_gibbs(h, lv, tag + (uint32_t)s, 0, h->ctrl + 3);
-        launch_sweep(lv, lv.scratch[1], lv.scratch[0], g, direction, noise, h->stream);
+        if (noise && lv.zsweep) {  // the fused z-marching kernel of the V-cycle (out of place)
+            launch_zsweep(lv, lv.scratch[cur], lv.scratch[3 - cur], lv.scratch[0], g, direction, nullptr, nullptr, 0.0,
+                          h->stream);
+            cur = 3 - cur;
+        } else {
+            launch_sweep(lv, lv.scratch[cur], lv.scratch[0], g, direction, noise, h->stream);
+        }
     }
     HIPCHK(h, hipGetLastError());
-    return download(h, level, lv.scratch[1], x);
+    return download(h, level, lv.scratch[cur], x);
 }
 
 int mgmc_smoother_apply(mgmc_handle* h, int level, int direction, int nsweeps, const double* b, double* x) {

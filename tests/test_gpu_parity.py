@@ -46,6 +46,12 @@ CONFIGS = {
     "3d8_1lvl": ((8, 8, 8), dict(nlevel=1)),
     "2d256_global_coarse": ((256, 256), dict(nlevel=2)),
     "3d32_W_ssor": ((32, 32, 32), dict(nlevel=3, cycle=2, smoother="SSOR")),
+    # fused z-marching fine sweep (nx % 128 == 0): ping-pong buffers, prolongation fused into the
+    # first post-sweep, odd sweep counts (copy back), both directions, omega != 1
+    "3d128_zsweep": ((128, 128, 128), dict(nlevel=3)),
+    "3d_aniso_zsweep_ssor": ((256, 128, 64), dict(nlevel=3, smoother="SSOR", npresmooth=2, npostsmooth=1,
+                                                  omega=1.1, coarse_scaling=0.9)),
+    "3d128_zsweep_odd": ((128, 64, 96), dict(nlevel=2, npresmooth=2, npostsmooth=1, ncoarsesmooth=2)),
 }
 
 
@@ -82,7 +88,8 @@ def test_component_kernels_bitwise(hip_device, name):
     s.close()
 
 
-@pytest.mark.parametrize("name", ["2d64_template_W", "3d16", "3d_aniso", "2d_aniso_ssor", "3d64_4lvl"])
+@pytest.mark.parametrize("name", ["2d64_template_W", "3d16", "3d_aniso", "2d_aniso_ssor", "3d64_4lvl",
+                                  "3d128_zsweep", "3d_aniso_zsweep_ssor"])
 def test_multicolour_sweeps_bitwise(hip_device, name):
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)
