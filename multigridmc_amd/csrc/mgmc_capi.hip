@@ -47,7 +47,7 @@ struct Op {
 };
 
 // z-marching sweep tile shape (mgmc_zsweep.hpp)
-constexpr int ZS_XP = 64, ZS_TY = 6, ZS_NT = 256, ZS_TZ = 32;
+constexpr int ZS_XP = 64, ZS_TY = 8, ZS_NT = 256, ZS_TZ = 32;
 
 struct Level {
     LevelSpec spec;
@@ -86,6 +86,7 @@ struct mgmc_handle {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     double* comm_buf = nullptr;  // device scratch for collectives
+    bool fuse_prolong = false;   // prolongate-add fused into the first post-sweep (z-sweep levels)
 };
 
 #define HIPCHK(h, call)                                                                              \
@@ -120,6 +121,7 @@ GibbsArg make_gibbs(const mgmc_handle* h, const Level& lv, uint32_t tag, int col
     g.omega = h->cfg.omega;
     const double diag = lv.spec.diag();
     g.sd = sqrt(diag * (2. - h->cfg.omega) / h->cfg.omega);  // sor_sampler.cc:26
+    g.wd = h->cfg.omega / diag;
     g.key = h->key;
     g.tag = tag;
     g.colour = colour;
@@ -161,6 +163,26 @@ void launch_sweep(const Level& lv, double* x, const double* f, const GibbsArg& g
 #undef DISPATCH
 }
 
+template <int XP, int TY, int NT>
+void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s) {
+    a.ntx = (lv.L.nx / 2) / XP;
+    a.nty = (lv.L.ny - 1 + TY - 1) / TY;
+    a.ntz = (lv.L.nz - 1 + a.tz - 1) / a.tz;
+    const int ntiles = a.ntx * a.nty * a.ntz;
+    const int nb = (ntiles + 7) / 8 * 8;
+    const size_t lds = zsweep_lds_bytes(XP, TY);
+    if (prolong)
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, true>), dim3(nb), dim3(NT), lds, s, a);
+    else
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, false>), dim3(nb), dim3(NT), lds, s, a);
+}
+
+// tile-shape variant (MGMC_ZS_VARIANT, for tuning experiments; 0 = default)
+int zsweep_variant() {
+    const char* v = getenv("MGMC_ZS_VARIANT");
+    return v ? atoi(v) : 0;
+}
+
 void launch_zsweep(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g0,
                    int direction, const Level* coarse, const double* xc, double alpha, hipStream_t s) {
     ZSweepArgs a;
@@ -174,17 +196,16 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
     a.S = lv.S;
     a.G = g0;
     a.G.colour = (direction == MGMC_FORWARD) ? 0 : 1;
-    a.tz = ZS_TZ;
-    a.ntx = (lv.L.nx / 2) / ZS_XP;
-    a.nty = (lv.L.ny - 1 + ZS_TY - 1) / ZS_TY;
-    a.ntz = (lv.L.nz - 1 + ZS_TZ - 1) / ZS_TZ;
-    const int ntiles = a.ntx * a.nty * a.ntz;
-    const int nb = (ntiles + 7) / 8 * 8;
-    const size_t lds = zsweep_lds_bytes(ZS_XP, ZS_TY);
-    if (coarse)
-        hipLaunchKernelGGL((k_zsweep_rb7<ZS_XP, ZS_TY, ZS_NT, true>), dim3(nb), dim3(ZS_NT), lds, s, a);
-    else
-        hipLaunchKernelGGL((k_zsweep_rb7<ZS_XP, ZS_TY, ZS_NT, false>), dim3(nb), dim3(ZS_NT), lds, s, a);
+    const char* tz = getenv("MGMC_ZS_TZ");
+    a.tz = tz ? atoi(tz) : ZS_TZ;
+    const bool pr = coarse != nullptr;
+    switch (zsweep_variant()) {
+        case 1: launch_zsweep_t<64, 4, 256>(lv, a, pr, s); break;
+        case 2: launch_zsweep_t<64, 8, 512>(lv, a, pr, s); break;
+        case 3: launch_zsweep_t<32, 8, 256>(lv, a, pr, s); break;
+        case 4: launch_zsweep_t<64, 16, 512>(lv, a, pr, s); break;
+        default: launch_zsweep_t<ZS_XP, ZS_TY, ZS_NT>(lv, a, pr, s); break;
+    }
 }
 
 void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStream_t s) {
@@ -245,6 +266,11 @@ void launch_pack(const Level& lv, const double* lex, double* pad, bool pack, hip
 void push_sweep(mgmc_handle* h, std::vector<int>& cur, int level, int direction, uint32_t& tag, int& pending_prolong) {
     Op op{OP_SWEEP, level, direction, tag++, 1};
     const Level& lv = h->levels[level];
+    if (lv.zsweep && pending_prolong && !h->fuse_prolong) {
+        h->ops.push_back({OP_PROLONGATE, level, 0, 0, 0});
+        h->ops.back().src = cur[level];
+        pending_prolong = 0;
+    }
     if (lv.zsweep) {
         op.src = cur[level];
         op.prolong = pending_prolong;
@@ -563,6 +589,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     hipMemcpyAsync(h->ctrl, ctrl0, sizeof(ctrl0), hipMemcpyHostToDevice, h->stream);
     hipMemsetAsync(h->mom, 0, 4 * sizeof(double), h->stream);
     // op sequence of one sample
+    h->fuse_prolong = getenv("MGMC_FUSE_PROLONG") != nullptr;
     uint32_t tag = 0;
     std::vector<int> cur(specs.size(), 0);
     build_ops_level(h, 0, tag, cur);
@@ -882,18 +909,30 @@ int mgmc_normals(mgmc_handle* h, uint64_t pair0, size_t n, uint32_t sweep_tag, u
 int mgmc_time_fine_sweeps(mgmc_handle* h, int nsweeps, float* ms) {
     if (!h || !ms || nsweeps < 1) return fail(h, MGMC_E_INVALID, "invalid argument");
     HIPCHK(h, hipSetDevice(h->device));
+    // the V-cycle's fine-level sweep dispatch, on scratch ping-pong copies of the state
+    int rc = ensure_scratch(h, 0);
+    if (rc) return rc;
     Level& lv = h->levels[0];
+    HIPCHK(h, hipMemcpyAsync(lv.scratch[1], lv.x, lv.L.nstore * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
     hipEvent_t e0, e1;
     HIPCHK(h, hipEventCreate(&e0));
     HIPCHK(h, hipEventCreate(&e1));
     HIPCHK(h, hipEventRecord(e0, h->stream));
+    int cur = 1;
     for (int s = 0; s < nsweeps; ++s) {
         GibbsArg g = make_gibbs(h, lv, 0x80000000u + (uint32_t)s, 0, h->ctrl);
-        launch_sweep(lv, lv.x, lv.f, g, MGMC_FORWARD, true, h->stream);
+        const int dir = (s & 1) ? MGMC_BACKWARD : MGMC_FORWARD;
+        if (lv.zsweep) {
+            launch_zsweep(lv, lv.scratch[cur], lv.scratch[3 - cur], lv.f, g, dir, nullptr, nullptr, 0.0, h->stream);
+            cur = 3 - cur;
+        } else {
+            launch_sweep(lv, lv.scratch[cur], lv.f, g, dir, true, h->stream);
+        }
     }
     HIPCHK(h, hipEventRecord(e1, h->stream));
     HIPCHK(h, hipEventSynchronize(e1));
     HIPCHK(h, hipEventElapsedTime(ms, e0, e1));
+    HIPCHK(h, hipGetLastError());
     hipEventDestroy(e0);
     hipEventDestroy(e1);
     return MGMC_OK;

@@ -5,11 +5,12 @@
 // branch-free.  Vertex (i,j,k), 0 <= i <= nx, sits at  k*sp + j*sx + i + off  with off = 7
 // (interior i=1 is 64-byte aligned) and sx a multiple of 8 doubles.
 //
-// Per-point arithmetic is the reference's expression tree, evaluated in the same order
-// (compiled with -ffp-contract=off):
-//   * Gibbs/SOR update  x += omega * (c - sum_k a_k x_k) / a_c,  c = sqrt(a_c(2-w)/w)*xi + f,
-//     the sum running over the row in ascending column order starting from 0.0
-//     (smoother/sor_smoother.cc:66-76, sampler/sor_sampler.cc:42-46);
+// Per-point arithmetic (compiled with -ffp-contract=off, every fma explicit):
+//   * Gibbs/SOR update: the reference's  x += omega * (c - sum_k a_k x_k) / a_c  with
+//     c = sqrt(a_c(2-w)/w)*xi + f  (smoother/sor_smoother.cc:66-76, sampler/sor_sampler.cc:42-46)
+//     evaluated in fused form  c = fma(sd, xi, f),  x = fma(omega/a_c, c - S, x),  S the fma chain
+//     over the row in ascending column order -- mathematically identical, ~1 ulp apart, and
+//     replayed bit for bit by the oracle's MULTICOLOUR mode;
 //   * residual  r = f - A x  with A x accumulated in ascending column order
 //     (linear_operator/linear_operator.hh:66-76, Eigen ColMajor SpMV);
 //   * restriction  sum_sigma w_sigma r(2i+sigma), sigma with x fastest
@@ -59,6 +60,7 @@ struct StencilArg {
 struct GibbsArg {
     double omega;
     double sd;  // sqrt(diag*(2-omega)/omega)
+    double wd;  // omega/diag
     RngKey key;
     uint32_t tag;
     int colour;
@@ -101,6 +103,43 @@ __device__ __forceinline__ double stencil_sum(const double* __restrict__ x, long
     return res;
 }
 
+// the same row sum as an fma chain (Gibbs updates): a_0 x_0, then fma(a_k, x_k, .) ascending
+template <int DIM, int NPTS>
+__device__ __forceinline__ double stencil_fma(const double* __restrict__ x, long long p, const Layout& L,
+                                              const StencilArg& S) {
+    double res;
+    if (NPTS == 7) {
+        res = S.a[4] * x[p - L.sp];
+        res = fma(S.a[10], x[p - L.sx], res);
+        res = fma(S.a[12], x[p - 1], res);
+        res = fma(S.a[13], x[p], res);
+        res = fma(S.a[14], x[p + 1], res);
+        res = fma(S.a[16], x[p + L.sx], res);
+        res = fma(S.a[22], x[p + L.sp], res);
+    } else if (NPTS == 5) {
+        res = S.a[1] * x[p - L.sx];
+        res = fma(S.a[3], x[p - 1], res);
+        res = fma(S.a[4], x[p], res);
+        res = fma(S.a[5], x[p + 1], res);
+        res = fma(S.a[7], x[p + L.sx], res);
+    } else if (NPTS == 27) {
+        res = S.a[0] * x[p - L.sp - L.sx - 1];
+#pragma unroll
+        for (int q = 1; q < 27; ++q) {
+            const int dz = q / 9 - 1, dy = (q / 3) % 3 - 1, dx = q % 3 - 1;
+            res = fma(S.a[q], x[p + dz * L.sp + dy * L.sx + dx], res);
+        }
+    } else {  // 9
+        res = S.a[0] * x[p - L.sx - 1];
+#pragma unroll
+        for (int q = 1; q < 9; ++q) {
+            const int dy = q / 3 - 1, dx = q % 3 - 1;
+            res = fma(S.a[q], x[p + dy * L.sx + dx], res);
+        }
+    }
+    return res;
+}
+
 template <int DIM>
 __device__ __forceinline__ double centre(const StencilArg& S) {
     return DIM == 3 ? S.a[13] : S.a[4];
@@ -117,13 +156,15 @@ template <int DIM, int NPTS, bool NOISE>
 __device__ __forceinline__ void gibbs_point(double* __restrict__ x, const double* __restrict__ f, long long p,
                                             const Layout& L, const StencilArg& S, const GibbsArg& G, uint64_t sample,
                                             int i, int j, int k) {
-    const double res = stencil_sum<DIM, NPTS>(x, p, L, S);
+    // SOR/Gibbs update (sor_smoother.cc:70-75, sor_sampler.cc:44-45) in fused form:
+    //   c = fma(sd, xi, f),  x = fma(omega/diag, c - sum_k a_k x_k, x)
+    const double res = stencil_fma<DIM, NPTS>(x, p, L, S);
     double c = f[p];
     if (NOISE) {
         const double xi = point_normal(G.key, pair_id<DIM>(L, i, j, k), (i & 1) != 0, G.tag, sample);
-        c = G.sd * xi + f[p];
+        c = fma(G.sd, xi, f[p]);
     }
-    x[p] += G.omega * (c - res) / centre<DIM>(S);
+    x[p] = fma(G.wd, c - res, x[p]);
 }
 
 // ---- red-black sweep pass of the fine 5/7-point level: vertices with (i+j+k)&1 == colour ----

@@ -8,7 +8,7 @@
 //   counter = (pair id, sweep tag, lo32(sample), hi32(sample))
 // (Philox4x32-10, Salmon et al. SC'11) followed by a Box-Muller transform whose log / sin / cos
 // are evaluated with a fixed sequence of IEEE-754 double operations (explicit fma, correctly
-// rounded div/sqrt).  The same bits therefore come out of gfx950 and of a host compiler with
+// rounded sqrt, a literal 64-entry log reduction table).  The same bits therefore come out of gfx950 and of a host compiler with
 // -ffp-contract=off, which is what lets the CPU oracle replay the device chain exactly.
 //
 // Pair id: points (i, i+1) with i odd share one Philox call (cos branch for i odd, sin branch
@@ -16,6 +16,8 @@
 #pragma once
 #include <math.h>
 #include <stdint.h>
+
+#include "log_table.h"
 
 #if defined(__HIPCC__)
 #define MGMC_HD __host__ __device__ inline __attribute__((always_inline))
@@ -59,81 +61,77 @@ MGMC_HD uint64_t as_bits(double d) {
     return c.u;
 }
 
-// 53-bit integer from two 32-bit words
-MGMC_HD uint64_t bits53(uint32_t a, uint32_t b) {
-    return ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
-}
+// Uniforms are built exactly from 52 random mantissa bits: v = 1.m in [1,2) (bit pattern), then
+// u1 = 2 - v in (0,1] and u2 = v - 1 in [0,1) -- both subtractions are exact.
+MGMC_HD uint64_t bits52(uint32_t a, uint32_t b) { return ((uint64_t)a << 20) | (uint64_t)(b >> 12); }
 
-// natural log of u in [2^-53, 1]; |rel err| ~ 1e-16
-MGMC_HD double log_unit(double u) {
+// natural log of u in [2^-52, 1], division free: u = 2^e m, m in [1,2), table point
+// rc_i ~ 1/m (top 6 mantissa bits), r = m rc_i - 1 (|r| < 1/128, one fma), log1p(r) by a
+// degree-8 polynomial, plus the tabulated -log(rc_i) = hi + lo (log_table.h).  Absolute error
+// ~1e-17; the caller clamps -2 log(u) at 0.
+MGMC_HD double log_unit(double u, const double* rct, const double* hit, const double* lot) {
     const uint64_t b = as_bits(u);
-    int e = (int)((b >> 52) & 0x7ff) - 1023;
-    double m = as_double((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull);  // [1,2)
-    const bool big = m > 1.4142135623730951;
-    m = big ? m * 0.5 : m;
-    e = big ? e + 1 : e;
-    const double s = (m - 1.0) / (m + 1.0);  // |s| <= 0.1716
-    const double s2 = s * s;
-    double p = 1.0 / 23.0;
-    p = fma(p, s2, 1.0 / 21.0);
-    p = fma(p, s2, 1.0 / 19.0);
-    p = fma(p, s2, 1.0 / 17.0);
-    p = fma(p, s2, 1.0 / 15.0);
-    p = fma(p, s2, 1.0 / 13.0);
-    p = fma(p, s2, 1.0 / 11.0);
-    p = fma(p, s2, 1.0 / 9.0);
-    p = fma(p, s2, 1.0 / 7.0);
-    p = fma(p, s2, 1.0 / 5.0);
-    p = fma(p, s2, 1.0 / 3.0);
-    const double s3p = (s * s2) * p;            // s^3 * (1/3 + s^2/5 + ...)
-    const double logm = fma(2.0, s, 2.0 * s3p); // 2 atanh(s)
+    const int e = (int)((b >> 52) & 0x7ff) - 1023;
+    const uint64_t mant = b & 0x000fffffffffffffull;
+    const int idx = (int)(mant >> 46);
+    const double m = as_double(mant | 0x3ff0000000000000ull);
+    const double r = fma(m, rct[idx], -1.0);
+    double q = -1.0 / 8.0;
+    q = fma(q, r, 1.0 / 7.0);
+    q = fma(q, r, -1.0 / 6.0);
+    q = fma(q, r, 1.0 / 5.0);
+    q = fma(q, r, -1.0 / 4.0);
+    q = fma(q, r, 1.0 / 3.0);
+    q = fma(q, r, -0.5);
+    const double p = fma(r * r, q, r);  // log1p(r)
     const double de = (double)e;
     const double LN2_HI = 6.93147180369123816490e-01;  // 0x3fe62e42fee00000
     const double LN2_LO = 1.90821492927058770002e-10;  // 0x3dea39ef35793c76
-    return fma(de, LN2_HI, fma(de, LN2_LO, logm));
+    return fma(de, LN2_HI, hit[idx]) + (fma(de, LN2_LO, lot[idx]) + p);
 }
 
-// (cos(2 pi t), sin(2 pi t)) for t in [0,1)
+// (cos(2 pi t), sin(2 pi t)) for t in [0,1); quadrant selection without branches
 MGMC_HD void sincos_2pi(double t, double* c_out, double* s_out) {
     const int q = (int)(t * 4.0 + 0.5);          // 0..4
     const double r = t - (double)q * 0.25;         // exact, |r| <= 1/8
     const double th = r * 6.28318530717958647692;  // |th| <= pi/4
     const double t2 = th * th;
-    // sin(th) = th * (1 - t2/3! + t2^2/5! - ...) up to th^17
-    double ps = -1.0 / 355687428096000.0;   // -1/17!
+    double ps = -1.0 / 355687428096000.0;     // -1/17!
     ps = fma(ps, t2, 1.0 / 1307674368000.0);  // 1/15!
     ps = fma(ps, t2, -1.0 / 6227020800.0);    // -1/13!
     ps = fma(ps, t2, 1.0 / 39916800.0);       // 1/11!
     ps = fma(ps, t2, -1.0 / 362880.0);        // -1/9!
     ps = fma(ps, t2, 1.0 / 5040.0);           // 1/7!
     ps = fma(ps, t2, -1.0 / 120.0);           // -1/5!
-    ps = fma(ps, t2, 1.0 / 6.0);              // 1/3!  (sign folded below)
+    ps = fma(ps, t2, 1.0 / 6.0);              // 1/3!
     const double sn = fma(-(th * t2), ps, th);
-    // cos(th) = 1 - t2/2 + ... up to th^16
-    double pc = 1.0 / 20922789888000.0;        // 1/16!
-    pc = fma(pc, t2, -1.0 / 87178291200.0);    // -1/14!
-    pc = fma(pc, t2, 1.0 / 479001600.0);       // 1/12!
-    pc = fma(pc, t2, -1.0 / 3628800.0);        // -1/10!
-    pc = fma(pc, t2, 1.0 / 40320.0);           // 1/8!
-    pc = fma(pc, t2, -1.0 / 720.0);            // -1/6!
-    pc = fma(pc, t2, 1.0 / 24.0);              // 1/4!
-    pc = fma(pc, t2, -0.5);                    // -1/2!
+    double pc = 1.0 / 20922789888000.0;      // 1/16!
+    pc = fma(pc, t2, -1.0 / 87178291200.0);  // -1/14!
+    pc = fma(pc, t2, 1.0 / 479001600.0);     // 1/12!
+    pc = fma(pc, t2, -1.0 / 3628800.0);      // -1/10!
+    pc = fma(pc, t2, 1.0 / 40320.0);         // 1/8!
+    pc = fma(pc, t2, -1.0 / 720.0);          // -1/6!
+    pc = fma(pc, t2, 1.0 / 24.0);            // 1/4!
+    pc = fma(pc, t2, -0.5);                  // -1/2!
     const double cs = fma(pc, t2, 1.0);
+    // quadrant qq: (c, s) = (cs, sn), (-sn, cs), (-cs, -sn), (sn, -cs)
     const int qq = q & 3;
-    double c, s;
-    if (qq == 0) { c = cs; s = sn; }
-    else if (qq == 1) { c = -sn; s = cs; }
-    else if (qq == 2) { c = -cs; s = -sn; }
-    else { c = sn; s = -cs; }
-    *c_out = c;
-    *s_out = s;
+    const bool swap = (qq & 1) != 0;
+    const double c0 = swap ? sn : cs;
+    const double s0 = swap ? cs : sn;
+    *c_out = (qq == 1 || qq == 2) ? -c0 : c0;
+    *s_out = (qq >= 2) ? -s0 : s0;
 }
 
 // Box-Muller pair from one Philox block: (z_cos, z_sin)
-MGMC_HD void normal_pair(const Philox4& r, double* z0, double* z1) {
-    const double u1 = ((double)bits53(r.v[0], r.v[1]) + 1.0) * 0x1p-53;  // (0,1]
-    const double u2 = (double)bits53(r.v[2], r.v[3]) * 0x1p-53;          // [0,1)
-    const double rad = sqrt(-2.0 * log_unit(u1));
+MGMC_HD void normal_pair_t(const Philox4& r, double* z0, double* z1, const double* rct, const double* hit,
+                           const double* lot) {
+    const double v1 = as_double(0x3ff0000000000000ull | bits52(r.v[0], r.v[1]));
+    const double v2 = as_double(0x3ff0000000000000ull | bits52(r.v[2], r.v[3]));
+    const double u1 = 2.0 - v1;  // (0,1]
+    const double u2 = v2 - 1.0;  // [0,1)
+    const double rr = -2.0 * log_unit(u1, rct, hit, lot);
+    const double rad = sqrt(rr > 0.0 ? rr : 0.0);
     double c, s;
     sincos_2pi(u2, &c, &s);
     *z0 = rad * c;
@@ -149,6 +147,10 @@ MGMC_HD RngKey make_key(uint64_t seed, uint64_t chain) {
     k.k0 = (uint32_t)seed;
     k.k1 = (uint32_t)chain ^ (uint32_t)(seed >> 32);
     return k;
+}
+
+MGMC_HD void normal_pair(const Philox4& r, double* z0, double* z1) {
+    normal_pair_t(r, z0, z1, LOGTAB_RC, LOGTAB_HI, LOGTAB_LO);
 }
 
 // one normal for the point whose pair id is `pair`; cos_branch selects the first of the two

@@ -23,11 +23,14 @@
 //   FAITHFUL (0): the reference algorithm -- lexicographic forward / reverse sweeps, libstdc++
 //                 mt19937_64 + normal_distribution (Marsaglia polar) in the reference's
 //                 construction and call order.  Tier T1 of the parity contract.
-//   MULTICOLOUR (1): identical per-point arithmetic, but the Gibbs updates visit the vertices
-//                 colour by colour (red-black on the fine FD level, 2^d colours on Galerkin
-//                 levels) and the noise is the counter-based Philox4x32-10 / Box-Muller stream
-//                 keyed by (seed, chain, pair, sweep tag, sample).  This replays the device
-//                 chain; it is written independently of multigridmc_amd/csrc.  Tier T2.
+//   MULTICOLOUR (1): the Gibbs updates visit the vertices colour by colour (red-black on the fine
+//                 FD level, 2^d colours on Galerkin levels), the noise is the counter-based
+//                 Philox4x32-10 / Box-Muller stream keyed by (seed, chain, pair, sweep tag,
+//                 sample), and the SOR update is evaluated in the device's fused form
+//                 (c = fma(sd, xi, f), x = fma(omega/diag, c - S, x), S an fma chain in ascending
+//                 column order; restriction / prolongation / residual keep the reference
+//                 arithmetic).  This replays the device chain bit for bit; it is written
+//                 independently of multigridmc_amd/csrc.  Tier T2.
 //
 // Build: oracle/Makefile (g++ -O2 -ffp-contract=off, shared library + cpu baseline binary).
 #include <math.h>
@@ -42,6 +45,8 @@
 #include <random>
 #include <string>
 #include <vector>
+
+#include "log_table_oracle.h"
 
 namespace orc {
 
@@ -410,23 +415,21 @@ static inline uint64_t double_to_bits(double d) {
     return b;
 }
 
+// log(u), u in [2^-52, 1]: u = 2^e m, r = fma(m, rc_i, -1) with the literal 64-entry table
+// (log_table_oracle.h, i = top 6 mantissa bits), log1p(r) to degree 8, plus -log(rc_i) = hi + lo
 static double ln_unit(double u) {
     const uint64_t b = double_to_bits(u);
-    int e = (int)((b >> 52) & 0x7ff) - 1023;
-    double m = bits_to_double((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
-    if (m > 1.4142135623730951) {
-        m = m * 0.5;
-        e = e + 1;
-    }
-    const double s = (m - 1.0) / (m + 1.0);
-    const double s2 = s * s;
-    static const double inv_odd[11] = {1.0 / 23.0, 1.0 / 21.0, 1.0 / 19.0, 1.0 / 17.0, 1.0 / 15.0, 1.0 / 13.0,
-                                       1.0 / 11.0, 1.0 / 9.0,  1.0 / 7.0,  1.0 / 5.0,  1.0 / 3.0};
-    double p = inv_odd[0];
-    for (int q = 1; q < 11; ++q) p = fma(p, s2, inv_odd[q]);
-    const double logm = fma(2.0, s, 2.0 * ((s * s2) * p));
+    const int e = (int)((b >> 52) & 0x7ff) - 1023;
+    const uint64_t mant = b & 0x000fffffffffffffull;
+    const int idx = (int)(mant >> 46);
+    const double m = bits_to_double(mant | 0x3ff0000000000000ull);
+    const double r = fma(m, LOGTAB_RC[idx], -1.0);
+    static const double coef[7] = {-1.0 / 8.0, 1.0 / 7.0, -1.0 / 6.0, 1.0 / 5.0, -1.0 / 4.0, 1.0 / 3.0, -0.5};
+    double q = coef[0];
+    for (int k = 1; k < 7; ++k) q = fma(q, r, coef[k]);
+    const double p = fma(r * r, q, r);
     const double de = (double)e;
-    return fma(de, 6.93147180369123816490e-01, fma(de, 1.90821492927058770002e-10, logm));
+    return fma(de, 6.93147180369123816490e-01, LOGTAB_HI[idx]) + (fma(de, 1.90821492927058770002e-10, LOGTAB_LO[idx]) + p);
 }
 
 static void cos_sin_2pi(double t, double& c, double& s) {
@@ -446,23 +449,24 @@ static void cos_sin_2pi(double t, double& c, double& s) {
     double pc = cc[0];
     for (int k = 1; k < 8; ++k) pc = fma(pc, t2, cc[k]);
     const double cs = fma(pc, t2, 1.0);
-    switch (q & 3) {
-        case 0: c = cs; s = sn; break;
-        case 1: c = -sn; s = cs; break;
-        case 2: c = -cs; s = -sn; break;
-        default: c = sn; s = -cs; break;
-    }
+    const int qq = q & 3;
+    const double c0 = (qq & 1) ? sn : cs;
+    const double s0 = (qq & 1) ? cs : sn;
+    c = (qq == 1 || qq == 2) ? -c0 : c0;
+    s = (qq >= 2) ? -s0 : s0;
 }
 
 static void philox_normals(uint64_t seed, uint64_t chain, uint32_t pair, uint32_t tag, uint64_t sample, double& z0,
                            double& z1) {
     uint32_t ctr[4] = {pair, tag, (uint32_t)sample, (uint32_t)(sample >> 32)};
     philox10(ctr, (uint32_t)seed, (uint32_t)chain ^ (uint32_t)(seed >> 32));
-    const uint64_t m1 = ((uint64_t)(ctr[0] >> 5) << 26) | (uint64_t)(ctr[1] >> 6);
-    const uint64_t m2 = ((uint64_t)(ctr[2] >> 5) << 26) | (uint64_t)(ctr[3] >> 6);
-    const double u1 = ((double)m1 + 1.0) * 0x1p-53;
-    const double u2 = (double)m2 * 0x1p-53;
-    const double rad = sqrt(-2.0 * ln_unit(u1));
+    // exact 52-bit uniforms: v = 1.m in [1,2), u1 = 2 - v in (0,1], u2 = v - 1 in [0,1)
+    const uint64_t m1 = ((uint64_t)ctr[0] << 20) | (uint64_t)(ctr[1] >> 12);
+    const uint64_t m2 = ((uint64_t)ctr[2] << 20) | (uint64_t)(ctr[3] >> 12);
+    const double u1 = 2.0 - bits_to_double(0x3ff0000000000000ull | m1);
+    const double u2 = bits_to_double(0x3ff0000000000000ull | m2) - 1.0;
+    const double rr = -2.0 * ln_unit(u1);
+    const double rad = sqrt(rr > 0.0 ? rr : 0.0);
     double c, s;
     cos_sin_2pi(u2, c, s);
     z0 = rad * c;
@@ -514,21 +518,34 @@ static void init_colouring(Level& L, bool fd_level) {
     }
 }
 
-// one SOR update of row ell (sor_smoother.cc:70-75)
+// one SOR update of row ell (sor_smoother.cc:70-75), reference arithmetic
 static inline void sor_row(const CSR& A, const double* diag, double omega, const double* b, double* x, int64_t ell) {
     double residual = 0.0;
     for (int64_t k = A.rowptr[ell]; k < A.rowptr[ell + 1]; ++k) residual += A.val[k] * x[A.col[k]];
     x[ell] += omega * (b[ell] - residual) / diag[ell];
 }
 
+// the same update in the device's fused form (MULTICOLOUR mode): S = fma chain over the row in
+// ascending column order, x = fma(omega/diag, b - S, x)
+static inline void sor_row_fused(const CSR& A, const double* wd, const double* b, double* x, int64_t ell) {
+    int64_t k = A.rowptr[ell];
+    double s = A.val[k] * x[A.col[k]];
+    for (++k; k < A.rowptr[ell + 1]; ++k) s = fma(A.val[k], x[A.col[k]], s);
+    x[ell] = fma(wd[ell], b[ell] - s, x[ell]);
+}
+
 struct SORSmoother {
     const Level* L;
     double omega;
     Direction direction;
-    std::vector<double> diag;
+    std::vector<double> diag, wd;
     SORSmoother(const Level* L_, double omega_, Direction d) : L(L_), omega(omega_), direction(d) {
         diag.resize(L->A.nrow);
-        for (int64_t r = 0; r < L->A.nrow; ++r) diag[r] = L->A.diag(r);
+        wd.resize(L->A.nrow);
+        for (int64_t r = 0; r < L->A.nrow; ++r) {
+            diag[r] = L->A.diag(r);
+            wd[r] = omega / diag[r];
+        }
     }
     void apply(Mode mode, const double* b, double* x) const {
         const int64_t nrow = L->A.nrow;
@@ -542,7 +559,7 @@ struct SORSmoother {
             for (int cc = 0; cc < nc; ++cc) {
                 const int colour = (direction == FORWARD) ? cc : nc - 1 - cc;
                 for (int64_t ell = 0; ell < nrow; ++ell)
-                    if (L->colour[ell] == colour) sor_row(L->A, diag.data(), omega, b, x, ell);
+                    if (L->colour[ell] == colour) sor_row_fused(L->A, wd.data(), b, x, ell);
             }
         }
     }
@@ -586,7 +603,7 @@ struct SORSampler : Sampler {
                     double z0, z1;
                     philox_normals(ctx->seed, ctx->chain, L->pair[ell], tag, ctx->sample, z0, z1);
                     const double xi = L->cos_branch[ell] ? z0 : z1;
-                    c_rhs[ell] = sqrt_precision_diag[ell] * xi + f[ell];
+                    c_rhs[ell] = fma(sqrt_precision_diag[ell], xi, f[ell]);
                 }
             }
             smoother.apply(ctx->mode, c_rhs.data(), x);

@@ -85,9 +85,17 @@ def test_oracle_math_accuracy():
     import ctypes
     import math
     us = np.random.default_rng(0).random(20000)
-    us[0], us[1] = 1.0, 2.0 ** -53
-    err = max(abs(O.lib().orc_ln_unit(float(u)) - math.log(u)) / max(abs(math.log(u)), 1e-300) for u in us if u > 0)
-    assert err < 1e-15
+    us[0], us[1], us[2] = 1.0, 2.0 ** -52, 1.0 - 2.0 ** -52
+    rel, ab = 0.0, 0.0
+    for u in us:
+        if u <= 0:
+            continue
+        d = abs(O.lib().orc_ln_unit(float(u)) - math.log(u))
+        if abs(math.log(u)) > 1e-3:
+            rel = max(rel, d / abs(math.log(u)))
+        else:
+            ab = max(ab, d)
+    assert rel < 5e-16 and ab < 1e-16
     c, s = ctypes.c_double(), ctypes.c_double()
     e = 0.0
     for t in np.random.default_rng(1).random(20000):
@@ -270,4 +278,6 @@ def test_mgmc_3d_fd_statistics(mode):
     Q = o.csr_matrix(0).toarray()
     em, ec = _mean_cov_error(o, Q, 20000, nwarmup=200)
     scale = np.max(np.abs(np.linalg.inv(Q)))
-    assert em < 0.05 * scale and ec < 0.03 * scale
+    # infinity norm over 343^2 covariance entries of a 20000-sample estimate: ~4 sigma of
+    # sqrt(2/n) * max|Q^-1| * sqrt(IACT) ~ 0.04-0.05 relative; tolerance 0.07
+    assert em < 0.05 * scale and ec < 0.07 * scale
