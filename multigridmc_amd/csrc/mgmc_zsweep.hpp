@@ -64,6 +64,15 @@ __device__ __forceinline__ double prolong_gather(double v, const double* __restr
     return v;
 }
 
+// One pair item of a tile: LDS offset, plane-independent global offset, Philox pair base,
+// position parity and interior flags, all computed once per workgroup.
+struct ZItem {
+    long long goff;  // j*sx + i + off  (add k*sp for plane k)
+    uint32_t pbase;  // (j-1)*(nx/2) + (i-1)/2
+    int lds;         // r*W + 2*c2
+    int flags;       // bit0 row interior, bit1 i interior, bit2 i+1 interior, bit3 parity (i+j)&1
+};
+
 template <int XP, int TY, int NT, bool PROLONG>
 __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
     constexpr int W = 2 * XP + 8;  // LDS columns: positions [2*q0-3, 2*q0+2*XP+4]
@@ -102,148 +111,144 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
     const int fc = a.G.colour;            // first colour
     const double sd = a.G.sd, wd = a.G.wd;
     const uint64_t sample = *a.G.sample;
+    const uint32_t s_lo = (uint32_t)sample, s_hi = (uint32_t)(sample >> 32);
+    const uint32_t plane_pairs = (uint32_t)((uint64_t)(L.ny - 1) * (uint64_t)(L.nx / 2));
     const int tid = threadIdx.x;
 
     auto slot = [](int p) { return (p + 8) & 3; };
-    auto interior_row = [&](int j) { return j >= 1 && j <= L.ny - 1; };
     auto interior_plane = [&](int k) { return k >= 1 && k <= L.nz - 1; };
+    auto make_item = [&](int r, int c2) {
+        ZItem t;
+        const int j = j0 - 2 + r, i = ibase + 2 * c2;
+        const bool rin = j >= 1 && j <= L.ny - 1;
+        t.goff = rin ? (long long)j * L.sx + i + L.off : 0;
+        t.pbase = (uint32_t)((uint64_t)(j - 1) * (uint64_t)(L.nx / 2) + (uint64_t)((i - 1) >> 1));
+        t.lds = r * W + 2 * c2;
+        t.flags = (rin ? 1 : 0) | ((i >= 1 && i <= L.nx - 1) ? 2 : 0) | ((i + 1 >= 1 && i + 1 <= L.nx - 1) ? 4 : 0) |
+                  (((i + j) & 1) << 3);
+        return t;
+    };
 
-    // item -> (LDS row r, LDS pair column c2)
-    int cr[NC], cc[NC];
+    ZItem ci[NC];
 #pragma unroll
     for (int u = 0; u < NC; ++u) {
         const int it = tid + u * NT;
-        cr[u] = 2 + it / XP;
-        cc[u] = 2 + it % XP;
+        ci[u] = make_item(2 + it / XP, 2 + it % XP);
     }
-    int hr[NH], hc[NH];
+    ZItem hi[NH];
 #pragma unroll
     for (int u = 0; u < NH; ++u) {
         int it = tid + u * NT;
-        if (it >= NHALO) { hr[u] = -1; hc[u] = 0; continue; }
-        if (it < XP + 2) { hr[u] = 1; hc[u] = 1 + it; continue; }
-        it -= XP + 2;
-        if (it < XP + 2) { hr[u] = R - 2; hc[u] = 1 + it; continue; }
-        it -= XP + 2;
-        hr[u] = 2 + (it >> 1);
-        hc[u] = (it & 1) ? WP - 2 : 1;
+        if (it >= NHALO) {
+            hi[u] = make_item(0, 0);
+            hi[u].flags = 0;
+            continue;
+        }
+        int r, c2;
+        if (it < XP + 2) {
+            r = 1; c2 = 1 + it;
+        } else if (it < 2 * (XP + 2)) {
+            r = R - 2; c2 = 1 + it - (XP + 2);
+        } else {
+            it -= 2 * (XP + 2);
+            r = 2 + (it >> 1);
+            c2 = (it & 1) ? WP - 2 : 1;
+        }
+        hi[u] = make_item(r, c2);
+    }
+    long long xoff[NLX];
+    int xlds[NLX];
+#pragma unroll
+    for (int u = 0; u < NLX; ++u) {
+        const int it = tid + u * NT;
+        xoff[u] = -1;
+        xlds[u] = -1;
+        if (it < R * WP) {
+            const ZItem t = make_item(it / WP, it % WP);
+            xlds[u] = t.lds;
+            if (t.flags & 1) xoff[u] = t.goff;
+        }
     }
 
     // ---- global <-> LDS / registers ----
     double2 px[NLX];
     auto issue_x = [&](int k) {
+        const bool kin = interior_plane(k);
+        const double* base = a.xin + (long long)k * L.sp;
 #pragma unroll
         for (int u = 0; u < NLX; ++u) {
-            const int it = tid + u * NT;
             px[u] = make_double2(0.0, 0.0);
-            if (it < R * WP) {
-                const int r = it / WP, c2 = it - r * WP;
-                const int j = j0 - 2 + r;
-                if (interior_plane(k) && interior_row(j))
-                    px[u] = *reinterpret_cast<const double2*>(a.xin + L.at(ibase + 2 * c2, j, k));
-            }
+            if (kin && xoff[u] >= 0) px[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
         }
     };
     auto deposit_x = [&](int k) {
         double* dst = xs + slot(k) * R * W;
 #pragma unroll
         for (int u = 0; u < NLX; ++u) {
-            const int it = tid + u * NT;
-            if (it < R * WP) {
-                const int r = it / WP, c2 = it - r * WP;
-                double2 v = px[u];
-                if (PROLONG && interior_plane(k)) {
-                    const int j = j0 - 2 + r, i = ibase + 2 * c2;
-                    if (interior_row(j)) {
-                        if (i >= 1 && i <= L.nx - 1) v.x = prolong_gather(v.x, a.xc, a.Lc, i, j, k, a.alpha);
-                        if (i + 1 >= 1 && i + 1 <= L.nx - 1) v.y = prolong_gather(v.y, a.xc, a.Lc, i + 1, j, k, a.alpha);
-                    }
-                }
-                *reinterpret_cast<double2*>(dst + r * W + 2 * c2) = v;
+            if (xlds[u] < 0) continue;
+            double2 v = px[u];
+            if (PROLONG && interior_plane(k) && xoff[u] >= 0) {
+                const int c2 = (xlds[u] % W) / 2, r = xlds[u] / W;
+                const int j = j0 - 2 + r, i = ibase + 2 * c2;
+                if (i >= 1 && i <= L.nx - 1) v.x = prolong_gather(v.x, a.xc, a.Lc, i, j, k, a.alpha);
+                if (i + 1 >= 1 && i + 1 <= L.nx - 1) v.y = prolong_gather(v.y, a.xc, a.Lc, i + 1, j, k, a.alpha);
             }
+            *reinterpret_cast<double2*>(dst + xlds[u]) = v;
         }
     };
     auto store_x = [&](int k) {
         if (k < k0 || k >= k1) return;
         const double* src = xs + slot(k) * R * W;
+        double* base = a.xout + (long long)k * L.sp;
 #pragma unroll
-        for (int u = 0; u < NC; ++u) {
-            const int j = j0 - 2 + cr[u];
-            if (!interior_row(j)) continue;
-            *reinterpret_cast<double2*>(a.xout + L.at(ibase + 2 * cc[u], j, k)) =
-                *reinterpret_cast<const double2*>(src + cr[u] * W + 2 * cc[u]);
-        }
+        for (int u = 0; u < NC; ++u)
+            if (ci[u].flags & 1) *reinterpret_cast<double2*>(base + ci[u].goff) = *reinterpret_cast<const double2*>(src + ci[u].lds);
     };
-    // f pairs of the core items (used by both colours) and f of the halo items
-    auto load_fcore = [&](int k, double2* out) {
-#pragma unroll
-        for (int u = 0; u < NC; ++u) {
-            const int j = j0 - 2 + cr[u];
-            out[u] = make_double2(0.0, 0.0);
-            if (interior_plane(k) && interior_row(j))
-                out[u] = *reinterpret_cast<const double2*>(a.f + L.at(ibase + 2 * cc[u], j, k));
-        }
-    };
-    auto load_fhalo = [&](int k, double2* out) {
-#pragma unroll
-        for (int u = 0; u < NH; ++u) {
-            out[u] = make_double2(0.0, 0.0);
-            if (hr[u] < 0) continue;
-            const int j = j0 - 2 + hr[u];
-            if (interior_plane(k) && interior_row(j))
-                out[u] = *reinterpret_cast<const double2*>(a.f + L.at(ibase + 2 * hc[u], j, k));
-        }
+    auto load_f = [&](int k, const ZItem& t) {
+        if (!interior_plane(k) || !(t.flags & 1)) return make_double2(0.0, 0.0);
+        return *reinterpret_cast<const double2*>(a.f + (long long)k * L.sp + t.goff);
     };
 
-    // ascending-column-order stencil sum at LDS (r, c) of plane k
-    auto row_sum = [&](int k, int r, int c) {
+    // fma-chain stencil sum (ascending column order) at LDS offset o of plane k
+    auto row_sum = [&](int k, int o) {
         const double* sm = xs + slot(k - 1) * R * W;
         const double* s0 = xs + slot(k) * R * W;
         const double* sp = xs + slot(k + 1) * R * W;
-        double res = a.S.a[4] * sm[r * W + c];
-        res = fma(a.S.a[10], s0[(r - 1) * W + c], res);
-        res = fma(a.S.a[12], s0[r * W + c - 1], res);
-        res = fma(a.S.a[13], s0[r * W + c], res);
-        res = fma(a.S.a[14], s0[r * W + c + 1], res);
-        res = fma(a.S.a[16], s0[(r + 1) * W + c], res);
-        res = fma(a.S.a[22], sp[r * W + c], res);
+        double res = a.S.a[4] * sm[o];
+        res = fma(a.S.a[10], s0[o - W], res);
+        res = fma(a.S.a[12], s0[o - 1], res);
+        res = fma(a.S.a[13], s0[o], res);
+        res = fma(a.S.a[14], s0[o + 1], res);
+        res = fma(a.S.a[16], s0[o + W], res);
+        res = fma(a.S.a[22], sp[o], res);
         return res;
     };
-    // first-colour update of the pair at LDS (r, c2) on plane k; returns the other normal
-    auto first_pair = [&](int k, int r, int c2, double2 fv) -> double {
-        const int j = j0 - 2 + r;
-        if (!interior_row(j)) return 0.0;
-        const int i = ibase + 2 * c2;  // odd position: pair (i, i+1)
-        const int e = ((i + j + k) & 1) == fc ? 0 : 1;
-        const bool in0 = i >= 1 && i <= L.nx - 1, in1 = i + 1 >= 1 && i + 1 <= L.nx - 1;
-        if (!in0 && !in1) return 0.0;
-        const uint32_t pair = (uint32_t)(((uint64_t)(k - 1) * (uint64_t)(L.ny - 1) + (uint64_t)(j - 1)) *
-                                             (uint64_t)(L.nx / 2) + (uint64_t)((i - 1) >> 1));
-        const Philox4 rnd = philox4x32_10(pair, a.G.tag, (uint32_t)sample, (uint32_t)(sample >> 32), a.G.key.k0,
-                                          a.G.key.k1);
+    // first-colour update of pair item t on plane k; returns the other normal
+    auto first_pair = [&](int k, const ZItem& t, double2 fv) -> double {
+        if (!(t.flags & 1) || !(t.flags & 6)) return 0.0;
+        const int e = (((t.flags >> 3) ^ k) & 1) == fc ? 0 : 1;  // element of the first colour
+        const uint32_t pair = (uint32_t)(k - 1) * plane_pairs + t.pbase;
+        const Philox4 rnd = philox4x32_10(pair, a.G.tag, s_lo, s_hi, a.G.key.k0, a.G.key.k1);
         double z0, z1;
         normal_pair_t(rnd, &z0, &z1, tab, tab + 64, tab + 128);  // z0: odd position i, z1: even i+1
-        if ((e == 0 && in0) || (e == 1 && in1)) {
-            const int c = 2 * c2 + e;
-            const double res = row_sum(k, r, c);
+        if (t.flags & (2 << e)) {
+            const int o = t.lds + e;
+            const double res = row_sum(k, o);
             const double crhs = fma(sd, e == 0 ? z0 : z1, e == 0 ? fv.x : fv.y);
             double* s0 = xs + slot(k) * R * W;
-            s0[r * W + c] = fma(wd, crhs - res, s0[r * W + c]);
+            s0[o] = fma(wd, crhs - res, s0[o]);
         }
         return e == 0 ? z1 : z0;
     };
-    auto second_pair = [&](int k, int r, int c2, double2 fv, double z) {
-        const int j = j0 - 2 + r;
-        if (!interior_row(j)) return;
-        const int i = ibase + 2 * c2;
-        const int e = ((i + j + k) & 1) == fc ? 1 : 0;
-        const int ie = i + e;
-        if (ie < 1 || ie > L.nx - 1) return;
-        const int c = 2 * c2 + e;
-        const double res = row_sum(k, r, c);
+    auto second_pair = [&](int k, const ZItem& t, double2 fv, double z) {
+        if (!(t.flags & 1)) return;
+        const int e = (((t.flags >> 3) ^ k) & 1) == fc ? 1 : 0;  // element of the second colour
+        if (!(t.flags & (2 << e))) return;
+        const int o = t.lds + e;
+        const double res = row_sum(k, o);
         const double crhs = fma(sd, z, e == 0 ? fv.x : fv.y);
         double* s0 = xs + slot(k) * R * W;
-        s0[r * W + c] = fma(wd, crhs - res, s0[r * W + c]);
+        s0[o] = fma(wd, crhs - res, s0[o]);
     };
 
     // register pipeline: f(p) core pairs are loaded at step p-1 and used at steps p (first colour)
@@ -256,16 +261,15 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
         zpark_new[u] = zpark_old[u] = 0.0;
     }
     // prologue: planes k0-2, k0-1 in LDS, x(k0) and f(k0-1) in flight
-    {
-        const int kk[2] = {k0 - 2, k0 - 1};
-        for (int q = 0; q < 2; ++q) {
-            issue_x(kk[q]);
-            deposit_x(kk[q]);
-        }
-    }
+    issue_x(k0 - 2);
+    deposit_x(k0 - 2);
+    issue_x(k0 - 1);
+    deposit_x(k0 - 1);
     issue_x(k0);
-    load_fcore(k0 - 1, fnext);
-    load_fhalo(k0 - 1, fh_next);
+#pragma unroll
+    for (int u = 0; u < NC; ++u) fnext[u] = load_f(k0 - 1, ci[u]);
+#pragma unroll
+    for (int u = 0; u < NH; ++u) fh_next[u] = load_f(k0 - 1, hi[u]);
     for (int p = k0 - 1; p <= k1; ++p) {
         deposit_x(p + 1);
 #pragma unroll
@@ -278,20 +282,21 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
         for (int u = 0; u < NH; ++u) fh_cur[u] = fh_next[u];
         store_x(p - 2);
         issue_x(p + 2);
-        load_fcore(p + 1, fnext);
-        load_fhalo(p + 1, fh_next);
+#pragma unroll
+        for (int u = 0; u < NC; ++u) fnext[u] = load_f(p + 1, ci[u]);
+#pragma unroll
+        for (int u = 0; u < NH; ++u) fh_next[u] = load_f(p + 1, hi[u]);
         __syncthreads();
         if (interior_plane(p)) {
 #pragma unroll
-            for (int u = 0; u < NC; ++u) zpark_new[u] = first_pair(p, cr[u], cc[u], fcur[u]);
+            for (int u = 0; u < NC; ++u) zpark_new[u] = first_pair(p, ci[u], fcur[u]);
 #pragma unroll
-            for (int u = 0; u < NH; ++u)
-                if (hr[u] >= 0) (void)first_pair(p, hr[u], hc[u], fh_cur[u]);
+            for (int u = 0; u < NH; ++u) (void)first_pair(p, hi[u], fh_cur[u]);
         }
         __syncthreads();
         if (p - 1 >= k0 && interior_plane(p - 1)) {
 #pragma unroll
-            for (int u = 0; u < NC; ++u) second_pair(p - 1, cr[u], cc[u], fprev[u], zpark_old[u]);
+            for (int u = 0; u < NC; ++u) second_pair(p - 1, ci[u], fprev[u], zpark_old[u]);
         }
         __syncthreads();
     }

@@ -169,13 +169,15 @@ def _mean_cov(s, f, nsamples, nwarmup=200):
 
 
 @pytest.mark.parametrize("shape,kw,nsamples,tol", [
-    ((8, 8), dict(nlevel=3, ncoarsesmooth=2), 40000, 0.02),
-    ((8, 8), dict(nlevel=3, smoother="SSOR", cycle=2), 40000, 0.02),
-    ((8, 8, 8), dict(nlevel=2, ncoarsesmooth=2), 20000, 0.03),
+    ((8, 8), dict(nlevel=3, ncoarsesmooth=2), 40000, 0.04),
+    ((8, 8), dict(nlevel=3, smoother="SSOR", cycle=2), 40000, 0.04),
+    ((8, 8, 8), dict(nlevel=2, ncoarsesmooth=2), 20000, 0.07),
 ])
 def test_mgmc_statistics_vs_exact_covariance(hip_device, shape, kw, nsamples, tol):
     """sampler/test_sampler.hh:113-153 on the device chain: sample mean and covariance against the
-    exact Q^-1 f and Q^-1 (infinity norm), relative to max|Q^-1|; tol stated per case."""
+    exact Q^-1 f and Q^-1 (infinity norm), relative to max|Q^-1|.  tol ~ 5 sigma of the max over
+    all entries: sqrt(2 IACT / n) per entry (IACT ~ 1.5); the CPU oracle in either mode shows
+    0.013-0.022 (2D, n = 40000) and 0.03 (3D, n = 20000) on the same cases."""
     s, p, lat = make(shape, kappa_sq=4.0, **kw)
     orc = O.Oracle.fd(lat.shape, p, 4.0, mode=O.FAITHFUL)
     Q = orc.csr_matrix(0).toarray()
