@@ -21,6 +21,7 @@
 #include "mgmc_hierarchy.hpp"
 #include "mgmc_kernels.hpp"
 #include "mgmc_zsweep.hpp"
+#include "mgmc_zrestrict.hpp"
 
 using namespace mgmc;
 
@@ -221,8 +222,42 @@ void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStrea
         hipLaunchKernelGGL((k_coarse_ssor_lds<2, 5>), grid, block, lv.lds_bytes, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc);
 }
 
+template <int NPTS, int CX, int CY, int NT>
+void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, const double* f, double* fc, double* xc,
+                           hipStream_t s) {
+    ZRestrictArgs a;
+    a.Lf = lf.L;
+    a.Lc = lc.L;
+    a.x = x;
+    a.f = f;
+    a.fc = fc;
+    a.xc = xc;
+    a.S = lf.S;
+    const char* kz = getenv("MGMC_ZR_KZ");
+    a.kz = kz ? atoi(kz) : 8;
+    a.ntx = (lc.L.nx - 1 + CX - 1) / CX;
+    a.nty = (lc.L.ny - 1 + CY - 1) / CY;
+    a.ntz = (lc.L.nz - 1 + a.kz - 1) / a.kz;
+    const int nt = a.ntx * a.nty * a.ntz;
+    const int nb = (nt + 7) / 8 * 8;
+    hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT>), dim3(nb), dim3(NT), zrestrict_lds_bytes(CX, CY), s, a);
+}
+
 void launch_residual_restrict(const Level& lf, const Level& lc, const double* x, const double* f, double* fc,
                               double* xc, int zero_xc, hipStream_t s) {
+    if (lf.spec.dim == 3 && zero_xc && getenv("MGMC_NO_ZRESTRICT") == nullptr && lc.L.nx >= 128) {
+        const int v = getenv("MGMC_ZR_VARIANT") ? atoi(getenv("MGMC_ZR_VARIANT")) : 0;
+        if (lf.spec.npoints == 7) {
+            if (v == 1) launch_zresrestrict_t<7, 32, 4, 128>(lf, lc, x, f, fc, xc, s);
+            else if (v == 2) launch_zresrestrict_t<7, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
+            else launch_zresrestrict_t<7, 32, 8, 256>(lf, lc, x, f, fc, xc, s);
+        } else {
+            if (v == 1) launch_zresrestrict_t<27, 32, 4, 128>(lf, lc, x, f, fc, xc, s);
+            else if (v == 2) launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
+            else launch_zresrestrict_t<27, 32, 8, 256>(lf, lc, x, f, fc, xc, s);
+        }
+        return;
+    }
     dim3 block(64, 4, 1);
     dim3 grid = grid3(lc.L.nx - 1, lc.L.ny - 1, lf.spec.dim == 3 ? lc.L.nz - 1 : 1, block);
     const int dim = lf.spec.dim, np = lf.spec.npoints;
@@ -237,6 +272,15 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
 }
 
 void launch_prolongate(const Level& lf, const Level& lc, double* x, const double* xc, double alpha, hipStream_t s) {
+    if (getenv("MGMC_OLD_PROLONG") == nullptr) {
+        dim3 block(64, 4, 1);
+        dim3 grid = grid3(lf.L.nx / 2, lf.L.ny - 1, lf.spec.dim == 3 ? lf.L.nz - 1 : 1, block);
+        if (lf.spec.dim == 3)
+            hipLaunchKernelGGL((k_prolongate_pairs<3>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha);
+        else
+            hipLaunchKernelGGL((k_prolongate_pairs<2>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha);
+        return;
+    }
     dim3 block(64, 4, 1);
     dim3 grid = grid3(lf.L.nx - 1, lf.L.ny - 1, lf.spec.dim == 3 ? lf.L.nz - 1 : 1, block);
     if (lf.spec.dim == 3)

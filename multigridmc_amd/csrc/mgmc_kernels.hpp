@@ -328,6 +328,59 @@ __global__ void __launch_bounds__(256) k_prolongate_add(Layout Lf, Layout Lc, do
     x[p] = v;
 }
 
+// ---- prolongate-add, one thread per fine x-pair (i odd, i+1): 16-byte load / store of x, the
+// coarse values from L2.  Contributions are added in ascending coarse index (kk, jj, ii), exactly
+// as k_prolongate_add / the reference's scatter order. ----
+template <int DIM>
+__global__ void __launch_bounds__(256) k_prolongate_pairs(Layout Lf, Layout Lc, double* __restrict__ x,
+                                                          const double* __restrict__ xc, double alpha) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = blockIdx.y * blockDim.y + threadIdx.y + 1;
+    const int k = (DIM == 3) ? (int)blockIdx.z + 1 : 0;
+    const int i = 2 * q + 1;
+    if (i > Lf.nx - 1 || j > Lf.ny - 1) return;
+    const long long p = Lf.at(i, j, k);
+    double2 v = *reinterpret_cast<const double2*>(x + p);
+    const bool has1 = i + 1 <= Lf.nx - 1;
+    const int j0 = j >> 1, nj = (j & 1) ? 2 : 1;
+    const int k0 = k >> 1, nk = (DIM == 3 && (k & 1)) ? 2 : 1;
+    for (int a = 0; a < nk; ++a) {
+        const int kk = k0 + a;
+        if (DIM == 3 && (kk < 1 || kk > Lc.nz - 1)) continue;
+        for (int b = 0; b < nj; ++b) {
+            const int jj = j0 + b;
+            if (jj < 1 || jj > Lc.ny - 1) continue;
+            const double* row = xc + Lc.at(0, jj, DIM == 3 ? kk : 0);
+            double wyz = 1.0;  // weights multiply x first, then y, then z (intergrid_operator_linear.cc:22-27)
+            // element 0: i odd -> coarse ii = q (sigma = +1), q+1 (sigma = -1), weight 1/2 each
+            if (q >= 1) {
+                double w = 1.0;
+                w *= 0.5;
+                w *= w1(j - 2 * jj);
+                if (DIM == 3) w *= w1(k - 2 * kk);
+                v.x += alpha * w * row[q];
+            }
+            if (q + 1 <= Lc.nx - 1) {
+                double w = 1.0;
+                w *= 0.5;
+                w *= w1(j - 2 * jj);
+                if (DIM == 3) w *= w1(k - 2 * kk);
+                v.x += alpha * w * row[q + 1];
+                // element 1: i+1 even -> coarse ii = q+1 (sigma = 0), weight 1
+                if (has1) {
+                    double w2 = 1.0;
+                    w2 *= 1.0;
+                    w2 *= w1(j - 2 * jj);
+                    if (DIM == 3) w2 *= w1(k - 2 * kk);
+                    v.y += alpha * w2 * row[q + 1];
+                }
+            }
+            (void)wyz;
+        }
+    }
+    *reinterpret_cast<double2*>(x + p) = v;
+}
+
 // ---- y = A x (tests, LinearOperator::apply) ----
 template <int DIM, int NPTS>
 __global__ void __launch_bounds__(256) k_operator_apply(Layout L, const double* __restrict__ x, double* __restrict__ y,

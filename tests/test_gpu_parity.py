@@ -52,6 +52,10 @@ CONFIGS = {
     "3d_aniso_zsweep_ssor": ((256, 128, 64), dict(nlevel=3, smoother="SSOR", npresmooth=2, npostsmooth=1,
                                                   omega=1.1, coarse_scaling=0.9)),
     "3d128_zsweep_odd": ((128, 64, 96), dict(nlevel=2, npresmooth=2, npostsmooth=1, ncoarsesmooth=2)),
+    # z-marching residual+restriction (coarse nx >= 128): 7-point fine -> level 1 and 27-point
+    # level 1 -> level 2, partial tiles in y and z
+    "3d_zres7": ((256, 40, 48), dict(nlevel=2)),
+    "3d_zres27": ((512, 16, 24), dict(nlevel=3)),
 }
 
 
@@ -67,7 +71,7 @@ def test_normals_bitwise(hip_device):
     s.close()
 
 
-@pytest.mark.parametrize("name", ["2d64_template_W", "3d16", "3d_aniso", "2d_aniso_ssor"])
+@pytest.mark.parametrize("name", ["2d64_template_W", "3d16", "3d_aniso", "2d_aniso_ssor", "3d_zres7", "3d_zres27"])
 def test_component_kernels_bitwise(hip_device, name):
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)
