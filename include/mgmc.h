@@ -95,7 +95,8 @@ typedef struct mgmc_handle mgmc_handle;
 
 /* ---- host-only helpers (no GPU touched) ---- */
 int mgmc_abi_version(void);
-/* Validate cfg and fill out[0..nlevel-1] with the level hierarchy and Galerkin stencils. */
+/* Validate cfg and fill out[0..nlevel-1] with the level hierarchy and Galerkin stencils.
+ * Returns the number of levels (> 0) or a negative MGMC_E* code. */
 int mgmc_describe(const mgmc_config* cfg, mgmc_level_desc* out, int max_levels);
 const char* mgmc_last_error(const mgmc_handle* h);
 

@@ -381,7 +381,14 @@ void build_ops_level(mgmc_handle* h, int level, uint32_t& tag, std::vector<int>&
             h->ops.push_back({OP_PROLONGATE, level, 0, 0, 0});
             h->ops.back().src = cur[level];
         }
-        if (level == 0) h->seg_end_post = h->ops.size();
+        if (level == 0) {
+            h->seg_end_post = h->ops.size();
+            // the timed fine segment starts at the first fine sweep: an unfused fine prolongation
+            // stays in the coarse-correction segment, so fine_ms times Gibbs sweeps only
+            while (h->seg_begin_post < h->seg_end_post &&
+                   !(h->ops[h->seg_begin_post].kind == OP_SWEEP && h->ops[h->seg_begin_post].level == 0))
+                ++h->seg_begin_post;
+        }
     }
 }
 

@@ -1,0 +1,26 @@
+# Round evidence on the GPU box: (optional) gpu tests, bench (with CPU baseline), rocprofv3 stats
+# of the bench command, PMC traffic of the fine sweep (separate FETCH_SIZE / WRITE_SIZE passes).
+#   RUN_PYTEST=1 bash scripts/profile_round.sh     BENCH_ARGS="--cpu-samples 1"
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/round && export TMPDIR=/tmp
+O=gpurun_out/round
+if [ -n "$RUN_PYTEST" ]; then
+  timeout -k 10 1100 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1; rc=$?
+  echo "pytest rc=$rc"; tail -3 $O/pytest_gpu.log
+  [ $rc -eq 0 ] || exit $rc
+fi
+if [ -z "$SKIP_BENCH" ]; then
+  timeout -k 10 900 python bench.py ${BENCH_ARGS} > $O/bench.log 2>&1; rc=$?
+  echo "bench rc=$rc"; tail -2 $O/bench.log
+  [ $rc -eq 0 ] || exit $rc
+fi
+if [ -z "$SKIP_PROF" ]; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/prof.log 2>&1; rc=$?
+  echo "rocprof rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+  for c in FETCH_SIZE WRITE_SIZE; do
+    K=6 timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $O/pmc_$c -o pmc -- python3 scripts/sweep_once.py > $O/pmc_$c.log 2>&1; rc=$?
+    echo "pmc $c rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+  done
+fi
+exit 0

@@ -269,3 +269,17 @@ def test_invalid_level_and_sizes_raise(hip_device):
     s.close()
     with pytest.raises(mg.MgmcError):
         make((16, 16), coarse_solver="Cholesky")
+
+
+def test_cpp_host_side_sample_matches_python_path(hip_device, tmp_path):
+    """The C++ host side (include/mgmc_sampler.hh, g++-built client) and the Python host side drive the
+    same C-ABI: the 3D 16^3 QoI series at vertex (8,8,8) agree bit for bit."""
+    import subprocess
+    from tests.cpp_client import build_client
+    exe = build_client(tmp_path)
+    r = subprocess.run([exe, "sample", "6"], capture_output=True, text=True, check=True)
+    zc = np.array([float(v) for v in r.stdout.split()])
+    s, p, lat = make((16, 16, 16), nlevel=3)
+    zp = s.sample(6, 7 * 15 * 15 + 7 * 15 + 7)
+    s.close()
+    assert np.array_equal(zc, zp)

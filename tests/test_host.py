@@ -190,3 +190,26 @@ def test_pooled_statistics_gloo_world2():
         assert res[r]["n"] == allv.size
         assert res[r]["mean"] == pytest.approx(allv.mean(), rel=1e-12)
         assert res[r]["variance"] == pytest.approx(allv.var(), rel=1e-12)
+
+
+def test_cpp_host_side_describe_and_loud_failure(tmp_path):
+    """include/mgmc_sampler.hh compiles with g++ against the C-ABI library; the host-only path matches
+    mgmc_describe through ctypes, and on a host without a GPU constructing the sampler prints the
+    library error and exits with -1 (the reference's error convention, multigridmc_sampler.cc:47-49)."""
+    import subprocess
+    from tests.cpp_client import build_client
+    exe = build_client(tmp_path)
+    out = subprocess.run([exe, "describe"], capture_output=True, text=True, check=True).stdout.split("\n")
+    assert out[0] == "abi 1"
+    cfg_levels = mg.describe(mg.make_config(mg.ShiftedLaplaceFDOperator(mg.Lattice3d(64, 64, 64), 25.0),
+                                            mg.MultigridParameters(nlevel=4)))
+    for level, line in enumerate(out[1:5]):
+        tok = line.split()
+        assert int(tok[5]) == cfg_levels[level]["ndof"]
+        assert float(tok[11]) == cfg_levels[level]["stencil"][13]
+    hip = ctypes.CDLL("libamdhip64.so")
+    n = ctypes.c_int(0)
+    if hip.hipGetDeviceCount(ctypes.byref(n)) == 0 and n.value > 0:
+        return
+    r = subprocess.run([exe, "sample", "2"], capture_output=True, text=True)
+    assert r.returncode == 255 and "ERROR: mgmc_create failed" in r.stderr
