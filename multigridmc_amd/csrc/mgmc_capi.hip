@@ -205,6 +205,10 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
         case 2: launch_zsweep_t<64, 8, 512>(lv, a, pr, s); break;
         case 3: launch_zsweep_t<32, 8, 256>(lv, a, pr, s); break;
         case 4: launch_zsweep_t<64, 16, 512>(lv, a, pr, s); break;
+        case 5: launch_zsweep_t<32, 16, 256>(lv, a, pr, s); break;
+        case 6: launch_zsweep_t<32, 24, 384>(lv, a, pr, s); break;
+        case 7: launch_zsweep_t<64, 12, 384>(lv, a, pr, s); break;
+        case 8: launch_zsweep_t<32, 12, 192>(lv, a, pr, s); break;
         default: launch_zsweep_t<ZS_XP, ZS_TY, ZS_NT>(lv, a, pr, s); break;
     }
 }
@@ -619,8 +623,10 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         hipMemsetAsync(lv.x, 0, bytes, h->stream);
         hipMemsetAsync(lv.f, 0, bytes, h->stream);
         // fused z-marching sweep: fine 3D 7-point levels whose row splits into 64-pair tiles
-        lv.zsweep = cfg->dim == 3 && lv.spec.npoints == 7 && l + 1 < specs.size() && (lv.L.nx % (2 * ZS_XP)) == 0 &&
-                    getenv("MGMC_NO_ZSWEEP") == nullptr;
+        const double* st = lv.spec.st;  // the z-sweep folds the symmetric FD stencil to 4 coefficients
+        const bool symmetric = st[4] == st[22] && st[10] == st[16] && st[12] == st[14];
+        lv.zsweep = cfg->dim == 3 && lv.spec.npoints == 7 && symmetric && l + 1 < specs.size() &&
+                    (lv.L.nx % (2 * ZS_XP)) == 0 && getenv("MGMC_NO_ZSWEEP") == nullptr;
         if (lv.zsweep) {
             if (hipMalloc(&lv.x2, bytes) != hipSuccess) {
                 h->levels.push_back(lv);

@@ -86,12 +86,13 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
     constexpr int NLX = (R * WP + NT - 1) / NT;    // pair loads of one x plane per thread
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* xs = smem;                 // [4][R][W] ring of x planes (p-2 .. p+1)
-    double* tab = xs + 4 * R * W;      // [3][64] log reduction table (rc, hi, lo)
+    double* tab = xs + 4 * R * W;      // [3][64] log reduction table (rc, hi, lo) + [130] cos/sin table
     for (int q = threadIdx.x; q < 64; q += NT) {
         tab[q] = LOGTAB_RC[q];
         tab[64 + q] = LOGTAB_HI[q];
         tab[128 + q] = LOGTAB_LO[q];
     }
+    for (int q = threadIdx.x; q < 130; q += NT) tab[192 + q] = SINCOS_TAB[q];
 
     const Layout& L = a.L;
     // XCD-aware tile order: blocks b and b+8 share an XCD, give them neighbouring tiles
@@ -121,7 +122,11 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
         ZItem t;
         const int j = j0 - 2 + r, i = ibase + 2 * c2;
         const bool rin = j >= 1 && j <= L.ny - 1;
-        t.goff = rin ? (long long)j * L.sx + i + L.off : 0;
+        // rows outside [0, ny] are clamped onto the zero boundary rows 0 / ny, so every load is
+        // unconditional and reads exactly the zeros the guarded form produced (columns past either
+        // end of a row land in the zero padding of the layout)
+        const int jc = j < 0 ? 0 : (j > L.ny ? L.ny : j);
+        t.goff = (long long)jc * L.sx + i + L.off;
         t.pbase = (uint32_t)((uint64_t)(j - 1) * (uint64_t)(L.nx / 2) + (uint64_t)((i - 1) >> 1));
         t.lds = r * W + 2 * c2;
         t.flags = (rin ? 1 : 0) | ((i >= 1 && i <= L.nx - 1) ? 2 : 0) | ((i + 1 >= 1 && i + 1 <= L.nx - 1) ? 4 : 0) |
@@ -161,25 +166,23 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
 #pragma unroll
     for (int u = 0; u < NLX; ++u) {
         const int it = tid + u * NT;
-        xoff[u] = -1;
+        xoff[u] = L.off + 1;  // threads without an item load a zero pad pair and deposit nothing
         xlds[u] = -1;
         if (it < R * WP) {
             const ZItem t = make_item(it / WP, it % WP);
             xlds[u] = t.lds;
-            if (t.flags & 1) xoff[u] = t.goff;
+            xoff[u] = t.goff;
         }
     }
+    // planes outside [0, nz] are clamped onto the zero boundary planes 0 / nz
+    auto plane_base = [&](const double* v, int k) { return v + (long long)(k < 0 ? 0 : (k > L.nz ? L.nz : k)) * L.sp; };
 
     // ---- global <-> LDS / registers ----
     double2 px[NLX];
     auto issue_x = [&](int k) {
-        const bool kin = interior_plane(k);
-        const double* base = a.xin + (long long)k * L.sp;
+        const double* base = plane_base(a.xin, k);
 #pragma unroll
-        for (int u = 0; u < NLX; ++u) {
-            px[u] = make_double2(0.0, 0.0);
-            if (kin && xoff[u] >= 0) px[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
-        }
+        for (int u = 0; u < NLX; ++u) px[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
     };
     auto deposit_x = [&](int k) {
         double* dst = xs + slot(k) * R * W;
@@ -187,11 +190,12 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
         for (int u = 0; u < NLX; ++u) {
             if (xlds[u] < 0) continue;
             double2 v = px[u];
-            if (PROLONG && interior_plane(k) && xoff[u] >= 0) {
+            if (PROLONG && interior_plane(k)) {
                 const int c2 = (xlds[u] % W) / 2, r = xlds[u] / W;
                 const int j = j0 - 2 + r, i = ibase + 2 * c2;
-                if (i >= 1 && i <= L.nx - 1) v.x = prolong_gather(v.x, a.xc, a.Lc, i, j, k, a.alpha);
-                if (i + 1 >= 1 && i + 1 <= L.nx - 1) v.y = prolong_gather(v.y, a.xc, a.Lc, i + 1, j, k, a.alpha);
+                const bool rin = j >= 1 && j <= L.ny - 1;
+                if (rin && i >= 1 && i <= L.nx - 1) v.x = prolong_gather(v.x, a.xc, a.Lc, i, j, k, a.alpha);
+                if (rin && i + 1 >= 1 && i + 1 <= L.nx - 1) v.y = prolong_gather(v.y, a.xc, a.Lc, i + 1, j, k, a.alpha);
             }
             *reinterpret_cast<double2*>(dst + xlds[u]) = v;
         }
@@ -204,33 +208,36 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
         for (int u = 0; u < NC; ++u)
             if (ci[u].flags & 1) *reinterpret_cast<double2*>(base + ci[u].goff) = *reinterpret_cast<const double2*>(src + ci[u].lds);
     };
-    auto load_f = [&](int k, const ZItem& t) {
-        if (!interior_plane(k) || !(t.flags & 1)) return make_double2(0.0, 0.0);
-        return *reinterpret_cast<const double2*>(a.f + (long long)k * L.sp + t.goff);
-    };
+    auto load_f = [&](int k, const ZItem& t) { return *reinterpret_cast<const double2*>(plane_base(a.f, k) + t.goff); };
 
-    // fma-chain stencil sum (ascending column order) at LDS offset o of plane k
+    // fma-chain stencil sum (ascending column order) at LDS offset o of plane k.  The fine FD
+    // stencil is symmetric (launch_zsweep checks a[4]=a[22], a[10]=a[16], a[12]=a[14]), so four
+    // coefficients serve the seven terms -- same values, same order, same bits.
+    const double cz = a.S.a[4], cy = a.S.a[10], cx = a.S.a[12], cc = a.S.a[13];
     auto row_sum = [&](int k, int o) {
         const double* sm = xs + slot(k - 1) * R * W;
         const double* s0 = xs + slot(k) * R * W;
         const double* sp = xs + slot(k + 1) * R * W;
-        double res = a.S.a[4] * sm[o];
-        res = fma(a.S.a[10], s0[o - W], res);
-        res = fma(a.S.a[12], s0[o - 1], res);
-        res = fma(a.S.a[13], s0[o], res);
-        res = fma(a.S.a[14], s0[o + 1], res);
-        res = fma(a.S.a[16], s0[o + W], res);
-        res = fma(a.S.a[22], sp[o], res);
+        double res = cz * sm[o];
+        res = fma(cy, s0[o - W], res);
+        res = fma(cx, s0[o - 1], res);
+        res = fma(cc, s0[o], res);
+        res = fma(cx, s0[o + 1], res);
+        res = fma(cy, s0[o + W], res);
+        res = fma(cz, sp[o], res);
         return res;
     };
-    // first-colour update of pair item t on plane k; returns the other normal
+    // first-colour update of pair item t on plane k; returns the second colour's right hand side
+    // c = fma(sd, z_other, f_other) (the same fma the second-colour update would evaluate)
     auto first_pair = [&](int k, const ZItem& t, double2 fv) -> double {
         if (!(t.flags & 1) || !(t.flags & 6)) return 0.0;
         const int e = (((t.flags >> 3) ^ k) & 1) == fc ? 0 : 1;  // element of the first colour
         const uint32_t pair = (uint32_t)(k - 1) * plane_pairs + t.pbase;
-        const Philox4 rnd = philox4x32_10(pair, a.G.tag, s_lo, s_hi, a.G.key.k0, a.G.key.k1);
+        uint32_t key0 = a.G.key.k0, key1 = a.G.key.k1;
+        asm volatile("" : "+s"(key0), "+s"(key1));  // keep the round-key schedule out of the SGPR budget
+        const Philox4 rnd = philox4x32_10(pair, a.G.tag, s_lo, s_hi, key0, key1);
         double z0, z1;
-        normal_pair_t(rnd, &z0, &z1, tab, tab + 64, tab + 128);  // z0: odd position i, z1: even i+1
+        normal_pair_t(rnd, &z0, &z1, tab, tab + 64, tab + 128, tab + 192);  // z0: odd position i, z1: even i+1
         if (t.flags & (2 << e)) {
             const int o = t.lds + e;
             const double res = row_sum(k, o);
@@ -238,28 +245,51 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
             double* s0 = xs + slot(k) * R * W;
             s0[o] = fma(wd, crhs - res, s0[o]);
         }
-        return e == 0 ? z1 : z0;
+        return e == 0 ? fma(sd, z1, fv.y) : fma(sd, z0, fv.x);
     };
-    auto second_pair = [&](int k, const ZItem& t, double2 fv, double z) {
+    auto second_pair = [&](int k, const ZItem& t, double crhs) {
         if (!(t.flags & 1)) return;
         const int e = (((t.flags >> 3) ^ k) & 1) == fc ? 1 : 0;  // element of the second colour
         if (!(t.flags & (2 << e))) return;
         const int o = t.lds + e;
         const double res = row_sum(k, o);
-        const double crhs = fma(sd, z, e == 0 ? fv.x : fv.y);
         double* s0 = xs + slot(k) * R * W;
         s0[o] = fma(wd, crhs - res, s0[o]);
     };
 
-    // register pipeline: f(p) core pairs are loaded at step p-1 and used at steps p (first colour)
-    // and p+1 (second colour); x(p+2) is loaded at step p and deposited at step p+1.
-    double2 fnext[NC], fcur[NC], fprev[NC], fh_next[NH], fh_cur[NH];
-    double zpark_new[NC], zpark_old[NC];
+    // One z step p: deposit x(p+1), store the finished plane p-2, issue x(p+2) and f(p+1); first
+    // colour on plane p (core + halo ring), second colour on plane p-1.  f(p) arrives in fcur
+    // (loaded one step earlier), f(p+1) goes to fnxt; the second colour's right hand sides of plane
+    // p go to pk_out and those of plane p-1 come from pk_in.  The loop below runs the steps in pairs
+    // with the register sets swapped, so nothing is copied between steps.
+    auto step = [&](int p, double2 (&fcur)[NC], double2 (&fnxt)[NC], double2 (&fhcur)[NH], double2 (&fhnxt)[NH],
+                    const double (&pk_in)[NC], double (&pk_out)[NC]) __attribute__((always_inline)) {
+        deposit_x(p + 1);
+        store_x(p - 2);
+        issue_x(p + 2);
 #pragma unroll
-    for (int u = 0; u < NC; ++u) {
-        fcur[u] = fprev[u] = make_double2(0.0, 0.0);
-        zpark_new[u] = zpark_old[u] = 0.0;
-    }
+        for (int u = 0; u < NC; ++u) fnxt[u] = load_f(p + 1, ci[u]);
+#pragma unroll
+        for (int u = 0; u < NH; ++u) fhnxt[u] = load_f(p + 1, hi[u]);
+        __syncthreads();
+        if (interior_plane(p)) {
+#pragma unroll
+            for (int u = 0; u < NC; ++u) pk_out[u] = first_pair(p, ci[u], fcur[u]);
+#pragma unroll
+            for (int u = 0; u < NH; ++u) (void)first_pair(p, hi[u], fhcur[u]);
+        }
+        __syncthreads();
+        if (p - 1 >= k0 && interior_plane(p - 1)) {
+#pragma unroll
+            for (int u = 0; u < NC; ++u) second_pair(p - 1, ci[u], pk_in[u]);
+        }
+        __syncthreads();
+    };
+
+    double2 fA[NC], fB[NC], fhA[NH], fhB[NH];
+    double pkA[NC], pkB[NC];
+#pragma unroll
+    for (int u = 0; u < NC; ++u) pkA[u] = pkB[u] = 0.0;
     // prologue: planes k0-2, k0-1 in LDS, x(k0) and f(k0-1) in flight
     issue_x(k0 - 2);
     deposit_x(k0 - 2);
@@ -267,45 +297,19 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
     deposit_x(k0 - 1);
     issue_x(k0);
 #pragma unroll
-    for (int u = 0; u < NC; ++u) fnext[u] = load_f(k0 - 1, ci[u]);
+    for (int u = 0; u < NC; ++u) fA[u] = load_f(k0 - 1, ci[u]);
 #pragma unroll
-    for (int u = 0; u < NH; ++u) fh_next[u] = load_f(k0 - 1, hi[u]);
-    for (int p = k0 - 1; p <= k1; ++p) {
-        deposit_x(p + 1);
-#pragma unroll
-        for (int u = 0; u < NC; ++u) {
-            fprev[u] = fcur[u];
-            fcur[u] = fnext[u];
-            zpark_old[u] = zpark_new[u];
-        }
-#pragma unroll
-        for (int u = 0; u < NH; ++u) fh_cur[u] = fh_next[u];
-        store_x(p - 2);
-        issue_x(p + 2);
-#pragma unroll
-        for (int u = 0; u < NC; ++u) fnext[u] = load_f(p + 1, ci[u]);
-#pragma unroll
-        for (int u = 0; u < NH; ++u) fh_next[u] = load_f(p + 1, hi[u]);
-        __syncthreads();
-        if (interior_plane(p)) {
-#pragma unroll
-            for (int u = 0; u < NC; ++u) zpark_new[u] = first_pair(p, ci[u], fcur[u]);
-#pragma unroll
-            for (int u = 0; u < NH; ++u) (void)first_pair(p, hi[u], fh_cur[u]);
-        }
-        __syncthreads();
-        if (p - 1 >= k0 && interior_plane(p - 1)) {
-#pragma unroll
-            for (int u = 0; u < NC; ++u) second_pair(p - 1, ci[u], fprev[u], zpark_old[u]);
-        }
-        __syncthreads();
+    for (int u = 0; u < NH; ++u) fhA[u] = load_f(k0 - 1, hi[u]);
+    for (int p = k0 - 1; p <= k1; p += 2) {
+        step(p, fA, fB, fhA, fhB, pkB, pkA);
+        if (p + 1 <= k1) step(p + 1, fB, fA, fhB, fhA, pkA, pkB);
     }
     store_x(k1 - 1);
 }
 
 inline size_t zsweep_lds_bytes(int XP, int TY) {
     const int W = 2 * XP + 8, R = TY + 4;
-    return (size_t)(4 * R * W + 3 * 64) * sizeof(double);
+    return (size_t)(4 * R * W + 3 * 64 + 130) * sizeof(double);
 }
 
 }  // namespace mgmc

@@ -31,6 +31,29 @@ struct Philox4 {
     uint32_t v[4];
 };
 
+// a ^ b ^ k with k wave-uniform (the Philox key): one v_bitop3_b32 (truth table 0x96 = 3-input xor)
+MGMC_HD uint32_t xor3_key(uint32_t a, uint32_t b, uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t d;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "s"(k));
+    return d;
+#else
+    return a ^ b ^ k;
+#endif
+}
+
+// fma(a, b, c) with c a literal constant: on the device one v_fma_f64 with c in SGPRs (the
+// compiler otherwise keeps such constants in VGPRs and copies them into a tied v_fmac accumulator)
+MGMC_HD double fma_k(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double d;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+    return d;
+#else
+    return fma(a, b, c);
+#endif
+}
+
 MGMC_HD Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
     const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
     const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
@@ -38,9 +61,9 @@ MGMC_HD Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3
     for (int r = 0; r < 10; ++r) {
         const uint64_t p0 = (uint64_t)M0 * c0;
         const uint64_t p1 = (uint64_t)M1 * c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n0 = xor3_key((uint32_t)(p1 >> 32), c1, k0);
         const uint32_t n1 = (uint32_t)p1;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        const uint32_t n2 = xor3_key((uint32_t)(p0 >> 32), c3, k1);
         const uint32_t n3 = (uint32_t)p0;
         c0 = n0; c1 = n1; c2 = n2; c3 = n3;
         k0 += W0; k1 += W1;
@@ -77,11 +100,11 @@ MGMC_HD double log_unit(double u, const double* rct, const double* hit, const do
     const double m = as_double(mant | 0x3ff0000000000000ull);
     const double r = fma(m, rct[idx], -1.0);
     double q = -1.0 / 8.0;
-    q = fma(q, r, 1.0 / 7.0);
-    q = fma(q, r, -1.0 / 6.0);
-    q = fma(q, r, 1.0 / 5.0);
-    q = fma(q, r, -1.0 / 4.0);
-    q = fma(q, r, 1.0 / 3.0);
+    q = fma_k(q, r, 1.0 / 7.0);
+    q = fma_k(q, r, -1.0 / 6.0);
+    q = fma_k(q, r, 1.0 / 5.0);
+    q = fma_k(q, r, -1.0 / 4.0);
+    q = fma_k(q, r, 1.0 / 3.0);
     q = fma(q, r, -0.5);
     const double p = fma(r * r, q, r);  // log1p(r)
     const double de = (double)e;
@@ -90,50 +113,61 @@ MGMC_HD double log_unit(double u, const double* rct, const double* hit, const do
     return fma(de, LN2_HI, hit[idx]) + (fma(de, LN2_LO, lot[idx]) + p);
 }
 
-// (cos(2 pi t), sin(2 pi t)) for t in [0,1); quadrant selection without branches
-MGMC_HD void sincos_2pi(double t, double* c_out, double* s_out) {
-    const int q = (int)(t * 4.0 + 0.5);          // 0..4
-    const double r = t - (double)q * 0.25;         // exact, |r| <= 1/8
-    const double th = r * 6.28318530717958647692;  // |th| <= pi/4
+// (cos(2 pi t), sin(2 pi t)) for t in [0,1) with at most 52 fractional bits.  t = k/64 + r with
+// k = round(64 t) in [0,64] and r exact (|r| <= 1/128); theta = 2 pi r, |theta| <= pi/64;
+// sin theta to degree 9 and cos theta - 1 to degree 8 (truncation < 1e-19), then the addition
+// theorem with the literal table sct[2k], sct[2k+1] = cos, sin(2 pi k/64) (log_table.h).
+MGMC_HD void sincos_2pi(double t, const double* sct, double* c_out, double* s_out) {
+    const int k = (int)fma(t, 64.0, 0.5);                // exact argument, k in [0, 64]
+    const double r = fma((double)(-k), 0.015625, t);     // exact
+    const double th = r * 6.28318530717958647692;
     const double t2 = th * th;
-    double ps = -1.0 / 355687428096000.0;     // -1/17!
-    ps = fma(ps, t2, 1.0 / 1307674368000.0);  // 1/15!
-    ps = fma(ps, t2, -1.0 / 6227020800.0);    // -1/13!
-    ps = fma(ps, t2, 1.0 / 39916800.0);       // 1/11!
-    ps = fma(ps, t2, -1.0 / 362880.0);        // -1/9!
-    ps = fma(ps, t2, 1.0 / 5040.0);           // 1/7!
-    ps = fma(ps, t2, -1.0 / 120.0);           // -1/5!
-    ps = fma(ps, t2, 1.0 / 6.0);              // 1/3!
-    const double sn = fma(-(th * t2), ps, th);
-    double pc = 1.0 / 20922789888000.0;      // 1/16!
-    pc = fma(pc, t2, -1.0 / 87178291200.0);  // -1/14!
-    pc = fma(pc, t2, 1.0 / 479001600.0);     // 1/12!
-    pc = fma(pc, t2, -1.0 / 3628800.0);      // -1/10!
-    pc = fma(pc, t2, 1.0 / 40320.0);         // 1/8!
-    pc = fma(pc, t2, -1.0 / 720.0);          // -1/6!
-    pc = fma(pc, t2, 1.0 / 24.0);            // 1/4!
-    pc = fma(pc, t2, -0.5);                  // -1/2!
-    const double cs = fma(pc, t2, 1.0);
-    // quadrant qq: (c, s) = (cs, sn), (-sn, cs), (-cs, -sn), (sn, -cs)
-    const int qq = q & 3;
-    const bool swap = (qq & 1) != 0;
-    const double c0 = swap ? sn : cs;
-    const double s0 = swap ? cs : sn;
-    *c_out = (qq == 1 || qq == 2) ? -c0 : c0;
-    *s_out = (qq >= 2) ? -s0 : s0;
+    double ps = 1.0 / 362880.0;
+    ps = fma_k(ps, t2, -1.0 / 5040.0);
+    ps = fma_k(ps, t2, 1.0 / 120.0);
+    ps = fma_k(ps, t2, -1.0 / 6.0);
+    const double sn = fma(th * t2, ps, th);              // sin theta
+    double pc = 1.0 / 40320.0;
+    pc = fma_k(pc, t2, -1.0 / 720.0);
+    pc = fma_k(pc, t2, 1.0 / 24.0);
+    pc = fma(pc, t2, -0.5);
+    const double w = pc * t2;                            // cos theta - 1
+    const double C = sct[2 * k], S = sct[2 * k + 1];
+    *c_out = fma(C, w, fma(-S, sn, C));
+    *s_out = fma(S, w, fma(C, sn, S));
+}
+
+// sqrt(x) for x = 0 or x >= 2^-700, correctly rounded: on the device the rsq + Newton sequence of
+// the compiler's IEEE sqrt lowering without its denormal-range scaling (never taken here), so the
+// bits equal the host's sqrt.
+MGMC_HD double sqrt_rad(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = 0.5 * y;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    g = fma(d, h, g);
+    return x > 0.0 ? g : 0.0;
+#else
+    return x > 0.0 ? sqrt(x) : 0.0;
+#endif
 }
 
 // Box-Muller pair from one Philox block: (z_cos, z_sin)
 MGMC_HD void normal_pair_t(const Philox4& r, double* z0, double* z1, const double* rct, const double* hit,
-                           const double* lot) {
+                           const double* lot, const double* sct) {
     const double v1 = as_double(0x3ff0000000000000ull | bits52(r.v[0], r.v[1]));
     const double v2 = as_double(0x3ff0000000000000ull | bits52(r.v[2], r.v[3]));
     const double u1 = 2.0 - v1;  // (0,1]
     const double u2 = v2 - 1.0;  // [0,1)
-    const double rr = -2.0 * log_unit(u1, rct, hit, lot);
-    const double rad = sqrt(rr > 0.0 ? rr : 0.0);
+    const double rad = sqrt_rad(-2.0 * log_unit(u1, rct, hit, lot));
     double c, s;
-    sincos_2pi(u2, &c, &s);
+    sincos_2pi(u2, sct, &c, &s);
     *z0 = rad * c;
     *z1 = rad * s;
 }
@@ -150,7 +184,7 @@ MGMC_HD RngKey make_key(uint64_t seed, uint64_t chain) {
 }
 
 MGMC_HD void normal_pair(const Philox4& r, double* z0, double* z1) {
-    normal_pair_t(r, z0, z1, LOGTAB_RC, LOGTAB_HI, LOGTAB_LO);
+    normal_pair_t(r, z0, z1, LOGTAB_RC, LOGTAB_HI, LOGTAB_LO, SINCOS_TAB);
 }
 
 // one normal for the point whose pair id is `pair`; cos_branch selects the first of the two

@@ -432,28 +432,25 @@ static double ln_unit(double u) {
     return fma(de, 6.93147180369123816490e-01, LOGTAB_HI[idx]) + (fma(de, 1.90821492927058770002e-10, LOGTAB_LO[idx]) + p);
 }
 
+// (cos 2 pi t, sin 2 pi t): k = round(64 t), exact remainder r = t - k/64, theta = 2 pi r, sin theta
+// to degree 9, cos theta - 1 to degree 8, addition theorem with the literal table SINCOS_TAB
+// (log_table_oracle.h: cos, sin of 2 pi k/64)
 static void cos_sin_2pi(double t, double& c, double& s) {
-    const int q = (int)(t * 4.0 + 0.5);
-    const double r = t - (double)q * 0.25;
+    const int k = (int)fma(t, 64.0, 0.5);
+    const double r = fma((double)(-k), 0.015625, t);
     const double th = r * 6.28318530717958647692;
     const double t2 = th * th;
-    static const double sc[8] = {-1.0 / 355687428096000.0, 1.0 / 1307674368000.0, -1.0 / 6227020800.0,
-                                 1.0 / 39916800.0,         -1.0 / 362880.0,      1.0 / 5040.0,
-                                 -1.0 / 120.0,             1.0 / 6.0};
+    static const double sc[4] = {1.0 / 362880.0, -1.0 / 5040.0, 1.0 / 120.0, -1.0 / 6.0};
     double ps = sc[0];
-    for (int k = 1; k < 8; ++k) ps = fma(ps, t2, sc[k]);
-    const double sn = fma(-(th * t2), ps, th);
-    static const double cc[8] = {1.0 / 20922789888000.0, -1.0 / 87178291200.0, 1.0 / 479001600.0,
-                                 -1.0 / 3628800.0,       1.0 / 40320.0,        -1.0 / 720.0,
-                                 1.0 / 24.0,             -0.5};
+    for (int q = 1; q < 4; ++q) ps = fma(ps, t2, sc[q]);
+    const double sn = fma(th * t2, ps, th);
+    static const double cc[4] = {1.0 / 40320.0, -1.0 / 720.0, 1.0 / 24.0, -0.5};
     double pc = cc[0];
-    for (int k = 1; k < 8; ++k) pc = fma(pc, t2, cc[k]);
-    const double cs = fma(pc, t2, 1.0);
-    const int qq = q & 3;
-    const double c0 = (qq & 1) ? sn : cs;
-    const double s0 = (qq & 1) ? cs : sn;
-    c = (qq == 1 || qq == 2) ? -c0 : c0;
-    s = (qq >= 2) ? -s0 : s0;
+    for (int q = 1; q < 4; ++q) pc = fma(pc, t2, cc[q]);
+    const double w = pc * t2;
+    const double C = SINCOS_TAB[2 * k], S = SINCOS_TAB[2 * k + 1];
+    c = fma(C, w, fma(-S, sn, C));
+    s = fma(S, w, fma(C, sn, S));
 }
 
 static void philox_normals(uint64_t seed, uint64_t chain, uint32_t pair, uint32_t tag, uint64_t sample, double& z0,

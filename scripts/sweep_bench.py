@@ -1,5 +1,5 @@
 """Micro-benchmark of the fine-level sweep kernel variants and of the whole V-cycle (GPU box).
-Usage: python scripts/sweep_bench.py [n] [nlevel]"""
+Usage: python scripts/sweep_bench.py [n] [nlevel] [zsweep variants, comma separated]"""
 import json
 import os
 import subprocess
@@ -25,16 +25,9 @@ print(json.dumps({"sweep_ms": ms, "GBps": 24 * lat.Nvertex / ms / 1e6, "vcycle_m
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 nlevel = int(sys.argv[2]) if len(sys.argv) > 2 else 7
-variants = [("colour-pass", {"MGMC_NO_ZSWEEP": "1"})]
-for v in ["0"]:
+variants = []
+for v in (sys.argv[3].split(",") if len(sys.argv) > 3 else ["0", "3", "5", "6", "7", "8"]):
     variants.append((f"zsweep-v{v}", {"MGMC_ZS_VARIANT": v}))
-variants.append(("zsweep-v0-tz64", {"MGMC_ZS_VARIANT": "0", "MGMC_ZS_TZ": "64"}))
-variants.append(("no-zrestrict", {"MGMC_NO_ZRESTRICT": "1"}))
-for v in ["1", "2"]:
-    variants.append((f"zrestrict-v{v}", {"MGMC_ZR_VARIANT": v}))
-variants.append(("zrestrict-kz16", {"MGMC_ZR_KZ": "16"}))
-variants.append(("zrestrict-kz4", {"MGMC_ZR_KZ": "4"}))
-variants.append(("old-prolong", {"MGMC_OLD_PROLONG": "1"}))
 for name, env in variants:
     e = dict(os.environ)
     e.update(env)

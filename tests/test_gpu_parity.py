@@ -144,6 +144,24 @@ def test_mgmc_cycles_bitwise(hip_device, name):
     s.close()
 
 
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "6", "7", "8"])
+def test_zsweep_tile_variants_bitwise(hip_device, monkeypatch, variant):
+    """Every z-sweep tile shape (MGMC_ZS_VARIANT: 64x4, 64x8/512, 32x8, 64x16, 32x16, 32x24, 64x12,
+    32x12 pairs x rows) gives the oracle's multicolour cycle exactly, on a shape whose y/z extents do
+    not divide the tiles."""
+    monkeypatch.setenv("MGMC_ZS_VARIANT", variant)
+    shape, kw = (128, 72, 40), dict(nlevel=2, npresmooth=2, npostsmooth=1)
+    s, p, lat = make(shape, **kw)
+    mc = oracle_for(s, p, lat)
+    f = np.random.default_rng(5).standard_normal(lat.Nvertex)
+    x_dev, x_orc = np.zeros(lat.Nvertex), np.zeros(lat.Nvertex)
+    for _ in range(2):
+        s.apply(f, x_dev)
+        mc.apply(f, x_orc)
+    assert np.array_equal(x_dev, x_orc)
+    s.close()
+
+
 def test_mgmc_seed_chain_independence(hip_device):
     a, p, lat = make((32, 32, 32))
     b, _, _ = make((32, 32, 32))

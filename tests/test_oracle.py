@@ -98,10 +98,17 @@ def test_oracle_math_accuracy():
     assert rel < 5e-16 and ab < 1e-16
     c, s = ctypes.c_double(), ctypes.c_double()
     e = 0.0
-    for t in np.random.default_rng(1).random(20000):
+    ts = list(np.random.default_rng(1).random(20000))
+    # exact quadrant points and the rounding boundaries k/64 +- 1/128 of the table reduction
+    ts += [0.0, 0.25, 0.5, 0.75, 1.0 - 2.0 ** -52] + [(k + 0.5) / 64 for k in range(64)]
+    ts += [(k + 0.5) / 64 - 2.0 ** -52 for k in range(64)]
+    for t in ts:
         O.lib().orc_cos_sin_2pi(float(t), ctypes.byref(c), ctypes.byref(s))
         e = max(e, abs(c.value - math.cos(2 * math.pi * t)), abs(s.value - math.sin(2 * math.pi * t)))
     assert e < 2e-15
+    for t, (ce, se) in ((0.0, (1.0, 0.0)), (0.25, (0.0, 1.0)), (0.5, (-1.0, 0.0)), (0.75, (0.0, -1.0))):
+        O.lib().orc_cos_sin_2pi(t, ctypes.byref(c), ctypes.byref(s))
+        assert (c.value, s.value) == (ce, se)
 
 
 # ---------------------------------------------------------------- intergrid (test_intergrid.hh)
