@@ -98,7 +98,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("MGMC_LIBRARY") or LIB_PATH  # MGMC_LIBRARY: experiment builds (build/)
     if not os.path.exists(p):
         raise ImportError(
             f"{p} not found: the HIP extension is not built (run `python -c 'import __graft_entry__ as g; g.build()'`)")

@@ -48,7 +48,9 @@ struct Op {
 };
 
 // z-marching sweep tile shape (mgmc_zsweep.hpp)
-constexpr int ZS_XP = 64, ZS_TY = 8, ZS_NT = 256, ZS_TZ = 32;
+// 32 x-pairs x 16 rows, 256 threads (2 core pairs per thread, 19.5 % halo), 38 KB of LDS -> 4
+// workgroups per CU; tuning history in DESIGN.md
+constexpr int ZS_XP = 32, ZS_TY = 16, ZS_NT = 256, ZS_MINW = 1, ZS_TZ = 32;
 
 struct Level {
     LevelSpec spec;
@@ -164,7 +166,7 @@ void launch_sweep(const Level& lv, double* x, const double* f, const GibbsArg& g
 #undef DISPATCH
 }
 
-template <int XP, int TY, int NT>
+template <int XP, int TY, int NT, int MINW = 1>
 void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s) {
     a.ntx = (lv.L.nx / 2) / XP;
     a.nty = (lv.L.ny - 1 + TY - 1) / TY;
@@ -173,15 +175,24 @@ void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s)
     const int nb = (ntiles + 7) / 8 * 8;
     const size_t lds = zsweep_lds_bytes(XP, TY);
     if (prolong)
-        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, true>), dim3(nb), dim3(NT), lds, s, a);
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, true, MINW>), dim3(nb), dim3(NT), lds, s, a);
     else
-        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, false>), dim3(nb), dim3(NT), lds, s, a);
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, false, MINW>), dim3(nb), dim3(NT), lds, s, a);
 }
 
 // tile-shape variant (MGMC_ZS_VARIANT, for tuning experiments; 0 = default)
 int zsweep_variant() {
     const char* v = getenv("MGMC_ZS_VARIANT");
     return v ? atoi(v) : 0;
+}
+
+// x-pairs per tile of the selected variant (the fine nx must be a multiple of 2 * xp)
+int zsweep_xp() {
+    switch (zsweep_variant()) {
+        case 1: case 2: case 3: case 4: case 7: case 11: return 64;
+        case 5: case 6: case 8: case 9: return 32;
+        default: return ZS_XP;
+    }
 }
 
 void launch_zsweep(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g0,
@@ -203,13 +214,15 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
     switch (zsweep_variant()) {
         case 1: launch_zsweep_t<64, 4, 256>(lv, a, pr, s); break;
         case 2: launch_zsweep_t<64, 8, 512>(lv, a, pr, s); break;
-        case 3: launch_zsweep_t<32, 8, 256>(lv, a, pr, s); break;
+        case 3: launch_zsweep_t<64, 8, 256>(lv, a, pr, s); break;
         case 4: launch_zsweep_t<64, 16, 512>(lv, a, pr, s); break;
         case 5: launch_zsweep_t<32, 16, 256>(lv, a, pr, s); break;
         case 6: launch_zsweep_t<32, 24, 384>(lv, a, pr, s); break;
         case 7: launch_zsweep_t<64, 12, 384>(lv, a, pr, s); break;
         case 8: launch_zsweep_t<32, 12, 192>(lv, a, pr, s); break;
-        default: launch_zsweep_t<ZS_XP, ZS_TY, ZS_NT>(lv, a, pr, s); break;
+        case 9: launch_zsweep_t<32, 8, 256>(lv, a, pr, s); break;
+        case 11: launch_zsweep_t<64, 16, 512, 4>(lv, a, pr, s); break;
+        default: launch_zsweep_t<ZS_XP, ZS_TY, ZS_NT, ZS_MINW>(lv, a, pr, s); break;
     }
 }
 
@@ -612,7 +625,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     for (size_t l = 0; l < specs.size(); ++l) {
         Level lv;
         lv.spec = specs[l];
-        lv.L = make_layout(cfg->dim, specs[l].n);
+        lv.L = make_layout(cfg->dim, specs[l].n, getenv("MGMC_LAYOUT_A64") == nullptr);  // 128-B rows
         memcpy(lv.S.a, specs[l].st, sizeof(lv.S.a));
         const size_t bytes = lv.L.nstore * sizeof(double);
         if (hipMalloc(&lv.x, bytes) != hipSuccess || hipMalloc(&lv.f, bytes) != hipSuccess) {
@@ -626,7 +639,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         const double* st = lv.spec.st;  // the z-sweep folds the symmetric FD stencil to 4 coefficients
         const bool symmetric = st[4] == st[22] && st[10] == st[16] && st[12] == st[14];
         lv.zsweep = cfg->dim == 3 && lv.spec.npoints == 7 && symmetric && l + 1 < specs.size() &&
-                    (lv.L.nx % (2 * ZS_XP)) == 0 && getenv("MGMC_NO_ZSWEEP") == nullptr;
+                    (lv.L.nx % (2 * zsweep_xp())) == 0 && getenv("MGMC_NO_ZSWEEP") == nullptr;
         if (lv.zsweep) {
             if (hipMalloc(&lv.x2, bytes) != hipSuccess) {
                 h->levels.push_back(lv);

@@ -39,15 +39,18 @@ struct Layout {
     }
 };
 
-inline Layout make_layout(int dim, const int n[3]) {
+// align128: the first interior vertex of every row on a 128-byte line (row stride a multiple of 16
+// doubles, off = 15); otherwise 64-byte rows with off = 7.  off stays odd either way, so interior
+// x-pairs (i odd, i+1) sit on 16-byte boundaries.
+inline Layout make_layout(int dim, const int n[3], bool align128 = false) {
     Layout L;
     L.dim = dim;
     L.nx = n[0];
     L.ny = n[1];
     L.nz = dim == 3 ? n[2] : 0;
-    L.off = 7;
+    L.off = align128 ? 15 : 7;
     L.pad_ = 0;
-    L.sx = ((long long)L.nx + 8 + 7) / 8 * 8;
+    L.sx = align128 ? ((long long)L.nx + 16 + 15) / 16 * 16 : ((long long)L.nx + 8 + 7) / 8 * 8;
     L.sp = L.sx * (L.ny + 1);
     L.nstore = (dim == 3 ? L.sp * (L.nz + 1) : L.sp) + 64;
     return L;

@@ -12,8 +12,10 @@
 //    the second colour on plane p-1 (tile only), which then is final and is stored.  A red update
 //    on plane p only reads black values of planes p-1..p+1 (still old), a black update on p-1 only
 //    reads red values of planes p-2..p (already new): this is exactly the two-pass result.
-//  * Planes live in an LDS ring (4 slots of x, 2 of f); global traffic is 16-byte pair loads and
-//    stores, one pass over x_in, f and x_out (+ halo re-reads that hit L2 / Infinity Cache).
+//  * Planes live in a 3-slot LDS ring (p-1, p, p+1) in a colour-split row layout; global traffic is
+//    16-byte pair loads and stores, one pass over x_in, f and x_out (+ halo re-reads that hit L2 /
+//    Infinity Cache).  Second-colour results never return to LDS (no update reads them), they go
+//    straight to the store; the z-below values of the second colour come from registers.
 //  * The two vertices of an x-pair share one Philox block: the first-colour update consumes one
 //    Box-Muller branch and parks the other in LDS for the second-colour update one step later.
 //  * Optional fused prolongate-add on the input: x_old = x_in + alpha P x_c, evaluated exactly as
@@ -69,14 +71,25 @@ __device__ __forceinline__ double prolong_gather(double v, const double* __restr
 struct ZItem {
     long long goff;  // j*sx + i + off  (add k*sp for plane k)
     uint32_t pbase;  // (j-1)*(nx/2) + (i-1)/2
-    int lds;         // r*W + 2*c2
+    int lds;         // r*RS + c2 (odd element; even element at +WP)
     int flags;       // bit0 row interior, bit1 i interior, bit2 i+1 interior, bit3 parity (i+j)&1
 };
 
-template <int XP, int TY, int NT, bool PROLONG>
-__global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
-    constexpr int W = 2 * XP + 8;  // LDS columns: positions [2*q0-3, 2*q0+2*XP+4]
-    constexpr int WP = W / 2;      // pairs per LDS row
+// MGMC_ZS_EXP (timing experiments only, scripts/build_exp.sh; 0 in the product): 1 no Box-Muller,
+// 2 no halo ring, 3 no Philox, 4 no stencil, 5 memory skeleton (1 + 2 + 4)
+#ifndef MGMC_ZS_EXP
+#define MGMC_ZS_EXP 0
+#endif
+// MINW: minimum waves per SIMD the register allocation must allow (1 = unconstrained)
+template <int XP, int TY, int NT, bool PROLONG, int MINW>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW))) k_zsweep_rb7(ZSweepArgs a) {
+    constexpr int WP = XP + 4;     // pairs per LDS row: positions [2*q0-3, 2*q0+2*XP+4]
+    // LDS row = [odd positions of the WP pairs | even positions | 2 pad]: lanes owning consecutive
+    // pairs read consecutive doubles (conflict-free); the row stride (2XP+10 doubles = 20 mod 64 banks)
+    // spreads the column
+    // accesses of the x-halo items over the banks
+    constexpr int RS = 2 * WP + 2;
+    constexpr int PS = (TY + 4) * RS;  // LDS plane
     constexpr int R = TY + 4;      // rows j0-2 .. j0+TY+1
     constexpr int NCORE = TY * XP;                 // core pairs (both colours)
     constexpr int NHALO = 2 * (XP + 2) + 2 * TY;   // first-colour halo ring pairs
@@ -85,8 +98,8 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
     constexpr int NH = (NHALO + NT - 1) / NT;      // halo pairs per thread
     constexpr int NLX = (R * WP + NT - 1) / NT;    // pair loads of one x plane per thread
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* xs = smem;                 // [4][R][W] ring of x planes (p-2 .. p+1)
-    double* tab = xs + 4 * R * W;      // [3][64] log reduction table (rc, hi, lo) + [130] cos/sin table
+    double* xs = smem;                 // [3][R][RS] ring of x planes (p-1 .. p+1)
+    double* tab = xs + 3 * PS;      // [3][64] log reduction table (rc, hi, lo) + [130] cos/sin table
     for (int q = threadIdx.x; q < 64; q += NT) {
         tab[q] = LOGTAB_RC[q];
         tab[64 + q] = LOGTAB_HI[q];
@@ -116,7 +129,7 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
     const uint32_t plane_pairs = (uint32_t)((uint64_t)(L.ny - 1) * (uint64_t)(L.nx / 2));
     const int tid = threadIdx.x;
 
-    auto slot = [](int p) { return (p + 8) & 3; };
+    auto slot = [](int p) { return (p + 9) % 3; };
     auto interior_plane = [&](int k) { return k >= 1 && k <= L.nz - 1; };
     auto make_item = [&](int r, int c2) {
         ZItem t;
@@ -128,7 +141,7 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
         const int jc = j < 0 ? 0 : (j > L.ny ? L.ny : j);
         t.goff = (long long)jc * L.sx + i + L.off;
         t.pbase = (uint32_t)((uint64_t)(j - 1) * (uint64_t)(L.nx / 2) + (uint64_t)((i - 1) >> 1));
-        t.lds = r * W + 2 * c2;
+        t.lds = r * RS + c2;  // odd element; the even element is at +WP
         t.flags = (rin ? 1 : 0) | ((i >= 1 && i <= L.nx - 1) ? 2 : 0) | ((i + 1 >= 1 && i + 1 <= L.nx - 1) ? 4 : 0) |
                   (((i + j) & 1) << 3);
         return t;
@@ -185,28 +198,21 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
         for (int u = 0; u < NLX; ++u) px[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
     };
     auto deposit_x = [&](int k) {
-        double* dst = xs + slot(k) * R * W;
+        double* dst = xs + slot(k) * PS;
 #pragma unroll
         for (int u = 0; u < NLX; ++u) {
             if (xlds[u] < 0) continue;
             double2 v = px[u];
             if (PROLONG && interior_plane(k)) {
-                const int c2 = (xlds[u] % W) / 2, r = xlds[u] / W;
+                const int c2 = xlds[u] % RS, r = xlds[u] / RS;
                 const int j = j0 - 2 + r, i = ibase + 2 * c2;
                 const bool rin = j >= 1 && j <= L.ny - 1;
                 if (rin && i >= 1 && i <= L.nx - 1) v.x = prolong_gather(v.x, a.xc, a.Lc, i, j, k, a.alpha);
                 if (rin && i + 1 >= 1 && i + 1 <= L.nx - 1) v.y = prolong_gather(v.y, a.xc, a.Lc, i + 1, j, k, a.alpha);
             }
-            *reinterpret_cast<double2*>(dst + xlds[u]) = v;
+            dst[xlds[u]] = v.x;
+            dst[xlds[u] + WP] = v.y;
         }
-    };
-    auto store_x = [&](int k) {
-        if (k < k0 || k >= k1) return;
-        const double* src = xs + slot(k) * R * W;
-        double* base = a.xout + (long long)k * L.sp;
-#pragma unroll
-        for (int u = 0; u < NC; ++u)
-            if (ci[u].flags & 1) *reinterpret_cast<double2*>(base + ci[u].goff) = *reinterpret_cast<const double2*>(src + ci[u].lds);
     };
     auto load_f = [&](int k, const ZItem& t) { return *reinterpret_cast<const double2*>(plane_base(a.f, k) + t.goff); };
 
@@ -214,16 +220,20 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
     // stencil is symmetric (launch_zsweep checks a[4]=a[22], a[10]=a[16], a[12]=a[14]), so four
     // coefficients serve the seven terms -- same values, same order, same bits.
     const double cz = a.S.a[4], cy = a.S.a[10], cx = a.S.a[12], cc = a.S.a[13];
-    auto row_sum = [&](int k, int o) {
-        const double* sm = xs + slot(k - 1) * R * W;
-        const double* s0 = xs + slot(k) * R * W;
-        const double* sp = xs + slot(k + 1) * R * W;
-        double res = cz * sm[o];
-        res = fma(cy, s0[o - W], res);
-        res = fma(cx, s0[o - 1], res);
+    // o = LDS offset of the vertex, e = 0 (odd position) / 1 (even position): the x neighbours are
+    // the even elements of pairs c-1, c (e = 0) or the odd elements of pairs c, c+1 (e = 1)
+    // below = the value at (i, j, k-1): from LDS for the first colour, from a register for the second
+    auto row_sum = [&](int k, int o, int e, double below) {
+        if (MGMC_ZS_EXP == 4 || MGMC_ZS_EXP == 5) return below;
+        const double* s0 = xs + slot(k) * PS;
+        const double* sp = xs + slot(k + 1) * PS;
+        const int xm = e ? o - WP : o + WP - 1;
+        double res = cz * below;
+        res = fma(cy, s0[o - RS], res);
+        res = fma(cx, s0[xm], res);
         res = fma(cc, s0[o], res);
-        res = fma(cx, s0[o + 1], res);
-        res = fma(cy, s0[o + W], res);
+        res = fma(cx, s0[xm + 1], res);
+        res = fma(cy, s0[o + RS], res);
         res = fma(cz, sp[o], res);
         return res;
     };
@@ -235,37 +245,55 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
         const uint32_t pair = (uint32_t)(k - 1) * plane_pairs + t.pbase;
         uint32_t key0 = a.G.key.k0, key1 = a.G.key.k1;
         asm volatile("" : "+s"(key0), "+s"(key1));  // keep the round-key schedule out of the SGPR budget
+#if MGMC_ZS_EXP == 3  // timing experiment: BM without Philox
+        Philox4 rnd;
+        rnd.v[0] = pair * 2654435761u; rnd.v[1] = pair ^ key0; rnd.v[2] = pair * 40503u; rnd.v[3] = pair + key1;
+#else
         const Philox4 rnd = philox4x32_10(pair, a.G.tag, s_lo, s_hi, key0, key1);
+#endif
         double z0, z1;
+#if MGMC_ZS_EXP == 1 || MGMC_ZS_EXP == 5  // timing experiment: no noise generation
+        z0 = (double)(rnd.v[0] & 1); z1 = (double)(rnd.v[2] & 1);
+#else
         normal_pair_t(rnd, &z0, &z1, tab, tab + 64, tab + 128, tab + 192);  // z0: odd position i, z1: even i+1
+#endif
         if (t.flags & (2 << e)) {
-            const int o = t.lds + e;
-            const double res = row_sum(k, o);
+            const int o = t.lds + (e ? WP : 0);
+            const double res = row_sum(k, o, e, xs[slot(k - 1) * PS + o]);
             const double crhs = fma(sd, e == 0 ? z0 : z1, e == 0 ? fv.x : fv.y);
-            double* s0 = xs + slot(k) * R * W;
+            double* s0 = xs + slot(k) * PS;
             s0[o] = fma(wd, crhs - res, s0[o]);
         }
         return e == 0 ? fma(sd, z1, fv.y) : fma(sd, z0, fv.x);
     };
-    auto second_pair = [&](int k, const ZItem& t, double crhs) {
-        if (!(t.flags & 1)) return;
+    // second-colour update of core item t on plane k; returns the new value (the old one where the
+    // vertex is not interior).  No update ever reads a second-colour value after its update (the first
+    // colour reads the old ones, the second colour only first-colour neighbours), so the result goes
+    // to the store and not back to LDS; below = the new first-colour value at (i, j, k-1), kept in a
+    // register since plane k-1 has already left the LDS ring.
+    auto second_pair = [&](int k, const ZItem& t, double crhs, double below) -> double {
         const int e = (((t.flags >> 3) ^ k) & 1) == fc ? 1 : 0;  // element of the second colour
-        if (!(t.flags & (2 << e))) return;
-        const int o = t.lds + e;
-        const double res = row_sum(k, o);
-        double* s0 = xs + slot(k) * R * W;
-        s0[o] = fma(wd, crhs - res, s0[o]);
+        const int o = t.lds + (e ? WP : 0);
+        const double old = xs[slot(k) * PS + o];
+        if (!(t.flags & 1) || !(t.flags & (2 << e))) return old;
+        const double res = row_sum(k, o, e, below);
+        return fma(wd, crhs - res, old);
     };
 
-    // One z step p: deposit x(p+1), store the finished plane p-2, issue x(p+2) and f(p+1); first
-    // colour on plane p (core + halo ring), second colour on plane p-1.  f(p) arrives in fcur
-    // (loaded one step earlier), f(p+1) goes to fnxt; the second colour's right hand sides of plane
-    // p go to pk_out and those of plane p-1 come from pk_in.  The loop below runs the steps in pairs
-    // with the register sets swapped, so nothing is copied between steps.
+    // One z step p (LDS ring = planes p-1, p, p+1):
+    //   deposit x(p+1) (into the slot plane p-2 left), issue x(p+2) and f(p+1)      | barrier
+    //   first colour on plane p (core + halo ring)                                 | barrier
+    //   second colour on plane p-1 (core); plane p-1 is final: store it from the new
+    //   second-colour values (registers) and the first-colour values (LDS), and keep
+    //   the latter as the next step's z-below values                               | barrier
+    // f(p) arrives in fcur (loaded one step earlier), f(p+1) goes to fnxt; the second colour's right
+    // hand sides of plane p go to pk_out, those of plane p-1 come from pk_in; fb_in / fb_out hold the
+    // first-colour values of planes p-2 / p-1 at the second-colour positions of planes p-1 / p.  The
+    // loop runs the steps in pairs with the register sets swapped, so nothing is copied.
     auto step = [&](int p, double2 (&fcur)[NC], double2 (&fnxt)[NC], double2 (&fhcur)[NH], double2 (&fhnxt)[NH],
-                    const double (&pk_in)[NC], double (&pk_out)[NC]) __attribute__((always_inline)) {
+                    const double (&pk_in)[NC], double (&pk_out)[NC], const double (&fb_in)[NC],
+                    double (&fb_out)[NC]) __attribute__((always_inline)) {
         deposit_x(p + 1);
-        store_x(p - 2);
         issue_x(p + 2);
 #pragma unroll
         for (int u = 0; u < NC; ++u) fnxt[u] = load_f(p + 1, ci[u]);
@@ -276,20 +304,31 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
 #pragma unroll
             for (int u = 0; u < NC; ++u) pk_out[u] = first_pair(p, ci[u], fcur[u]);
 #pragma unroll
-            for (int u = 0; u < NH; ++u) (void)first_pair(p, hi[u], fhcur[u]);
+            for (int u = 0; u < NH; ++u)
+                if (MGMC_ZS_EXP != 2 && MGMC_ZS_EXP != 5) (void)first_pair(p, hi[u], fhcur[u]);
         }
         __syncthreads();
-        if (p - 1 >= k0 && interior_plane(p - 1)) {
+        const int k = p - 1;
+        const bool own = k >= k0 && k < k1;  // a core plane of this tile (interior)
+        double sv[NC];
 #pragma unroll
-            for (int u = 0; u < NC; ++u) second_pair(p - 1, ci[u], pk_in[u]);
+        for (int u = 0; u < NC; ++u) sv[u] = own ? second_pair(k, ci[u], pk_in[u], fb_in[u]) : 0.0;
+        double* base = a.xout + (long long)k * L.sp;
+#pragma unroll
+        for (int u = 0; u < NC; ++u) {
+            const int ef = (((ci[u].flags >> 3) ^ k) & 1) == fc ? 0 : 1;  // first-colour element on plane k
+            const double fv = xs[slot(k) * PS + ci[u].lds + (ef ? WP : 0)];
+            fb_out[u] = fv;
+            if (own && (ci[u].flags & 1))
+                *reinterpret_cast<double2*>(base + ci[u].goff) = ef == 0 ? make_double2(fv, sv[u]) : make_double2(sv[u], fv);
         }
         __syncthreads();
     };
 
     double2 fA[NC], fB[NC], fhA[NH], fhB[NH];
-    double pkA[NC], pkB[NC];
+    double pkA[NC], pkB[NC], fbA[NC], fbB[NC];
 #pragma unroll
-    for (int u = 0; u < NC; ++u) pkA[u] = pkB[u] = 0.0;
+    for (int u = 0; u < NC; ++u) pkA[u] = pkB[u] = fbA[u] = fbB[u] = 0.0;
     // prologue: planes k0-2, k0-1 in LDS, x(k0) and f(k0-1) in flight
     issue_x(k0 - 2);
     deposit_x(k0 - 2);
@@ -301,15 +340,14 @@ __global__ void __launch_bounds__(NT) k_zsweep_rb7(ZSweepArgs a) {
 #pragma unroll
     for (int u = 0; u < NH; ++u) fhA[u] = load_f(k0 - 1, hi[u]);
     for (int p = k0 - 1; p <= k1; p += 2) {
-        step(p, fA, fB, fhA, fhB, pkB, pkA);
-        if (p + 1 <= k1) step(p + 1, fB, fA, fhB, fhA, pkA, pkB);
+        step(p, fA, fB, fhA, fhB, pkB, pkA, fbB, fbA);
+        if (p + 1 <= k1) step(p + 1, fB, fA, fhB, fhA, pkA, pkB, fbA, fbB);
     }
-    store_x(k1 - 1);
 }
 
 inline size_t zsweep_lds_bytes(int XP, int TY) {
-    const int W = 2 * XP + 8, R = TY + 4;
-    return (size_t)(4 * R * W + 3 * 64 + 130) * sizeof(double);
+    const int RS = 2 * (XP + 4) + 2, R = TY + 4;
+    return (size_t)(3 * R * RS + 3 * 64 + 130) * sizeof(double);
 }
 
 }  // namespace mgmc

@@ -1,0 +1,8 @@
+# Timing-experiment builds of the library (MGMC_ZS_EXP=1..4, see mgmc_zsweep.hpp) into build/.
+# Never loaded by the product; select one with MGMC_LIBRARY=build/libmgmc_exp<N>.so.
+cd "$(dirname "$0")/../multigridmc_amd/csrc" && mkdir -p ../../build
+for n in ${EXPS:-1 2 3 4}; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off -fPIC -w --offload-arch=gfx950 -DMGMC_ZS_EXP=$n -shared \
+    -o ../../build/libmgmc_exp$n.so mgmc_capi.hip mgmc_hierarchy.cpp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib &
+done
+wait

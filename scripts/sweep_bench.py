@@ -26,7 +26,7 @@ print(json.dumps({"sweep_ms": ms, "GBps": 24 * lat.Nvertex / ms / 1e6, "vcycle_m
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 nlevel = int(sys.argv[2]) if len(sys.argv) > 2 else 7
 variants = []
-for v in (sys.argv[3].split(",") if len(sys.argv) > 3 else ["0", "3", "5", "6", "7", "8"]):
+for v in (sys.argv[3].split(",") if len(sys.argv) > 3 else ["0", "5", "11"]):
     variants.append((f"zsweep-v{v}", {"MGMC_ZS_VARIANT": v}))
 for name, env in variants:
     e = dict(os.environ)

@@ -52,6 +52,7 @@ CONFIGS = {
     "3d_aniso_zsweep_ssor": ((256, 128, 64), dict(nlevel=3, smoother="SSOR", npresmooth=2, npostsmooth=1,
                                                   omega=1.1, coarse_scaling=0.9)),
     "3d128_zsweep_odd": ((128, 64, 96), dict(nlevel=2, npresmooth=2, npostsmooth=1, ncoarsesmooth=2)),
+    "3d192_zsweep": ((192, 48, 40), dict(nlevel=2)),  # nx multiple of 64 (32-pair tiles), not of 128
     # z-marching residual+restriction (coarse nx >= 128): 7-point fine -> level 1 and 27-point
     # level 1 -> level 2, partial tiles in y and z
     "3d_zres7": ((256, 40, 48), dict(nlevel=2)),
@@ -144,10 +145,10 @@ def test_mgmc_cycles_bitwise(hip_device, name):
     s.close()
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "6", "7", "8"])
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "6", "7", "8", "9", "11"])
 def test_zsweep_tile_variants_bitwise(hip_device, monkeypatch, variant):
-    """Every z-sweep tile shape (MGMC_ZS_VARIANT: 64x4, 64x8/512, 32x8, 64x16, 32x16, 32x24, 64x12,
-    32x12 pairs x rows) gives the oracle's multicolour cycle exactly, on a shape whose y/z extents do
+    """Every z-sweep tile shape (MGMC_ZS_VARIANT: 64x4, 64x8/512, 64x8, 64x16, 32x16, 32x24, 64x12,
+    32x12, 32x8 unconstrained registers, 64x16/512; default 32x8 at 5 waves/SIMD) gives the oracle's multicolour cycle exactly, on a shape whose y/z extents do
     not divide the tiles."""
     monkeypatch.setenv("MGMC_ZS_VARIANT", variant)
     shape, kw = (128, 72, 40), dict(nlevel=2, npresmooth=2, npostsmooth=1)
