@@ -22,6 +22,7 @@
 #include "mgmc_kernels.hpp"
 #include "mgmc_zsweep.hpp"
 #include "mgmc_zrestrict.hpp"
+#include "mgmc_gsweep.hpp"
 
 using namespace mgmc;
 
@@ -62,6 +63,8 @@ struct Level {
     double* scratch[3] = {nullptr, nullptr, nullptr};
     size_t lds_bytes = 0;  // >0 if the whole-level LDS kernel can hold x and f
     bool zsweep = false;   // fused z-marching red-black sweep available
+    bool pairs = false;    // Galerkin level swept in colour-pair passes (mgmc_gsweep.hpp)
+    bool pingpong() const { return zsweep; }  // out-of-place sweeps: x <-> x2
     double* buf(int i) const { return i == 0 ? x : x2; }
 };
 
@@ -226,6 +229,47 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
     }
 }
 
+// colour-pair passes of a Galerkin 9/27-point level (in place): forward colours (0,1), (2,3), ...,
+// backward (7,6), (5,4), ... -- 2^(d-1) passes per sweep
+bool pairs_eligible(const LevelSpec& sp, const Layout& L) {
+    return (sp.npoints == 27 || sp.npoints == 9) && L.nx / 2 >= 1 && L.nx / 2 <= 256 && L.nx % 2 == 0;
+}
+
+void launch_pairs(const Level& lv, double* x, const double* f, const GibbsArg& g, int direction, hipStream_t s) {
+    PairPassArgs a;
+    a.L = lv.L;
+    a.x = x;
+    a.f = f;
+    a.S = lv.S;
+    a.G = g;
+    const int dim = lv.spec.dim;
+    const int npair = lv.L.nx / 2;
+    a.rows_per_block = 256 / npair;
+    const int npass = dim == 3 ? 4 : 2;
+    auto count = [](int n, int parity) {  // coordinates 2 - parity + 2t in [1, n-1]
+        const int first = 2 - parity;
+        return first > n - 1 ? 0 : (n - 1 - first) / 2 + 1;
+    };
+    for (int ps = 0; ps < npass; ++ps) {
+        const int c = direction == MGMC_FORWARD ? 2 * ps : 2 * (npass - 1 - ps) + 1;  // first colour
+        a.jp = (c >> 1) & 1;
+        a.kp = (c >> 2) & 1;
+        a.nrows_j = count(lv.L.ny, a.jp);
+        a.nrows = a.nrows_j * (dim == 3 ? count(lv.L.nz, a.kp) : 1);
+        if (a.nrows == 0) continue;
+        const int nb = (a.nrows + a.rows_per_block - 1) / a.rows_per_block;
+        const int nt = a.rows_per_block * npair;
+        const bool odd = c & 1;
+        if (dim == 3) {
+            if (odd) hipLaunchKernelGGL((k_sweep_pairs<3, true>), dim3(nb), dim3(nt), 0, s, a);
+            else hipLaunchKernelGGL((k_sweep_pairs<3, false>), dim3(nb), dim3(nt), 0, s, a);
+        } else {
+            if (odd) hipLaunchKernelGGL((k_sweep_pairs<2, true>), dim3(nb), dim3(nt), 0, s, a);
+            else hipLaunchKernelGGL((k_sweep_pairs<2, false>), dim3(nb), dim3(nt), 0, s, a);
+        }
+    }
+}
+
 void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStream_t s) {
     const int dim = lv.spec.dim, np = lv.spec.npoints, nc = lv.spec.ncolours;
     dim3 block(1024), grid(1);
@@ -327,12 +371,12 @@ void launch_pack(const Level& lv, const double* lex, double* pad, bool pack, hip
 void push_sweep(mgmc_handle* h, std::vector<int>& cur, int level, int direction, uint32_t& tag, int& pending_prolong) {
     Op op{OP_SWEEP, level, direction, tag++, 1};
     const Level& lv = h->levels[level];
-    if (lv.zsweep && pending_prolong && !h->fuse_prolong) {
+    if (lv.pingpong() && pending_prolong && !(lv.zsweep && h->fuse_prolong)) {
         h->ops.push_back({OP_PROLONGATE, level, 0, 0, 0});
         h->ops.back().src = cur[level];
         pending_prolong = 0;
     }
-    if (lv.zsweep) {
+    if (lv.pingpong()) {
         op.src = cur[level];
         op.prolong = pending_prolong;
         pending_prolong = 0;
@@ -421,6 +465,8 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                     const Level* lc = op.prolong ? &h->levels[op.level + 1] : nullptr;
                     launch_zsweep(lv, lv.buf(op.src), lv.buf(1 - op.src), lv.f, g, op.direction, lc,
                                   lc ? lc->x : nullptr, h->cfg.coarse_scaling, s);
+                } else if (lv.pairs) {
+                    launch_pairs(lv, lv.x, lv.f, g, op.direction, s);
                 } else {
                     launch_sweep(lv, lv.x, lv.f, g, op.direction, true, s);
                 }
@@ -640,7 +686,8 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         const bool symmetric = st[4] == st[22] && st[10] == st[16] && st[12] == st[14];
         lv.zsweep = cfg->dim == 3 && lv.spec.npoints == 7 && symmetric && l + 1 < specs.size() &&
                     (lv.L.nx % (2 * zsweep_xp())) == 0 && getenv("MGMC_NO_ZSWEEP") == nullptr;
-        if (lv.zsweep) {
+        lv.pairs = pairs_eligible(lv.spec, lv.L) && getenv("MGMC_NO_PAIRS") == nullptr;
+        if (lv.pingpong()) {
             if (hipMalloc(&lv.x2, bytes) != hipSuccess) {
                 h->levels.push_back(lv);
                 h->last_error = "device allocation failed";
@@ -891,6 +938,8 @@ static int sweep_component(mgmc_handle* h, int level, int direction, int nsweeps
             launch_zsweep(lv, lv.scratch[cur], lv.scratch[3 - cur], lv.scratch[0], g, direction, nullptr, nullptr, 0.0,
                           h->stream);
             cur = 3 - cur;
+        } else if (noise && lv.pairs) {  // the colour-pair passes of the V-cycle (in place)
+            launch_pairs(lv, lv.scratch[cur], lv.scratch[0], g, direction, h->stream);
         } else {
             launch_sweep(lv, lv.scratch[cur], lv.scratch[0], g, direction, noise, h->stream);
         }

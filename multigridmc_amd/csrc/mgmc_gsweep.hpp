@@ -1,0 +1,127 @@
+// mgmc_gsweep.hpp -- pair passes of the 2^d-colour Gibbs sweep of a Galerkin (9/27-point) level.
+//
+// One SOR Gibbs sweep of a coarse level (SORSampler::apply, sampler/sor_sampler.cc:37-59) in the
+// 2^d-colour order of k_sweep_mc (colour bit d = parity of coordinate d; forward = colours 0..2^d-1,
+// backward = reversed) takes 2^(d-1) passes instead of 2^d:
+//
+//  * Colours c and c^1 differ only in the parity of i.  A c^1 vertex reads c vertices only at i-1 and
+//    i+1 in its own row (every other neighbour changes the parity of j or k), and neither colour
+//    reads any other vertex of the pass's rows.  So one pass updates both colours of the rows of
+//    parity (jp, kp): a thread owns the Philox pair (2m+1, 2m+2), updates the vertex of the first
+//    colour, trades the new value with its row neighbour through LDS (one barrier), then updates
+//    the vertex of the second colour.  Rows are independent, so the pass runs in place.
+//  * The two vertices of a pair take the cos / sin branch of one Box-Muller draw: one evaluation per
+//    pair and sweep, no recomputation.
+//  * Whole rows sit in one workgroup (nx/2 threads per row), so the exchange never leaves it.
+// Arithmetic is gibbs_point's (stencil fma chain in ascending column order, c = fma(sd, xi, f),
+// x = fma(omega/diag, c - sum, x)) with the Philox pair ids / tags of k_sweep_mc: bitwise equal to
+// the colour passes.
+#pragma once
+#include <type_traits>
+
+#include "mgmc_kernels.hpp"
+
+namespace mgmc {
+
+struct PairPassArgs {
+    Layout L;
+    double* x;
+    const double* f;
+    StencilArg S;
+    GibbsArg G;
+    int jp, kp;        // row parities of the pass (kp unused in 2D)
+    int rows_per_block, nrows_j, nrows;  // pass rows: j = 2 - jp + 2 t (t < nrows_j), k likewise
+};
+
+// FIRST_ODD: the odd position (i parity 1) is updated first (backward sweeps).  A template parameter,
+// so every index into the register window below is static.
+template <int DIM, bool FIRST_ODD>
+__global__ void __launch_bounds__(256) k_sweep_pairs(PairPassArgs a) {
+    constexpr int NPTS = DIM == 3 ? 27 : 9;
+    __shared__ double xnew[256 + 2];  // new first-colour values, [1 + tid]; zero guards at both ends
+    const Layout& L = a.L;
+    const int npair = L.nx / 2;
+    const int tid = threadIdx.x;
+    const int rloc = tid / npair, m = tid - rloc * npair;
+    const int row = blockIdx.x * a.rows_per_block + rloc;
+    const bool active = rloc < a.rows_per_block && row < a.nrows;
+    const int tj = active ? row % a.nrows_j : 0, tk = active ? row / a.nrows_j : 0;
+    const int j = 2 - a.jp + 2 * tj;
+    const int k = DIM == 3 ? 2 - a.kp + 2 * tk : 0;
+    const int i0 = 2 * m + 1;  // odd position of the pair
+    if (tid < 2) xnew[tid == 0 ? 0 : 257] = 0.0;
+    const long long p0 = active ? L.at(i0, j, k) : 0;  // offset of the odd vertex
+
+    // vertex values around the pair: rows (dz, dy) x positions 2m .. 2m+3 (3 aligned pairs loaded)
+    constexpr int NR = DIM == 3 ? 9 : 3;
+    double w[NR][4];
+    double2 fv = make_double2(0.0, 0.0);
+    if (active) {
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) {
+            const int dz = DIM == 3 ? rr / 3 - 1 : 0, dy = rr % 3 - 1;
+            const double* q = a.x + p0 + (long long)dz * L.sp + (long long)dy * L.sx;
+            const double2 lo = *reinterpret_cast<const double2*>(q - 2);
+            const double2 mid = *reinterpret_cast<const double2*>(q);
+            const double2 hi = *reinterpret_cast<const double2*>(q + 2);
+            w[rr][0] = lo.y;   // 2m
+            w[rr][1] = mid.x;  // 2m+1
+            w[rr][2] = mid.y;  // 2m+2
+            w[rr][3] = hi.x;   // 2m+3
+        }
+        fv = *reinterpret_cast<const double2*>(a.f + p0);
+    }
+    constexpr int C = DIM == 3 ? 4 : 1;  // row index (dz, dy) = (0, 0)
+    // stencil fma chain of the vertex at window position s (1: odd 2m+1, 2: even 2m+2)
+    auto chain = [&](auto sc) {
+        constexpr int s = decltype(sc)::value;
+        double res = a.S.a[0] * w[0][s - 1];
+#pragma unroll
+        for (int q = 1; q < NPTS; ++q) {
+            const int rr = q / 3, dx = q % 3 - 1;
+            res = fma(a.S.a[q], w[rr][s + dx], res);
+        }
+        return res;
+    };
+
+    double z0 = 0.0, z1 = 0.0;  // Box-Muller pair: cos -> odd position, sin -> even position
+    const bool odd_in = active && i0 <= L.nx - 1;
+    const bool even_in = active && i0 + 1 <= L.nx - 1;
+    if (odd_in) {
+        const uint32_t pair = pair_id<DIM>(L, i0, j, k);
+        const Philox4 rnd = philox4x32_10(pair, a.G.tag, (uint32_t)*a.G.sample, (uint32_t)(*a.G.sample >> 32),
+                                          a.G.key.k0, a.G.key.k1);
+        normal_pair(rnd, &z0, &z1);
+    }
+    const double sd = a.G.sd, wd = a.G.wd;
+    // first colour
+    constexpr int s1 = FIRST_ODD ? 1 : 2;
+    const bool in1 = FIRST_ODD ? odd_in : even_in;
+    double v1 = w[C][s1];
+    if (in1) {
+        const double res = chain(std::integral_constant<int, s1>{});
+        const double c = fma(sd, FIRST_ODD ? z0 : z1, FIRST_ODD ? fv.x : fv.y);
+        v1 = fma(wd, c - res, v1);
+    }
+    xnew[1 + tid] = v1;
+    __syncthreads();
+    // second colour: its row neighbours are first-colour vertices (own pair + adjacent pair)
+    constexpr int s2 = 3 - s1;
+    const bool in2 = FIRST_ODD ? even_in : odd_in;
+    w[C][s1] = v1;
+    if (FIRST_ODD) {  // second = even 2m+2, neighbours 2m+1 (own) and 2m+3 (next pair's odd)
+        w[C][3] = (m + 1 < npair) ? xnew[2 + tid] : 0.0;
+    } else {            // second = odd 2m+1, neighbours 2m (previous pair's even) and 2m+2 (own)
+        w[C][0] = (m > 0) ? xnew[tid] : 0.0;
+    }
+    double v2 = w[C][s2];
+    if (in2) {
+        const double res = chain(std::integral_constant<int, s2>{});
+        const double c = fma(sd, FIRST_ODD ? z1 : z0, FIRST_ODD ? fv.y : fv.x);
+        v2 = fma(wd, c - res, v2);
+    }
+    if (active)
+        *reinterpret_cast<double2*>(a.x + p0) = FIRST_ODD ? make_double2(v1, v2) : make_double2(v2, v1);
+}
+
+}  // namespace mgmc
