@@ -176,7 +176,7 @@ void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s)
     a.ntz = (lv.L.nz - 1 + a.tz - 1) / a.tz;
     const int ntiles = a.ntx * a.nty * a.ntz;
     const int nb = (ntiles + 7) / 8 * 8;
-    const size_t lds = zsweep_lds_bytes(XP, TY);
+    const size_t lds = zsweep_lds_bytes(XP, TY, prolong);
     if (prolong)
         hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, true, MINW>), dim3(nb), dim3(NT), lds, s, a);
     else
@@ -212,7 +212,7 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
     a.G = g0;
     a.G.colour = (direction == MGMC_FORWARD) ? 0 : 1;
     const char* tz = getenv("MGMC_ZS_TZ");
-    a.tz = tz ? atoi(tz) : ZS_TZ;
+    a.tz = std::max(2, (tz ? atoi(tz) : ZS_TZ) & ~1);  // even: chunks start on odd planes (coarse ring schedule)
     const bool pr = coarse != nullptr;
     switch (zsweep_variant()) {
         case 1: launch_zsweep_t<64, 4, 256>(lv, a, pr, s); break;
@@ -294,10 +294,11 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
     a.fc = fc;
     a.xc = xc;
     a.S = lf.S;
-    const char* kz = getenv("MGMC_ZR_KZ");
-    a.kz = kz ? atoi(kz) : 8;
     a.ntx = (lc.L.nx - 1 + CX - 1) / CX;
     a.nty = (lc.L.ny - 1 + CY - 1) / CY;
+    // 8 coarse planes per workgroup, fewer on small levels so the grid still fills the chip
+    const char* kz = getenv("MGMC_ZR_KZ");
+    a.kz = kz ? atoi(kz) : ((long long)a.ntx * a.nty * (lc.L.nz - 1) >= 8 * 1024 ? 8 : 2);
     a.ntz = (lc.L.nz - 1 + a.kz - 1) / a.kz;
     const int nt = a.ntx * a.nty * a.ntz;
     const int nb = (nt + 7) / 8 * 8;
@@ -306,7 +307,7 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
 
 void launch_residual_restrict(const Level& lf, const Level& lc, const double* x, const double* f, double* fc,
                               double* xc, int zero_xc, hipStream_t s) {
-    if (lf.spec.dim == 3 && zero_xc && getenv("MGMC_NO_ZRESTRICT") == nullptr && lc.L.nx >= 128) {
+    if (lf.spec.dim == 3 && zero_xc && getenv("MGMC_NO_ZRESTRICT") == nullptr && lc.L.nx >= 32) {
         const int v = getenv("MGMC_ZR_VARIANT") ? atoi(getenv("MGMC_ZR_VARIANT")) : 0;
         if (lf.spec.npoints == 7) {
             if (v == 1) launch_zresrestrict_t<7, 32, 4, 128>(lf, lc, x, f, fc, xc, s);

@@ -2,13 +2,21 @@
 //
 //   f_c = R (f - A x),  x_c = 0           (sampler/multigridmc_sampler.cc:118-122)
 //
-// Each workgroup owns CX x CY coarse points and marches a chunk of coarse planes K.  The fine
-// residual r = f - A x is evaluated exactly once per fine vertex (plus a one-vertex tile overlap)
-// into an LDS ring of three residual planes (fine planes 2K-1, 2K, 2K+1; plane 2K+1 is reused by
-// coarse plane K+1), from x planes staged in an LDS ring with a one-vertex halo.  The restriction
-// then reads the 3^3 weighted residuals from LDS.  Arithmetic is the reference's, in the
-// reference's order (A x ascending from 0.0, r = f - Ax, restriction sum sigma with x fastest),
-// so f_c is bitwise equal to k_residual_restrict and to the CPU oracle.
+// Each workgroup owns CX x CY coarse points and marches fine planes k = 2K0-1 .. 2K1-1 of a chunk
+// of coarse planes [K0, K1).  Per fine plane: the residual r = f - A x of the plane is evaluated
+// once per fine vertex (plus a one-vertex tile overlap) into one LDS plane, from x planes staged in
+// a 3-slot LDS ring with a one-vertex halo; then every coarse point adds the 9 weighted residuals of
+// its 3x3 fine neighbourhood in that plane to a register accumulator.  The restriction sums over
+// (sz, sy, sx) with sz outermost, so plane-by-plane accumulation adds exactly the reference's terms
+// in the reference's order: fine plane 2K-1 is sz = 0 of coarse plane K, 2K is sz = 1, and 2K+1 is
+// sz = 2 of K (which is then final) and sz = 0 of K+1.  Arithmetic is the reference's (A x ascending
+// from 0.0, r = f - Ax, restriction weights multiplied x, y, z), so f_c is bitwise equal to
+// k_residual_restrict and to the CPU oracle.
+//
+// LDS rows are colour-split as in mgmc_zsweep.hpp -- [odd positions | even positions | pad] -- so
+// lanes owning consecutive pairs (residual) or consecutive coarse points (restriction) read
+// consecutive doubles.  All global loads are unconditional: rows / planes outside the level are
+// clamped onto the zero boundary rows / planes, columns past a row end land in the zero padding.
 // Global traffic: x and f once (16 B per fine vertex) + f_c, x_c (2 B per fine vertex).
 #pragma once
 #include "mgmc_kernels.hpp"
@@ -28,16 +36,21 @@ struct ZRestrictArgs {
 
 template <int NPTS, int CX, int CY, int NT>
 __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
-    // fine x range of the residual region: [2*I0-1, 2*I0+2*CX-1]; as pairs starting at odd
-    // positions: RP = CX+1 pairs.  x is staged with one more vertex on each side: positions
-    // [2*I0-3, 2*I0+2*CX+2] = XP = CX+3 pairs (starting at an odd position).
-    constexpr int RP = CX + 1, RW = 2 * RP;      // residual row: pairs / doubles
+    // fine x range of the residual region: [2*I0-1, 2*I0+2*CX-1] = RP pairs from an odd position.
+    // x is staged with one more vertex on each side: positions [2*I0-3, 2*I0+2*CX+2] = XPP pairs.
+    constexpr int RP = CX + 1;                   // residual pairs per row
     constexpr int RR = 2 * CY + 1;               // residual rows
-    constexpr int XPP = CX + 3, XW = 2 * XPP;    // x row: pairs / doubles
+    constexpr int RSr = 2 * RP + 2;              // residual row stride (odd | even | pad)
+    constexpr int XPP = CX + 3;                  // x pairs per row
     constexpr int XR = 2 * CY + 3;               // x rows
+    constexpr int XS = 2 * XPP + 2;              // x row stride (odd | even | pad)
+    constexpr int XPS = XR * XS;                 // x plane
+    constexpr int NLX = (XR * XPP + NT - 1) / NT;  // x pair loads per plane per thread
+    constexpr int NLR = (RR * RP + NT - 1) / NT;   // residual pair items per plane per thread
+    constexpr int NCP = (CX * CY + NT - 1) / NT;   // coarse points per thread
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* xs = smem;                 // [4][XR][XW] x planes
-    double* rs = xs + 4 * XR * XW;     // [3][RR][RW] residual planes
+    double* xs = smem;                 // [3][XR][XS] x planes k-1, k, k+1
+    double* rs = xs + 3 * XPS;         // [RR][RSr] residual of plane k
 
     const Layout& Lf = a.Lf;
     const Layout& Lc = a.Lc;
@@ -49,193 +62,190 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
     if (tzi >= a.ntz) return;
     const int I0 = 1 + txi * CX, J0 = 1 + tyi * CY;
     const int K0 = 1 + tzi * a.kz, K1 = min(K0 + a.kz, Lc.nz);  // coarse planes [K0, K1)
-    const int xi0 = 2 * I0 - 3;  // fine position of x column 0
+    const int xi0 = 2 * I0 - 3;  // fine position of x pair column 0 (odd)
     const int xj0 = 2 * J0 - 2;  // fine row of x row 0
-    const int ri0 = 2 * I0 - 1;  // fine position of r column 0
-    const int rj0 = 2 * J0 - 1;  // fine row of r row 0
+    const int ri0 = 2 * I0 - 1;  // fine position of residual pair column 0 (odd)
+    const int rj0 = 2 * J0 - 1;  // fine row of residual row 0
     const int tid = threadIdx.x;
 
-    auto xslot = [](int k) { return (k + 8) & 3; };
-    auto rslot = [](int k) { return (k + 9) % 3; };
-    auto fine_row_in = [&](int j) { return j >= 1 && j <= Lf.ny - 1; };
-    auto fine_plane_in = [&](int k) { return k >= 1 && k <= Lf.nz - 1; };
+    auto xslot = [](int k) { return (k + 9) % 3; };
+    auto clamp_row = [&](int j) { return j < 0 ? 0 : (j > Lf.ny ? Lf.ny : j); };
+    auto plane_ptr = [&](const double* v, int k) { return v + (long long)(k < 0 ? 0 : (k > Lf.nz ? Lf.nz : k)) * Lf.sp; };
 
-    // ---- register pipeline: x(2K+1), x(2K+2) and f(2K), f(2K+1) of step K are loaded during
-    // step K-1 (into registers) and deposited / consumed at step K ----
-    constexpr int NLX = (XR * XPP + NT - 1) / NT;  // x pair loads per plane per thread
-    constexpr int NLR = (RR * RP + NT - 1) / NT;   // residual pair items per plane per thread
-    long long xoff[NLX];
-    int xlds[NLX];
+    int xoff[NLX], xlds[NLX];
 #pragma unroll
     for (int u = 0; u < NLX; ++u) {
         const int it = tid + u * NT;
-        xoff[u] = -1;
+        xoff[u] = Lf.off + 1;  // spare threads load a zero pad pair and deposit nothing
         xlds[u] = -1;
         if (it < XR * XPP) {
             const int r = it / XPP, c2 = it - r * XPP;
-            const int j = xj0 + r;
-            xlds[u] = r * XW + 2 * c2;
-            if (fine_row_in(j)) xoff[u] = (long long)j * Lf.sx + (xi0 + 2 * c2) + Lf.off;
+            xlds[u] = r * XS + c2;
+            xoff[u] = (int)((long long)clamp_row(xj0 + r) * Lf.sx + (xi0 + 2 * c2) + Lf.off);
         }
     }
-    long long roff[NLR];
-    int rlds[NLR], rflag[NLR];
+    int roff[NLR], rlds[NLR], rflag[NLR], rxo[NLR];
 #pragma unroll
     for (int u = 0; u < NLR; ++u) {
         const int it = tid + u * NT;
-        roff[u] = -1;
+        roff[u] = Lf.off + 1;
         rlds[u] = -1;
         rflag[u] = 0;
+        rxo[u] = 0;
         if (it < RR * RP) {
             const int r = it / RP, c2 = it - r * RP;
             const int j = rj0 + r, i = ri0 + 2 * c2;
-            rlds[u] = r * RW + 2 * c2;
-            if (fine_row_in(j)) {
-                roff[u] = (long long)j * Lf.sx + i + Lf.off;
-                rflag[u] = ((i >= 1 && i <= Lf.nx - 1) ? 1 : 0) | ((i + 1 <= Lf.nx - 1) ? 2 : 0);
-            }
+            rlds[u] = r * RSr + c2;
+            rxo[u] = (r + 1) * XS + (c2 + 1);  // x LDS offset of the same odd vertex
+            roff[u] = (int)((long long)clamp_row(j) * Lf.sx + i + Lf.off);
+            const bool rin = j >= 1 && j <= Lf.ny - 1;
+            rflag[u] = (rin && i >= 1 && i <= Lf.nx - 1 ? 1 : 0) | (rin && i + 1 <= Lf.nx - 1 ? 2 : 0);
         }
     }
-    double2 px[2][NLX], pf[2][NLR];
-    auto issue_x = [&](int k, double2* dst) {
-        const bool kin = fine_plane_in(k);
-        const double* base = a.x + (long long)k * Lf.sp;
+    // coarse points: (I, J) and the residual LDS offset of the odd element left of the centre 2I
+    int cpo[NCP];
+    long long cpg[NCP];
+    bool cpin[NCP];
 #pragma unroll
-        for (int u = 0; u < NLX; ++u) {
-            dst[u] = make_double2(0.0, 0.0);
-            if (kin && xoff[u] >= 0) dst[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
-        }
+    for (int u = 0; u < NCP; ++u) {
+        const int it = tid + u * NT;
+        const int cy = it / CX, cx = it - cy * CX;
+        cpin[u] = it < CX * CY && I0 + cx <= Lc.nx - 1 && J0 + cy <= Lc.ny - 1;
+        cpo[u] = (2 * cy + 1) * RSr + cx;
+        cpg[u] = cpin[u] ? Lc.at(I0 + cx, J0 + cy, 0) : 0;
+    }
+
+    double2 px[NLX], pf[NLR];
+    auto issue_x = [&](int k) {
+        const double* base = plane_ptr(a.x, k);
+#pragma unroll
+        for (int u = 0; u < NLX; ++u) px[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
     };
-    auto deposit_x = [&](int k, const double2* src) {
-        double* dst = xs + xslot(k) * XR * XW;
+    auto deposit_x = [&](int k) {
+        double* dst = xs + xslot(k) * XPS;
 #pragma unroll
         for (int u = 0; u < NLX; ++u)
-            if (xlds[u] >= 0) *reinterpret_cast<double2*>(dst + xlds[u]) = src[u];
+            if (xlds[u] >= 0) {
+                dst[xlds[u]] = px[u].x;
+                dst[xlds[u] + XPP] = px[u].y;
+            }
     };
-    auto issue_f = [&](int k, double2* dst) {
-        const bool kin = fine_plane_in(k);
-        const double* base = a.f + (long long)k * Lf.sp;
+    auto issue_f = [&](int k) {
+        const double* base = plane_ptr(a.f, k);
 #pragma unroll
-        for (int u = 0; u < NLR; ++u) {
-            dst[u] = make_double2(0.0, 0.0);
-            if (kin && roff[u] >= 0) dst[u] = *reinterpret_cast<const double2*>(base + roff[u]);
-        }
+        for (int u = 0; u < NLR; ++u) pf[u] = *reinterpret_cast<const double2*>(base + roff[u]);
     };
     // residual of fine plane k over the residual region (vertices outside the fine interior -> 0)
-    auto residual = [&](int k, const double2* fv) {
-        double* dst = rs + rslot(k) * RR * RW;
-        const bool kin = fine_plane_in(k);
-        const double* xm = xs + xslot(k - 1) * XR * XW;
-        const double* x0 = xs + xslot(k) * XR * XW;
-        const double* xp = xs + xslot(k + 1) * XR * XW;
+    auto residual = [&](int k, const double2 (&fv)[NLR]) {
+        const bool kin = k >= 1 && k <= Lf.nz - 1;
+        const double* pl[3] = {xs + xslot(k - 1) * XPS, xs + xslot(k) * XPS, xs + xslot(k + 1) * XPS};
 #pragma unroll
         for (int u = 0; u < NLR; ++u) {
             if (rlds[u] < 0) continue;
-            double2 out = make_double2(0.0, 0.0);
-            if (kin) {
 #pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    if (!(rflag[u] & (1 << e))) continue;
-                    const int r = rlds[u] / RW, c = rlds[u] - r * RW + e;
-                    const int o = (r + 1) * XW + c + 2;  // x LDS offset of the same vertex
+            for (int e = 0; e < 2; ++e) {
+                double out = 0.0;
+                if (kin && (rflag[u] & (1 << e))) {
+                    const int o = rxo[u] + (e ? XPP : 0);
+                    const int xm = e ? o - XPP : o + XPP - 1;  // x-1; x+1 is xm + 1
                     double y = 0.0;
                     if (NPTS == 7) {
-                        y += a.S.a[4] * xm[o];
-                        y += a.S.a[10] * x0[o - XW];
-                        y += a.S.a[12] * x0[o - 1];
-                        y += a.S.a[13] * x0[o];
-                        y += a.S.a[14] * x0[o + 1];
-                        y += a.S.a[16] * x0[o + XW];
-                        y += a.S.a[22] * xp[o];
+                        y += a.S.a[4] * pl[0][o];
+                        y += a.S.a[10] * pl[1][o - XS];
+                        y += a.S.a[12] * pl[1][xm];
+                        y += a.S.a[13] * pl[1][o];
+                        y += a.S.a[14] * pl[1][xm + 1];
+                        y += a.S.a[16] * pl[1][o + XS];
+                        y += a.S.a[22] * pl[2][o];
                     } else {
-                        const double* pl[3] = {xm, x0, xp};
 #pragma unroll
                         for (int dz = 0; dz < 3; ++dz)
 #pragma unroll
-                            for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-                                for (int dx = -1; dx <= 1; ++dx)
-                                    y += a.S.a[dz * 9 + (dy + 1) * 3 + (dx + 1)] * pl[dz][o + dy * XW + dx];
+                            for (int dy = -1; dy <= 1; ++dy) {
+                                const double* rowp = pl[dz] + dy * XS;
+                                y += a.S.a[dz * 9 + (dy + 1) * 3 + 0] * rowp[xm];
+                                y += a.S.a[dz * 9 + (dy + 1) * 3 + 1] * rowp[o];
+                                y += a.S.a[dz * 9 + (dy + 1) * 3 + 2] * rowp[xm + 1];
+                            }
                     }
-                    const double rv = (e == 0 ? fv[u].x : fv[u].y) - y;
-                    if (e == 0) out.x = rv; else out.y = rv;
+                    out = (e == 0 ? fv[u].x : fv[u].y) - y;
                 }
+                rs[rlds[u] + (e ? RP : 0)] = out;
             }
-            *reinterpret_cast<double2*>(dst + rlds[u]) = out;
         }
     };
-    auto restrict_plane = [&](int K) {
-        const double* rm = rs + rslot(2 * K - 1) * RR * RW;
-        const double* r0 = rs + rslot(2 * K) * RR * RW;
-        const double* rp = rs + rslot(2 * K + 1) * RR * RW;
-        const double* pl[3] = {rm, r0, rp};
-        for (int it = tid; it < CX * CY; it += NT) {
-            const int cy = it / CX, cx = it - cy * CX;
-            const int I = I0 + cx, J = J0 + cy;
-            if (I > Lc.nx - 1 || J > Lc.ny - 1) continue;
-            const int o = (2 * cy + 1) * RW + 2 * cx + 1;  // r LDS offset of fine (2I, 2J)
-            double result = 0.0;
+    // acc += the 9 terms (sy, sx ascending) of restriction plane index sz from the residual plane
+    auto accumulate = [&](double (&acc)[NCP], int sz) {
 #pragma unroll
-            for (int sz = 0; sz < 3; ++sz)
+        for (int u = 0; u < NCP; ++u) {
+            double result = acc[u];
 #pragma unroll
-                for (int sy = -1; sy <= 1; ++sy)
+            for (int sy = -1; sy <= 1; ++sy)
 #pragma unroll
-                    for (int sx = -1; sx <= 1; ++sx) {
-                        double w = 1.0;
-                        w *= w1(sx);
-                        w *= w1(sy);
-                        w *= w1(sz - 1);
-                        result += w * pl[sz][o + sy * RW + sx];
-                    }
-            const long long pc = Lc.at(I, J, K);
-            a.fc[pc] = result;
-            a.xc[pc] = 0.0;
+                for (int sx = -1; sx <= 1; ++sx) {
+                    double w = 1.0;
+                    w *= w1(sx);
+                    w *= w1(sy);
+                    w *= w1(sz - 1);
+                    result += w * rs[cpo[u] + sy * RSr + (sx < 0 ? 0 : (sx == 0 ? RP : 1))];
+                }
+            acc[u] = result;
         }
+    };
+    auto finish = [&](const double (&acc)[NCP], int K) {
+        const long long pk = (long long)K * Lc.sp;
+#pragma unroll
+        for (int u = 0; u < NCP; ++u)
+            if (cpin[u]) {
+                a.fc[pk + cpg[u]] = acc[u];
+                a.xc[pk + cpg[u]] = 0.0;
+            }
     };
 
-    // prologue: x planes 2K0-2 .. 2K0 and residual plane 2K0-1; step K0's loads in flight
-    issue_x(2 * K0 - 2, px[0]);
-    deposit_x(2 * K0 - 2, px[0]);
-    issue_x(2 * K0 - 1, px[0]);
-    deposit_x(2 * K0 - 1, px[0]);
-    issue_x(2 * K0, px[0]);
-    deposit_x(2 * K0, px[0]);
-    issue_f(2 * K0 - 1, pf[0]);
-    __syncthreads();
-    residual(2 * K0 - 1, pf[0]);
-    __syncthreads();  // the first deposit below overwrites the slot of x(2K0-2) read just above
-    issue_x(2 * K0 + 1, px[0]);
-    issue_x(2 * K0 + 2, px[1]);
-    issue_f(2 * K0, pf[0]);
-    issue_f(2 * K0 + 1, pf[1]);
-    for (int K = K0; K < K1; ++K) {
-        // x planes 2K-1, 2K in LDS; deposit 2K+1, 2K+2 (slots of 2K-3, 2K-2, free since the last barrier)
-        deposit_x(2 * K + 1, px[0]);
-        deposit_x(2 * K + 2, px[1]);
-        double2 fa[NLR], fb[NLR];
+    // One fine plane k: deposit x(k+1), issue x(k+2), f(k+1) | barrier | residual(k) | barrier |
+    // accumulate.  The next step's residual writes the residual plane only after its own first
+    // barrier, i.e. after every thread accumulated; x(k+2) overwrites the slot of x(k-1), last read
+    // by residual(k) before the second barrier.
+    double acc[NCP], accn[NCP];
+    double2 fcur[NLR];
+    auto step = [&](int k) __attribute__((always_inline)) {
+        deposit_x(k + 1);
 #pragma unroll
-        for (int u = 0; u < NLR; ++u) {
-            fa[u] = pf[0][u];
-            fb[u] = pf[1][u];
-        }
-        if (K + 1 < K1) {  // next step's loads, in flight during this step's compute
-            issue_x(2 * K + 3, px[0]);
-            issue_x(2 * K + 4, px[1]);
-            issue_f(2 * K + 2, pf[0]);
-            issue_f(2 * K + 3, pf[1]);
-        }
+        for (int u = 0; u < NLR; ++u) fcur[u] = pf[u];
+        issue_x(k + 2);
+        issue_f(k + 1);
         __syncthreads();
-        residual(2 * K, fa);
-        residual(2 * K + 1, fb);
+        residual(k, fcur);
         __syncthreads();
-        restrict_plane(K);
-        __syncthreads();
+    };
+    // prologue: x planes 2K0-2, 2K0-1 in LDS, x(2K0) and f(2K0-1) in flight
+    issue_x(2 * K0 - 2);
+    deposit_x(2 * K0 - 2);
+    issue_x(2 * K0 - 1);
+    deposit_x(2 * K0 - 1);
+    issue_x(2 * K0);
+    issue_f(2 * K0 - 1);
+#pragma unroll
+    for (int u = 0; u < NCP; ++u) acc[u] = 0.0;
+    step(2 * K0 - 1);
+    accumulate(acc, 0);  // sz = 0 of coarse plane K0
+    for (int K = K0; K < K1; ++K) {
+        step(2 * K);
+        accumulate(acc, 1);
+        step(2 * K + 1);
+        accumulate(acc, 2);
+        finish(acc, K);
+#pragma unroll
+        for (int u = 0; u < NCP; ++u) accn[u] = 0.0;
+        accumulate(accn, 0);  // sz = 0 of coarse plane K+1
+#pragma unroll
+        for (int u = 0; u < NCP; ++u) acc[u] = accn[u];
     }
 }
 
 inline size_t zrestrict_lds_bytes(int CX, int CY) {
-    const int XW = 2 * (CX + 3), XR = 2 * CY + 3, RW = 2 * (CX + 1), RR = 2 * CY + 1;
-    return (size_t)(4 * XR * XW + 3 * RR * RW) * sizeof(double);
+    const int XS = 2 * (CX + 3) + 2, XR = 2 * CY + 3, RSr = 2 * (CX + 1) + 2, RR = 2 * CY + 1;
+    return (size_t)(3 * XR * XS + RR * RSr) * sizeof(double);
 }
 
 }  // namespace mgmc

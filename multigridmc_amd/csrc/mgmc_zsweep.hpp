@@ -41,31 +41,6 @@ struct ZSweepArgs {
     int ntx, nty, ntz;         // tile counts
 };
 
-// prolongate-add gather of one fine vertex (identical arithmetic to k_prolongate_add)
-__device__ __forceinline__ double prolong_gather(double v, const double* __restrict__ xc, const Layout& Lc, int i,
-                                                 int j, int k, double alpha) {
-    const int i0 = i >> 1, j0 = j >> 1, k0 = k >> 1;
-    const int ni = (i & 1) ? 2 : 1, nj = (j & 1) ? 2 : 1, nk = (k & 1) ? 2 : 1;
-    for (int a = 0; a < nk; ++a) {
-        const int kk = k0 + a;
-        if (kk < 1 || kk > Lc.nz - 1) continue;
-        for (int b = 0; b < nj; ++b) {
-            const int jj = j0 + b;
-            if (jj < 1 || jj > Lc.ny - 1) continue;
-            for (int c = 0; c < ni; ++c) {
-                const int ii = i0 + c;
-                if (ii < 1 || ii > Lc.nx - 1) continue;
-                double w = 1.0;
-                w *= w1(i - 2 * ii);
-                w *= w1(j - 2 * jj);
-                w *= w1(k - 2 * kk);
-                v += alpha * w * xc[Lc.at(ii, jj, kk)];
-            }
-        }
-    }
-    return v;
-}
-
 // One pair item of a tile: LDS offset, plane-independent global offset, Philox pair base,
 // position parity and interior flags, all computed once per workgroup.
 struct ZItem {
@@ -106,6 +81,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         tab[128 + q] = LOGTAB_LO[q];
     }
     for (int q = threadIdx.x; q < 130; q += NT) tab[192 + q] = SINCOS_TAB[q];
+    // PROLONG: ring of two coarse planes (slot K & 1) over the tile's coarse footprint, coarse
+    // columns [q0-2, q0+XP+3] x rows [(j0-3)/2, (j0+TY+1)/2]
+    constexpr int CW = XP + 6, CR = TY / 2 + 3, CPS = CR * CW;
+    constexpr int NLC = PROLONG ? (CPS + NT - 1) / NT : 1;
+    double* cring = tab + 322;
 
     const Layout& L = a.L;
     // XCD-aware tile order: blocks b and b+8 share an XCD, give them neighbouring tiles
@@ -190,6 +170,68 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     // planes outside [0, nz] are clamped onto the zero boundary planes 0 / nz
     auto plane_base = [&](const double* v, int k) { return v + (long long)(k < 0 ? 0 : (k > L.nz ? L.nz : k)) * L.sp; };
 
+    // ---- PROLONG: coarse planes (loads one step ahead, deposited into the coarse ring) ----
+    const Layout& Lc = a.Lc;
+    const int Jst = (j0 - 2) >> 1;  // first coarse row of the footprint
+    int coff[NLC], clds[NLC];
+    double pcv[NLC];
+#pragma unroll
+    for (int u = 0; u < NLC; ++u) {
+        const int it = tid + u * NT;
+        clds[u] = (PROLONG && it < CPS) ? it : -1;
+        const int r = it / CW, c = it % CW;
+        const int jr = Jst + r;
+        const int jc = jr < 0 ? 0 : (jr > Lc.ny ? Lc.ny : jr);
+        coff[u] = clds[u] >= 0 ? (int)((long long)jc * Lc.sx + (q0 - 2 + c) + Lc.off) : Lc.off - 1;
+    }
+    auto issue_c = [&](int K) {
+        const double* base = a.xc + (long long)(K < 0 ? 0 : (K > Lc.nz ? Lc.nz : K)) * Lc.sp;
+#pragma unroll
+        for (int u = 0; u < NLC; ++u) pcv[u] = base[coff[u]];
+    };
+    auto deposit_c = [&](int K) {
+        double* dst = cring + (K & 1) * CPS;
+#pragma unroll
+        for (int u = 0; u < NLC; ++u)
+            if (clds[u] >= 0) dst[clds[u]] = pcv[u];
+    };
+    // x_old + alpha P x_c at the fine pair (i odd, i+1) of row j, plane k, from the coarse ring.  The
+    // same terms in the same order as k_prolongate_pairs: coarse parents in ascending (kk, jj, ii),
+    // each added as v += (alpha w) x_c, boundary parents skipped.
+    auto prolong_pair = [&](double2 v, int i, int j, int k, int cq) {
+        if (!(j >= 1 && j <= L.ny - 1)) return v;
+        const int q = (i - 1) >> 1;  // coarse index of the odd vertex's left parent (LDS column cq)
+        const bool in0 = i >= 1 && i <= L.nx - 1, in1 = i + 1 >= 1 && i + 1 <= L.nx - 1;
+        const int K0 = k >> 1, nk = (k & 1) ? 2 : 1;
+        const int J0 = j >> 1, nj = (j & 1) ? 2 : 1;
+        for (int aa = 0; aa < nk; ++aa) {
+            const int kk = K0 + aa;
+            if (kk < 1 || kk > Lc.nz - 1) continue;
+            const double* cp = cring + (kk & 1) * CPS;
+            for (int bb = 0; bb < nj; ++bb) {
+                const int jj = J0 + bb;
+                if (jj < 1 || jj > Lc.ny - 1) continue;
+                const double* row = cp + (jj - Jst) * CW + cq;
+                double w = 1.0;
+                w *= 0.5;
+                w *= w1(j - 2 * jj);
+                w *= w1(k - 2 * kk);
+                if (in0 && q >= 1) v.x += a.alpha * w * row[0];
+                if (q + 1 <= Lc.nx - 1) {
+                    if (in0) v.x += a.alpha * w * row[1];
+                    if (in1) {
+                        double w2 = 1.0;
+                        w2 *= 1.0;
+                        w2 *= w1(j - 2 * jj);
+                        w2 *= w1(k - 2 * kk);
+                        v.y += a.alpha * w2 * row[1];
+                    }
+                }
+            }
+        }
+        return v;
+    };
+
     // ---- global <-> LDS / registers ----
     double2 px[NLX];
     auto issue_x = [&](int k) {
@@ -205,10 +247,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
             double2 v = px[u];
             if (PROLONG && interior_plane(k)) {
                 const int c2 = xlds[u] % RS, r = xlds[u] / RS;
-                const int j = j0 - 2 + r, i = ibase + 2 * c2;
-                const bool rin = j >= 1 && j <= L.ny - 1;
-                if (rin && i >= 1 && i <= L.nx - 1) v.x = prolong_gather(v.x, a.xc, a.Lc, i, j, k, a.alpha);
-                if (rin && i + 1 >= 1 && i + 1 <= L.nx - 1) v.y = prolong_gather(v.y, a.xc, a.Lc, i + 1, j, k, a.alpha);
+                v = prolong_pair(v, ibase + 2 * c2, j0 - 2 + r, k, c2);
             }
             dst[xlds[u]] = v.x;
             dst[xlds[u] + WP] = v.y;
@@ -290,10 +329,17 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     // hand sides of plane p go to pk_out, those of plane p-1 come from pk_in; fb_in / fb_out hold the
     // first-colour values of planes p-2 / p-1 at the second-colour positions of planes p-1 / p.  The
     // loop runs the steps in pairs with the register sets swapped, so nothing is copied.
-    auto step = [&](int p, double2 (&fcur)[NC], double2 (&fnxt)[NC], double2 (&fhcur)[NH], double2 (&fhnxt)[NH],
-                    const double (&pk_in)[NC], double (&pk_out)[NC], const double (&fb_in)[NC],
+    // PROLONG, coarse ring: the deposit of fine plane p+1 reads coarse planes (p+1)>>1 .. (p+2)>>1;
+    // even steps (p even: chunks start on odd planes) issue coarse plane (p+4)/2, odd steps deposit it
+    // (its slot held plane (p-1)/2, last read at step p-1).
+    auto step = [&](int p, bool odd_step, double2 (&fcur)[NC], double2 (&fnxt)[NC], double2 (&fhcur)[NH],
+                    double2 (&fhnxt)[NH], const double (&pk_in)[NC], double (&pk_out)[NC], const double (&fb_in)[NC],
                     double (&fb_out)[NC]) __attribute__((always_inline)) {
         deposit_x(p + 1);
+        if (PROLONG) {
+            if (odd_step) deposit_c((p + 3) / 2);
+            else issue_c((p + 4) / 2);
+        }
         issue_x(p + 2);
 #pragma unroll
         for (int u = 0; u < NC; ++u) fnxt[u] = load_f(p + 1, ci[u]);
@@ -329,25 +375,39 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     double pkA[NC], pkB[NC], fbA[NC], fbB[NC];
 #pragma unroll
     for (int u = 0; u < NC; ++u) pkA[u] = pkB[u] = fbA[u] = fbB[u] = 0.0;
-    // prologue: planes k0-2, k0-1 in LDS, x(k0) and f(k0-1) in flight
+    // prologue: planes k0-2, k0-1 in LDS, x(k0) and f(k0-1) in flight (k0 is odd: tz even)
+    if (PROLONG) {  // coarse planes (k0-3)/2, (k0-1)/2 for the first two deposits, then (k0+1)/2
+        issue_c((k0 - 3) / 2);
+        deposit_c((k0 - 3) / 2);
+        issue_c((k0 - 1) / 2);
+        deposit_c((k0 - 1) / 2);
+        __syncthreads();
+    }
     issue_x(k0 - 2);
     deposit_x(k0 - 2);
     issue_x(k0 - 1);
     deposit_x(k0 - 1);
+    if (PROLONG) {
+        __syncthreads();
+        issue_c((k0 + 1) / 2);
+        deposit_c((k0 + 1) / 2);
+        __syncthreads();
+    }
     issue_x(k0);
 #pragma unroll
     for (int u = 0; u < NC; ++u) fA[u] = load_f(k0 - 1, ci[u]);
 #pragma unroll
     for (int u = 0; u < NH; ++u) fhA[u] = load_f(k0 - 1, hi[u]);
     for (int p = k0 - 1; p <= k1; p += 2) {
-        step(p, fA, fB, fhA, fhB, pkB, pkA, fbB, fbA);
-        if (p + 1 <= k1) step(p + 1, fB, fA, fhB, fhA, pkA, pkB, fbA, fbB);
+        step(p, false, fA, fB, fhA, fhB, pkB, pkA, fbB, fbA);
+        if (p + 1 <= k1) step(p + 1, true, fB, fA, fhB, fhA, pkA, pkB, fbA, fbB);
     }
 }
 
-inline size_t zsweep_lds_bytes(int XP, int TY) {
+inline size_t zsweep_lds_bytes(int XP, int TY, bool prolong) {
     const int RS = 2 * (XP + 4) + 2, R = TY + 4;
-    return (size_t)(3 * R * RS + 3 * 64 + 130) * sizeof(double);
+    const int coarse = prolong ? 2 * (TY / 2 + 3) * (XP + 6) : 0;
+    return (size_t)(3 * R * RS + 3 * 64 + 130 + coarse) * sizeof(double);
 }
 
 }  // namespace mgmc

@@ -26,8 +26,10 @@ print(json.dumps({"sweep_ms": ms, "GBps": 24 * lat.Nvertex / ms / 1e6, "vcycle_m
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 nlevel = int(sys.argv[2]) if len(sys.argv) > 2 else 7
 variants = []
-for v in (sys.argv[3].split(",") if len(sys.argv) > 3 else ["0", "5", "11"]):
+for v in (sys.argv[3].split(",") if len(sys.argv) > 3 else ["0"]):
     variants.append((f"zsweep-v{v}", {"MGMC_ZS_VARIANT": v}))
+variants.append(("zrestrict-v1-32x4", {"MGMC_ZR_VARIANT": "1"}))
+variants.append(("zrestrict-v2-64x4", {"MGMC_ZR_VARIANT": "2"}))
 for name, env in variants:
     e = dict(os.environ)
     e.update(env)

@@ -163,6 +163,23 @@ def test_zsweep_tile_variants_bitwise(hip_device, monkeypatch, variant):
     s.close()
 
 
+@pytest.mark.parametrize("name", ["3d128_zsweep", "3d_aniso_zsweep_ssor", "3d128_zsweep_odd"])
+def test_fused_prolongation_cycles_bitwise(hip_device, monkeypatch, name):
+    """MGMC_FUSE_PROLONG: the fine prolongate-add folded into the first post-sweep's plane loads gives
+    the oracle's cycle exactly."""
+    monkeypatch.setenv("MGMC_FUSE_PROLONG", "1")
+    shape, kw = CONFIGS[name]
+    s, p, lat = make(shape, **kw)
+    mc = oracle_for(s, p, lat)
+    f = np.random.default_rng(7).standard_normal(lat.Nvertex)
+    x_dev, x_orc = np.zeros(lat.Nvertex), np.zeros(lat.Nvertex)
+    for _ in range(2):
+        s.apply(f, x_dev)
+        mc.apply(f, x_orc)
+    assert np.array_equal(x_dev, x_orc)
+    s.close()
+
+
 def test_mgmc_seed_chain_independence(hip_device):
     a, p, lat = make((32, 32, 32))
     b, _, _ = make((32, 32, 32))
