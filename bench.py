@@ -19,7 +19,8 @@ Rank 0 prints ONE JSON line.  Field notes:
   value      = chains x K / max-over-ranks time (whole job, samples/s)
   roofline   = fine-level (level 0) Gibbs sweep: algorithmic 24 B/unknown (read x, read f,
                write x) x N0 / average sweep time, measured with HIP events on the library's
-               stream around the fine pre/post-sampler graph segments inside the timed region
+               stream around the fine pre-sampler graph segment (plain sweep kernel) inside the
+               timed region
   cpu_baseline = the CPU oracle (oracle/refcpu.cpp, FAITHFUL mode = the reference algorithm,
                1 thread) timed on a bounded sample of the same workload on rank 0 at N=1
 """

@@ -156,8 +156,9 @@ int mgmc_time_fine_sweeps(mgmc_handle* h, int nsweeps, float* ms);
 /* Same as mgmc_sample_async + synchronize, but each cycle is replayed as four graph segments
  * [fine pre-sampler | coarse-grid correction | fine post-sampler | QoI] with HIP events recorded
  * between them on the handle's stream.  *total_ms = first-to-last event time of the nsteps
- * cycles, *fine_ms = summed time of the fine-level (level 0) pre- and post-sampler segments,
- * *nfine = number of fine-level sweeps they contain. */
+ * cycles, *fine_ms = summed time of the fine-level (level 0) pre-sampler segments (plain Gibbs
+ * sweeps; the first post-sweep also carries the fused prolongation), *nfine = number of fine-level
+ * sweeps they contain. */
 int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* fine_ms,
                       int* nfine);
 

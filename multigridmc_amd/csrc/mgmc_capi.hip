@@ -192,8 +192,8 @@ int zsweep_variant() {
 // x-pairs per tile of the selected variant (the fine nx must be a multiple of 2 * xp)
 int zsweep_xp() {
     switch (zsweep_variant()) {
-        case 1: case 2: case 3: case 4: case 7: case 11: return 64;
-        case 5: case 6: case 8: case 9: return 32;
+        case 1: case 2: case 3: case 4: case 7: case 11: case 13: return 64;
+        case 5: case 6: case 8: case 9: case 12: return 32;
         default: return ZS_XP;
     }
 }
@@ -225,6 +225,8 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
         case 8: launch_zsweep_t<32, 12, 192>(lv, a, pr, s); break;
         case 9: launch_zsweep_t<32, 8, 256>(lv, a, pr, s); break;
         case 11: launch_zsweep_t<64, 16, 512, 4>(lv, a, pr, s); break;
+        case 12: launch_zsweep_t<32, 32, 512, 4>(lv, a, pr, s); break;
+        case 13: launch_zsweep_t<64, 32, 1024, 4>(lv, a, pr, s); break;
         default: launch_zsweep_t<ZS_XP, ZS_TY, ZS_NT, ZS_MINW>(lv, a, pr, s); break;
     }
 }
@@ -311,12 +313,12 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
         const int v = getenv("MGMC_ZR_VARIANT") ? atoi(getenv("MGMC_ZR_VARIANT")) : 0;
         if (lf.spec.npoints == 7) {
             if (v == 1) launch_zresrestrict_t<7, 32, 4, 128>(lf, lc, x, f, fc, xc, s);
-            else if (v == 2) launch_zresrestrict_t<7, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
-            else launch_zresrestrict_t<7, 32, 8, 256>(lf, lc, x, f, fc, xc, s);
+            else if (v == 3) launch_zresrestrict_t<7, 32, 8, 256>(lf, lc, x, f, fc, xc, s);
+            else launch_zresrestrict_t<7, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
         } else {
             if (v == 1) launch_zresrestrict_t<27, 32, 4, 128>(lf, lc, x, f, fc, xc, s);
-            else if (v == 2) launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
-            else launch_zresrestrict_t<27, 32, 8, 256>(lf, lc, x, f, fc, xc, s);
+            else if (v == 3) launch_zresrestrict_t<27, 32, 8, 256>(lf, lc, x, f, fc, xc, s);
+            else launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
         }
         return;
     }
@@ -707,7 +709,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     hipMemcpyAsync(h->ctrl, ctrl0, sizeof(ctrl0), hipMemcpyHostToDevice, h->stream);
     hipMemsetAsync(h->mom, 0, 4 * sizeof(double), h->stream);
     // op sequence of one sample
-    h->fuse_prolong = getenv("MGMC_FUSE_PROLONG") != nullptr;
+    h->fuse_prolong = getenv("MGMC_NO_FUSE_PROLONG") == nullptr;  // default: fused (A/B in DESIGN.md)
     uint32_t tag = 0;
     std::vector<int> cur(specs.size(), 0);
     build_ops_level(h, 0, tag, cur);
@@ -1079,17 +1081,15 @@ int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* tot
     HIPCHK(h, hipEventSynchronize(ev[4 * nsteps]));
     float t = 0.f;
     double fine = 0.0;
-    for (int s = 0; s < nsteps; ++s) {
+    for (int s = 0; s < nsteps; ++s) {  // pre-sampler segment: plain fine sweeps only
         HIPCHK(h, hipEventElapsedTime(&t, ev[4 * s], ev[4 * s + 1]));
-        fine += t;
-        HIPCHK(h, hipEventElapsedTime(&t, ev[4 * s + 2], ev[4 * s + 3]));
         fine += t;
     }
     HIPCHK(h, hipEventElapsedTime(&t, ev[0], ev[4 * nsteps]));
     *total_ms = t;
     *fine_ms = fine;
     int cnt = 0;
-    for (size_t q = 0; q < h->ops.size(); ++q)
+    for (size_t q = 0; q < h->seg_end_pre; ++q)
         if (h->ops[q].kind == OP_SWEEP && h->ops[q].level == 0) ++cnt;
     *nfine = cnt * nsteps;
     for (auto& e : ev) hipEventDestroy(e);

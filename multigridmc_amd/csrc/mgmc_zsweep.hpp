@@ -51,9 +51,21 @@ struct ZItem {
 };
 
 // MGMC_ZS_EXP (timing experiments only, scripts/build_exp.sh; 0 in the product): 1 no Box-Muller,
-// 2 no halo ring, 3 no Philox, 4 no stencil, 5 memory skeleton (1 + 2 + 4)
+// 2 no halo ring, 3 no Philox, 4 no stencil, 5 memory skeleton (1 + 2 + 4), 6 no step barriers
+// (wrong results: sync cost only)
 #ifndef MGMC_ZS_EXP
 #define MGMC_ZS_EXP 0
+#endif
+#ifndef MGMC_ZS_NT_STORE
+#define MGMC_ZS_NT_STORE 1
+#endif
+#ifndef MGMC_ZS_NT_F
+#define MGMC_ZS_NT_F 0
+#endif
+#if MGMC_ZS_EXP == 6
+#define ZS_STEP_SYNC() ((void)0)
+#else
+#define ZS_STEP_SYNC() __syncthreads()
 #endif
 // MINW: minimum waves per SIMD the register allocation must allow (1 = unconstrained)
 template <int XP, int TY, int NT, bool PROLONG, int MINW>
@@ -198,7 +210,37 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     // x_old + alpha P x_c at the fine pair (i odd, i+1) of row j, plane k, from the coarse ring.  The
     // same terms in the same order as k_prolongate_pairs: coarse parents in ascending (kk, jj, ii),
     // each added as v += (alpha w) x_c, boundary parents skipped.
+    // tiles whose whole footprint (x region, rows, chunk planes) keeps 2 vertices off the boundary
+    // -- every fine vertex and all its coarse parents interior -- take a check-free path
+    const bool prolong_fast = PROLONG && ibase >= 3 && ibase + 2 * WP - 1 <= L.nx - 2 && j0 - 2 >= 2 &&
+                              j0 + TY + 1 <= L.ny - 2 && k0 - 2 >= 2 && k1 + 1 <= L.nz - 2;
     auto prolong_pair = [&](double2 v, int i, int j, int k, int cq) {
+        if (prolong_fast) {  // every fine vertex and every coarse parent is interior
+            const int K0 = k >> 1, J0 = j >> 1;
+            const bool kodd = k & 1, jodd = j & 1;
+#pragma unroll
+            for (int aa = 0; aa < 2; ++aa) {
+                if (aa == 1 && !kodd) break;
+                const double* cp = cring + ((K0 + aa) & 1) * CPS + (J0 - Jst) * CW + cq;
+#pragma unroll
+                for (int bb = 0; bb < 2; ++bb) {
+                    if (bb == 1 && !jodd) break;
+                    const double c0 = cp[bb * CW], c1 = cp[bb * CW + 1];
+                    double w = 1.0;
+                    w *= 0.5;
+                    w *= jodd ? 0.5 : 1.0;
+                    w *= kodd ? 0.5 : 1.0;
+                    double w2 = 1.0;
+                    w2 *= 1.0;
+                    w2 *= jodd ? 0.5 : 1.0;
+                    w2 *= kodd ? 0.5 : 1.0;
+                    v.x += a.alpha * w * c0;
+                    v.x += a.alpha * w * c1;
+                    v.y += a.alpha * w2 * c1;
+                }
+            }
+            return v;
+        }
         if (!(j >= 1 && j <= L.ny - 1)) return v;
         const int q = (i - 1) >> 1;  // coarse index of the odd vertex's left parent (LDS column cq)
         const bool in0 = i >= 1 && i <= L.nx - 1, in1 = i + 1 >= 1 && i + 1 <= L.nx - 1;
@@ -253,7 +295,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
             dst[xlds[u] + WP] = v.y;
         }
     };
-    auto load_f = [&](int k, const ZItem& t) { return *reinterpret_cast<const double2*>(plane_base(a.f, k) + t.goff); };
+    auto load_f = [&](int k, const ZItem& t) {
+        const double* q = plane_base(a.f, k) + t.goff;
+        if (MGMC_ZS_NT_F) return make_double2(__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1));
+        return *reinterpret_cast<const double2*>(q);
+    };
 
     // fma-chain stencil sum (ascending column order) at LDS offset o of plane k.  The fine FD
     // stencil is symmetric (launch_zsweep checks a[4]=a[22], a[10]=a[16], a[12]=a[14]), so four
@@ -345,7 +391,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         for (int u = 0; u < NC; ++u) fnxt[u] = load_f(p + 1, ci[u]);
 #pragma unroll
         for (int u = 0; u < NH; ++u) fhnxt[u] = load_f(p + 1, hi[u]);
-        __syncthreads();
+        ZS_STEP_SYNC();
         if (interior_plane(p)) {
 #pragma unroll
             for (int u = 0; u < NC; ++u) pk_out[u] = first_pair(p, ci[u], fcur[u]);
@@ -353,7 +399,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
             for (int u = 0; u < NH; ++u)
                 if (MGMC_ZS_EXP != 2 && MGMC_ZS_EXP != 5) (void)first_pair(p, hi[u], fhcur[u]);
         }
-        __syncthreads();
+        ZS_STEP_SYNC();
         const int k = p - 1;
         const bool own = k >= k0 && k < k1;  // a core plane of this tile (interior)
         double sv[NC];
@@ -365,10 +411,17 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
             const int ef = (((ci[u].flags >> 3) ^ k) & 1) == fc ? 0 : 1;  // first-colour element on plane k
             const double fv = xs[slot(k) * PS + ci[u].lds + (ef ? WP : 0)];
             fb_out[u] = fv;
-            if (own && (ci[u].flags & 1))
-                *reinterpret_cast<double2*>(base + ci[u].goff) = ef == 0 ? make_double2(fv, sv[u]) : make_double2(sv[u], fv);
+            if (own && (ci[u].flags & 1)) {
+                const double2 out = ef == 0 ? make_double2(fv, sv[u]) : make_double2(sv[u], fv);
+                if (MGMC_ZS_NT_STORE) {  // streaming store: keep the write stream out of L2
+                    __builtin_nontemporal_store(out.x, base + ci[u].goff);
+                    __builtin_nontemporal_store(out.y, base + ci[u].goff + 1);
+                } else {
+                    *reinterpret_cast<double2*>(base + ci[u].goff) = out;
+                }
+            }
         }
-        __syncthreads();
+        ZS_STEP_SYNC();
     };
 
     double2 fA[NC], fB[NC], fhA[NH], fhB[NH];

@@ -16,7 +16,7 @@ print(min(s.time_fine_sweeps(10) / 10 for _ in range(3)))
 '''
 variants = sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "5", "11"]
 exps = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1", "2", "3", "4"]
-names = {"0": "product", "1": "no-BoxMuller", "2": "no-halo", "3": "no-Philox", "4": "no-stencil", "5": "skeleton"}
+names = {"0": "product", "1": "no-BoxMuller", "2": "no-halo", "3": "no-Philox", "4": "no-stencil", "5": "skeleton", "6": "no-barriers", "7": "nt-store", "8": "nt-f", "9": "nt-store+f"}
 tzs = os.environ.get("TZS", "32").split(",")
 aligns = os.environ.get("ALIGNS", "1").split(",")
 for v, x, tz, al in [(v, x, tz, al) for v in variants for x in exps for tz in tzs for al in aligns]:

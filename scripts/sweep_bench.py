@@ -28,8 +28,8 @@ nlevel = int(sys.argv[2]) if len(sys.argv) > 2 else 7
 variants = []
 for v in (sys.argv[3].split(",") if len(sys.argv) > 3 else ["0"]):
     variants.append((f"zsweep-v{v}", {"MGMC_ZS_VARIANT": v}))
-variants.append(("zrestrict-v1-32x4", {"MGMC_ZR_VARIANT": "1"}))
-variants.append(("zrestrict-v2-64x4", {"MGMC_ZR_VARIANT": "2"}))
+variants.append(("zrestrict-v3-32x8", {"MGMC_ZR_VARIANT": "3"}))
+variants.append(("no-fuse-prolong", {"MGMC_NO_FUSE_PROLONG": "1"}))
 for name, env in variants:
     e = dict(os.environ)
     e.update(env)

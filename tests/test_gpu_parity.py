@@ -145,7 +145,7 @@ def test_mgmc_cycles_bitwise(hip_device, name):
     s.close()
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "6", "7", "8", "9", "11"])
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "6", "7", "8", "9", "11", "12", "13"])
 def test_zsweep_tile_variants_bitwise(hip_device, monkeypatch, variant):
     """Every z-sweep tile shape (MGMC_ZS_VARIANT: 64x4, 64x8/512, 64x8, 64x16, 32x16, 32x24, 64x12,
     32x12, 32x8 unconstrained registers, 64x16/512; default 32x8 at 5 waves/SIMD) gives the oracle's multicolour cycle exactly, on a shape whose y/z extents do
@@ -164,10 +164,10 @@ def test_zsweep_tile_variants_bitwise(hip_device, monkeypatch, variant):
 
 
 @pytest.mark.parametrize("name", ["3d128_zsweep", "3d_aniso_zsweep_ssor", "3d128_zsweep_odd"])
-def test_fused_prolongation_cycles_bitwise(hip_device, monkeypatch, name):
-    """MGMC_FUSE_PROLONG: the fine prolongate-add folded into the first post-sweep's plane loads gives
-    the oracle's cycle exactly."""
-    monkeypatch.setenv("MGMC_FUSE_PROLONG", "1")
+def test_unfused_prolongation_cycles_bitwise(hip_device, monkeypatch, name):
+    """MGMC_NO_FUSE_PROLONG: the separate prolongate-add pass (instead of the default fold into the
+    first post-sweep's plane loads) gives the oracle's cycle exactly."""
+    monkeypatch.setenv("MGMC_NO_FUSE_PROLONG", "1")
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)
     mc = oracle_for(s, p, lat)
