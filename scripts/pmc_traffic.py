@@ -1,5 +1,5 @@
 """HBM traffic per fine-sweep launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) of
-scripts/sweep_once.py, corrected as MI355X_MICROARCH.md (HBM section) prescribes: counters are in KiB,
+scripts/vcycle_once.py (plain pre-sweep kernel instance inside V-cycles), corrected as MI355X_MICROARCH.md (HBM section) prescribes: counters are in KiB,
 and on gfx950 FETCH_SIZE reports half the bytes of 16-B-per-lane streaming reads (the z-sweep's loads
 are all 16-B double2 loads) -> FETCH x 2; WRITE_SIZE is exact for 16-B stores.
 
@@ -10,10 +10,12 @@ import json
 import sys
 
 KERNEL = "k_zsweep_rb7"
+PLAIN = ", false,"  # the plain sweep instance (PROLONG = false): the fine pre-sweep of the V-cycle
 
 
 def per_launch(path):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if KERNEL in r["Kernel_Name"]]
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if KERNEL in r["Kernel_Name"] and PLAIN in r["Kernel_Name"]]
     return sum(vals) / len(vals), len(vals)
 
 

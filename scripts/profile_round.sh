@@ -1,5 +1,6 @@
 # Round evidence on the GPU box: (optional) gpu tests, bench (with CPU baseline), rocprofv3 stats
-# of the bench command, PMC traffic of the fine sweep (separate FETCH_SIZE / WRITE_SIZE passes).
+# of the bench command, PMC traffic of the fine sweep inside V-cycles (separate FETCH_SIZE /
+# WRITE_SIZE passes; the plain pre-sweep kernel instance, as timed by bench.py).
 #   RUN_PYTEST=1 bash scripts/profile_round.sh     BENCH_ARGS="--cpu-samples 1"
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/round && export TMPDIR=/tmp
 O=gpurun_out/round
@@ -18,7 +19,7 @@ if [ -z "$SKIP_PROF" ]; then
   echo "rocprof rc=$rc"
   [ $rc -eq 0 ] || exit $rc
   for c in FETCH_SIZE WRITE_SIZE; do
-    K=6 timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $O/pmc_$c -o pmc -- python3 scripts/sweep_once.py > $O/pmc_$c.log 2>&1; rc=$?
+    K=6 timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $O/pmc_$c -o pmc -- python3 scripts/vcycle_once.py > $O/pmc_$c.log 2>&1; rc=$?
     echo "pmc $c rc=$rc"
     [ $rc -eq 0 ] || exit $rc
   done
