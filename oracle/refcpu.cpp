@@ -474,7 +474,19 @@ static void philox_normals(uint64_t seed, uint64_t chain, uint32_t pair, uint32_
 // Samplers
 // =============================================================================================
 enum Mode { FAITHFUL = 0, MULTICOLOUR = 1 };
+static const uint32_t LR_PAIR0 = 0xFFFFF000u;  // Philox pair ids of the low-rank noise (above any lattice pair)
 enum Direction { FORWARD = 1, BACKWARD = 2 };
+
+// Low-rank measurement part of a posterior operator (measured_operator.cc:9-49,
+// linear_operator.hh:187-197): B (N x m, sparse columns, rows ascending), Sigma (diagonal).  Coarse
+// levels carry B_c = R B (linear_operator.cc:15-19), Sigma_c = Sigma.  A column that covers every
+// vertex (the global average measurement and its restrictions) is "dense".
+struct LowRank {
+    int m = 0;
+    std::vector<std::vector<std::pair<int64_t, double>>> cols;
+    std::vector<char> dense;
+    std::vector<double> sigma;
+};
 
 struct Level {
     Lattice lat;
@@ -483,6 +495,7 @@ struct Level {
     std::vector<int> colour;  // per row
     std::vector<uint32_t> pair;
     std::vector<char> cos_branch;
+    LowRank lr;
 };
 
 struct Ctx {
@@ -531,11 +544,86 @@ static inline void sor_row_fused(const CSR& A, const double* wd, const double* b
     x[ell] = fma(wd[ell], b[ell] - s, x[ell]);
 }
 
+// ---- low-rank helpers ----
+// sum_i (sc B_ik) v_i.  FAITHFUL: sequential over the column's entries (the reference's sparse
+// products).  MULTICOLOUR (= device order): sparse columns sequential; dense columns nested as
+// row sums (i ascending) -> plane sums (rows ascending) -> total (planes ascending).
+static double lr_dot(const Level& L, int k, double sc, const double* v, Mode mode) {
+    const auto& col = L.lr.cols[k];
+    if (mode == FAITHFUL || !L.lr.dense[k]) {
+        double s = 0.0;
+        for (const auto& e : col) s += (sc * e.second) * v[e.first];
+        return s;
+    }
+    const Lattice& lat = L.lat;
+    const int64_t nxr = lat.n[0] - 1, nyr = lat.dim >= 2 ? lat.n[1] - 1 : 1, nzr = lat.dim == 3 ? lat.n[2] - 1 : 1;
+    double total = 0.0;
+    size_t q = 0;
+    for (int64_t kk = 0; kk < nzr; ++kk) {
+        double ps = 0.0;
+        for (int64_t jj = 0; jj < nyr; ++jj) {
+            double rs = 0.0;
+            for (int64_t ii = 0; ii < nxr; ++ii, ++q) rs += (sc * col[q].second) * v[col[q].first];
+            ps += rs;
+        }
+        total += ps;
+    }
+    return total;
+}
+// e = B s (e_i accumulates its columns in ascending k; Eigen's sparse-times-dense order)
+static void lr_expand(const Level& L, const double* s, double* e) {
+    std::fill(e, e + L.A.nrow, 0.0);
+    for (int k = 0; k < L.lr.m; ++k)
+        for (const auto& en : L.lr.cols[k]) e[en.first] += en.second * s[k];
+}
+// y = A x + B (Sigma^{-1} B^T x)  (linear_operator.hh:66-76); t_k in lr_dot order with the
+// Sigma^{-1}-scaled column values of Sigma_inv_BT (measured_operator.cc:48)
+static void posterior_apply(const Level& L, const double* x, double* y, Mode mode) {
+    spmv(L.A, x, y);
+    if (L.lr.m == 0) return;
+    std::vector<double> t(L.lr.m), g(L.A.nrow);
+    for (int k = 0; k < L.lr.m; ++k) t[k] = lr_dot(L, k, 1.0 / L.lr.sigma[k], x, mode);
+    lr_expand(L, t.data(), g.data());
+    for (int64_t i = 0; i < L.A.nrow; ++i) y[i] += g[i];
+}
+
+// inverse of a small dense matrix (row-major m x m): Gauss-Jordan with partial pivoting
+static std::vector<double> small_inverse(std::vector<double> M, int m) {
+    std::vector<double> I((size_t)m * m, 0.0);
+    for (int i = 0; i < m; ++i) I[(size_t)i * m + i] = 1.0;
+    for (int c = 0; c < m; ++c) {
+        int piv = c;
+        for (int r = c + 1; r < m; ++r)
+            if (fabs(M[(size_t)r * m + c]) > fabs(M[(size_t)piv * m + c])) piv = r;
+        if (piv != c)
+            for (int q = 0; q < m; ++q) {
+                std::swap(M[(size_t)c * m + q], M[(size_t)piv * m + q]);
+                std::swap(I[(size_t)c * m + q], I[(size_t)piv * m + q]);
+            }
+        const double d = M[(size_t)c * m + c];
+        for (int q = 0; q < m; ++q) {
+            M[(size_t)c * m + q] /= d;
+            I[(size_t)c * m + q] /= d;
+        }
+        for (int r = 0; r < m; ++r) {
+            if (r == c) continue;
+            const double f = M[(size_t)r * m + c];
+            for (int q = 0; q < m; ++q) {
+                M[(size_t)r * m + q] -= f * M[(size_t)c * m + q];
+                I[(size_t)r * m + q] -= f * I[(size_t)c * m + q];
+            }
+        }
+    }
+    return I;
+}
+
 struct SORSmoother {
     const Level* L;
     double omega;
     Direction direction;
     std::vector<double> diag, wd;
+    mutable std::vector<double> bbar;  // N x m row-major; built on first use (low-rank operators)
+    mutable Mode bbar_mode = FAITHFUL;
     SORSmoother(const Level* L_, double omega_, Direction d) : L(L_), omega(omega_), direction(d) {
         diag.resize(L->A.nrow);
         wd.resize(L->A.nrow);
@@ -544,7 +632,66 @@ struct SORSmoother {
             wd[r] = omega / diag[r];
         }
     }
+    // bar(B) = (L + D/omega)^{-1} B (Sigma + B^T (L + D/omega)^{-1} B)^{-1} (forward; L^T backward),
+    // sor_smoother.cc:17-37.  The triangular solves: FAITHFUL = lexicographic substitution (the
+    // reference's split), MULTICOLOUR = one noise-free multicolour sweep from zero in this
+    // smoother's colour order (the split of the multicolour sweep; the device computes the same).
+    void build_bbar(Mode mode) const {
+        const int m = L->lr.m;
+        const int64_t n = L->A.nrow;
+        std::vector<double> Y((size_t)n * m), b(n), y(n);
+        for (int l = 0; l < m; ++l) {
+            std::fill(b.begin(), b.end(), 0.0);
+            for (const auto& e : L->lr.cols[l]) b[e.first] = e.second;
+            std::fill(y.begin(), y.end(), 0.0);
+            if (mode == FAITHFUL) {
+                const CSR& A = L->A;
+                for (int64_t e_ = 0; e_ < n; ++e_) {
+                    const int64_t i = direction == FORWARD ? e_ : n - 1 - e_;
+                    double s = b[i];
+                    for (int64_t q = A.rowptr[i]; q < A.rowptr[i + 1]; ++q) {
+                        const int64_t j = A.col[q];
+                        if (direction == FORWARD ? j < i : j > i) s -= A.val[q] * y[j];
+                    }
+                    y[i] = s / (diag[i] + (1. - omega) / omega * diag[i]);
+                }
+            } else {
+                sweep(MULTICOLOUR, b.data(), y.data());
+            }
+            for (int64_t i = 0; i < n; ++i) Y[(size_t)i * m + l] = y[i];
+        }
+        std::vector<double> M((size_t)m * m), col(n);
+        for (int l = 0; l < m; ++l) {
+            for (int64_t i = 0; i < n; ++i) col[i] = Y[(size_t)i * m + l];
+            for (int k = 0; k < m; ++k) M[(size_t)k * m + l] = (k == l ? L->lr.sigma[k] : 0.0) + lr_dot(*L, k, 1.0, col.data(), mode);
+        }
+        const std::vector<double> Minv = small_inverse(M, m);
+        bbar.assign((size_t)n * m, 0.0);
+        for (int64_t i = 0; i < n; ++i)
+            for (int k = 0; k < m; ++k) {
+                double u = 0.0;
+                for (int l = 0; l < m; ++l)
+                    u = mode == FAITHFUL ? u + Y[(size_t)i * m + l] * Minv[(size_t)l * m + k]
+                                         : fma(Y[(size_t)i * m + l], Minv[(size_t)l * m + k], u);
+                bbar[(size_t)i * m + k] = u;
+            }
+        bbar_mode = mode;
+    }
+    // SORSmoother::apply (sor_smoother.cc:41-53): sweep, then x -= bar(B) (B^T x)
     void apply(Mode mode, const double* b, double* x) const {
+        sweep(mode, b, x);
+        const int m = L->lr.m;
+        if (m == 0) return;
+        if (bbar.empty() || bbar_mode != mode) build_bbar(mode);
+        std::vector<double> w(m);
+        for (int k = 0; k < m; ++k) w[k] = lr_dot(*L, k, 1.0, x, mode);
+        for (int64_t i = 0; i < L->A.nrow; ++i) {
+            double u = 0.0;
+            for (int k = 0; k < m; ++k) u = mode == FAITHFUL ? u + bbar[(size_t)i * m + k] * w[k] : fma(bbar[(size_t)i * m + k], w[k], u);
+            x[i] = x[i] - u;
+        }
+    }
+    void sweep(Mode mode, const double* b, double* x) const {
         const int64_t nrow = L->A.nrow;
         if (mode == FAITHFUL) {
             for (int64_t e_ = 0; e_ < nrow; ++e_) {
@@ -594,13 +741,35 @@ struct SORSampler : Sampler {
                     const double tmp = sqrt_precision_diag[ell];
                     c_rhs[ell] = tmp * normal_dist(ctx->rng) + f[ell];
                 }
+                if (L->lr.m > 0) {  // c += (B Sigma^{-1/2}) xi' (sor_sampler.cc:48-56)
+                    std::vector<double> xi(L->lr.m), e(n, 0.0);
+                    for (int k = 0; k < L->lr.m; ++k) xi[k] = normal_dist(ctx->rng);
+                    for (int k = 0; k < L->lr.m; ++k) {
+                        const double s = sqrt(1.0 / L->lr.sigma[k]);
+                        for (const auto& en : L->lr.cols[k]) e[en.first] += (en.second * s) * xi[k];
+                    }
+                    for (int64_t ell = 0; ell < n; ++ell) c_rhs[ell] += e[ell];
+                }
             } else {
                 const uint32_t tag = ctx->tag++;
+                // low-rank noise first: f_eff = f + B Sigma^{-1/2} xi', xi'_k from Philox pair
+                // LR_PAIR0 + k/2 (cos for even k) of this sweep's tag; c = fma(sd, xi, f_eff)
+                std::vector<double> feff(f, f + n);
+                if (L->lr.m > 0) {
+                    std::vector<double> sv(L->lr.m), e(n);
+                    for (int k = 0; k < L->lr.m; ++k) {
+                        double z0, z1;
+                        philox_normals(ctx->seed, ctx->chain, LR_PAIR0 + (uint32_t)(k >> 1), tag, ctx->sample, z0, z1);
+                        sv[k] = sqrt(1.0 / L->lr.sigma[k]) * ((k & 1) ? z1 : z0);
+                    }
+                    lr_expand(*L, sv.data(), e.data());
+                    for (int64_t ell = 0; ell < n; ++ell) feff[ell] = f[ell] + e[ell];
+                }
                 for (int64_t ell = 0; ell < n; ++ell) {
                     double z0, z1;
                     philox_normals(ctx->seed, ctx->chain, L->pair[ell], tag, ctx->sample, z0, z1);
                     const double xi = L->cos_branch[ell] ? z0 : z1;
-                    c_rhs[ell] = fma(sqrt_precision_diag[ell], xi, f[ell]);
+                    c_rhs[ell] = fma(sqrt_precision_diag[ell], xi, feff[ell]);
                 }
             }
             smoother.apply(ctx->mode, c_rhs.data(), x);
@@ -632,6 +801,17 @@ struct DenseCholeskySampler : Sampler {
         Lmat.assign((size_t)n * n, 0.0);
         for (int64_t r = 0; r < n; ++r)
             for (int64_t q = L->A.rowptr[r]; q < L->A.rowptr[r + 1]; ++q) Lmat[(size_t)r * n + L->A.col[q]] = L->A.val[q];
+        if (L->lr.m > 0) {  // A += B Sigma^{-1} B^T (cholesky_sampler.cc:30-36)
+            std::vector<double> Bd((size_t)n * L->lr.m, 0.0);
+            for (int k = 0; k < L->lr.m; ++k)
+                for (const auto& e : L->lr.cols[k]) Bd[(size_t)e.first * L->lr.m + k] = e.second;
+            for (int64_t i = 0; i < n; ++i)
+                for (int64_t j = 0; j < n; ++j) {
+                    double s = 0.0;
+                    for (int k = 0; k < L->lr.m; ++k) s += Bd[(size_t)i * L->lr.m + k] / L->lr.sigma[k] * Bd[(size_t)j * L->lr.m + k];
+                    Lmat[(size_t)i * n + j] += s;
+                }
+        }
         for (int64_t j = 0; j < n; ++j) {
             double d = Lmat[(size_t)j * n + j];
             for (int64_t k = 0; k < j; ++k) d -= Lmat[(size_t)j * n + k] * Lmat[(size_t)j * n + k];
@@ -742,7 +922,7 @@ struct MGMC : Sampler {
         const int cycle_ = (level > 0) ? p.cycle : 1;
         for (int j = 0; j < cycle_; ++j) {
             pre[level]->apply(f_ell[level].data(), x_ell[level].data());
-            spmv(levels[level]->A, x_ell[level].data(), r_ell[level].data());
+            posterior_apply(*levels[level], x_ell[level].data(), r_ell[level].data(), ctx->mode);
             for (size_t q = 0; q < r_ell[level].size(); ++q) r_ell[level][q] = f_ell[level][q] - r_ell[level][q];
             ig[level]->restrict_(r_ell[level].data(), f_ell[level + 1].data());
             std::fill(x_ell[level + 1].begin(), x_ell[level + 1].end(), 0.0);
@@ -821,6 +1001,7 @@ orc_handle* orc_create_fd(const orc_params* q, int mode, uint64_t seed, uint64_t
 // Generic fine operator given as CSR on a 1D/2D/3D lattice (e.g. test_sampler.hh TestOperator1d)
 orc_handle* orc_create_csr(const orc_params* q, int mode, uint64_t seed, int64_t nrow, const int64_t* rowptr,
                            const int32_t* col, const double* val) {
+    if (mode == MULTICOLOUR && q->dim < 2) return nullptr;  // colour / pair maps exist for 2D / 3D only
     orc_handle* h = new orc_handle();
     h->ctx.mode = (Mode)mode;
     h->ctx.rng.seed(seed);
@@ -894,7 +1075,66 @@ void orc_mean_cov(orc_handle* h, const double* f, int nwarmup, int64_t nsamples,
     }
 }
 
-void orc_operator_apply(orc_handle* h, int level, const double* x, double* y) { spmv(h->mg->levels[level]->A, x, y); }
+void orc_operator_apply(orc_handle* h, int level, const double* x, double* y) {
+    posterior_apply(*h->mg->levels[level], x, y, h->ctx.mode);
+}
+
+// Low-rank measurement part of the fine operator (MeasuredOperator): m columns of B as CSC
+// (colptr[m+1], rows ascending in [0, N), values) and Sigma[m].  Coarse levels get B_c = R B
+// (linear_operator.cc:17) -- columns restricted as dense vectors; a column covering every vertex
+// stays dense, others keep their nonzeros -- and Sigma_c = Sigma.  The coarse Cholesky sampler, if
+// used, is rebuilt on the posterior precision.
+void orc_set_lowrank(orc_handle* h, int m, const int64_t* colptr, const int64_t* rows, const double* vals,
+                     const double* sigma) {
+    MGMC& mg = *h->mg;
+    for (size_t level = 0; level < mg.levels.size(); ++level) {
+        Level& L = *mg.levels[level];
+        L.lr = LowRank();
+        L.lr.m = m;
+        L.lr.sigma.assign(sigma, sigma + m);
+        L.lr.cols.resize(m);
+        L.lr.dense.resize(m);
+        const int64_t n = L.A.nrow;
+        if (level == 0) {
+            for (int k = 0; k < m; ++k) {
+                for (int64_t q = colptr[k]; q < colptr[k + 1]; ++q) L.lr.cols[k].push_back({rows[q], vals[q]});
+                L.lr.dense[k] = (colptr[k + 1] - colptr[k]) == n;
+            }
+        } else {
+            const Level& F = *mg.levels[level - 1];
+            std::vector<double> fine(F.A.nrow), coarse(n);
+            for (int k = 0; k < m; ++k) {
+                std::fill(fine.begin(), fine.end(), 0.0);
+                for (const auto& e : F.lr.cols[k]) fine[e.first] = e.second;
+                mg.ig[level - 1]->restrict_(fine.data(), coarse.data());
+                L.lr.dense[k] = F.lr.dense[k];
+                for (int64_t i = 0; i < n; ++i)
+                    if (L.lr.dense[k] || coarse[i] != 0.0) L.lr.cols[k].push_back({i, coarse[i]});
+            }
+        }
+    }
+    if (mg.p.coarse_solver == 1) mg.coarse.reset(new DenseCholeskySampler(&h->ctx, mg.levels.back().get()));
+}
+
+// the low-rank columns of a level (CSC, reference layout) -- for host cross-checks
+int64_t orc_lowrank_nnz(orc_handle* h, int level) {
+    int64_t s = 0;
+    for (const auto& c : h->mg->levels[level]->lr.cols) s += (int64_t)c.size();
+    return s;
+}
+void orc_get_lowrank(orc_handle* h, int level, int64_t* colptr, int64_t* rows, double* vals) {
+    const LowRank& lr = h->mg->levels[level]->lr;
+    colptr[0] = 0;
+    int64_t q = 0;
+    for (int k = 0; k < lr.m; ++k) {
+        for (const auto& e : lr.cols[k]) {
+            rows[q] = e.first;
+            vals[q] = e.second;
+            ++q;
+        }
+        colptr[k + 1] = q;
+    }
+}
 
 void orc_smoother_apply(orc_handle* h, int level, int direction, int nsweeps, const double* b, double* x) {
     SORSmoother s(h->mg->levels[level].get(), h->mg->p.omega, (Direction)direction);
@@ -922,7 +1162,7 @@ void orc_prolongate_add(orc_handle* h, int level, double alpha, const double* xc
 void orc_residual_restrict(orc_handle* h, int level, const double* f, const double* x, double* fc) {
     const CSR& A = h->mg->levels[level]->A;
     std::vector<double> r(A.nrow);
-    spmv(A, x, r.data());
+    posterior_apply(*h->mg->levels[level], x, r.data(), h->ctx.mode);
     for (int64_t q = 0; q < A.nrow; ++q) r[q] = f[q] - r[q];
     h->mg->ig[level]->restrict_(r.data(), fc);
 }

@@ -60,6 +60,9 @@ def lib():
             "orc_restrict": (None, [c_void_p, c_int, _DP, _DP]),
             "orc_prolongate_add": (None, [c_void_p, c_int, c_double, _DP, _DP]),
             "orc_residual_restrict": (None, [c_void_p, c_int, _DP, _DP, _DP]),
+            "orc_set_lowrank": (None, [c_void_p, c_int, POINTER(c_int64), POINTER(c_int64), _DP, _DP]),
+            "orc_lowrank_nnz": (c_int64, [c_void_p, c_int]),
+            "orc_get_lowrank": (None, [c_void_p, c_int, POINTER(c_int64), POINTER(c_int64), _DP]),
             "orc_philox_normals": (None, [c_uint64, c_uint64, c_uint64, c_int64, c_uint32, c_uint64, _DP]),
             "orc_philox_raw": (None, [POINTER(c_uint32), c_uint32, c_uint32, POINTER(c_uint32)]),
             "orc_ln_unit": (c_double, [c_double]),
@@ -135,6 +138,8 @@ class Oracle:
         h = lib().orc_create_csr(ctypes.byref(p), mode, seed, len(rowptr) - 1,
                                  rowptr.ctypes.data_as(POINTER(c_int64)), col.ctypes.data_as(POINTER(c_int32)),
                                  dp(val))
+        if not h:
+            raise ValueError("the multicolour order needs a 2D / 3D lattice")
         return cls(h, p)
 
     def __del__(self):
@@ -221,6 +226,24 @@ class Oracle:
         out = np.ascontiguousarray(x, dtype=np.float64).copy()
         self.L.orc_prolongate_add(self.h, level, alpha, dp(xc), dp(out))
         return out
+
+    def set_lowrank(self, lr):
+        """lr: multigridmc_amd.measured.LowRankUpdate (B as CSC, Sigma)."""
+        self._lr = lr  # keep the arrays alive for the call
+        P = POINTER(c_int64)
+        self.L.orc_set_lowrank(self.h, lr.m, lr.colptr.ctypes.data_as(P), lr.rows.ctypes.data_as(P),
+                               dp(lr.vals), dp(lr.sigma))
+
+    def lowrank(self, level):
+        """(colptr, rows, vals) of B on a level (B_c = R B on coarse levels)."""
+        m = len(self._lr.sigma)
+        nnz = int(self.L.orc_lowrank_nnz(self.h, level))
+        colptr = np.empty(m + 1, dtype=np.int64)
+        rows = np.empty(nnz, dtype=np.int64)
+        vals = np.empty(nnz)
+        P = POINTER(c_int64)
+        self.L.orc_get_lowrank(self.h, level, colptr.ctypes.data_as(P), rows.ctypes.data_as(P), dp(vals))
+        return colptr, rows, vals
 
     def residual_restrict(self, level, f, x):
         f = np.ascontiguousarray(f, dtype=np.float64)
