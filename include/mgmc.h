@@ -105,6 +105,22 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
 int mgmc_destroy(mgmc_handle* h);
 int mgmc_level_desc_get(const mgmc_handle* h, int level, mgmc_level_desc* out);
 
+/* ---- posterior operator Q = A + B Sigma^{-1} B^T (MeasuredOperator) ----
+ * Replaces MeasuredOperator's B / Sigma (linear_operator/measured_operator.cc:9-49,
+ * LinearOperator::get_B / get_Sigma, linear_operator.hh:187-197).  B is N x m in CSC form:
+ * column k holds rows[colptr[k] .. colptr[k+1]) (reference vertex indices, strictly ascending)
+ * with values vals[...]; sigma[k] > 0 is the diagonal of Sigma.  A column listing all N rows is a
+ * dense column (the global average measurement).  Coarse levels get B_c = R B, Sigma_c = Sigma
+ * (linear_operator.cc:10-23); every SOR smoother sets up its B_bar (sor_smoother.cc:17-37) here,
+ * so the call costs 2 m noise-free sweeps per level.  From then on every sweep applies the
+ * low-rank fix and noise, and residuals / operator applications include B Sigma^{-1} B^T.
+ * m = 0 restores the prior operator.  1 <= m <= 64. */
+int mgmc_set_lowrank(mgmc_handle* h, int m, const int64_t* colptr, const int64_t* rows, const double* vals,
+                     const double* sigma);
+/* m of the current low-rank part (LinearOperator::get_m_lowrank); *nrows_bbar = rows stored for
+ * B_bar of (level, direction) */
+int mgmc_lowrank_info(const mgmc_handle* h, int level, int direction, int* m, int64_t* nrows_bbar);
+
 /* ---- Sampler interface (host buffers, reference layout) ---- */
 int mgmc_set_rhs(mgmc_handle* h, const double* f, size_t n);       /* fix_rhs: f stays in HBM */
 int mgmc_set_state(mgmc_handle* h, const double* x, size_t n);
@@ -130,9 +146,9 @@ int mgmc_get_sample_index(mgmc_handle* h, uint64_t* index);
 int mgmc_get_stream(mgmc_handle* h, void** stream);
 
 /* ---- component entry points (host buffers, reference layout) used by the parity tests ---- */
-/* y = A_level x  (LinearOperator::apply) */
+/* y = Q_level x  (LinearOperator::apply; Q = A + B Sigma^{-1} B^T once mgmc_set_lowrank ran) */
 int mgmc_operator_apply(mgmc_handle* h, int level, const double* x, double* y);
-/* deterministic multicolour SOR sweeps (SORSmoother::apply, no noise) */
+/* deterministic multicolour SOR sweeps (SORSmoother::apply, no noise; with the B_bar fix) */
 int mgmc_smoother_apply(mgmc_handle* h, int level, int direction, int nsweeps,
                         const double* b, double* x);
 /* one noisy multicolour SOR Gibbs sweep with explicit RNG counter (SORSampler::apply, nsmooth=1) */
@@ -142,7 +158,7 @@ int mgmc_sor_sampler_apply(mgmc_handle* h, int level, int direction, uint32_t sw
 int mgmc_restrict(mgmc_handle* h, int level, const double* r, double* rc);
 /* x += alpha * P xc  (prolongate_add, level+1 -> level) */
 int mgmc_prolongate_add(mgmc_handle* h, int level, double alpha, const double* xc, double* x);
-/* fc = R (f - A x)  (fused residual + restriction of multigridmc_sampler.cc:118-120) */
+/* fc = R (f - Q x)  (fused residual + restriction of multigridmc_sampler.cc:118-120) */
 int mgmc_residual_restrict(mgmc_handle* h, int level, const double* f, const double* x, double* fc);
 /* n standard normals of pair ids [pair0, pair0+n/2) for (sweep_tag, sample_index):
  * out[2p] = cos branch, out[2p+1] = sin branch of the Box-Muller pair p */

@@ -61,6 +61,8 @@ SIGNATURES = [
     ("mgmc_create", c_int, [POINTER(MgmcConfig), c_int, c_uint64, c_uint64, POINTER(c_void_p)]),
     ("mgmc_destroy", c_int, [_H]),
     ("mgmc_level_desc_get", c_int, [_H, c_int, POINTER(MgmcLevelDesc)]),
+    ("mgmc_set_lowrank", c_int, [_H, c_int, POINTER(c_int64), POINTER(c_int64), _DP, _DP]),
+    ("mgmc_lowrank_info", c_int, [_H, c_int, c_int, POINTER(c_int), POINTER(c_int64)]),
     ("mgmc_set_rhs", c_int, [_H, _DP, c_size_t]),
     ("mgmc_set_state", c_int, [_H, _DP, c_size_t]),
     ("mgmc_get_state", c_int, [_H, _DP, c_size_t]),

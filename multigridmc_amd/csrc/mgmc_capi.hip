@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -23,6 +24,7 @@
 #include "mgmc_zsweep.hpp"
 #include "mgmc_zrestrict.hpp"
 #include "mgmc_gsweep.hpp"
+#include "mgmc_lowrank.hpp"
 
 using namespace mgmc;
 
@@ -53,6 +55,31 @@ struct Op {
 // workgroups per CU; tuning history in DESIGN.md
 constexpr int ZS_XP = 32, ZS_TY = 16, ZS_NT = 256, ZS_MINW = 1, ZS_TZ = 32;
 
+// device copy of a level's low-rank part (mgmc_lowrank.hpp); one allocation list, freed together
+struct LowRankDev {
+    int m = 0;
+    int nblk = 0;                 // dot-product blocks over all columns
+    LRColMeta* meta = nullptr;
+    int* blk_col = nullptr;
+    long long* ent_off = nullptr;  // sparse column entries: padded offsets, values
+    double* ent_val = nullptr;
+    double* dense_val = nullptr;   // dense columns: padded value arrays, L.nstore apart
+    int nrows = 0;                 // rows of B: padded offsets, m coefficients, column masks, saved f
+    long long* rows_off = nullptr;
+    double* rows_coef = nullptr;
+    uint64_t* rows_mask = nullptr;
+    double* save = nullptr;
+    int nbar[2] = {0, 0};          // B_bar rows, [0] forward [1] backward
+    long long* bar_off[2] = {nullptr, nullptr};
+    double* bar_val[2] = {nullptr, nullptr};
+    double* sc_one = nullptr;      // dot scales: 1 (B^T x), 1/Sigma_k (Sigma^{-1} B^T x)
+    double* sc_inv = nullptr;
+    double* sq = nullptr;          // sqrt(1/Sigma_k)
+    double* part = nullptr;        // block partials
+    double* w = nullptr;           // m-vector of dots
+    std::vector<void*> allocs;
+};
+
 struct Level {
     LevelSpec spec;
     Layout L;
@@ -66,7 +93,13 @@ struct Level {
     bool pairs = false;    // Galerkin level swept in colour-pair passes (mgmc_gsweep.hpp)
     bool pingpong() const { return zsweep; }  // out-of-place sweeps: x <-> x2
     double* buf(int i) const { return i == 0 ? x : x2; }
+    LowRankDev lr;
 };
+
+void free_lowrank(LowRankDev& lr) {
+    for (void* p : lr.allocs) hipFree(p);
+    lr = LowRankDev();
+}
 
 }  // namespace
 
@@ -369,6 +402,60 @@ void launch_pack(const Level& lv, const double* lex, double* pad, bool pack, hip
     }
 }
 
+// ---- low-rank part (mgmc_lowrank.hpp) ----
+// w = (sc_k B_k)^T v for all columns
+void lr_dots(const Level& lv, const double* v, const double* sc, hipStream_t s) {
+    const LowRankDev& r = lv.lr;
+    if (r.nblk > 0)
+        hipLaunchKernelGGL(k_lr_partials, dim3(r.nblk), dim3(64), 0, s, lv.L, (const LRColMeta*)r.meta,
+                           (const int*)r.blk_col, (const long long*)r.ent_off, (const double*)r.ent_val,
+                           (const double*)r.dense_val, sc, v, r.part);
+    hipLaunchKernelGGL(k_lr_totals, dim3(r.m), dim3(64), 0, s, (const LRColMeta*)r.meta, (const double*)r.part, r.w);
+}
+
+// patch y on the rows of B (LR_PATCH_NOISE: y += B Sigma^{-1/2} xi'; RESIDUAL: y -= B w; APPLY: y += B w)
+void lr_patch(const mgmc_handle* h, const Level& lv, int mode, double* y, uint32_t tag, const uint64_t* sample,
+              hipStream_t s) {
+    const LowRankDev& r = lv.lr;
+    if (r.nrows == 0) return;
+    LRPatchArgs a;
+    a.m = r.m;
+    a.nrows = r.nrows;
+    a.off = r.rows_off;
+    a.coef = r.rows_coef;
+    a.mask = r.rows_mask;
+    a.t = r.w;
+    a.sq = r.sq;
+    a.key = h->key;
+    a.tag = tag;
+    a.sample = sample;
+    a.y = y;
+    a.save = r.save;
+    a.mode = mode;
+    hipLaunchKernelGGL(k_lr_patch, dim3((r.nrows + 255) / 256), dim3(256), 0, s, a);
+}
+
+// after a sweep in `direction`: x -= B_bar (B^T x) (sor_smoother.cc:47-51); restores f_restore
+// on the rows of B when the sweep ran on a noise-patched f
+void lr_fix(const Level& lv, double* x, int direction, double* f_restore, hipStream_t s) {
+    const LowRankDev& r = lv.lr;
+    lr_dots(lv, x, r.sc_one, s);
+    const int d = direction == MGMC_FORWARD ? 0 : 1;
+    const int nrest = f_restore ? r.nrows : 0;
+    const int n = std::max(r.nbar[d], nrest);
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_lr_update, dim3((n + 255) / 256), dim3(256), 0, s, r.m, r.nbar[d],
+                       (const long long*)r.bar_off[d], (const double*)r.bar_val[d], (const double*)r.w, x, nrest,
+                       (const long long*)r.rows_off, (const double*)r.save, f_restore);
+}
+
+void lr_restore(const Level& lv, double* f, hipStream_t s) {
+    const LowRankDev& r = lv.lr;
+    if (r.nrows == 0) return;
+    hipLaunchKernelGGL(k_lr_restore, dim3((r.nrows + 255) / 256), dim3(256), 0, s, r.nrows,
+                       (const long long*)r.rows_off, (const double*)r.save, f);
+}
+
 // ---- the op sequence of one sample (multigridmc_sampler.cc:103-138) ----
 // cur[l] tracks which buffer holds x_l while the ops are generated (z-sweeps ping-pong).
 void push_sweep(mgmc_handle* h, std::vector<int>& cur, int level, int direction, uint32_t& tag, int& pending_prolong) {
@@ -399,7 +486,7 @@ void build_ops_level(mgmc_handle* h, int level, uint32_t& tag, std::vector<int>&
     if (level == nlevel - 1) {
         // coarse sampler: SSORSampler(ncoarsesmooth) = ncoarsesmooth x (fwd SOR sampler, bwd SOR sampler)
         const Level& lv = h->levels[level];
-        if (lv.lds_bytes > 0) {
+        if (lv.lds_bytes > 0 && lv.lr.m == 0) {
             h->ops.push_back({OP_COARSE_LDS, level, MGMC_FORWARD, tag, 2 * c.ncoarsesmooth});
             tag += 2 * c.ncoarsesmooth;
         } else {
@@ -456,6 +543,22 @@ void build_ops_level(mgmc_handle* h, int level, uint32_t& tag, std::vector<int>&
     }
 }
 
+void build_ops(mgmc_handle* h) {
+    h->ops.clear();
+    h->seg_end_pre = h->seg_begin_post = h->seg_end_post = 0;
+    uint32_t tag = 0;
+    std::vector<int> cur(h->levels.size(), 0);
+    build_ops_level(h, 0, tag, cur);
+    if (cur[0] != 0) {
+        Op cp{OP_COPY, 0, 0, 0, 0};
+        cp.src = cur[0];
+        h->ops.push_back(cp);
+        h->seg_end_post = h->ops.size();
+    }
+    h->ops.push_back({OP_QOI, 0, 0, 0, 0});
+    if (h->levels.size() == 1) h->seg_end_pre = h->seg_begin_post = h->seg_end_post = 0;
+}
+
 void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
     const uint64_t* sample = h->ctrl;  // ctrl[0]
     for (size_t q = begin; q < end; ++q) {
@@ -464,15 +567,20 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
         switch (op.kind) {
             case OP_SWEEP: {
                 GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
+                const bool lr = lv.lr.m > 0;
+                if (lr) lr_patch(h, lv, LR_PATCH_NOISE, lv.f, op.tag, sample, s);
+                double* xo = lv.x;
                 if (lv.zsweep) {
                     const Level* lc = op.prolong ? &h->levels[op.level + 1] : nullptr;
-                    launch_zsweep(lv, lv.buf(op.src), lv.buf(1 - op.src), lv.f, g, op.direction, lc,
-                                  lc ? lc->x : nullptr, h->cfg.coarse_scaling, s);
+                    xo = lv.buf(1 - op.src);
+                    launch_zsweep(lv, lv.buf(op.src), xo, lv.f, g, op.direction, lc, lc ? lc->x : nullptr,
+                                  h->cfg.coarse_scaling, s);
                 } else if (lv.pairs) {
                     launch_pairs(lv, lv.x, lv.f, g, op.direction, s);
                 } else {
                     launch_sweep(lv, lv.x, lv.f, g, op.direction, true, s);
                 }
+                if (lr) lr_fix(lv, xo, op.direction, lv.f, s);
                 break;
             }
             case OP_COARSE_LDS: {
@@ -482,7 +590,13 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
             }
             case OP_RESIDUAL_RESTRICT: {
                 Level& lc = h->levels[op.level + 1];
+                const bool lr = lv.lr.m > 0;
+                if (lr) {  // r = (f - B Sigma^{-1} B^T x) - A x
+                    lr_dots(lv, lv.buf(op.src), lv.lr.sc_inv, s);
+                    lr_patch(h, lv, LR_PATCH_RESIDUAL, lv.f, 0, sample, s);
+                }
                 launch_residual_restrict(lv, lc, lv.buf(op.src), lv.f, lc.f, lc.x, 1, s);
+                if (lr) lr_restore(lv, lv.f, s);
                 break;
             }
             case OP_PROLONGATE: {
@@ -710,19 +824,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     hipMemsetAsync(h->mom, 0, 4 * sizeof(double), h->stream);
     // op sequence of one sample
     h->fuse_prolong = getenv("MGMC_NO_FUSE_PROLONG") == nullptr;  // default: fused (A/B in DESIGN.md)
-    uint32_t tag = 0;
-    std::vector<int> cur(specs.size(), 0);
-    build_ops_level(h, 0, tag, cur);
-    if (cur[0] != 0) {
-        Op cp{OP_COPY, 0, 0, 0, 0};
-        cp.src = cur[0];
-        h->ops.push_back(cp);
-        h->seg_end_post = h->ops.size();
-    }
-    h->ops.push_back({OP_QOI, 0, 0, 0, 0});
-    if (specs.size() == 1) {
-        h->seg_end_pre = h->seg_begin_post = h->seg_end_post = 0;
-    }
+    build_ops(h);
     if ((rc = ensure_series(h, 1024)) != MGMC_OK) return bail(rc);
     if (hipStreamSynchronize(h->stream) != hipSuccess) {
         h->last_error = "stream sync failed after setup";
@@ -745,6 +847,7 @@ int mgmc_destroy(mgmc_handle* h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     destroy_graphs(h);
     for (auto& lv : h->levels) {
+        free_lowrank(lv.lr);
         if (lv.x) hipFree(lv.x);
         if (lv.x2) hipFree(lv.x2);
         if (lv.f) hipFree(lv.f);
@@ -918,6 +1021,10 @@ int mgmc_operator_apply(mgmc_handle* h, int level, const double* x, double* y) {
         hipLaunchKernelGGL((k_operator_apply<2, 5>), grid, block, 0, h->stream, lv.L, xs, ys, lv.S);
     else
         hipLaunchKernelGGL((k_operator_apply<2, 9>), grid, block, 0, h->stream, lv.L, xs, ys, lv.S);
+    if (lv.lr.m > 0) {  // y += B (Sigma^{-1} B^T x)  (linear_operator.hh:71-75)
+        lr_dots(lv, xs, lv.lr.sc_inv, h->stream);
+        lr_patch(h, lv, LR_PATCH_APPLY, ys, 0, h->ctrl + 3, h->stream);
+    }
     HIPCHK(h, hipGetLastError());
     return download(h, level, ys, y);
 }
@@ -934,9 +1041,11 @@ static int sweep_component(mgmc_handle* h, int level, int direction, int nsweeps
     if ((rc = upload(h, level, b, lv.scratch[0]))) return rc;
     if ((rc = upload(h, level, x, lv.scratch[1]))) return rc;
     HIPCHK(h, hipMemcpyAsync(h->ctrl + 3, &sample, sizeof(sample), hipMemcpyHostToDevice, h->stream));
+    const bool lr = lv.lr.m > 0;
     int cur = 1;
     for (int s = 0; s < nsweeps; ++s) {
         GibbsArg g = make_gibbs(h, lv, tag + (uint32_t)s, 0, h->ctrl + 3);
+        if (lr && noise) lr_patch(h, lv, LR_PATCH_NOISE, lv.scratch[0], tag + (uint32_t)s, h->ctrl + 3, h->stream);
         if (noise && lv.zsweep) {  // the fused z-marching kernel of the V-cycle (out of place)
             launch_zsweep(lv, lv.scratch[cur], lv.scratch[3 - cur], lv.scratch[0], g, direction, nullptr, nullptr, 0.0,
                           h->stream);
@@ -946,6 +1055,7 @@ static int sweep_component(mgmc_handle* h, int level, int direction, int nsweeps
         } else {
             launch_sweep(lv, lv.scratch[cur], lv.scratch[0], g, direction, noise, h->stream);
         }
+        if (lr) lr_fix(lv, lv.scratch[cur], direction, noise ? lv.scratch[0] : nullptr, h->stream);
     }
     HIPCHK(h, hipGetLastError());
     return download(h, level, lv.scratch[cur], x);
@@ -1006,6 +1116,10 @@ int mgmc_residual_restrict(mgmc_handle* h, int level, const double* f, const dou
     Level& lc = h->levels[level + 1];
     if ((rc = upload(h, level, f, lf.scratch[0]))) return rc;
     if ((rc = upload(h, level, x, lf.scratch[1]))) return rc;
+    if (lf.lr.m > 0) {  // f - B Sigma^{-1} B^T x, then the residual kernel
+        lr_dots(lf, lf.scratch[1], lf.lr.sc_inv, h->stream);
+        lr_patch(h, lf, LR_PATCH_RESIDUAL, lf.scratch[0], 0, h->ctrl + 3, h->stream);
+    }
     launch_residual_restrict(lf, lc, lf.scratch[1], lf.scratch[0], lc.scratch[0], lc.scratch[1], 1, h->stream);
     HIPCHK(h, hipGetLastError());
     return download(h, level + 1, lc.scratch[0], fc);
@@ -1093,6 +1207,244 @@ int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* tot
         if (h->ops[q].kind == OP_SWEEP && h->ops[q].level == 0) ++cnt;
     *nfine = cnt * nsteps;
     for (auto& e : ev) hipEventDestroy(e);
+    return MGMC_OK;
+}
+
+// ---------------- low-rank posterior part ----------------
+}  // extern "C"
+
+namespace {
+
+long long ref_to_padded(const Level& lv, long long row) {
+    const long long nxi = lv.L.nx - 1, nyi = lv.L.ny - 1;
+    const int i = (int)(row % nxi) + 1;
+    const long long r = row / nxi;
+    const int j = (int)(r % nyi) + 1;
+    const int k = lv.spec.dim == 3 ? (int)(r / nyi) + 1 : 0;
+    return lv.L.at(i, j, k);
+}
+
+template <class T>
+int lr_to_device(mgmc_handle* h, LowRankDev& r, T** dst, const std::vector<T>& src) {
+    *dst = nullptr;
+    if (src.empty()) return MGMC_OK;
+    if (hipMalloc((void**)dst, src.size() * sizeof(T)) != hipSuccess) {
+        *dst = nullptr;
+        return fail(h, MGMC_E_NOMEM, "device allocation failed (low-rank part)");
+    }
+    r.allocs.push_back(*dst);
+    HIPCHK(h, hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return MGMC_OK;
+}
+
+// B_c = R B, column by column on the device restriction kernel (bitwise the oracle's restrict_)
+int lr_restrict_columns(mgmc_handle* h, int level, std::vector<LRColumn>& cols) {
+    Level& lf = h->levels[level];
+    Level& lc = h->levels[level + 1];
+    int rc;
+    if ((rc = ensure_scratch(h, level)) || (rc = ensure_scratch(h, level + 1))) return rc;
+    std::vector<double> fine(lf.spec.ndof), coarse(lc.spec.ndof);
+    for (auto& col : cols) {
+        std::fill(fine.begin(), fine.end(), 0.0);
+        for (const auto& e : col.ent) fine[e.first] = e.second;
+        if ((rc = upload(h, level, fine.data(), lf.scratch[0]))) return rc;
+        dim3 block(64, 4, 1);
+        dim3 grid = grid3(lc.L.nx - 1, lc.L.ny - 1, lf.spec.dim == 3 ? lc.L.nz - 1 : 1, block);
+        if (lf.spec.dim == 3)
+            hipLaunchKernelGGL((k_restrict<3>), grid, block, 0, h->stream, lf.L, lc.L, (const double*)lf.scratch[0],
+                               lc.scratch[0]);
+        else
+            hipLaunchKernelGGL((k_restrict<2>), grid, block, 0, h->stream, lf.L, lc.L, (const double*)lf.scratch[0],
+                               lc.scratch[0]);
+        HIPCHK(h, hipGetLastError());
+        if ((rc = download(h, level + 1, lc.scratch[0], coarse.data()))) return rc;
+        col.ent.clear();
+        for (long long i = 0; i < (long long)coarse.size(); ++i)
+            if (col.dense || coarse[i] != 0.0) col.ent.push_back({i, coarse[i]});
+    }
+    return MGMC_OK;
+}
+
+// device data of one level: columns, rows of B, and B_bar for both sweep directions
+// (sor_smoother.cc:17-37 with the multicolour splitting: Y = one noise-free multicolour sweep
+// from zero per column, M = Sigma + B^T Y, B_bar = Y M^{-1} on the rows where Y is nonzero)
+int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols, const double* sigma, int m) {
+    Level& lv = h->levels[level];
+    LowRankDev& r = lv.lr;
+    r.m = m;
+    const long long N = (long long)lv.spec.ndof;
+    int rc;
+    // columns: entry lists (sparse) or padded value arrays (dense), dot-product blocks
+    std::vector<LRColMeta> meta(m);
+    std::vector<int> blk_col;
+    std::vector<long long> ent_off;
+    std::vector<double> ent_val;
+    int ndense = 0;
+    for (int k = 0; k < m; ++k) {
+        const LRColumn& c = cols[k];
+        LRColMeta& mt = meta[k];
+        mt.n = (long long)c.ent.size();
+        mt.blk0 = (int)blk_col.size();
+        mt.nblk = (int)((mt.n + LR_BLK - 1) / LR_BLK);
+        mt.pad_ = 0;
+        for (int b = 0; b < mt.nblk; ++b) blk_col.push_back(k);
+        if (c.dense) {
+            mt.dense = ndense++;
+            mt.ent0 = 0;
+        } else {
+            mt.dense = -1;
+            mt.ent0 = (long long)ent_off.size();
+            for (const auto& e : c.ent) {
+                ent_off.push_back(ref_to_padded(lv, e.first));
+                ent_val.push_back(e.second);
+            }
+        }
+    }
+    r.nblk = (int)blk_col.size();
+    if ((rc = lr_to_device(h, r, &r.meta, meta)) || (rc = lr_to_device(h, r, &r.blk_col, blk_col)) ||
+        (rc = lr_to_device(h, r, &r.ent_off, ent_off)) || (rc = lr_to_device(h, r, &r.ent_val, ent_val)))
+        return rc;
+    if (ndense > 0) {
+        const size_t bytes = (size_t)ndense * lv.L.nstore * sizeof(double);
+        if (hipMalloc(&r.dense_val, bytes) != hipSuccess) return fail(h, MGMC_E_NOMEM, "device allocation failed");
+        r.allocs.push_back(r.dense_val);
+        HIPCHK(h, hipMemsetAsync(r.dense_val, 0, bytes, h->stream));
+        std::vector<double> v(N);
+        for (int k = 0; k < m; ++k) {
+            if (!cols[k].dense) continue;
+            for (long long i = 0; i < N; ++i) v[i] = cols[k].ent[i].second;
+            if ((rc = upload(h, level, v.data(), r.dense_val + (size_t)meta[k].dense * lv.L.nstore))) return rc;
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+        }
+    }
+    // rows of B (ascending), with the row's coefficients of every column
+    std::vector<int> slot(N, -1);
+    for (const auto& c : cols)
+        for (const auto& e : c.ent) slot[e.first] = 0;
+    int nrows = 0;
+    std::vector<long long> rows_off;
+    for (long long i = 0; i < N; ++i)
+        if (slot[i] == 0) {
+            slot[i] = nrows++;
+            rows_off.push_back(ref_to_padded(lv, i));
+        }
+    std::vector<double> coef((size_t)nrows * m, 0.0);
+    std::vector<uint64_t> mask(nrows, 0);
+    for (int k = 0; k < m; ++k)
+        for (const auto& e : cols[k].ent) {
+            const int u = slot[e.first];
+            coef[(size_t)u * m + k] = e.second;
+            mask[u] |= 1ull << k;
+        }
+    r.nrows = nrows;
+    std::vector<double> sc_one(m, 1.0), sc_inv(m), sq(m), zeros(std::max(nrows, 1), 0.0);
+    for (int k = 0; k < m; ++k) {
+        sc_inv[k] = 1.0 / sigma[k];
+        sq[k] = sqrt(1.0 / sigma[k]);  // Sigma^{-1/2} (sor_sampler.cc:30-33)
+    }
+    if ((rc = lr_to_device(h, r, &r.rows_off, rows_off)) || (rc = lr_to_device(h, r, &r.rows_coef, coef)) ||
+        (rc = lr_to_device(h, r, &r.rows_mask, mask)) || (rc = lr_to_device(h, r, &r.save, zeros)) ||
+        (rc = lr_to_device(h, r, &r.sc_one, sc_one)) || (rc = lr_to_device(h, r, &r.sc_inv, sc_inv)) ||
+        (rc = lr_to_device(h, r, &r.sq, sq)))
+        return rc;
+    std::vector<double> partz(std::max(r.nblk, 1), 0.0), wz(m, 0.0);
+    if ((rc = lr_to_device(h, r, &r.part, partz)) || (rc = lr_to_device(h, r, &r.w, wz))) return rc;
+
+    // B_bar for the forward and backward splittings
+    if ((rc = ensure_scratch(h, level))) return rc;
+    std::vector<double> Y((size_t)N * m), b(N), y(N), col(N);
+    for (int d = 0; d < 2; ++d) {
+        const int direction = d == 0 ? MGMC_FORWARD : MGMC_BACKWARD;
+        for (int l = 0; l < m; ++l) {
+            std::fill(b.begin(), b.end(), 0.0);
+            for (const auto& e : cols[l].ent) b[e.first] = e.second;
+            if ((rc = upload(h, level, b.data(), lv.scratch[0]))) return rc;
+            HIPCHK(h, hipMemsetAsync(lv.scratch[1], 0, lv.L.nstore * sizeof(double), h->stream));
+            GibbsArg g = make_gibbs(h, lv, 0, 0, h->ctrl + 3);
+            launch_sweep(lv, lv.scratch[1], lv.scratch[0], g, direction, false, h->stream);
+            HIPCHK(h, hipGetLastError());
+            if ((rc = download(h, level, lv.scratch[1], y.data()))) return rc;
+            for (long long i = 0; i < N; ++i) Y[(size_t)i * m + l] = y[i];
+        }
+        std::vector<double> M((size_t)m * m), Minv;
+        for (int l = 0; l < m; ++l) {
+            for (long long i = 0; i < N; ++i) col[i] = Y[(size_t)i * m + l];
+            for (int k = 0; k < m; ++k)
+                M[(size_t)k * m + l] = (k == l ? sigma[k] : 0.0) + lr_dot_host(cols[k], 1.0, col.data());
+        }
+        if (!lr_small_inverse(M, m, Minv))
+            return fail(h, MGMC_E_INVALID, "Sigma + B^T (L + D/omega)^{-1} B is singular");
+        std::vector<long long> boff;
+        std::vector<double> bval;
+        for (long long i = 0; i < N; ++i) {
+            const double* yi = &Y[(size_t)i * m];
+            bool nz = false;
+            for (int l = 0; l < m; ++l) nz = nz || yi[l] != 0.0;
+            if (!nz) continue;  // B_bar row is exactly zero: x - 0 = x
+            boff.push_back(ref_to_padded(lv, i));
+            for (int k = 0; k < m; ++k) {
+                double u = 0.0;
+                for (int l = 0; l < m; ++l) u = std::fma(yi[l], Minv[(size_t)l * m + k], u);
+                bval.push_back(u);
+            }
+        }
+        r.nbar[d] = (int)boff.size();
+        if ((rc = lr_to_device(h, r, &r.bar_off[d], boff)) || (rc = lr_to_device(h, r, &r.bar_val[d], bval))) return rc;
+    }
+    return MGMC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mgmc_set_lowrank(mgmc_handle* h, int m, const int64_t* colptr, const int64_t* rows, const double* vals,
+                     const double* sigma) {
+    if (!h) return fail(nullptr, MGMC_E_INVALID, "null handle");
+    if (m < 0 || m > LR_MAX_M) return fail(h, MGMC_E_INVALID, "m_lowrank must be in [0, 64]");
+    const long long N0 = (long long)h->levels[0].spec.ndof;
+    std::vector<LRColumn> cols(m);
+    if (m > 0) {
+        if (!colptr || !sigma) return fail(h, MGMC_E_INVALID, "null argument");
+        if (colptr[0] != 0) return fail(h, MGMC_E_INVALID, "colptr[0] must be 0");
+        if (colptr[m] > 0 && (!rows || !vals)) return fail(h, MGMC_E_INVALID, "null argument");
+        for (int k = 0; k < m; ++k) {
+            if (!(sigma[k] > 0.0) || !std::isfinite(sigma[k])) return fail(h, MGMC_E_INVALID, "Sigma must be positive");
+            if (colptr[k + 1] < colptr[k]) return fail(h, MGMC_E_INVALID, "colptr must be non-decreasing");
+            for (int64_t q = colptr[k]; q < colptr[k + 1]; ++q) {
+                if (rows[q] < 0 || rows[q] >= N0 || (q > colptr[k] && rows[q] <= rows[q - 1]))
+                    return fail(h, MGMC_E_INVALID, "row indices of a column must be strictly ascending in [0, N)");
+                if (!std::isfinite(vals[q])) return fail(h, MGMC_E_INVALID, "non-finite entry of B");
+                cols[k].ent.push_back({rows[q], vals[q]});
+            }
+            cols[k].dense = (long long)cols[k].ent.size() == N0;
+        }
+    }
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    destroy_graphs(h);
+    for (auto& lv : h->levels) free_lowrank(lv.lr);
+    int rc = MGMC_OK;
+    for (size_t l = 0; m > 0 && l < h->levels.size(); ++l) {
+        if (l > 0 && (rc = lr_restrict_columns(h, (int)l - 1, cols))) break;
+        if ((rc = lr_setup_level(h, (int)l, cols, sigma, m))) break;
+    }
+    if (rc) {
+        for (auto& lv : h->levels) free_lowrank(lv.lr);
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    build_ops(h);
+    const int rc2 = build_graphs(h);
+    return rc ? rc : rc2;
+}
+
+int mgmc_lowrank_info(const mgmc_handle* h, int level, int direction, int* m, int64_t* nrows_bbar) {
+    if (!h || !m || !nrows_bbar) return fail(nullptr, MGMC_E_INVALID, "null argument");
+    if (level < 0 || level >= (int)h->levels.size()) return fail(nullptr, MGMC_E_INVALID, "level out of range");
+    if (direction != MGMC_FORWARD && direction != MGMC_BACKWARD) return fail(nullptr, MGMC_E_INVALID, "invalid direction");
+    const LowRankDev& r = h->levels[level].lr;
+    *m = r.m;
+    *nrows_bbar = r.nbar[direction == MGMC_FORWARD ? 0 : 1];
     return MGMC_OK;
 }
 

@@ -1,0 +1,257 @@
+// mgmc_lowrank.hpp -- low-rank posterior part of a level: Q = A + B Sigma^{-1} B^T.
+//
+// Reference (nilsfriess/MultigridMC, src/):
+//   * SORSmoother::apply: after every sweep  x -= B_bar (B^T x)          smoother/sor_smoother.cc:41-53
+//     B_bar = (L + D/omega)^{-1} B (Sigma + B^T (L + D/omega)^{-1} B)^{-1}  (forward; L^T backward),
+//     set up once per smoother                                          smoother/sor_smoother.cc:17-37
+//   * SORSampler::apply: c += B Sigma^{-1/2} xi'  (m extra normals per sweep) sampler/sor_sampler.cc:48-56
+//   * LinearOperator::apply: y = A x + B (Sigma^{-1} B^T x)              linear_operator.hh:66-76
+//   * coarse levels: B_c = R B, Sigma_c = Sigma                          linear_operator.cc:10-23
+//
+// Why the multicolour splitting makes this cheap.  The reference's B_bar is a dense N x m matrix:
+// the lexicographic triangular solve (L + D/omega)^{-1} spreads every column of B over all later
+// vertices, so each sweep reads N*m doubles (1.07 GB at 256^3, m = 8).  Under the multicolour
+// splitting the same solve is one noise-free multicolour sweep from zero: colour c only reads
+// colours < c at distance one, so the fill of a column stays within a few vertices of its
+// support.  B_bar keeps that row support (B_bar = Y M^{-1} mixes columns, not rows), and the
+// device stores only those rows: a point measurement costs a few dozen rows instead of N.  A dense
+// column of B (the global average measurement) makes B_bar dense again, as in the reference.
+//
+// Device arithmetic order (replayed by the oracle's MULTICOLOUR mode, oracle/refcpu.cpp):
+//   * B^T-type dots  sum_e (sc_k B_ek) v_e  over a column's entry list (rows ascending; a dense
+//     column lists every row): blocks of LR_BLK entries, lane l of a 64-wide wavefront sums
+//     entries l, l+64, ... from 0.0, lanes combine by the xor butterfly 32, 16, ..., 1; the block
+//     partials are combined the same way.  sc_k = 1 for the smoother fix, 1/Sigma_k for the
+//     residual's Sigma^{-1} B^T x.
+//   * e = B s: e_i = sum over the columns of row i in ascending k of B_ik s_k (plain mul + add);
+//     sampler noise  f_eff = f + e, s_k = sqrt(1/Sigma_k) xi'_k with xi' from Philox pair
+//     LR_PAIR0 + k/2 (cos branch for even k) of the sweep's tag;
+//   * smoother fix  u_i = fma chain over k of B_bar_ik w_k,  x_i = x_i - u_i;
+//   * posterior residual  r = (f - B t) - A x,  t = Sigma^{-1} B^T x: f is patched on the rows of
+//     B, the residual kernels run unchanged, f is restored.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cmath>
+#include <utility>
+#include <vector>
+
+#include "mgmc_kernels.hpp"
+
+namespace mgmc {
+
+constexpr int LR_BLK = 4096;            // entries per dot-product block
+constexpr uint32_t LR_PAIR0 = 0xFFFFF000u;  // Philox pair ids of the low-rank noise (above any lattice pair)
+constexpr int LR_MAX_M = 64;
+
+struct LRColMeta {
+    long long n;     // entries in the column's list
+    long long ent0;  // first entry in the sparse entry arrays (sparse columns)
+    int dense;       // index of the column's padded value array, or -1
+    int blk0, nblk;  // dot-product blocks
+    int pad_;
+};
+
+// ---- dot products, stage 1: one wavefront per block of LR_BLK entries ----
+__global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRColMeta* __restrict__ meta,
+                                                     const int* __restrict__ blk_col,
+                                                     const long long* __restrict__ ent_off,
+                                                     const double* __restrict__ ent_val,
+                                                     const double* __restrict__ dense_val,
+                                                     const double* __restrict__ sc, const double* __restrict__ v,
+                                                     double* __restrict__ part) {
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int k = blk_col[b];
+    const LRColMeta c = meta[k];
+    const long long e0 = (long long)(b - c.blk0) * LR_BLK;
+    const long long end = min(c.n, e0 + LR_BLK);
+    const double s = sc[k];
+    double acc = 0.0;
+    if (c.dense >= 0) {
+        const double* dv = dense_val + (long long)c.dense * L.nstore;
+        const long long nxi = L.nx - 1, nyi = L.ny - 1;
+        for (long long e = e0 + lane; e < end; e += 64) {
+            const int i = (int)(e % nxi) + 1;
+            const long long r = e / nxi;
+            const int j = (int)(r % nyi) + 1;
+            const int kk = L.dim == 3 ? (int)(r / nyi) + 1 : 0;
+            const long long p = L.at(i, j, kk);
+            acc = acc + (s * dv[p]) * v[p];
+        }
+    } else {
+        for (long long e = e0 + lane; e < end; e += 64) {
+            const long long q = c.ent0 + e;
+            acc = acc + (s * ent_val[q]) * v[ent_off[q]];
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+    if (lane == 0) part[b] = acc;
+}
+
+// ---- dot products, stage 2: one wavefront per column ----
+__global__ void __launch_bounds__(64) k_lr_totals(const LRColMeta* __restrict__ meta, const double* __restrict__ part,
+                                                   double* __restrict__ out) {
+    const int k = blockIdx.x;
+    const int lane = threadIdx.x;
+    const LRColMeta c = meta[k];
+    double acc = 0.0;
+    for (int b = lane; b < c.nblk; b += 64) acc = acc + part[c.blk0 + b];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+    if (lane == 0) out[k] = acc;
+}
+
+// ---- patch a vector on the rows of B with e = B s ----
+//   mode 0: sampler noise  f_save = f, f = f + B s  with s_k = sq_k xi'_k drawn here
+//   mode 1: residual       f_save = f, f = f - B t  (t = Sigma^{-1} B^T x, precomputed)
+//   mode 2: operator       y = y + B t
+enum { LR_PATCH_NOISE = 0, LR_PATCH_RESIDUAL = 1, LR_PATCH_APPLY = 2 };
+
+struct LRPatchArgs {
+    int m, nrows;
+    const long long* off;    // padded offsets of the rows of B
+    const double* coef;      // nrows x m, B_ik (0 where absent)
+    const uint64_t* mask;    // bit k: column k has an entry in the row
+    const double* t;         // mode 1/2: the m-vector
+    const double* sq;        // mode 0: sqrt(1 / Sigma_k)
+    RngKey key;
+    uint32_t tag;
+    const uint64_t* sample;
+    double* y;
+    double* save;
+    int mode;
+};
+
+__global__ void __launch_bounds__(256) k_lr_patch(LRPatchArgs a) {
+    __shared__ double s[LR_MAX_M];
+    if (a.mode == LR_PATCH_NOISE) {
+        const int t = threadIdx.x;
+        if (2 * t < a.m) {
+            const uint64_t sample = *a.sample;
+            const Philox4 r = philox4x32_10(LR_PAIR0 + (uint32_t)t, a.tag, (uint32_t)sample, (uint32_t)(sample >> 32),
+                                            a.key.k0, a.key.k1);
+            double z0, z1;
+            normal_pair(r, &z0, &z1);
+            s[2 * t] = a.sq[2 * t] * z0;
+            if (2 * t + 1 < a.m) s[2 * t + 1] = a.sq[2 * t + 1] * z1;
+        }
+    } else if ((int)threadIdx.x < a.m) {
+        s[threadIdx.x] = a.t[threadIdx.x];
+    }
+    __syncthreads();
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= a.nrows) return;
+    const long long p = a.off[u];
+    const uint64_t msk = a.mask[u];
+    const double* cf = a.coef + (long long)u * a.m;
+    double e = 0.0;
+    for (int k = 0; k < a.m; ++k)
+        if ((msk >> k) & 1) e = e + cf[k] * s[k];
+    const double y = a.y[p];
+    if (a.mode != LR_PATCH_APPLY) a.save[u] = y;
+    a.y[p] = a.mode == LR_PATCH_RESIDUAL ? y - e : y + e;
+}
+
+// ---- smoother fix x -= B_bar w on B_bar's rows; optionally restore f on the rows of B ----
+__global__ void __launch_bounds__(256) k_lr_update(int m, int nbar, const long long* __restrict__ bar_off,
+                                                    const double* __restrict__ bar_val, const double* __restrict__ w,
+                                                    double* __restrict__ x, int nrest,
+                                                    const long long* __restrict__ rest_off,
+                                                    const double* __restrict__ rest_val, double* __restrict__ f) {
+    __shared__ double ws[LR_MAX_M];
+    if ((int)threadIdx.x < m) ws[threadIdx.x] = w[threadIdx.x];
+    __syncthreads();
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u < nbar) {
+        const double* bv = bar_val + (long long)u * m;
+        double acc = 0.0;
+        for (int k = 0; k < m; ++k) acc = fma(bv[k], ws[k], acc);
+        const long long p = bar_off[u];
+        x[p] = x[p] - acc;
+    }
+    if (u < nrest) f[rest_off[u]] = rest_val[u];
+}
+
+// ---- restore f on the rows of B ----
+__global__ void __launch_bounds__(256) k_lr_restore(int n, const long long* __restrict__ off,
+                                                     const double* __restrict__ save, double* __restrict__ f) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u < n) f[off[u]] = save[u];
+}
+
+// ============================================================================================
+// host side: the same orders, for the B_bar setup (M = Sigma + B^T Y needs the dots of Y)
+// ============================================================================================
+struct LRColumn {
+    std::vector<std::pair<long long, double>> ent;  // (row in reference order, value), rows ascending
+    bool dense = false;
+};
+
+inline double lr_butterfly64_host(double* v) {
+    for (int off = 32; off >= 1; off >>= 1) {
+        double t[64];
+        for (int l = 0; l < 64; ++l) t[l] = v[l] + v[l ^ off];
+        std::copy(t, t + 64, v);
+    }
+    return v[0];
+}
+
+// sum_e (sc B_ek) v_e in the device order (v in reference order)
+inline double lr_dot_host(const LRColumn& col, double sc, const double* v) {
+    const long long n = (long long)col.ent.size();
+    const long long nblk = (n + LR_BLK - 1) / LR_BLK;
+    std::vector<double> part((size_t)nblk);
+    double acc[64];
+    for (long long b = 0; b < nblk; ++b) {
+        const long long end = std::min(n, (b + 1) * LR_BLK);
+        for (int l = 0; l < 64; ++l) {
+            acc[l] = 0.0;
+            for (long long e = b * LR_BLK + l; e < end; e += 64)
+                acc[l] = acc[l] + (sc * col.ent[e].second) * v[col.ent[e].first];
+        }
+        part[b] = lr_butterfly64_host(acc);
+    }
+    for (int l = 0; l < 64; ++l) {
+        acc[l] = 0.0;
+        for (long long b = l; b < nblk; b += 64) acc[l] = acc[l] + part[b];
+    }
+    return lr_butterfly64_host(acc);
+}
+
+// inverse of a small dense row-major m x m matrix: Gauss-Jordan with partial pivoting (the
+// oracle's small_inverse, operation for operation); returns false if singular
+inline bool lr_small_inverse(std::vector<double> M, int m, std::vector<double>& I) {
+    I.assign((size_t)m * m, 0.0);
+    for (int i = 0; i < m; ++i) I[(size_t)i * m + i] = 1.0;
+    for (int c = 0; c < m; ++c) {
+        int piv = c;
+        for (int r = c + 1; r < m; ++r)
+            if (std::fabs(M[(size_t)r * m + c]) > std::fabs(M[(size_t)piv * m + c])) piv = r;
+        if (piv != c)
+            for (int q = 0; q < m; ++q) {
+                std::swap(M[(size_t)c * m + q], M[(size_t)piv * m + q]);
+                std::swap(I[(size_t)c * m + q], I[(size_t)piv * m + q]);
+            }
+        const double d = M[(size_t)c * m + c];
+        if (d == 0.0 || !std::isfinite(d)) return false;
+        for (int q = 0; q < m; ++q) {
+            M[(size_t)c * m + q] /= d;
+            I[(size_t)c * m + q] /= d;
+        }
+        for (int r = 0; r < m; ++r) {
+            if (r == c) continue;
+            const double f = M[(size_t)r * m + c];
+            for (int q = 0; q < m; ++q) {
+                M[(size_t)r * m + q] -= f * M[(size_t)c * m + q];
+                I[(size_t)r * m + q] -= f * I[(size_t)c * m + q];
+            }
+        }
+    }
+    return true;
+}
+
+}  // namespace mgmc

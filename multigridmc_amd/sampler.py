@@ -168,7 +168,7 @@ class MultigridMCSampler:
     state and the right hand side stay resident in HBM between calls; apply() moves both across
     PCIe (like the reference's by-reference vectors), sample() runs the device-resident loop."""
 
-    def __init__(self, linear_operator: ShiftedLaplaceFDOperator, seed: int, params: MultigridParameters,
+    def __init__(self, linear_operator, seed: int, params: MultigridParameters,
                  device: int = 0, chain_id: int = 0):
         self.linear_operator = linear_operator
         self.params = params
@@ -181,6 +181,29 @@ class MultigridMCSampler:
         self.ndof = linear_operator.get_ndof()
         self.nlevel = params.nlevel
         self._fixed_rhs = None
+        if linear_operator.get_m_lowrank() > 0:  # MeasuredOperator (measured.py): Q = A + B Sigma^-1 B^T
+            self.set_lowrank(linear_operator.get_B())
+
+    def set_lowrank(self, lr):
+        """Low-rank part B, Sigma (a measured.LowRankUpdate, or None to drop it); sets up B_bar of
+        every level's smoothers (sor_smoother.cc:17-37)."""
+        P = ctypes.POINTER(ctypes.c_int64)
+        if lr is None or lr.m == 0:
+            self._chk(self.lib.mgmc_set_lowrank(self.handle, 0, None, None, None, None))
+            self._lowrank = None
+            return
+        if lr.n != self.ndof:
+            raise ValueError(f"B has {lr.n} rows, the operator {self.ndof}")
+        self._lowrank = lr  # arrays stay alive for the call
+        self._chk(self.lib.mgmc_set_lowrank(self.handle, lr.m, lr.colptr.ctypes.data_as(P), lr.rows.ctypes.data_as(P),
+                                            _dp(lr.vals), _dp(lr.sigma)))
+
+    def lowrank_info(self, level: int, direction: int):
+        """(m, rows stored for B_bar of this level and sweep direction)"""
+        m = ctypes.c_int()
+        n = ctypes.c_int64()
+        self._chk(self.lib.mgmc_lowrank_info(self.handle, int(level), int(direction), ctypes.byref(m), ctypes.byref(n)))
+        return m.value, n.value
 
     # -- lifetime --
     def close(self):

@@ -546,29 +546,43 @@ static inline void sor_row_fused(const CSR& A, const double* wd, const double* b
 
 // ---- low-rank helpers ----
 // sum_i (sc B_ik) v_i.  FAITHFUL: sequential over the column's entries (the reference's sparse
-// products).  MULTICOLOUR (= device order): sparse columns sequential; dense columns nested as
-// row sums (i ascending) -> plane sums (rows ascending) -> total (planes ascending).
+// products).  MULTICOLOUR (= device order, mgmc_lowrank.hpp): the column's entry list (rows
+// ascending; a dense column lists every row) is cut into blocks of LR_BLK entries; in each block
+// lane l of 64 sums entries l, l+64, ... from 0.0 and the lanes combine by the xor butterfly
+// (32, 16, 8, 4, 2, 1); the block partials are combined the same way (lane-strided + butterfly).
+static const int LR_BLK = 4096;
+static double butterfly64(double* v) {
+    for (int off = 32; off >= 1; off >>= 1) {
+        double t[64];
+        for (int l = 0; l < 64; ++l) t[l] = v[l] + v[l ^ off];
+        std::copy(t, t + 64, v);
+    }
+    return v[0];
+}
 static double lr_dot(const Level& L, int k, double sc, const double* v, Mode mode) {
     const auto& col = L.lr.cols[k];
-    if (mode == FAITHFUL || !L.lr.dense[k]) {
+    if (mode == FAITHFUL) {
         double s = 0.0;
         for (const auto& e : col) s += (sc * e.second) * v[e.first];
         return s;
     }
-    const Lattice& lat = L.lat;
-    const int64_t nxr = lat.n[0] - 1, nyr = lat.dim >= 2 ? lat.n[1] - 1 : 1, nzr = lat.dim == 3 ? lat.n[2] - 1 : 1;
-    double total = 0.0;
-    size_t q = 0;
-    for (int64_t kk = 0; kk < nzr; ++kk) {
-        double ps = 0.0;
-        for (int64_t jj = 0; jj < nyr; ++jj) {
-            double rs = 0.0;
-            for (int64_t ii = 0; ii < nxr; ++ii, ++q) rs += (sc * col[q].second) * v[col[q].first];
-            ps += rs;
+    const int64_t n = (int64_t)col.size();
+    const int64_t nblk = (n + LR_BLK - 1) / LR_BLK;
+    std::vector<double> part(nblk);
+    double acc[64];
+    for (int64_t b = 0; b < nblk; ++b) {
+        const int64_t end = std::min(n, (b + 1) * LR_BLK);
+        for (int l = 0; l < 64; ++l) {
+            acc[l] = 0.0;
+            for (int64_t e = b * LR_BLK + l; e < end; e += 64) acc[l] = acc[l] + (sc * col[e].second) * v[col[e].first];
         }
-        total += ps;
+        part[b] = butterfly64(acc);
     }
-    return total;
+    for (int l = 0; l < 64; ++l) {
+        acc[l] = 0.0;
+        for (int64_t b = l; b < nblk; b += 64) acc[l] = acc[l] + part[b];
+    }
+    return butterfly64(acc);
 }
 // e = B s (e_i accumulates its columns in ascending k; Eigen's sparse-times-dense order)
 static void lr_expand(const Level& L, const double* s, double* e) {
@@ -585,6 +599,23 @@ static void posterior_apply(const Level& L, const double* x, double* y, Mode mod
     for (int k = 0; k < L.lr.m; ++k) t[k] = lr_dot(L, k, 1.0 / L.lr.sigma[k], x, mode);
     lr_expand(L, t.data(), g.data());
     for (int64_t i = 0; i < L.A.nrow; ++i) y[i] += g[i];
+}
+
+// r = f - (A x + B Sigma^{-1} B^T x).  FAITHFUL: the reference's apply then subtract.  MULTICOLOUR
+// (device order): the low-rank term is folded into f first, r = (f - g) - A x, so the device's
+// residual kernels run unchanged on a patched f.
+static void posterior_residual(const Level& L, const double* f, const double* x, double* r, Mode mode) {
+    const int64_t n = L.A.nrow;
+    if (mode == FAITHFUL || L.lr.m == 0) {
+        posterior_apply(L, x, r, mode);
+        for (int64_t q = 0; q < n; ++q) r[q] = f[q] - r[q];
+        return;
+    }
+    std::vector<double> t(L.lr.m), g(n);
+    for (int k = 0; k < L.lr.m; ++k) t[k] = lr_dot(L, k, 1.0 / L.lr.sigma[k], x, mode);
+    lr_expand(L, t.data(), g.data());
+    spmv(L.A, x, r);
+    for (int64_t q = 0; q < n; ++q) r[q] = (f[q] - g[q]) - r[q];
 }
 
 // inverse of a small dense matrix (row-major m x m): Gauss-Jordan with partial pivoting
@@ -922,8 +953,7 @@ struct MGMC : Sampler {
         const int cycle_ = (level > 0) ? p.cycle : 1;
         for (int j = 0; j < cycle_; ++j) {
             pre[level]->apply(f_ell[level].data(), x_ell[level].data());
-            posterior_apply(*levels[level], x_ell[level].data(), r_ell[level].data(), ctx->mode);
-            for (size_t q = 0; q < r_ell[level].size(); ++q) r_ell[level][q] = f_ell[level][q] - r_ell[level][q];
+            posterior_residual(*levels[level], f_ell[level].data(), x_ell[level].data(), r_ell[level].data(), ctx->mode);
             ig[level]->restrict_(r_ell[level].data(), f_ell[level + 1].data());
             std::fill(x_ell[level + 1].begin(), x_ell[level + 1].end(), 0.0);
             sample(level + 1);
@@ -1162,8 +1192,7 @@ void orc_prolongate_add(orc_handle* h, int level, double alpha, const double* xc
 void orc_residual_restrict(orc_handle* h, int level, const double* f, const double* x, double* fc) {
     const CSR& A = h->mg->levels[level]->A;
     std::vector<double> r(A.nrow);
-    posterior_apply(*h->mg->levels[level], x, r.data(), h->ctx.mode);
-    for (int64_t q = 0; q < A.nrow; ++q) r[q] = f[q] - r[q];
+    posterior_residual(*h->mg->levels[level], f, x, r.data(), h->ctx.mode);
     h->mg->ig[level]->restrict_(r.data(), fc);
 }
 

@@ -1,0 +1,167 @@
+"""GPU parity of the low-rank posterior path (-m gpu): Q = A + B Sigma^{-1} B^T.
+
+T2 (bitwise, np.array_equal) against the oracle's MULTICOLOUR replay of the same arithmetic order
+(mgmc_lowrank.hpp header): posterior operator apply, SOR smoother with the B_bar fix
+(sor_smoother.cc:41-53), SOR sampler with the low-rank noise (sor_sampler.cc:48-56), posterior
+residual + restriction, and whole MGMC cycles on every level with B_c = R B.  Columns of B cover
+radius-0 point measurements, radius > 0 ball averages (measured_operator.cc:92-170) and the dense
+global column.  T3: the device chain's mean / covariance against the exact posterior Q^-1.
+"""
+import numpy as np
+import pytest
+
+import multigridmc_amd as mg
+from multigridmc_amd.parameters import MeasurementParameters
+from tests import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+SEED = 5418513
+
+# shape, multigrid parameters, (radius, number of measurements, measure_global)
+CONFIGS = {
+    "2d32_point_global": ((32, 32), dict(nlevel=3), (0.0, 3, True)),
+    "2d64_ball_ssor_W": ((64, 64), dict(nlevel=4, cycle=2, smoother="SSOR", omega=0.9), (0.06, 4, False)),
+    "3d32_ball_global": ((32, 32, 32), dict(nlevel=3, ncoarsesmooth=2), (0.1, 2, True)),
+    "3d128_zsweep_points": ((128, 128, 128), dict(nlevel=3, smoother="SSOR"), (0.0, 8, False)),
+    "3d_aniso_zres_points": ((256, 40, 48), dict(nlevel=2, omega=1.1), (0.0, 5, False)),
+}
+
+
+def measured(shape, kappa_sq, radius, nmeas, glob, seed=1212417, scale=1e-3):
+    rng = np.random.default_rng(seed)
+    lat = mg.Lattice(*shape)
+    mp = MeasurementParameters(radius=radius, variance_scaling=scale, measure_global=glob, variance_global=0.02)
+    mp.measurement_locations = [list(rng.uniform(0.15, 0.85, len(shape))) for _ in range(nmeas)]
+    mp.variance = list(1.0 + 2.0 * rng.random(nmeas))
+    return mg.MeasuredOperator(mg.ShiftedLaplaceFDOperator(lat, kappa_sq), mp), lat
+
+
+def make(name, kappa_sq=25.0, chain=0):
+    shape, kw, (radius, nmeas, glob) = CONFIGS[name]
+    p = mg.MultigridParameters(**{"nlevel": 3, "smoother": "SOR", "coarse_solver": "SSOR", **kw})
+    op, lat = measured(shape, kappa_sq, radius, nmeas, glob)
+    s = mg.MultigridMCSampler(op, SEED, p, device=0, chain_id=chain)
+    st = np.concatenate([s.level_desc(level)["stencil"] for level in range(p.nlevel)])
+    mc = O.Oracle.fd(lat.shape, p, kappa_sq, mode=O.MULTICOLOUR, seed=SEED, chain=chain, override_stencils=st)
+    mc.set_lowrank(op.get_B())
+    return s, mc, p, lat, op
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_lowrank_components_bitwise(hip_device, name):
+    s, mc, p, lat, op = make(name)
+    rng = np.random.default_rng(3)
+    for level in range(p.nlevel):
+        n = s.level_desc(level)["ndof"]
+        x = rng.standard_normal(n)
+        b = rng.standard_normal(n)
+        assert np.array_equal(s.operator_apply(level, x), mc.operator_apply(level, x)), f"level {level} apply"
+        for direction in (mg.FORWARD, mg.BACKWARD):
+            d = s.smoother_apply(level, direction, 2, b, x)
+            o = mc.smoother_apply(level, direction, 2, b, x)
+            assert np.array_equal(d, o), f"level {level} dir {direction} smoother"
+            d = s.sor_sampler_apply(level, direction, 9 + level, 31, b, x)
+            o = mc.sor_sampler_apply(level, direction, 9 + level, 31, b, x)
+            assert np.array_equal(d, o), f"level {level} dir {direction} sampler"
+        if level + 1 < p.nlevel:
+            assert np.array_equal(s.residual_restrict(level, b, x), mc.residual_restrict(level, b, x)), \
+                f"level {level} residual"
+    s.close()
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_lowrank_cycles_bitwise(hip_device, name):
+    s, mc, p, lat, op = make(name)
+    rng = np.random.default_rng(11)
+    f = rng.standard_normal(lat.Nvertex)
+    x_dev = np.zeros(lat.Nvertex)
+    x_orc = np.zeros(lat.Nvertex)
+    for _ in range(2):
+        s.apply(f, x_dev)
+        mc.apply(f, x_orc)
+        assert np.array_equal(x_dev, x_orc)
+    qoi = mg.measurement_vector_index(lat, [0.5] * lat.dim)
+    s.fix_rhs(f)
+    s.set_state(x_dev)
+    mc.set_rhs(f)
+    mc.set_state(x_orc)
+    assert np.array_equal(s.sample(4, qoi), mc.sample(4, qoi))
+    assert np.array_equal(s.get_state(), mc.get_state())
+    s.close()
+
+
+def test_bbar_rows_stay_local_for_point_measurements(hip_device):
+    """Multicolour splitting: B_bar of a point measurement lives on a few vertices around it (the
+    reference's lexicographic B_bar is dense, N rows)."""
+    s, mc, p, lat, op = make("3d128_zsweep_points")
+    m = op.get_m_lowrank()
+    for level in range(p.nlevel):
+        for direction in (mg.FORWARD, mg.BACKWARD):
+            mm, rows = s.lowrank_info(level, direction)
+            assert mm == m
+            assert 0 < rows <= m * 200, f"level {level}: {rows} B_bar rows"
+    s.close()
+
+
+def test_set_lowrank_validation_and_reset(hip_device):
+    s, mc, p, lat, op = make("2d32_point_global")
+    lr = op.get_B()
+    bad = mg.LowRankUpdate.__new__(mg.LowRankUpdate)  # bypass host validation: the C-ABI must check
+    bad.__dict__.update(lr.__dict__)
+    bad.sigma = lr.sigma.copy()
+    bad.sigma[0] = -1.0
+    with pytest.raises(mg.MgmcError):
+        s.set_lowrank(bad)
+    bad.sigma = lr.sigma.copy()
+    bad.rows = lr.rows.copy()
+    bad.rows[0] = lat.Nvertex
+    with pytest.raises(mg.MgmcError):
+        s.set_lowrank(bad)
+    # m = 0 restores the prior: cycles equal the prior oracle
+    s.set_lowrank(None)
+    assert s.lowrank_info(0, mg.FORWARD) == (0, 0)
+    st = np.concatenate([s.level_desc(level)["stencil"] for level in range(p.nlevel)])
+    prior = O.Oracle.fd(lat.shape, p, 25.0, mode=O.MULTICOLOUR, seed=SEED, override_stencils=st)
+    f = np.random.default_rng(5).standard_normal(lat.Nvertex)
+    xd = np.zeros(lat.Nvertex)
+    xo = np.zeros(lat.Nvertex)
+    s.apply(f, xd)
+    prior.apply(f, xo)
+    assert np.array_equal(xd, xo)
+    s.close()
+
+
+@pytest.mark.parametrize("shape,kw,glob,nsamples,tol", [
+    ((8, 8), dict(nlevel=3, smoother="SSOR"), False, 40000, 0.04),
+    ((8, 8), dict(nlevel=3), True, 40000, 0.04),
+    ((8, 8, 8), dict(nlevel=2, ncoarsesmooth=2), True, 20000, 0.07),
+])
+def test_posterior_statistics_vs_exact_covariance(hip_device, shape, kw, glob, nsamples, tol):
+    """sampler/test_sampler.hh:260-323 on the device chain with the posterior operator (4 ball
+    measurements, radius 0.05 in 2D / 0.15 in 3D, Sigma = 1e-2 (1 + 2u), optional global
+    measurement): sample mean and covariance against the exact Q^-1 f and Q^-1, relative to
+    max|Q^-1| (tolerances as for the prior chain, test_gpu_parity.py)."""
+    radius = 0.05 if len(shape) == 2 else 0.15
+    op, lat = measured(shape, 4.0, radius, 4, glob, scale=1e-2)
+    p = mg.MultigridParameters(**{"nlevel": 3, "smoother": "SOR", "coarse_solver": "SSOR", **kw})
+    s = mg.MultigridMCSampler(op, SEED, p)
+    orc = O.Oracle.fd(lat.shape, p, 4.0, mode=O.FAITHFUL)
+    Q = orc.csr_matrix(0).toarray() + op.get_B().precision_update()
+    mu = np.random.default_rng(1342517).random(lat.Nvertex)
+    s.fix_rhs(Q @ mu)
+    s.sample(500)
+    n = lat.Nvertex
+    ex = np.zeros(n)
+    exx = np.zeros((n, n))
+    for k in range(nsamples):
+        s.sample(1)
+        x = s.get_state()
+        ex += (x - ex) / (k + 1)
+        exx += (np.outer(x, x) - exx) / (k + 1)
+    cov = exx - np.outer(ex, ex)
+    Qinv = np.linalg.inv(Q)
+    scale = np.max(np.abs(Qinv))
+    assert np.max(np.abs(ex - mu)) < 2 * tol * scale
+    assert np.max(np.abs(cov - Qinv)) < tol * scale
+    s.close()
