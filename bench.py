@@ -56,6 +56,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--plain", action="store_true", help="time the single-graph loop instead of the segmented one")
+    ap.add_argument("--posterior", type=int, default=0, metavar="M",
+                    help="BASELINE config 5: posterior operator with M point measurements (default lattice 256^3, "
+                         "6 levels); not the headline line")
+    ap.add_argument("--radius", type=float, default=0.0, help="measurement radius (--posterior)")
+    ap.add_argument("--measure-global", action="store_true", help="add the global average measurement (--posterior)")
     return ap.parse_args()
 
 
@@ -71,14 +76,18 @@ def cpu_info():
     return model
 
 
-def cpu_baseline(n, nlevel, nsamples):
+def cpu_baseline(n, nlevel, nsamples, posterior=None):
     """FAITHFUL oracle (reference algorithm: lexicographic SOR Gibbs sweeps, mt19937_64 +
-    normal_distribution, CSR operators) on the same 512^3 hierarchy, 1 thread."""
+    normal_distribution, CSR operators; with a posterior operator the reference's dense
+    lexicographic B_bar fix) on the same hierarchy, 1 thread."""
     from tests import oracle_lib as O
     p = mg.MultigridParameters(nlevel=nlevel, smoother="SOR", coarse_solver="SSOR", npresmooth=1, npostsmooth=1,
                                ncoarsesmooth=1, omega=1.0, cycle=1, coarse_scaling=1.0)
     t0 = time.perf_counter()
     o = O.Oracle.fd((n, n, n), p, kappa_sq=25.0, mode=O.FAITHFUL, seed=SEED, galerkin=1)
+    if posterior is not None:
+        o.set_lowrank(posterior.get_B())
+        o.time_samples(1)  # B_bar setup of every smoother happens on first use: keep it out of the timing
     setup = time.perf_counter() - t0
     secs = o.time_samples(nsamples)
     del o
@@ -93,6 +102,20 @@ def cpu_baseline(n, nlevel, nsamples):
     }
 
 
+def posterior_operator(prior, m, radius, measure_global):
+    """BASELINE config 5: m measurements at fixed pseudo-random interior locations with the
+    variances of measurements_template.cfg's scale (~1e-6), optional global average
+    (parameters_template.cfg: variance_global 0.01)."""
+    import numpy as np
+    from multigridmc_amd.parameters import MeasurementParameters
+    rng = np.random.default_rng(20250219)
+    mp = MeasurementParameters(radius=radius, variance_scaling=1.0, measure_global=measure_global,
+                               variance_global=0.01)
+    mp.measurement_locations = [list(rng.uniform(0.1, 0.9, 3)) for _ in range(m)]
+    mp.variance = list(1e-6 * (1.0 + rng.random(m)))
+    return mg.MeasuredOperator(prior, mp)
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -100,11 +123,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
 
     n, nlevel = args.n, args.nlevel
+    if args.posterior and "--n" not in sys.argv:
+        n = 256
+    if args.posterior and "--nlevel" not in sys.argv:
+        nlevel = 6
     lat = mg.Lattice3d(n, n, n)
     op = mg.ShiftedLaplaceFDOperator(lat, kappa_sq=1.0 / 0.2 ** 2)  # Lambda = 0.2 (parameters_template.cfg)
+    if args.posterior:
+        op = posterior_operator(op, args.posterior, args.radius, args.measure_global)
     params = mg.MultigridParameters(nlevel=nlevel, smoother="SOR", coarse_solver="SSOR", npresmooth=1, npostsmooth=1,
                                     ncoarsesmooth=1, omega=1.0, cycle=1, coarse_scaling=1.0)
+    t_setup = time.perf_counter()
     sampler = mg.MultigridMCSampler(op, SEED, params, device=local_rank, chain_id=rank)
+    t_setup = time.perf_counter() - t_setup
     qoi = mg.measurement_vector_index(lat, [0.5, 0.5, 0.5])
     n0 = lat.Nvertex
 
@@ -158,7 +189,7 @@ def main():
                     "bytes_per_launch": bytes_sweep, "avg_launch_ms": round(t_sweep * 1e3, 4)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.cpu_samples > 0:
-            cpu = cpu_baseline(n, nlevel, args.cpu_samples)
+            cpu = cpu_baseline(n, nlevel, args.cpu_samples, op if args.posterior else None)
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -180,6 +211,20 @@ def main():
             "cpu_baseline": cpu,
             "qoi": {"index": qoi, "samples": nq, "mean": mean, "variance": m2 / nq if nq else None, "chains": len(parts)},
         }
+        if args.posterior:
+            m = op.get_m_lowrank()
+            rows = [sampler.lowrank_info(lv, mg.FORWARD)[1] for lv in range(nlevel)]
+            line["metric"] = "MGMC V-cycle samples/sec, 3D posterior (low-rank measurement update)"
+            line["data"] = ("synthetic: posterior operator, f = 0, x0 = 0, Philox4x32-10 noise; "
+                            f"{args.posterior} measurements of radius {args.radius}"
+                            + (" + global average" if args.measure_global else ""))
+            line["config"]["workload"] = (f"BASELINE config 5: 3D {n}^3 posterior Q = A + B Sigma^-1 B^T (m = {m}), "
+                                          f"{nlevel}-level V-cycle, SOR Gibbs 1/1 with the B_bar fix, SSOR coarse 1")
+            line["config"]["m_lowrank"] = m
+            line["config"]["bbar_rows_forward_per_level"] = rows
+            line["config"]["setup_s"] = round(t_setup, 2)
+            if roof:
+                roof["kernel"] = "fine pre-sampler segment: Gibbs sweep + low-rank noise patch + B_bar fix"
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

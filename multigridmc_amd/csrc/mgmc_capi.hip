@@ -48,12 +48,18 @@ struct Op {
     int nsweeps;    // OP_COARSE_LDS
     int src = 0;    // buffer index read (x[src]); z-sweeps write x[1-src]
     int prolong = 0;  // z-sweep with fused prolongate-add of the coarser level's x
+    int lr_next = 0;       // sweep on a small low-rank level: the patch of the next op, fused (LR_NEXT_*)
+    uint32_t lr_next_tag = 0;
+    int lr_skip_patch = 0;  // this op's low-rank patch was done by the previous sweep's kernel
 };
 
 // z-marching sweep tile shape (mgmc_zsweep.hpp)
 // 32 x-pairs x 16 rows, 256 threads (2 core pairs per thread, 19.5 % halo), 38 KB of LDS -> 4
 // workgroups per CU; tuning history in DESIGN.md
 constexpr int ZS_XP = 32, ZS_TY = 16, ZS_NT = 256, ZS_MINW = 1, ZS_TZ = 32;
+#ifndef MGMC_ZS_MINW_PROLONG
+#define MGMC_ZS_MINW_PROLONG 1  // waves/SIMD floor of the fused-prolongation variant (4 spills: 148 B/lane)
+#endif
 
 // device copy of a level's low-rank part (mgmc_lowrank.hpp); one allocation list, freed together
 struct LowRankDev {
@@ -77,6 +83,7 @@ struct LowRankDev {
     double* sq = nullptr;          // sqrt(1/Sigma_k)
     double* part = nullptr;        // block partials
     double* w = nullptr;           // m-vector of dots
+    bool small = false;            // k_lr_small path (sparse columns, one block each, few rows)
     std::vector<void*> allocs;
 };
 
@@ -210,8 +217,9 @@ void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s)
     const int ntiles = a.ntx * a.nty * a.ntz;
     const int nb = (ntiles + 7) / 8 * 8;
     const size_t lds = zsweep_lds_bytes(XP, TY, prolong);
+    constexpr int MINWP = MINW > MGMC_ZS_MINW_PROLONG ? MINW : MGMC_ZS_MINW_PROLONG;
     if (prolong)
-        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, true, MINW>), dim3(nb), dim3(NT), lds, s, a);
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, true, MINWP>), dim3(nb), dim3(NT), lds, s, a);
     else
         hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, false, MINW>), dim3(nb), dim3(NT), lds, s, a);
 }
@@ -246,6 +254,11 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
     a.G.colour = (direction == MGMC_FORWARD) ? 0 : 1;
     const char* tz = getenv("MGMC_ZS_TZ");
     a.tz = std::max(2, (tz ? atoi(tz) : ZS_TZ) & ~1);  // even: chunks start on odd planes (coarse ring schedule)
+    if (!tz) {  // shallower z chunks until the grid has >= 1024 tiles (4 per CU): 256^3 -> 16 planes
+        const int xp = zsweep_xp(), ty = zsweep_variant() == 0 ? ZS_TY : 16;
+        const long long txy = (long long)((lv.L.nx / 2) / xp) * ((lv.L.ny - 1 + ty - 1) / ty);
+        while (a.tz > 8 && txy * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 1024) a.tz /= 2;
+    }
     const bool pr = coarse != nullptr;
     switch (zsweep_variant()) {
         case 1: launch_zsweep_t<64, 4, 256>(lv, a, pr, s); break;
@@ -449,6 +462,37 @@ void lr_fix(const Level& lv, double* x, int direction, double* f_restore, hipStr
                        (const long long*)r.rows_off, (const double*)r.save, f_restore);
 }
 
+// the fused between-sweeps kernel (k_lr_small): fix x, restore f, patch f for the next op
+void lr_small(const mgmc_handle* h, const Level& lv, double* x, int direction, int next, uint32_t next_tag,
+              const uint64_t* sample, hipStream_t s) {
+    const LowRankDev& r = lv.lr;
+    const int d = direction == MGMC_FORWARD ? 0 : 1;
+    LRSmallArgs a;
+    a.m = r.m;
+    a.meta = r.meta;
+    a.ent_off = r.ent_off;
+    a.ent_val = r.ent_val;
+    a.sc_one = r.sc_one;
+    a.sc_inv = r.sc_inv;
+    a.sq = r.sq;
+    a.x = x;
+    a.nbar = r.nbar[d];
+    a.bar_off = r.bar_off[d];
+    a.bar_val = r.bar_val[d];
+    a.nrows = r.nrows;
+    a.rows_off = r.rows_off;
+    a.coef = r.rows_coef;
+    a.mask = r.rows_mask;
+    a.save = r.save;
+    a.f = lv.f;
+    a.restore = 1;
+    a.next = next;
+    a.key = h->key;
+    a.tag = next_tag;
+    a.sample = sample;
+    hipLaunchKernelGGL(k_lr_small, dim3(1), dim3(1024), 0, s, a);
+}
+
 void lr_restore(const Level& lv, double* f, hipStream_t s) {
     const LowRankDev& r = lv.lr;
     if (r.nrows == 0) return;
@@ -557,6 +601,20 @@ void build_ops(mgmc_handle* h) {
     }
     h->ops.push_back({OP_QOI, 0, 0, 0, 0});
     if (h->levels.size() == 1) h->seg_end_pre = h->seg_begin_post = h->seg_end_post = 0;
+    // small low-rank levels: the kernel after a sweep also patches f for the level's next op
+    for (size_t q = 0; q + 1 < h->ops.size(); ++q) {
+        Op& op = h->ops[q];
+        Op& nx = h->ops[q + 1];
+        if (op.kind != OP_SWEEP || !h->levels[op.level].lr.small || nx.level != op.level) continue;
+        if (nx.kind == OP_SWEEP) {
+            op.lr_next = LR_NEXT_NOISE;
+            op.lr_next_tag = nx.tag;
+            nx.lr_skip_patch = 1;
+        } else if (nx.kind == OP_RESIDUAL_RESTRICT) {
+            op.lr_next = LR_NEXT_RESIDUAL;
+            nx.lr_skip_patch = 1;
+        }
+    }
 }
 
 void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
@@ -568,7 +626,7 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
             case OP_SWEEP: {
                 GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
                 const bool lr = lv.lr.m > 0;
-                if (lr) lr_patch(h, lv, LR_PATCH_NOISE, lv.f, op.tag, sample, s);
+                if (lr && !op.lr_skip_patch) lr_patch(h, lv, LR_PATCH_NOISE, lv.f, op.tag, sample, s);
                 double* xo = lv.x;
                 if (lv.zsweep) {
                     const Level* lc = op.prolong ? &h->levels[op.level + 1] : nullptr;
@@ -580,7 +638,10 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 } else {
                     launch_sweep(lv, lv.x, lv.f, g, op.direction, true, s);
                 }
-                if (lr) lr_fix(lv, xo, op.direction, lv.f, s);
+                if (lr && lv.lr.small)
+                    lr_small(h, lv, xo, op.direction, op.lr_next, op.lr_next_tag, sample, s);
+                else if (lr)
+                    lr_fix(lv, xo, op.direction, lv.f, s);
                 break;
             }
             case OP_COARSE_LDS: {
@@ -591,7 +652,7 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
             case OP_RESIDUAL_RESTRICT: {
                 Level& lc = h->levels[op.level + 1];
                 const bool lr = lv.lr.m > 0;
-                if (lr) {  // r = (f - B Sigma^{-1} B^T x) - A x
+                if (lr && !op.lr_skip_patch) {  // r = (f - B Sigma^{-1} B^T x) - A x
                     lr_dots(lv, lv.buf(op.src), lv.lr.sc_inv, s);
                     lr_patch(h, lv, LR_PATCH_RESIDUAL, lv.f, 0, sample, s);
                 }
@@ -1391,6 +1452,10 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
         r.nbar[d] = (int)boff.size();
         if ((rc = lr_to_device(h, r, &r.bar_off[d], boff)) || (rc = lr_to_device(h, r, &r.bar_val[d], bval))) return rc;
     }
+    bool small = getenv("MGMC_LR_NO_SMALL") == nullptr && ndense == 0 && r.nrows <= (1 << 16) &&
+                 r.nbar[0] <= (1 << 16) && r.nbar[1] <= (1 << 16);
+    for (int k = 0; k < m; ++k) small = small && meta[k].nblk <= 1;
+    r.small = small;
     return MGMC_OK;
 }
 

@@ -183,6 +183,108 @@ __global__ void __launch_bounds__(256) k_lr_restore(int n, const long long* __re
     if (u < n) f[off[u]] = save[u];
 }
 
+// ---- one workgroup for everything between two sweeps of a level with a small low-rank part ----
+// (every column sparse with <= LR_BLK entries, few B_bar rows): the fix after a sweep, the restore
+// of f, and the patch the next op of the level needs (noise of the next sweep, or the posterior
+// residual's f - B Sigma^{-1} B^T x) -- one launch instead of up to six.  Same arithmetic as the
+// separate kernels: the single-block dot is the block butterfly followed by the totals butterfly
+// over (partial, 0, 0, ...).
+enum { LR_NEXT_NONE = 0, LR_NEXT_NOISE = 1, LR_NEXT_RESIDUAL = 2 };
+
+struct LRSmallArgs {
+    int m;
+    const LRColMeta* meta;
+    const long long* ent_off;
+    const double* ent_val;
+    const double* sc_one;
+    const double* sc_inv;
+    const double* sq;
+    double* x;  // state after the sweep
+    int nbar;
+    const long long* bar_off;
+    const double* bar_val;
+    int nrows;  // rows of B
+    const long long* rows_off;
+    const double* coef;
+    const uint64_t* mask;
+    double* save;
+    double* f;
+    int restore;  // f is noise-patched on the rows of B; save holds the true f
+    int next;     // LR_NEXT_*
+    RngKey key;
+    uint32_t tag;  // sweep tag of the next sweep (LR_NEXT_NOISE)
+    const uint64_t* sample;
+};
+
+__device__ __forceinline__ double lr_wave_dot(const LRColMeta& c, const long long* __restrict__ ent_off,
+                                              const double* __restrict__ ent_val, double sc,
+                                              const double* __restrict__ v, int lane) {
+    double acc = 0.0;
+    for (long long e = lane; e < c.n; e += 64) {
+        const long long q = c.ent0 + e;
+        acc = acc + (sc * ent_val[q]) * v[ent_off[q]];
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+    double tot = lane == 0 ? 0.0 + acc : 0.0;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) tot = tot + __shfl_xor(tot, off, 64);
+    return tot;
+}
+
+__global__ void __launch_bounds__(1024) k_lr_small(LRSmallArgs a) {
+    __shared__ double ws[LR_MAX_M], ts[LR_MAX_M];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nwave = blockDim.x >> 6;
+    // 1. w = B^T x
+    for (int k = wave; k < a.m; k += nwave) {
+        const double t = lr_wave_dot(a.meta[k], a.ent_off, a.ent_val, a.sc_one[k], a.x, lane);
+        if (lane == 0) ws[k] = t;
+    }
+    __syncthreads();
+    // 2. x -= B_bar w
+    for (int u = tid; u < a.nbar; u += blockDim.x) {
+        const double* bv = a.bar_val + (long long)u * a.m;
+        double acc = 0.0;
+        for (int k = 0; k < a.m; ++k) acc = fma(bv[k], ws[k], acc);
+        const long long p = a.bar_off[u];
+        a.x[p] = a.x[p] - acc;
+    }
+    // 3. the next op's vector: Sigma^{-1} B^T x of the fixed state, or the next sweep's noise
+    if (a.next == LR_NEXT_RESIDUAL) {
+        __syncthreads();  // the fixed x rows of other waves
+        for (int k = wave; k < a.m; k += nwave) {
+            const double t = lr_wave_dot(a.meta[k], a.ent_off, a.ent_val, a.sc_inv[k], a.x, lane);
+            if (lane == 0) ts[k] = t;
+        }
+    } else if (a.next == LR_NEXT_NOISE && 2 * tid < a.m) {
+        const uint64_t sample = *a.sample;
+        const Philox4 r = philox4x32_10(LR_PAIR0 + (uint32_t)tid, a.tag, (uint32_t)sample, (uint32_t)(sample >> 32),
+                                        a.key.k0, a.key.k1);
+        double z0, z1;
+        normal_pair(r, &z0, &z1);
+        ts[2 * tid] = a.sq[2 * tid] * z0;
+        if (2 * tid + 1 < a.m) ts[2 * tid + 1] = a.sq[2 * tid + 1] * z1;
+    }
+    __syncthreads();
+    // 4. f on the rows of B: restore and / or patch
+    for (int u = tid; u < a.nrows; u += blockDim.x) {
+        const long long p = a.rows_off[u];
+        const double base = a.restore ? a.save[u] : a.f[p];
+        if (a.next == LR_NEXT_NONE) {
+            if (a.restore) a.f[p] = base;
+            continue;
+        }
+        const uint64_t msk = a.mask[u];
+        const double* cf = a.coef + (long long)u * a.m;
+        double e = 0.0;
+        for (int k = 0; k < a.m; ++k)
+            if ((msk >> k) & 1) e = e + cf[k] * ts[k];
+        if (!a.restore) a.save[u] = base;
+        a.f[p] = a.next == LR_NEXT_NOISE ? base + e : base - e;
+    }
+}
+
 // ============================================================================================
 // host side: the same orders, for the B_bar setup (M = Sigma + B^T Y needs the dots of Y)
 // ============================================================================================
