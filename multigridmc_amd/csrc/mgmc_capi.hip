@@ -58,7 +58,7 @@ struct Op {
 // workgroups per CU; tuning history in DESIGN.md
 constexpr int ZS_XP = 32, ZS_TY = 16, ZS_NT = 256, ZS_MINW = 1, ZS_TZ = 32;
 #ifndef MGMC_ZS_MINW_PROLONG
-#define MGMC_ZS_MINW_PROLONG 1  // waves/SIMD floor of the fused-prolongation variant (4 spills: 148 B/lane)
+#define MGMC_ZS_MINW_PROLONG 3  // waves/SIMD floor of the fused-prolongation variant (3: 167 VGPRs, no spill; 4 spills)
 #endif
 
 // device copy of a level's low-rank part (mgmc_lowrank.hpp); one allocation list, freed together

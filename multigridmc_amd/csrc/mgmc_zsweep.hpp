@@ -174,11 +174,16 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         xoff[u] = L.off + 1;  // threads without an item load a zero pad pair and deposit nothing
         xlds[u] = -1;
         if (it < R * WP) {
-            const ZItem t = make_item(it / WP, it % WP);
+            // rows of one parity first: a wavefront's pairs then share the row parity, so the
+            // prolongation's odd-row terms (PROLONG) are skipped by whole wavefronts
+            constexpr int NE = (R + 1) / 2;  // rows r = 0, 2, 4, ...
+            const int r = it < NE * WP ? 2 * (it / WP) : 2 * ((it - NE * WP) / WP) + 1;
+            const ZItem t = make_item(r, it % WP);
             xlds[u] = t.lds;
             xoff[u] = t.goff;
         }
     }
+    int pmask[NLX];  // PROLONG: existing terms of the item's pair (prolong_mask)
     // planes outside [0, nz] are clamped onto the zero boundary planes 0 / nz
     auto plane_base = [&](const double* v, int k) { return v + (long long)(k < 0 ? 0 : (k > L.nz ? L.nz : k)) * L.sp; };
 
@@ -209,70 +214,60 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     };
     // x_old + alpha P x_c at the fine pair (i odd, i+1) of row j, plane k, from the coarse ring.  The
     // same terms in the same order as k_prolongate_pairs: coarse parents in ascending (kk, jj, ii),
-    // each added as v += (alpha w) x_c, boundary parents skipped.
-    // tiles whose whole footprint (x region, rows, chunk planes) keeps 2 vertices off the boundary
-    // -- every fine vertex and all its coarse parents interior -- take a check-free path
-    const bool prolong_fast = PROLONG && ibase >= 3 && ibase + 2 * WP - 1 <= L.nx - 2 && j0 - 2 >= 2 &&
-                              j0 + TY + 1 <= L.ny - 2 && k0 - 2 >= 2 && k1 + 1 <= L.nz - 2;
-    auto prolong_pair = [&](double2 v, int i, int j, int k, int cq) {
-        if (prolong_fast) {  // every fine vertex and every coarse parent is interior
-            const int K0 = k >> 1, J0 = j >> 1;
-            const bool kodd = k & 1, jodd = j & 1;
-#pragma unroll
-            for (int aa = 0; aa < 2; ++aa) {
-                if (aa == 1 && !kodd) break;
-                const double* cp = cring + ((K0 + aa) & 1) * CPS + (J0 - Jst) * CW + cq;
-#pragma unroll
-                for (int bb = 0; bb < 2; ++bb) {
-                    if (bb == 1 && !jodd) break;
-                    const double c0 = cp[bb * CW], c1 = cp[bb * CW + 1];
-                    double w = 1.0;
-                    w *= 0.5;
-                    w *= jodd ? 0.5 : 1.0;
-                    w *= kodd ? 0.5 : 1.0;
-                    double w2 = 1.0;
-                    w2 *= 1.0;
-                    w2 *= jodd ? 0.5 : 1.0;
-                    w2 *= kodd ? 0.5 : 1.0;
-                    v.x += a.alpha * w * c0;
-                    v.x += a.alpha * w * c1;
-                    v.y += a.alpha * w2 * c1;
-                }
-            }
-            return v;
-        }
-        if (!(j >= 1 && j <= L.ny - 1)) return v;
-        const int q = (i - 1) >> 1;  // coarse index of the odd vertex's left parent (LDS column cq)
+    // each added as v += (alpha w) x_c, boundary parents skipped.  Branch-free: which of the six
+    // (row, column) terms of a pair exist depends only on the pair's (i, j) -- fixed per thread for
+    // the whole kernel -- so it is a 6-bit mask computed once; terms that do not exist are computed
+    // and dropped by a select.  The plane parents (kk) depend on k only, uniform across the
+    // workgroup.  alpha w = alpha 2^-(#odd of j, k) / 2 (odd position) or alpha 2^-(...) (even
+    // position): exact scalings, equal to the reference's products alpha * w.
+    const double al0 = a.alpha, al1 = a.alpha * 0.5;
+    auto prolong_mask = [&](int i, int j) {
+        const int q = (i - 1) >> 1;
         const bool in0 = i >= 1 && i <= L.nx - 1, in1 = i + 1 >= 1 && i + 1 <= L.nx - 1;
-        const int K0 = k >> 1, nk = (k & 1) ? 2 : 1;
-        const int J0 = j >> 1, nj = (j & 1) ? 2 : 1;
-        for (int aa = 0; aa < nk; ++aa) {
+        const bool cx0 = in0 && q >= 1, cx1 = in0 && q + 1 <= Lc.nx - 1, cy = in1 && q + 1 <= Lc.nx - 1;
+        const bool rin = j >= 1 && j <= L.ny - 1;
+        int m = 0;
+        for (int bb = 0; bb < 2; ++bb) {
+            const int jj = (j >> 1) + bb;
+            const bool rowok = rin && (bb == 0 || (j & 1)) && jj >= 1 && jj <= Lc.ny - 1;
+            m |= ((rowok && cx0) ? 1 : 0) << (3 * bb);
+            m |= ((rowok && cx1) ? 2 : 0) << (3 * bb);
+            m |= ((rowok && cy) ? 4 : 0) << (3 * bb);
+        }
+        return m;
+    };
+    auto prolong_pair = [&](double2 v, int j, int k, int cq, int msk) {
+#if MGMC_ZS_EXP == 8  // timing experiment: coarse ring loads only, no prolongation arithmetic
+        return v;
+#endif
+        const int K0 = k >> 1, J0 = j >> 1;
+        const int kodd = k & 1, jodd = j & 1;
+        const double awx = ldexp(al1, -(jodd + kodd)), awy = ldexp(al0, -(jodd + kodd));
+#pragma unroll
+        for (int aa = 0; aa < 2; ++aa) {
+            if (aa == 1 && !kodd) break;
             const int kk = K0 + aa;
             if (kk < 1 || kk > Lc.nz - 1) continue;
-            const double* cp = cring + (kk & 1) * CPS;
-            for (int bb = 0; bb < nj; ++bb) {
-                const int jj = J0 + bb;
-                if (jj < 1 || jj > Lc.ny - 1) continue;
-                const double* row = cp + (jj - Jst) * CW + cq;
-                double w = 1.0;
-                w *= 0.5;
-                w *= w1(j - 2 * jj);
-                w *= w1(k - 2 * kk);
-                if (in0 && q >= 1) v.x += a.alpha * w * row[0];
-                if (q + 1 <= Lc.nx - 1) {
-                    if (in0) v.x += a.alpha * w * row[1];
-                    if (in1) {
-                        double w2 = 1.0;
-                        w2 *= 1.0;
-                        w2 *= w1(j - 2 * jj);
-                        w2 *= w1(k - 2 * kk);
-                        v.y += a.alpha * w2 * row[1];
-                    }
-                }
+            const double* cp = cring + (kk & 1) * CPS + cq;
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb) {
+                if (bb == 1 && !jodd) break;
+                int rr = J0 + bb - Jst;
+                rr = rr < 0 ? 0 : (rr > CR - 1 ? CR - 1 : rr);
+                const double c0 = cp[rr * CW], c1 = cp[rr * CW + 1];
+                const double t0 = awx * c0, t1 = awx * c1, t2 = awy * c1;
+                const int bits = msk >> (3 * bb);
+                v.x = (bits & 1) ? v.x + t0 : v.x;
+                v.x = (bits & 2) ? v.x + t1 : v.x;
+                v.y = (bits & 4) ? v.y + t2 : v.y;
             }
         }
         return v;
     };
+
+#pragma unroll
+    for (int u = 0; u < NLX; ++u)
+        pmask[u] = (PROLONG && xlds[u] >= 0) ? prolong_mask(ibase + 2 * (xlds[u] % RS), j0 - 2 + xlds[u] / RS) : 0;
 
     // ---- global <-> LDS / registers ----
     double2 px[NLX];
@@ -289,7 +284,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
             double2 v = px[u];
             if (PROLONG && interior_plane(k)) {
                 const int c2 = xlds[u] % RS, r = xlds[u] / RS;
-                v = prolong_pair(v, ibase + 2 * c2, j0 - 2 + r, k, c2);
+                v = prolong_pair(v, j0 - 2 + r, k, c2, pmask[u]);
             }
             dst[xlds[u]] = v.x;
             dst[xlds[u] + WP] = v.y;
