@@ -97,6 +97,11 @@ class HipMultigridMCSampler {
         rhs_fixed_ = true;
     }
     void unfix_rhs() { rhs_fixed_ = false; }
+    // Posterior operator (MeasuredOperator, measured_operator.cc:9-49): B as CSC (m columns, rows
+    // ascending), Sigma diagonal; m = 0 drops it.  Sets up every level's B_bar (sor_smoother.cc:17-37).
+    void set_lowrank(int m, const int64_t* colptr, const int64_t* rows, const double* vals, const double* sigma) {
+        check(mgmc_set_lowrank(h_.get(), m, colptr, rows, vals, sigma), h_.get(), "mgmc_set_lowrank");
+    }
 
     // Device-resident sampling loop (driver_mgmc.cc:66-94): nsteps cycles, QoI x[qoi_index] recorded
     // after each; the state never leaves HBM.
