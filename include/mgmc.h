@@ -160,6 +160,19 @@ int mgmc_restrict(mgmc_handle* h, int level, const double* r, double* rc);
 int mgmc_prolongate_add(mgmc_handle* h, int level, double alpha, const double* xc, double* x);
 /* fc = R (f - Q x)  (fused residual + restriction of multigridmc_sampler.cc:118-120) */
 int mgmc_residual_restrict(mgmc_handle* h, int level, const double* f, const double* x, double* fc);
+/* ---- exact-statistics engine (linear_operator.hh:119-174 targets at any lattice size) ----
+ * x = Q^{-1} b with the multigrid preconditioner of MultigridPreconditioner
+ * (preconditioner/multigrid_preconditioner.cc:74-109): one deterministic cycle of the handle's
+ * hierarchy from x = 0 (its smoothers without noise, with the B_bar fix; ncoarsesmooth SSOR sweeps
+ * on the coarsest level in place of the reference's Cholesky).  method MGMC_SOLVER_LOOP is the
+ * reference's LoopSolver (solver/loop_solver.cc:9-53, x -= M(Qx - b)); MGMC_SOLVER_CG wraps the
+ * same (symmetric) cycle in conjugate gradients.  Stops when ||r||/||b|| < rtol and ||r|| < atol
+ * (the reference's test) or after maxiter iterations; *iters and *rnorm report the outcome.
+ * Host buffers, reference layout; the chain state is untouched. */
+#define MGMC_SOLVER_LOOP 0
+#define MGMC_SOLVER_CG 1
+int mgmc_solve(mgmc_handle* h, int method, const double* b, double* x, double rtol, double atol, int maxiter,
+               int* iters, double* rnorm);
 /* n standard normals of pair ids [pair0, pair0+n/2) for (sweep_tag, sample_index):
  * out[2p] = cos branch, out[2p+1] = sin branch of the Box-Muller pair p */
 int mgmc_normals(mgmc_handle* h, uint64_t pair0, size_t n, uint32_t sweep_tag, uint64_t sample_index,

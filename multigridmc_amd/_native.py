@@ -22,6 +22,8 @@ SMOOTHER_SOR = 0
 SMOOTHER_SSOR = 1
 COARSE_SSOR = 0
 COARSE_CHOLESKY = 1
+SOLVER_LOOP = 0
+SOLVER_CG = 1
 FORWARD = 1
 BACKWARD = 2
 
@@ -82,6 +84,7 @@ SIGNATURES = [
     ("mgmc_prolongate_add", c_int, [_H, c_int, c_double, _DP, _DP]),
     ("mgmc_residual_restrict", c_int, [_H, c_int, _DP, _DP, _DP]),
     ("mgmc_normals", c_int, [_H, c_uint64, c_size_t, c_uint32, c_uint64, _DP]),
+    ("mgmc_solve", c_int, [_H, c_int, _DP, _DP, c_double, c_double, c_int, POINTER(c_int), _DP]),
     ("mgmc_time_fine_sweeps", c_int, [_H, c_int, POINTER(c_float)]),
     ("mgmc_sample_timed", c_int, [_H, c_int, c_int64, _DP, _DP, POINTER(c_int)]),
     ("mgmc_comm_unique_id", c_int, [ctypes.c_char_p]),

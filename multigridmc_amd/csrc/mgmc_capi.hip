@@ -25,6 +25,7 @@
 #include "mgmc_zrestrict.hpp"
 #include "mgmc_gsweep.hpp"
 #include "mgmc_lowrank.hpp"
+#include "mgmc_solver.hpp"
 
 using namespace mgmc;
 
@@ -133,6 +134,9 @@ struct mgmc_handle {
     int nranks = 1, rank = 0;
     double* comm_buf = nullptr;  // device scratch for collectives
     bool fuse_prolong = false;   // prolongate-add fused into the first post-sweep (z-sweep levels)
+    double* sv[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // solver: b x r z p q (level 0)
+    double* sv_scal = nullptr;   // solver scalars
+    double* sv_part = nullptr;   // reduction partials
 };
 
 #define HIPCHK(h, call)                                                                              \
@@ -498,6 +502,25 @@ void lr_restore(const Level& lv, double* f, hipStream_t s) {
     if (r.nrows == 0) return;
     hipLaunchKernelGGL(k_lr_restore, dim3((r.nrows + 255) / 256), dim3(256), 0, s, r.nrows,
                        (const long long*)r.rows_off, (const double*)r.save, f);
+}
+
+// y = Q x on a level (LinearOperator::apply, linear_operator.hh:66-76)
+void launch_operator_apply(const mgmc_handle* h, const Level& lv, const double* xs, double* ys, hipStream_t s) {
+    dim3 block(64, 4, 1);
+    dim3 grid = grid3(lv.L.nx - 1, lv.L.ny - 1, lv.spec.dim == 3 ? lv.L.nz - 1 : 1, block);
+    const int dim = lv.spec.dim, np = lv.spec.npoints;
+    if (dim == 3 && np == 7)
+        hipLaunchKernelGGL((k_operator_apply<3, 7>), grid, block, 0, s, lv.L, xs, ys, lv.S);
+    else if (dim == 3)
+        hipLaunchKernelGGL((k_operator_apply<3, 27>), grid, block, 0, s, lv.L, xs, ys, lv.S);
+    else if (np == 5)
+        hipLaunchKernelGGL((k_operator_apply<2, 5>), grid, block, 0, s, lv.L, xs, ys, lv.S);
+    else
+        hipLaunchKernelGGL((k_operator_apply<2, 9>), grid, block, 0, s, lv.L, xs, ys, lv.S);
+    if (lv.lr.m > 0) {  // y += B (Sigma^{-1} B^T x)  (linear_operator.hh:71-75)
+        lr_dots(lv, xs, lv.lr.sc_inv, s);
+        lr_patch(h, lv, LR_PATCH_APPLY, ys, 0, h->ctrl + 3, s);
+    }
 }
 
 // ---- the op sequence of one sample (multigridmc_sampler.cc:103-138) ----
@@ -915,6 +938,10 @@ int mgmc_destroy(mgmc_handle* h) {
         for (auto p : lv.scratch)
             if (p) hipFree(p);
     }
+    for (auto p : h->sv)
+        if (p) hipFree(p);
+    if (h->sv_scal) hipFree(h->sv_scal);
+    if (h->sv_part) hipFree(h->sv_part);
     if (h->comm) ncclCommDestroy(h->comm);
     if (h->comm_buf) hipFree(h->comm_buf);
     if (h->ctrl) hipFree(h->ctrl);
@@ -1069,25 +1096,9 @@ int mgmc_operator_apply(mgmc_handle* h, int level, const double* x, double* y) {
     if ((rc = ensure_scratch(h, level))) return rc;
     Level& lv = h->levels[level];
     if ((rc = upload(h, level, x, lv.scratch[0]))) return rc;
-    dim3 block(64, 4, 1);
-    dim3 grid = grid3(lv.L.nx - 1, lv.L.ny - 1, lv.spec.dim == 3 ? lv.L.nz - 1 : 1, block);
-    const int dim = lv.spec.dim, np = lv.spec.npoints;
-    const double* xs = lv.scratch[0];
-    double* ys = lv.scratch[1];
-    if (dim == 3 && np == 7)
-        hipLaunchKernelGGL((k_operator_apply<3, 7>), grid, block, 0, h->stream, lv.L, xs, ys, lv.S);
-    else if (dim == 3)
-        hipLaunchKernelGGL((k_operator_apply<3, 27>), grid, block, 0, h->stream, lv.L, xs, ys, lv.S);
-    else if (np == 5)
-        hipLaunchKernelGGL((k_operator_apply<2, 5>), grid, block, 0, h->stream, lv.L, xs, ys, lv.S);
-    else
-        hipLaunchKernelGGL((k_operator_apply<2, 9>), grid, block, 0, h->stream, lv.L, xs, ys, lv.S);
-    if (lv.lr.m > 0) {  // y += B (Sigma^{-1} B^T x)  (linear_operator.hh:71-75)
-        lr_dots(lv, xs, lv.lr.sc_inv, h->stream);
-        lr_patch(h, lv, LR_PATCH_APPLY, ys, 0, h->ctrl + 3, h->stream);
-    }
+    launch_operator_apply(h, lv, lv.scratch[0], lv.scratch[1], h->stream);
     HIPCHK(h, hipGetLastError());
-    return download(h, level, ys, y);
+    return download(h, level, lv.scratch[1], y);
 }
 
 static int sweep_component(mgmc_handle* h, int level, int direction, int nsweeps, bool noise, uint32_t tag,
@@ -1269,6 +1280,150 @@ int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* tot
     *nfine = cnt * nsteps;
     for (auto& e : ev) hipEventDestroy(e);
     return MGMC_OK;
+}
+
+// ---------------- exact-statistics engine: multigrid-preconditioned solvers ----------------
+}  // extern "C"
+
+namespace {
+
+// x = M f: one deterministic multigrid cycle from x = 0 (MultigridPreconditioner::solve,
+// multigrid_preconditioner.cc:74-101) with the hierarchy's noise-free smoothers (B_bar fix
+// included) and ncoarsesmooth SSOR sweeps on the coarsest level.  Levels >= 1 work in their
+// scratch buffers; x of level 0 must be zero on entry.
+void mg_precond(mgmc_handle* h, int level, double* x, double* f, hipStream_t s) {
+    const mgmc_config& c = h->cfg;
+    Level& lv = h->levels[level];
+    auto sweep = [&](int dir) {
+        GibbsArg g = make_gibbs(h, lv, 0, 0, h->ctrl + 3);
+        launch_sweep(lv, x, f, g, dir, false, s);
+        if (lv.lr.m > 0) lr_fix(lv, x, dir, nullptr, s);
+    };
+    if (level == (int)h->levels.size() - 1) {
+        for (int t = 0; t < c.ncoarsesmooth; ++t) {
+            sweep(MGMC_FORWARD);
+            sweep(MGMC_BACKWARD);
+        }
+        return;
+    }
+    Level& lc = h->levels[level + 1];
+    const int cycle_ = level > 0 ? c.cycle : 1;
+    for (int j = 0; j < cycle_; ++j) {
+        for (int t = 0; t < c.npresmooth; ++t) {
+            sweep(MGMC_FORWARD);
+            if (c.smoother == MGMC_SMOOTHER_SSOR) sweep(MGMC_BACKWARD);
+        }
+        if (lv.lr.m > 0) {
+            lr_dots(lv, x, lv.lr.sc_inv, s);
+            lr_patch(h, lv, LR_PATCH_RESIDUAL, f, 0, h->ctrl + 3, s);
+        }
+        launch_residual_restrict(lv, lc, x, f, lc.scratch[1], lc.scratch[0], 1, s);  // zeroes x_{l+1}
+        if (lv.lr.m > 0) lr_restore(lv, f, s);
+        mg_precond(h, level + 1, lc.scratch[0], lc.scratch[1], s);
+        launch_prolongate(lv, lc, x, lc.scratch[0], c.coarse_scaling, s);
+        for (int t = 0; t < c.npostsmooth; ++t) {
+            if (c.smoother == MGMC_SMOOTHER_SSOR) sweep(MGMC_FORWARD);
+            sweep(MGMC_BACKWARD);
+        }
+    }
+}
+
+void dev_dot(mgmc_handle* h, const double* a, const double* b, int slot) {
+    const long long n = h->levels[0].L.nstore;
+    hipLaunchKernelGGL(k_dot_partial, dim3(SOLVE_NB), dim3(256), 0, h->stream, n, a, b, h->sv_part);
+    hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, h->stream, (const double*)h->sv_part, SOLVE_NB, h->sv_scal,
+                       slot);
+}
+
+int host_scalar(mgmc_handle* h, int slot, double* v) {
+    HIPCHK(h, hipMemcpyAsync(v, h->sv_scal + slot, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return MGMC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mgmc_solve(mgmc_handle* h, int method, const double* b, double* x, double rtol, double atol, int maxiter,
+               int* iters, double* rnorm) {
+    if (!h || !b || !x || !iters || !rnorm) return fail(h, MGMC_E_INVALID, "null argument");
+    if (method != MGMC_SOLVER_LOOP && method != MGMC_SOLVER_CG) return fail(h, MGMC_E_INVALID, "invalid solver method");
+    if (maxiter < 0) return fail(h, MGMC_E_INVALID, "maxiter must be >= 0");
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc;
+    for (size_t l = 1; l < h->levels.size(); ++l)
+        if ((rc = ensure_scratch(h, (int)l))) return rc;
+    Level& l0 = h->levels[0];
+    const long long n = l0.L.nstore;
+    const size_t bytes = (size_t)n * sizeof(double);
+    for (auto& p : h->sv) {
+        if (!p) {
+            if (hipMalloc(&p, bytes) != hipSuccess) {
+                p = nullptr;
+                return fail(h, MGMC_E_NOMEM, "device allocation failed (solver vectors)");
+            }
+            HIPCHK(h, hipMemsetAsync(p, 0, bytes, h->stream));
+        }
+    }
+    if (!h->sv_scal) HIPCHK(h, hipMalloc(&h->sv_scal, 16 * sizeof(double)));
+    if (!h->sv_part) HIPCHK(h, hipMalloc(&h->sv_part, SOLVE_NB * sizeof(double)));
+    double *vb = h->sv[0], *vx = h->sv[1], *vr = h->sv[2], *vz = h->sv[3], *vp = h->sv[4], *vq = h->sv[5];
+    hipStream_t s = h->stream;
+    const dim3 gv(4096), bv(256);
+    if ((rc = upload(h, 0, b, vb))) return rc;
+    HIPCHK(h, hipMemsetAsync(vx, 0, bytes, s));
+    dev_dot(h, vb, vb, 4);
+    double bb = 0.0;
+    if ((rc = host_scalar(h, 4, &bb))) return rc;
+    const double r0 = sqrt(bb);
+    *iters = 0;
+    *rnorm = r0;
+    if (r0 == 0.0) return download(h, 0, vx, x);
+    if (method == MGMC_SOLVER_LOOP) {  // LoopSolver::apply (loop_solver.cc:9-53): x -= M (A x - b)
+        for (int k = 0; k < maxiter; ++k) {
+            launch_operator_apply(h, l0, vx, vq, s);
+            hipLaunchKernelGGL(k_sub, gv, bv, 0, s, n, (const double*)vq, (const double*)vb, vr);
+            dev_dot(h, vr, vr, 2);
+            double rr;
+            if ((rc = host_scalar(h, 2, &rr))) return rc;
+            *rnorm = sqrt(rr);
+            *iters = k;
+            if (*rnorm / r0 < rtol && *rnorm < atol) break;
+            HIPCHK(h, hipMemsetAsync(vz, 0, bytes, s));
+            mg_precond(h, 0, vz, vr, s);
+            hipLaunchKernelGGL(k_sub, gv, bv, 0, s, n, (const double*)vx, (const double*)vz, vx);
+            *iters = k + 1;
+        }
+    } else {  // conjugate gradients preconditioned by the same multigrid cycle
+        HIPCHK(h, hipMemcpyAsync(vr, vb, bytes, hipMemcpyDeviceToDevice, s));
+        HIPCHK(h, hipMemsetAsync(vz, 0, bytes, s));
+        mg_precond(h, 0, vz, vr, s);
+        HIPCHK(h, hipMemcpyAsync(vp, vz, bytes, hipMemcpyDeviceToDevice, s));
+        dev_dot(h, vr, vz, 0);  // rz
+        for (int k = 0; k < maxiter; ++k) {
+            launch_operator_apply(h, l0, vp, vq, s);
+            dev_dot(h, vp, vq, 1);  // pq
+            hipLaunchKernelGGL(k_axpy_ratio, gv, bv, 0, s, n, (const double*)h->sv_scal, (const double*)(h->sv_scal + 1),
+                               1.0, (const double*)vp, vx);
+            hipLaunchKernelGGL(k_axpy_ratio, gv, bv, 0, s, n, (const double*)h->sv_scal, (const double*)(h->sv_scal + 1),
+                               -1.0, (const double*)vq, vr);
+            dev_dot(h, vr, vr, 2);
+            double rr;
+            if ((rc = host_scalar(h, 2, &rr))) return rc;
+            *rnorm = sqrt(rr);
+            *iters = k + 1;
+            if (*rnorm / r0 < rtol && *rnorm < atol) break;
+            HIPCHK(h, hipMemsetAsync(vz, 0, bytes, s));
+            mg_precond(h, 0, vz, vr, s);
+            dev_dot(h, vr, vz, 3);  // rz_new
+            hipLaunchKernelGGL(k_xpby_ratio, gv, bv, 0, s, n, (const double*)vz, (const double*)(h->sv_scal + 3),
+                               (const double*)h->sv_scal, vp);
+            HIPCHK(h, hipMemcpyAsync(h->sv_scal, h->sv_scal + 3, sizeof(double), hipMemcpyDeviceToDevice, s));
+        }
+    }
+    HIPCHK(h, hipGetLastError());
+    return download(h, 0, vx, x);
 }
 
 // ---------------- low-rank posterior part ----------------

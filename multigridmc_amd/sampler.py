@@ -198,6 +198,21 @@ class MultigridMCSampler:
         self._chk(self.lib.mgmc_set_lowrank(self.handle, lr.m, lr.colptr.ctypes.data_as(P), lr.rows.ctypes.data_as(P),
                                             _dp(lr.vals), _dp(lr.sigma)))
 
+    def solve(self, b, method: str = "cg", rtol: float = 1e-12, atol: float = 1e300, maxiter: int = 100):
+        """x = Q^{-1} b with the hierarchy as multigrid preconditioner (MultigridPreconditioner,
+        preconditioner/multigrid_preconditioner.cc:74-109) in LoopSolver (method="loop",
+        solver/loop_solver.cc:9-53) or CG (method="cg").  Returns (x, iterations, ||r||)."""
+        m = {"loop": _native.SOLVER_LOOP, "cg": _native.SOLVER_CG}.get(method)
+        if m is None:
+            raise ValueError(f"unknown solver method '{method}'")
+        b = _as_f64(b, self.ndof, "b")
+        x = np.empty(self.ndof)
+        it = ctypes.c_int()
+        rn = ctypes.c_double()
+        self._chk(self.lib.mgmc_solve(self.handle, m, _dp(b), _dp(x), float(rtol), float(atol), int(maxiter),
+                                      ctypes.byref(it), ctypes.byref(rn)))
+        return x, it.value, rn.value
+
     def lowrank_info(self, level: int, direction: int):
         """(m, rows stored for B_bar of this level and sweep direction)"""
         m = ctypes.c_int()

@@ -828,6 +828,7 @@ struct DenseCholeskySampler : Sampler {
     std::vector<double> Lmat;  // row-major lower factor
     std::vector<double> xi, g;
     DenseCholeskySampler(Ctx* c, const Level* L) : Sampler(c) {
+        lev = L;
         n = L->A.nrow;
         Lmat.assign((size_t)n * n, 0.0);
         for (int64_t r = 0; r < n; ++r)
@@ -858,17 +859,43 @@ struct DenseCholeskySampler : Sampler {
         xi.resize(n);
         g.resize(n);
     }
-    void apply(const double* f, double* x) override {
-        for (int64_t ell = 0; ell < n; ++ell) xi[ell] = normal_dist(ctx->rng);
+    // cholesky_sampler.hh:50-66: xi ~ N(0, I), x = L^{-T} (xi + L^{-1} f).  MULTICOLOUR (device order):
+    // xi from the Philox pair / branch of each vertex under the op's sweep tag, as a Gibbs sweep
+    // of this level would draw it, and the back substitution column-oriented (x_i = y_i / L_ii,
+    // then y_j -= L_ij x_i for j < i) -- the order the single-workgroup device kernel has.
+    const Level* lev = nullptr;
+    void apply(const double* f, double* x) override { solve(f, x, true); }
+    void solve(const double* f, double* x, bool noise) {
+        if (noise) {
+            if (ctx->mode == FAITHFUL) {
+                for (int64_t ell = 0; ell < n; ++ell) xi[ell] = normal_dist(ctx->rng);
+            } else {
+                const uint32_t tag = ctx->tag++;
+                for (int64_t ell = 0; ell < n; ++ell) {
+                    double z0, z1;
+                    philox_normals(ctx->seed, ctx->chain, lev->pair[ell], tag, ctx->sample, z0, z1);
+                    xi[ell] = lev->cos_branch[ell] ? z0 : z1;
+                }
+            }
+        }
         for (int64_t i = 0; i < n; ++i) {  // L g = f
             double s = f[i];
             for (int64_t k = 0; k < i; ++k) s -= Lmat[(size_t)i * n + k] * g[k];
             g[i] = s / Lmat[(size_t)i * n + i];
         }
-        for (int64_t i = n - 1; i >= 0; --i) {  // L^T x = xi + g
-            double s = xi[i] + g[i];
-            for (int64_t k = i + 1; k < n; ++k) s -= Lmat[(size_t)k * n + i] * x[k];
-            x[i] = s / Lmat[(size_t)i * n + i];
+        if (ctx->mode == FAITHFUL) {
+            for (int64_t i = n - 1; i >= 0; --i) {  // L^T x = xi + g
+                double s = noise ? xi[i] + g[i] : g[i];
+                for (int64_t k = i + 1; k < n; ++k) s -= Lmat[(size_t)k * n + i] * x[k];
+                x[i] = s / Lmat[(size_t)i * n + i];
+            }
+        } else {
+            std::vector<double> y(n);
+            for (int64_t i = 0; i < n; ++i) y[i] = noise ? xi[i] + g[i] : g[i];
+            for (int64_t i = n - 1; i >= 0; --i) {
+                x[i] = y[i] / Lmat[(size_t)i * n + i];
+                for (int64_t j = 0; j < i; ++j) y[j] -= Lmat[(size_t)i * n + j] * x[i];
+            }
         }
     }
 };
