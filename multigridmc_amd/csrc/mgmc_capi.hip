@@ -26,6 +26,7 @@
 #include "mgmc_gsweep.hpp"
 #include "mgmc_lowrank.hpp"
 #include "mgmc_solver.hpp"
+#include "mgmc_cholesky.hpp"
 
 using namespace mgmc;
 
@@ -39,7 +40,15 @@ void set_global_error(const std::string& s) {
     g_last_error = s;
 }
 
-enum OpKind { OP_SWEEP = 0, OP_RESIDUAL_RESTRICT = 1, OP_PROLONGATE = 2, OP_COARSE_LDS = 3, OP_QOI = 4, OP_COPY = 5 };
+enum OpKind {
+    OP_SWEEP = 0,
+    OP_RESIDUAL_RESTRICT = 1,
+    OP_PROLONGATE = 2,
+    OP_COARSE_LDS = 3,
+    OP_QOI = 4,
+    OP_COPY = 5,
+    OP_COARSE_CHOL = 6
+};
 
 struct Op {
     OpKind kind;
@@ -137,6 +146,11 @@ struct mgmc_handle {
     double* sv[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // solver: b x r z p q (level 0)
     double* sv_scal = nullptr;   // solver scalars
     double* sv_part = nullptr;   // reduction partials
+    std::vector<LRColumn> lr_cols;  // low-rank columns of the coarsest level, and Sigma (for the factors)
+    std::vector<double> lr_sigma;
+    int chol_n = 0;              // dense Cholesky factors of the coarsest level (mgmc_cholesky.hpp)
+    double* chol_G = nullptr;
+    double* chol_Li = nullptr;
 };
 
 #define HIPCHK(h, call)                                                                              \
@@ -523,6 +537,28 @@ void launch_operator_apply(const mgmc_handle* h, const Level& lv, const double* 
     }
 }
 
+// coarsest level: x = G f (+ U xi) with the dense Cholesky factors (mgmc_cholesky.hpp)
+void launch_coarse_chol(const mgmc_handle* h, const Level& lv, const double* f, double* x, bool noise, uint32_t tag,
+                        const uint64_t* sample, hipStream_t s) {
+    CholArgs a;
+    a.L = lv.L;
+    a.n = h->chol_n;
+    a.G = h->chol_G;
+    a.Li = h->chol_Li;
+    a.f = f;
+    a.x = x;
+    a.noise = noise ? 1 : 0;
+    a.key = h->key;
+    a.tag = tag;
+    a.sample = sample;
+    const dim3 grid((unsigned)((a.n + 255) / 256)), block(256);
+    const size_t lds = 2 * (size_t)a.n * sizeof(double);
+    if (lv.spec.dim == 3)
+        hipLaunchKernelGGL(k_coarse_chol<3>, grid, block, lds, s, a);
+    else
+        hipLaunchKernelGGL(k_coarse_chol<2>, grid, block, lds, s, a);
+}
+
 // ---- the op sequence of one sample (multigridmc_sampler.cc:103-138) ----
 // cur[l] tracks which buffer holds x_l while the ops are generated (z-sweeps ping-pong).
 void push_sweep(mgmc_handle* h, std::vector<int>& cur, int level, int direction, uint32_t& tag, int& pending_prolong) {
@@ -553,7 +589,9 @@ void build_ops_level(mgmc_handle* h, int level, uint32_t& tag, std::vector<int>&
     if (level == nlevel - 1) {
         // coarse sampler: SSORSampler(ncoarsesmooth) = ncoarsesmooth x (fwd SOR sampler, bwd SOR sampler)
         const Level& lv = h->levels[level];
-        if (lv.lds_bytes > 0 && lv.lr.m == 0) {
+        if (c.coarse_solver == MGMC_COARSE_CHOLESKY) {  // CholeskySampler (cholesky_sampler.hh:50-66)
+            h->ops.push_back({OP_COARSE_CHOL, level, 0, tag++, 1});
+        } else if (lv.lds_bytes > 0 && lv.lr.m == 0) {
             h->ops.push_back({OP_COARSE_LDS, level, MGMC_FORWARD, tag, 2 * c.ncoarsesmooth});
             tag += 2 * c.ncoarsesmooth;
         } else {
@@ -665,6 +703,10 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                     lr_small(h, lv, xo, op.direction, op.lr_next, op.lr_next_tag, sample, s);
                 else if (lr)
                     lr_fix(lv, xo, op.direction, lv.f, s);
+                break;
+            }
+            case OP_COARSE_CHOL: {
+                launch_coarse_chol(h, lv, lv.f, lv.x, true, op.tag, sample, s);
                 break;
             }
             case OP_COARSE_LDS: {
@@ -798,6 +840,58 @@ int check_level(mgmc_handle* h, int level, bool need_coarser) {
     return MGMC_OK;
 }
 
+// dense precision of the coarsest level (+ B Sigma^{-1} B^T: cholesky_sampler.cc:30-36, the oracle's
+// order), its Cholesky factor and the inverses G, L^{-1} (mgmc_cholesky.hpp); O(n^3) on the host
+int build_coarse_chol(mgmc_handle* h, const std::vector<LRColumn>* cols, const double* sigma, int m) {
+    const Level& lv = h->levels.back();
+    const long long n = (long long)lv.spec.ndof;
+    if (n > CHOL_MAX_N)
+        return fail(h, MGMC_E_UNSUPPORTED,
+                    "coarse Cholesky needs a coarsest level of at most " + std::to_string(CHOL_MAX_N) + " unknowns");
+    const int dim = lv.spec.dim;
+    const int nx = lv.spec.n[0], ny = lv.spec.n[1], nz = dim == 3 ? lv.spec.n[2] : 2;
+    std::vector<double> Q((size_t)n * n, 0.0);
+    for (long long r = 0; r < n; ++r) {
+        const int i = (int)(r % (nx - 1)) + 1, j = (int)((r / (nx - 1)) % (ny - 1)) + 1;
+        const int k = dim == 3 ? (int)(r / ((long long)(nx - 1) * (ny - 1))) + 1 : 1;
+        for (int dz = (dim == 3 ? -1 : 0); dz <= (dim == 3 ? 1 : 0); ++dz)
+            for (int dy = -1; dy <= 1; ++dy)
+                for (int dx = -1; dx <= 1; ++dx) {
+                    const int ii = i + dx, jj = j + dy, kk = k + dz;
+                    if (ii < 1 || ii > nx - 1 || jj < 1 || jj > ny - 1 || (dim == 3 && (kk < 1 || kk > nz - 1))) continue;
+                    const double v = dim == 3 ? lv.spec.st[(dz + 1) * 9 + (dy + 1) * 3 + (dx + 1)]
+                                              : lv.spec.st[(dy + 1) * 3 + (dx + 1)];
+                    const long long c = ((long long)(dim == 3 ? kk - 1 : 0) * (ny - 1) + (jj - 1)) * (nx - 1) + (ii - 1);
+                    Q[(size_t)r * n + c] = v;
+                }
+    }
+    if (m > 0) {
+        std::vector<double> Bd((size_t)n * m, 0.0);
+        for (int k = 0; k < m; ++k)
+            for (const auto& e : (*cols)[k].ent) Bd[(size_t)e.first * m + k] = e.second;
+        for (long long i = 0; i < n; ++i)
+            for (long long j = 0; j < n; ++j) {
+                double s = 0.0;
+                for (int k = 0; k < m; ++k) s += Bd[(size_t)i * m + k] / sigma[k] * Bd[(size_t)j * m + k];
+                Q[(size_t)i * n + j] += s;
+            }
+    }
+    if (!chol_factor_host(Q, n)) return fail(h, MGMC_E_INVALID, "coarse precision is not positive definite");
+    std::vector<double> Li, G;
+    chol_inverses_host(Q, n, Li, G);
+    if (h->chol_G) hipFree(h->chol_G);
+    if (h->chol_Li) hipFree(h->chol_Li);
+    h->chol_G = h->chol_Li = nullptr;
+    h->chol_n = 0;
+    const size_t bytes = (size_t)n * n * sizeof(double);
+    if (hipMalloc(&h->chol_G, bytes) != hipSuccess || hipMalloc(&h->chol_Li, bytes) != hipSuccess)
+        return fail(h, MGMC_E_NOMEM, "device allocation failed (coarse Cholesky factors)");
+    HIPCHK(h, hipMemcpy(h->chol_G, G.data(), bytes, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->chol_Li, Li.data(), bytes, hipMemcpyHostToDevice));
+    h->chol_n = (int)n;
+    return MGMC_OK;
+}
+
 void fill_desc(const LevelSpec& s, mgmc_level_desc* d) {
     memset(d, 0, sizeof(*d));
     d->nx = s.n[0];
@@ -842,8 +936,6 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     *out = nullptr;
     const std::string err = validate_config(*cfg);
     if (!err.empty()) return fail(nullptr, MGMC_E_INVALID, err);
-    if (cfg->coarse_solver == MGMC_COARSE_CHOLESKY)
-        return fail(nullptr, MGMC_E_UNSUPPORTED, "coarse_solver=Cholesky is not on the device path yet");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(nullptr, MGMC_E_HIP, "no HIP device");
     if (device < 0 || device >= ndev) return fail(nullptr, MGMC_E_INVALID, "device index out of range");
@@ -906,6 +998,8 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     uint64_t ctrl0[8] = {0, 0, (uint64_t)(int64_t)-1, 0, 0, 0, 0, 0};
     hipMemcpyAsync(h->ctrl, ctrl0, sizeof(ctrl0), hipMemcpyHostToDevice, h->stream);
     hipMemsetAsync(h->mom, 0, 4 * sizeof(double), h->stream);
+    if (cfg->coarse_solver == MGMC_COARSE_CHOLESKY && (rc = build_coarse_chol(h, nullptr, nullptr, 0)) != MGMC_OK)
+        return bail(rc);
     // op sequence of one sample
     h->fuse_prolong = getenv("MGMC_NO_FUSE_PROLONG") == nullptr;  // default: fused (A/B in DESIGN.md)
     build_ops(h);
@@ -940,6 +1034,8 @@ int mgmc_destroy(mgmc_handle* h) {
     }
     for (auto p : h->sv)
         if (p) hipFree(p);
+    if (h->chol_G) hipFree(h->chol_G);
+    if (h->chol_Li) hipFree(h->chol_Li);
     if (h->sv_scal) hipFree(h->sv_scal);
     if (h->sv_part) hipFree(h->sv_part);
     if (h->comm) ncclCommDestroy(h->comm);
@@ -1300,6 +1396,10 @@ void mg_precond(mgmc_handle* h, int level, double* x, double* f, hipStream_t s) 
         if (lv.lr.m > 0) lr_fix(lv, x, dir, nullptr, s);
     };
     if (level == (int)h->levels.size() - 1) {
+        if (h->chol_n > 0) {  // exact coarse solve, as the reference's CholeskySolver
+            launch_coarse_chol(h, lv, f, x, false, 0, h->ctrl + 3, s);
+            return;
+        }
         for (int t = 0; t < c.ncoarsesmooth; ++t) {
             sweep(MGMC_FORWARD);
             sweep(MGMC_BACKWARD);
@@ -1365,6 +1465,13 @@ int mgmc_solve(mgmc_handle* h, int method, const double* b, double* x, double rt
             }
             HIPCHK(h, hipMemsetAsync(p, 0, bytes, h->stream));
         }
+    }
+    // MultigridPreconditioner always solves the coarsest level exactly (Cholesky,
+    // multigrid_preconditioner.cc:41-45): build the dense factors if the level is small enough
+    if (h->chol_n == 0 && h->levels.back().spec.ndof <= 2048) {
+        if ((rc = build_coarse_chol(h, h->lr_cols.empty() ? nullptr : &h->lr_cols, h->lr_sigma.data(),
+                                    (int)h->lr_cols.size())))
+            return rc;
     }
     if (!h->sv_scal) HIPCHK(h, hipMalloc(&h->sv_scal, 16 * sizeof(double)));
     if (!h->sv_part) HIPCHK(h, hipMalloc(&h->sv_part, SOLVE_NB * sizeof(double)));
@@ -1652,6 +1759,14 @@ int mgmc_set_lowrank(mgmc_handle* h, int m, const int64_t* colptr, const int64_t
     if (rc) {
         for (auto& lv : h->levels) free_lowrank(lv.lr);
     }
+    h->lr_cols.clear();
+    h->lr_sigma.clear();
+    if (!rc && m > 0) {
+        h->lr_cols = cols;
+        h->lr_sigma.assign(sigma, sigma + m);
+    }
+    if (!rc && h->chol_n > 0)  // the coarse factors carry B_c Sigma^{-1} B_c^T
+        rc = build_coarse_chol(h, m > 0 ? &cols : nullptr, sigma, m);
     HIPCHK(h, hipStreamSynchronize(h->stream));
     build_ops(h);
     const int rc2 = build_graphs(h);

@@ -823,6 +823,30 @@ struct SSORSampler : Sampler {
 
 // DenseCholeskySampler (cholesky_sampler.hh:50-66, EigenDenseLLT): A = L L^T,
 // x = L^{-T}(xi + L^{-1} f)
+// U = L^{-T} (upper triangular) and G = U U^T = Q^{-1} from the lower Cholesky factor L (row-major):
+// L^{-1} by forward substitution column by column, G_ij = sum_{k >= max(i,j)} U_ik U_jk ascending k.
+// The device's host setup (mgmc_capi.hip) runs the same loops.
+static void dense_factor_inverses(const std::vector<double>& L, int64_t n, std::vector<double>& U,
+                                  std::vector<double>& G) {
+    std::vector<double> Li((size_t)n * n, 0.0);  // L^{-1}, lower
+    for (int64_t c = 0; c < n; ++c)
+        for (int64_t i = c; i < n; ++i) {
+            double s = i == c ? 1.0 : 0.0;
+            for (int64_t k = c; k < i; ++k) s -= L[(size_t)i * n + k] * Li[(size_t)k * n + c];
+            Li[(size_t)i * n + c] = s / L[(size_t)i * n + i];
+        }
+    U.assign((size_t)n * n, 0.0);
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t j = i; j < n; ++j) U[(size_t)i * n + j] = Li[(size_t)j * n + i];
+    G.assign((size_t)n * n, 0.0);
+    for (int64_t i = 0; i < n; ++i)
+        for (int64_t j = 0; j < n; ++j) {
+            double s = 0.0;
+            for (int64_t k = std::max(i, j); k < n; ++k) s += U[(size_t)i * n + k] * U[(size_t)j * n + k];
+            G[(size_t)i * n + j] = s;
+        }
+}
+
 struct DenseCholeskySampler : Sampler {
     int64_t n;
     std::vector<double> Lmat;  // row-major lower factor
@@ -860,10 +884,12 @@ struct DenseCholeskySampler : Sampler {
         g.resize(n);
     }
     // cholesky_sampler.hh:50-66: xi ~ N(0, I), x = L^{-T} (xi + L^{-1} f).  MULTICOLOUR (device order):
-    // xi from the Philox pair / branch of each vertex under the op's sweep tag, as a Gibbs sweep
-    // of this level would draw it, and the back substitution column-oriented (x_i = y_i / L_ii,
-    // then y_j -= L_ij x_i for j < i) -- the order the single-workgroup device kernel has.
+    // xi from the Philox pair / branch of each vertex under the op's sweep tag, as a Gibbs sweep of
+    // this level would draw it, and the two triangular solves replaced by products with the
+    // precomputed U = L^{-T} and G = Q^{-1} = U U^T (dense_factor_inverses): x = G f + U xi, each
+    // row an fma chain in ascending column order -- every row independent, as the device computes it.
     const Level* lev = nullptr;
+    std::vector<double> U, G;  // row-major n x n (MULTICOLOUR)
     void apply(const double* f, double* x) override { solve(f, x, true); }
     void solve(const double* f, double* x, bool noise) {
         if (noise) {
@@ -878,24 +904,27 @@ struct DenseCholeskySampler : Sampler {
                 }
             }
         }
+        if (ctx->mode == MULTICOLOUR) {
+            if (U.empty()) dense_factor_inverses(Lmat, n, U, G);
+            for (int64_t i = 0; i < n; ++i) {
+                double a = 0.0;
+                for (int64_t j = 0; j < n; ++j) a = fma(G[(size_t)i * n + j], f[j], a);
+                double b = 0.0;
+                if (noise)
+                    for (int64_t j = i; j < n; ++j) b = fma(U[(size_t)i * n + j], xi[j], b);
+                x[i] = a + b;
+            }
+            return;
+        }
         for (int64_t i = 0; i < n; ++i) {  // L g = f
             double s = f[i];
             for (int64_t k = 0; k < i; ++k) s -= Lmat[(size_t)i * n + k] * g[k];
             g[i] = s / Lmat[(size_t)i * n + i];
         }
-        if (ctx->mode == FAITHFUL) {
-            for (int64_t i = n - 1; i >= 0; --i) {  // L^T x = xi + g
-                double s = noise ? xi[i] + g[i] : g[i];
-                for (int64_t k = i + 1; k < n; ++k) s -= Lmat[(size_t)k * n + i] * x[k];
-                x[i] = s / Lmat[(size_t)i * n + i];
-            }
-        } else {
-            std::vector<double> y(n);
-            for (int64_t i = 0; i < n; ++i) y[i] = noise ? xi[i] + g[i] : g[i];
-            for (int64_t i = n - 1; i >= 0; --i) {
-                x[i] = y[i] / Lmat[(size_t)i * n + i];
-                for (int64_t j = 0; j < i; ++j) y[j] -= Lmat[(size_t)i * n + j] * x[i];
-            }
+        for (int64_t i = n - 1; i >= 0; --i) {  // L^T x = xi + g
+            double s = noise ? xi[i] + g[i] : g[i];
+            for (int64_t k = i + 1; k < n; ++k) s -= Lmat[(size_t)k * n + i] * x[k];
+            x[i] = s / Lmat[(size_t)i * n + i];
         }
     }
 };

@@ -25,6 +25,8 @@ CONFIGS = {
     "3d32_ball_global": ((32, 32, 32), dict(nlevel=3, ncoarsesmooth=2), (0.1, 2, True)),
     "3d128_zsweep_points": ((128, 128, 128), dict(nlevel=3, smoother="SSOR"), (0.0, 8, False)),
     "3d_aniso_zres_points": ((256, 40, 48), dict(nlevel=2, omega=1.1), (0.0, 5, False)),
+    "2d32_point_global_chol": ((32, 32), dict(nlevel=3, coarse_solver="Cholesky"), (0.0, 3, True)),
+    "3d32_ball_chol_ssor": ((32, 32, 32), dict(nlevel=3, smoother="SSOR", coarse_solver="Cholesky"), (0.1, 2, False)),
 }
 
 
@@ -133,7 +135,7 @@ def test_set_lowrank_validation_and_reset(hip_device):
 
 
 @pytest.mark.parametrize("shape,kw,glob,nsamples,tol", [
-    ((8, 8), dict(nlevel=3, smoother="SSOR"), False, 40000, 0.04),
+    ((8, 8), dict(nlevel=3, smoother="SSOR", coarse_solver="Cholesky"), False, 40000, 0.04),
     ((8, 8), dict(nlevel=3), True, 40000, 0.04),
     ((8, 8, 8), dict(nlevel=2, ncoarsesmooth=2), True, 20000, 0.07),
 ])

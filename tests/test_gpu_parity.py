@@ -57,6 +57,10 @@ CONFIGS = {
     # level 1 -> level 2, partial tiles in y and z
     "3d_zres7": ((256, 40, 48), dict(nlevel=2)),
     "3d_zres27": ((512, 16, 24), dict(nlevel=3)),
+    # dense Cholesky coarse sampler (CholeskySampler, x = G f + U xi on the coarsest level)
+    "2d64_chol_W": ((64, 64), dict(nlevel=4, cycle=2, coarse_solver="Cholesky")),
+    "3d32_chol_ssor": ((32, 32, 32), dict(nlevel=3, smoother="SSOR", coarse_solver="Cholesky")),
+    "3d128_zsweep_chol": ((128, 128, 128), dict(nlevel=5, coarse_solver="Cholesky")),
 }
 
 
@@ -211,6 +215,7 @@ def _mean_cov(s, f, nsamples, nwarmup=200):
 @pytest.mark.parametrize("shape,kw,nsamples,tol", [
     ((8, 8), dict(nlevel=3, ncoarsesmooth=2), 40000, 0.04),
     ((8, 8), dict(nlevel=3, smoother="SSOR", cycle=2), 40000, 0.04),
+    ((8, 8), dict(nlevel=3, smoother="SSOR", coarse_solver="Cholesky"), 40000, 0.04),
     ((8, 8, 8), dict(nlevel=2, ncoarsesmooth=2), 20000, 0.07),
 ])
 def test_mgmc_statistics_vs_exact_covariance(hip_device, shape, kw, nsamples, tol):
@@ -303,8 +308,8 @@ def test_invalid_level_and_sizes_raise(hip_device):
     with pytest.raises(mg.MgmcError):
         s.sample(3, lat.Nvertex + 5)
     s.close()
-    with pytest.raises(mg.MgmcError):
-        make((16, 16), coarse_solver="Cholesky")
+    with pytest.raises(mg.MgmcError):  # dense coarse Cholesky needs a small coarsest level
+        make((128, 128), nlevel=1, coarse_solver="Cholesky")
 
 
 def test_cpp_host_side_sample_matches_python_path(hip_device, tmp_path):
