@@ -363,8 +363,10 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
     a.ntx = (lc.L.nx - 1 + CX - 1) / CX;
     a.nty = (lc.L.ny - 1 + CY - 1) / CY;
     // 8 coarse planes per workgroup, fewer on small levels so the grid still fills the chip
+    // (512^3 level 1 -> 2: kz 4, 103 us against 116 / 146 us with 2 / 8)
     const char* kz = getenv("MGMC_ZR_KZ");
-    a.kz = kz ? atoi(kz) : ((long long)a.ntx * a.nty * (lc.L.nz - 1) >= 8 * 1024 ? 8 : 2);
+    const long long work = (long long)a.ntx * a.nty * (lc.L.nz - 1);
+    a.kz = kz ? atoi(kz) : (work >= 8 * 1024 ? 8 : (work >= 4 * 1024 ? 4 : 2));
     a.ntz = (lc.L.nz - 1 + a.kz - 1) / a.kz;
     const int nt = a.ntx * a.nty * a.ntz;
     const int nb = (nt + 7) / 8 * 8;

@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
         roff[u] = Lf.off + 1;
         rlds[u] = -1;
         rflag[u] = 0;
-        rxo[u] = 0;
+        rxo[u] = XS + 1;  // spare items read (and discard) an in-range LDS neighbourhood
         if (it < RR * RP) {
             const int r = it / RP, c2 = it - r * RP;
             const int j = rj0 + r, i = ri0 + 2 * c2;
@@ -135,43 +135,50 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
 #pragma unroll
         for (int u = 0; u < NLR; ++u) pf[u] = *reinterpret_cast<const double2*>(base + roff[u]);
     };
-    // residual of fine plane k over the residual region (vertices outside the fine interior -> 0)
+    // residual of fine plane k over the residual region (vertices outside the fine interior -> 0).
+    // The two vertices of a pair advance together through the stencil terms, so their dependent
+    // adds interleave; each chain still adds its terms in ascending column order from 0.0.
     auto residual = [&](int k, const double2 (&fv)[NLR]) {
         const bool kin = k >= 1 && k <= Lf.nz - 1;
         const double* pl[3] = {xs + xslot(k - 1) * XPS, xs + xslot(k) * XPS, xs + xslot(k + 1) * XPS};
 #pragma unroll
         for (int u = 0; u < NLR; ++u) {
             if (rlds[u] < 0) continue;
+            const int o0 = rxo[u], o1 = rxo[u] + XPP;  // odd / even vertex
+            const int m0 = o0 + XPP - 1, m1 = o1 - XPP;   // their x-1 neighbours (x+1 = m + 1)
+            double y0 = 0.0, y1 = 0.0;
+            if (NPTS == 7) {
+                y0 += a.S.a[4] * pl[0][o0];
+                y1 += a.S.a[4] * pl[0][o1];
+                y0 += a.S.a[10] * pl[1][o0 - XS];
+                y1 += a.S.a[10] * pl[1][o1 - XS];
+                y0 += a.S.a[12] * pl[1][m0];
+                y1 += a.S.a[12] * pl[1][m1];
+                y0 += a.S.a[13] * pl[1][o0];
+                y1 += a.S.a[13] * pl[1][o1];
+                y0 += a.S.a[14] * pl[1][m0 + 1];
+                y1 += a.S.a[14] * pl[1][m1 + 1];
+                y0 += a.S.a[16] * pl[1][o0 + XS];
+                y1 += a.S.a[16] * pl[1][o1 + XS];
+                y0 += a.S.a[22] * pl[2][o0];
+                y1 += a.S.a[22] * pl[2][o1];
+            } else {
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                double out = 0.0;
-                if (kin && (rflag[u] & (1 << e))) {
-                    const int o = rxo[u] + (e ? XPP : 0);
-                    const int xm = e ? o - XPP : o + XPP - 1;  // x-1; x+1 is xm + 1
-                    double y = 0.0;
-                    if (NPTS == 7) {
-                        y += a.S.a[4] * pl[0][o];
-                        y += a.S.a[10] * pl[1][o - XS];
-                        y += a.S.a[12] * pl[1][xm];
-                        y += a.S.a[13] * pl[1][o];
-                        y += a.S.a[14] * pl[1][xm + 1];
-                        y += a.S.a[16] * pl[1][o + XS];
-                        y += a.S.a[22] * pl[2][o];
-                    } else {
+                for (int dz = 0; dz < 3; ++dz)
 #pragma unroll
-                        for (int dz = 0; dz < 3; ++dz)
-#pragma unroll
-                            for (int dy = -1; dy <= 1; ++dy) {
-                                const double* rowp = pl[dz] + dy * XS;
-                                y += a.S.a[dz * 9 + (dy + 1) * 3 + 0] * rowp[xm];
-                                y += a.S.a[dz * 9 + (dy + 1) * 3 + 1] * rowp[o];
-                                y += a.S.a[dz * 9 + (dy + 1) * 3 + 2] * rowp[xm + 1];
-                            }
+                    for (int dy = -1; dy <= 1; ++dy) {
+                        const double* rowp = pl[dz] + dy * XS;
+                        const int c = dz * 9 + (dy + 1) * 3;
+                        y0 += a.S.a[c] * rowp[m0];
+                        y1 += a.S.a[c] * rowp[m1];
+                        y0 += a.S.a[c + 1] * rowp[o0];
+                        y1 += a.S.a[c + 1] * rowp[o1];
+                        y0 += a.S.a[c + 2] * rowp[m0 + 1];
+                        y1 += a.S.a[c + 2] * rowp[m1 + 1];
                     }
-                    out = (e == 0 ? fv[u].x : fv[u].y) - y;
-                }
-                rs[rlds[u] + (e ? RP : 0)] = out;
             }
+            rs[rlds[u]] = (kin && (rflag[u] & 1)) ? fv[u].x - y0 : 0.0;
+            rs[rlds[u] + RP] = (kin && (rflag[u] & 2)) ? fv[u].y - y1 : 0.0;
         }
     };
     // acc += the 9 terms (sy, sx ascending) of restriction plane index sz from the residual plane
