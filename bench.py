@@ -102,6 +102,63 @@ def cpu_baseline(n, nlevel, nsamples, posterior=None):
     }
 
 
+class Collectives:
+    """The bench's three collectives (barrier, max of the timed interval, all-gather of the per-chain
+    QoI moments -- 24 B per chain).  N > 1: RCCL on the library's stream, with the unique id shipped
+    by torch.distributed gloo on the CPU; if the RCCL communicator cannot be created (e.g. ranks
+    sharing one device), the same three host-side collectives run on gloo."""
+
+    def __init__(self, sampler, rank, world):
+        self.s, self.rank, self.world, self.rccl = sampler, rank, world, False
+        if world == 1:
+            return
+        import torch.distributed as dist
+        self.dist = dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        obj = [None]
+        if rank == 0:
+            try:
+                obj[0] = mg.comm_unique_id()
+            except mg.MgmcError as e:
+                print(f"rank 0: no RCCL unique id ({e})", file=sys.stderr)
+        dist.broadcast_object_list(obj, src=0)
+        try:
+            if obj[0] is None:
+                raise mg.MgmcError(-2, "no RCCL unique id")
+            sampler.comm_init(world, rank, obj[0])
+            ok = 1
+        except mg.MgmcError as e:
+            print(f"rank {rank}: RCCL communicator unavailable ({e}); host collectives on gloo", file=sys.stderr)
+            ok = 0
+        flags = [None] * world
+        dist.all_gather_object(flags, ok)
+        self.rccl = all(f == 1 for f in flags)
+        if not self.rccl and ok:
+            sampler.comm_destroy()
+
+    def barrier(self):
+        if self.rccl or self.world == 1:
+            self.s.comm_barrier()  # RCCL all-reduce + device synchronisation
+        else:
+            self.s.synchronize()
+            self.dist.barrier()
+
+    def max(self, v):
+        if self.rccl or self.world == 1:
+            return self.s.comm_allreduce_max(v)
+        out = [None] * self.world
+        self.dist.all_gather_object(out, v)
+        return max(out)
+
+    def allgather_moments(self):
+        if self.rccl or self.world == 1:
+            return self.s.comm_allgather_moments(self.world)
+        import numpy as np
+        out = [None] * self.world
+        self.dist.all_gather_object(out, list(self.s.qoi_moments()))
+        return np.array(out)
+
+
 def posterior_operator(prior, m, radius, measure_global):
     """BASELINE config 5: m measurements at fixed pseudo-random interior locations with the
     variances of measurements_template.cfg's scale (~1e-6), optional global average
@@ -134,24 +191,19 @@ def main():
     params = mg.MultigridParameters(nlevel=nlevel, smoother="SOR", coarse_solver="SSOR", npresmooth=1, npostsmooth=1,
                                     ncoarsesmooth=1, omega=1.0, cycle=1, coarse_scaling=1.0)
     t_setup = time.perf_counter()
-    sampler = mg.MultigridMCSampler(op, SEED, params, device=local_rank, chain_id=rank)
+    # MGMC_BENCH_DEVICE pins every rank to one device (rehearsing the N>1 path on a 1-GPU box)
+    device = int(os.environ.get("MGMC_BENCH_DEVICE", local_rank))
+    sampler = mg.MultigridMCSampler(op, SEED, params, device=device, chain_id=rank)
     t_setup = time.perf_counter() - t_setup
     qoi = mg.measurement_vector_index(lat, [0.5, 0.5, 0.5])
     n0 = lat.Nvertex
 
-    if world > 1:
-        # host rendezvous only (gloo, CPU): ship rank 0's RCCL id; every device-side collective
-        # (barrier, max-time, QoI all-gather) then runs on RCCL inside the library
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        obj = [mg.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        sampler.comm_init(world, rank, obj[0])
+    coll = Collectives(sampler, rank, world)
 
     # warmup (prior: f = 0, x0 = 0 -- driver_mgmc.cc:61-69 with mean_x_exact = xbar = 0)
     sampler.sample(args.warmup, qoi)
     sampler.reset_moments()
-    sampler.comm_barrier()  # RCCL barrier + device synchronisation
+    coll.barrier()  # barrier + device synchronisation
     t0 = time.perf_counter()
     if args.plain:
         sampler.sample_async(args.steps, qoi)
@@ -161,11 +213,11 @@ def main():
         _, fine_ms, nfine = sampler.sample_timed(args.steps, qoi)
     sampler.synchronize()
     t1 = time.perf_counter()
-    sampler.comm_barrier()
-    elapsed = sampler.comm_allreduce_max(t1 - t0)
+    coll.barrier()
+    elapsed = coll.max(t1 - t0)
 
     from multigridmc_amd.distributed import merge_moments
-    parts = sampler.comm_allgather_moments(world)
+    parts = coll.allgather_moments()
     nq, mean, m2 = merge_moments([tuple(r) for r in parts])
 
     if rank == 0:
@@ -206,7 +258,8 @@ def main():
             "config": {"workload": f"3D {n}^3 shifted-Laplace FD prior (kappa^2 = 25), {nlevel}-level V-cycle, "
                                    f"SOR Gibbs 1/1, SSOR coarse 1, omega 1, one independent chain per GPU",
                        "lattice": [n, n, n], "unknowns": n0, "nlevel": nlevel, "chains": world,
-                       "parallelism": f"chains{world} (independent MCMC chains, 1 per GPU; RCCL all-gather of QoI moments)"},
+                       "parallelism": f"chains{world} (independent MCMC chains, 1 per GPU; "
+                                      f"{'RCCL' if coll.rccl or world == 1 else 'gloo'} all-gather of QoI moments)"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "qoi": {"index": qoi, "samples": nq, "mean": mean, "variance": m2 / nq if nq else None, "chains": len(parts)},

@@ -376,6 +376,9 @@ class MultigridMCSampler:
     def comm_barrier(self):
         self._chk(self.lib.mgmc_comm_barrier(self.handle))
 
+    def comm_destroy(self):
+        self._chk(self.lib.mgmc_comm_destroy(self.handle))
+
     def time_fine_sweeps(self, nsweeps: int) -> float:
         ms = ctypes.c_float()
         self._chk(self.lib.mgmc_time_fine_sweeps(self.handle, int(nsweeps), ctypes.byref(ms)))

@@ -213,3 +213,55 @@ def test_cpp_host_side_describe_and_loud_failure(tmp_path):
         return
     r = subprocess.run([exe, "sample", "2"], capture_output=True, text=True)
     assert r.returncode == 255 and "ERROR: mgmc_create failed" in r.stderr
+
+
+class _FakeChain:
+    """Stands in for a device sampler in bench.Collectives: RCCL unavailable, per-rank moments."""
+
+    def __init__(self, rank):
+        self.rank = rank
+
+    def comm_init(self, world, rank, uid):
+        raise mg.MgmcError(-2, "RCCL error invalid usage (test)")
+
+    def synchronize(self):
+        pass
+
+    def qoi_moments(self):
+        return np.array([10.0 + self.rank, 0.5 * self.rank, 2.0])
+
+
+def _bench_coll_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import bench
+    c = bench.Collectives(_FakeChain(rank), rank, world)
+    c.barrier()
+    q.put((rank, c.rccl, c.max(1.0 + rank), c.allgather_moments().tolist()))
+    c.dist.barrier()
+    c.dist.destroy_process_group()
+
+
+def test_bench_collectives_fall_back_to_gloo_world2():
+    """bench.py's N > 1 collectives (barrier, max time, per-chain moments) when the RCCL
+    communicator cannot be created: the same values over gloo, identical on every rank."""
+    import socket
+
+    import torch.multiprocessing as tmp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_coll_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        rccl, tmax, parts = res[r]
+        assert rccl is False and tmax == 2.0
+        assert parts == [[10.0, 0.0, 2.0], [11.0, 0.5, 2.0]]
