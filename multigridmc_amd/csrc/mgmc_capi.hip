@@ -236,10 +236,15 @@ void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s)
     const int nb = (ntiles + 7) / 8 * 8;
     const size_t lds = zsweep_lds_bytes(XP, TY, prolong);
     constexpr int MINWP = MINW > MGMC_ZS_MINW_PROLONG ? MINW : MGMC_ZS_MINW_PROLONG;
-    if (prolong)
-        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, true, MINWP>), dim3(nb), dim3(NT), lds, s, a);
+    // alpha a power of two (coarse_scaling 1): fma prolongation terms, same bits (mgmc_zsweep.hpp)
+    int ex;
+    const bool pow2 = std::isnormal(a.alpha) && std::frexp(std::fabs(a.alpha), &ex) == 0.5 && ex > -900 && ex < 900;
+    if (prolong && pow2)
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 2, MINWP>), dim3(nb), dim3(NT), lds, s, a);
+    else if (prolong)
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 1, MINWP>), dim3(nb), dim3(NT), lds, s, a);
     else
-        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, false, MINW>), dim3(nb), dim3(NT), lds, s, a);
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 0, MINW>), dim3(nb), dim3(NT), lds, s, a);
 }
 
 // tile-shape variant (MGMC_ZS_VARIANT, for tuning experiments; 0 = default)

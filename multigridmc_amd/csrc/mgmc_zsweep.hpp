@@ -67,8 +67,11 @@ struct ZItem {
 #else
 #define ZS_STEP_SYNC() __syncthreads()
 #endif
+// PROLONG: 0 plain sweep; 1 fused prolongation, terms v + (alpha w) x_c (any alpha); 2 the same with
+// v = fma(alpha w, x_c, v), selected when alpha is a power of two: alpha w x_c is then exact, so the
+// fma rounds once like the separate add and the bits are the same.
 // MINW: minimum waves per SIMD the register allocation must allow (1 = unconstrained)
-template <int XP, int TY, int NT, bool PROLONG, int MINW>
+template <int XP, int TY, int NT, int PROLONG, int MINW>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW))) k_zsweep_rb7(ZSweepArgs a) {
     constexpr int WP = XP + 4;     // pairs per LDS row: positions [2*q0-3, 2*q0+2*XP+4]
     // LDS row = [odd positions of the WP pairs | even positions | 2 pad]: lanes owning consecutive
@@ -183,7 +186,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
             xoff[u] = t.goff;
         }
     }
-    int pmask[NLX];  // PROLONG: existing terms of the item's pair (prolong_mask)
+    // PROLONG: per staged pair, the row parity and the coarse-ring offset of its first parent
+    // (coarse column q = (i-1)/2 = q0-2+c2, coarse row j>>1)
+    int pjodd[NLX], pcro[NLX];
     // planes outside [0, nz] are clamped onto the zero boundary planes 0 / nz
     auto plane_base = [&](const double* v, int k) { return v + (long long)(k < 0 ? 0 : (k > L.nz ? L.nz : k)) * L.sp; };
 
@@ -214,60 +219,52 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     };
     // x_old + alpha P x_c at the fine pair (i odd, i+1) of row j, plane k, from the coarse ring.  The
     // same terms in the same order as k_prolongate_pairs: coarse parents in ascending (kk, jj, ii),
-    // each added as v += (alpha w) x_c, boundary parents skipped.  Branch-free: which of the six
-    // (row, column) terms of a pair exist depends only on the pair's (i, j) -- fixed per thread for
-    // the whole kernel -- so it is a 6-bit mask computed once; terms that do not exist are computed
-    // and dropped by a select.  The plane parents (kk) depend on k only, uniform across the
-    // workgroup.  alpha w = alpha 2^-(#odd of j, k) / 2 (odd position) or alpha 2^-(...) (even
-    // position): exact scalings, equal to the reference's products alpha * w.
+    // each added as v += (alpha w) x_c.  No existence tests: a parent on the coarse boundary (index 0
+    // or n_c) is a zero of the padded layout (boundary vertices and pads are zero, and the ring's
+    // clamped rows / planes are boundary rows / planes), so its term adds +0 and leaves v unchanged
+    // -- the reference skips it (intergrid_operator.hh:106-120); the two agree bit for bit except for
+    // the sign of an exact zero (-0 + 0 = +0).  Fine positions outside the domain (staged halo
+    // columns / rows past the boundary) only ever combine zero parents or are never read.  The plane
+    // parents (kk) depend on k only, the row parents on the row, both uniform across a wavefront.
+    // alpha w = alpha 2^-(#odd of j, k) / 2 (odd position) or alpha 2^-(...) (even position): exact
+    // scalings, equal to the reference's products alpha * w.
     const double al0 = a.alpha, al1 = a.alpha * 0.5;
-    auto prolong_mask = [&](int i, int j) {
-        const int q = (i - 1) >> 1;
-        const bool in0 = i >= 1 && i <= L.nx - 1, in1 = i + 1 >= 1 && i + 1 <= L.nx - 1;
-        const bool cx0 = in0 && q >= 1, cx1 = in0 && q + 1 <= Lc.nx - 1, cy = in1 && q + 1 <= Lc.nx - 1;
-        const bool rin = j >= 1 && j <= L.ny - 1;
-        int m = 0;
-        for (int bb = 0; bb < 2; ++bb) {
-            const int jj = (j >> 1) + bb;
-            const bool rowok = rin && (bb == 0 || (j & 1)) && jj >= 1 && jj <= Lc.ny - 1;
-            m |= ((rowok && cx0) ? 1 : 0) << (3 * bb);
-            m |= ((rowok && cx1) ? 2 : 0) << (3 * bb);
-            m |= ((rowok && cy) ? 4 : 0) << (3 * bb);
-        }
-        return m;
-    };
-    auto prolong_pair = [&](double2 v, int j, int k, int cq, int msk) {
+    auto prolong_pair = [&](double2 v, int jodd, int k, int cro) {
 #if MGMC_ZS_EXP == 8  // timing experiment: coarse ring loads only, no prolongation arithmetic
         return v;
 #endif
-        const int K0 = k >> 1, J0 = j >> 1;
-        const int kodd = k & 1, jodd = j & 1;
+        const int K0 = k >> 1;
+        const int kodd = k & 1;
         const double awx = ldexp(al1, -(jodd + kodd)), awy = ldexp(al0, -(jodd + kodd));
+        const double* cp0 = cring + cro;
 #pragma unroll
         for (int aa = 0; aa < 2; ++aa) {
             if (aa == 1 && !kodd) break;
-            const int kk = K0 + aa;
-            if (kk < 1 || kk > Lc.nz - 1) continue;
-            const double* cp = cring + (kk & 1) * CPS + cq;
+            const double* cp = cp0 + ((K0 + aa) & 1) * CPS;
 #pragma unroll
             for (int bb = 0; bb < 2; ++bb) {
                 if (bb == 1 && !jodd) break;
-                int rr = J0 + bb - Jst;
-                rr = rr < 0 ? 0 : (rr > CR - 1 ? CR - 1 : rr);
-                const double c0 = cp[rr * CW], c1 = cp[rr * CW + 1];
-                const double t0 = awx * c0, t1 = awx * c1, t2 = awy * c1;
-                const int bits = msk >> (3 * bb);
-                v.x = (bits & 1) ? v.x + t0 : v.x;
-                v.x = (bits & 2) ? v.x + t1 : v.x;
-                v.y = (bits & 4) ? v.y + t2 : v.y;
+                const double c0 = cp[bb * CW], c1 = cp[bb * CW + 1];
+                if (PROLONG == 2) {
+                    v.x = fma(awx, c0, v.x);
+                    v.x = fma(awx, c1, v.x);
+                    v.y = fma(awy, c1, v.y);
+                } else {
+                    v.x = v.x + awx * c0;
+                    v.x = v.x + awx * c1;
+                    v.y = v.y + awy * c1;
+                }
             }
         }
         return v;
     };
 
 #pragma unroll
-    for (int u = 0; u < NLX; ++u)
-        pmask[u] = (PROLONG && xlds[u] >= 0) ? prolong_mask(ibase + 2 * (xlds[u] % RS), j0 - 2 + xlds[u] / RS) : 0;
+    for (int u = 0; u < NLX; ++u) {
+        const int c2 = xlds[u] < 0 ? 0 : xlds[u] % RS, j = xlds[u] < 0 ? j0 : j0 - 2 + xlds[u] / RS;
+        pjodd[u] = j & 1;
+        pcro[u] = c2 + ((j >> 1) - Jst) * CW;
+    }
 
     // ---- global <-> LDS / registers ----
     double2 px[NLX];
@@ -282,10 +279,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         for (int u = 0; u < NLX; ++u) {
             if (xlds[u] < 0) continue;
             double2 v = px[u];
-            if (PROLONG && interior_plane(k)) {
-                const int c2 = xlds[u] % RS, r = xlds[u] / RS;
-                v = prolong_pair(v, j0 - 2 + r, k, c2, pmask[u]);
-            }
+            if (PROLONG && interior_plane(k)) v = prolong_pair(v, pjodd[u], k, pcro[u]);
             dst[xlds[u]] = v.x;
             dst[xlds[u] + WP] = v.y;
         }
@@ -452,10 +446,13 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     }
 }
 
+#ifndef MGMC_ZS_LDS_EXTRA
+#define MGMC_ZS_LDS_EXTRA 0  // timing experiments only: extra LDS bytes of the plain variant (occupancy)
+#endif
 inline size_t zsweep_lds_bytes(int XP, int TY, bool prolong) {
     const int RS = 2 * (XP + 4) + 2, R = TY + 4;
     const int coarse = prolong ? 2 * (TY / 2 + 3) * (XP + 6) : 0;
-    return (size_t)(3 * R * RS + 3 * 64 + 130 + coarse) * sizeof(double);
+    return (size_t)(3 * R * RS + 3 * 64 + 130 + coarse) * sizeof(double) + (prolong ? 0 : MGMC_ZS_LDS_EXTRA);
 }
 
 }  // namespace mgmc
