@@ -23,6 +23,7 @@
 #include "mgmc_kernels.hpp"
 #include "mgmc_zsweep.hpp"
 #include "mgmc_zrestrict.hpp"
+#include "mgmc_zsweepres.hpp"
 #include "mgmc_gsweep.hpp"
 #include "mgmc_lowrank.hpp"
 #include "mgmc_solver.hpp"
@@ -61,6 +62,8 @@ struct Op {
     int lr_next = 0;       // sweep on a small low-rank level: the patch of the next op, fused (LR_NEXT_*)
     uint32_t lr_next_tag = 0;
     int lr_skip_patch = 0;  // this op's low-rank patch was done by the previous sweep's kernel
+    int restrict_fused = 0;  // OP_SWEEP: also does the following residual + restriction (k_zsweep_res7);
+                             // OP_RESIDUAL_RESTRICT: done by the previous sweep (no launch)
 };
 
 // z-marching sweep tile shape (mgmc_zsweep.hpp)
@@ -108,7 +111,8 @@ struct Level {
     size_t lds_bytes = 0;  // >0 if the whole-level LDS kernel can hold x and f
     bool zsweep = false;   // fused z-marching red-black sweep available
     bool pairs = false;    // Galerkin level swept in colour-pair passes (mgmc_gsweep.hpp)
-    bool pingpong() const { return zsweep; }  // out-of-place sweeps: x <-> x2
+    bool quads = false;    // ... two pairs per launch, out of place (k_sweep_quads)
+    bool pingpong() const { return zsweep || quads; }  // out-of-place sweeps: x <-> x2
     double* buf(int i) const { return i == 0 ? x : x2; }
     LowRankDev lr;
 };
@@ -143,6 +147,7 @@ struct mgmc_handle {
     int nranks = 1, rank = 0;
     double* comm_buf = nullptr;  // device scratch for collectives
     bool fuse_prolong = false;   // prolongate-add fused into the first post-sweep (z-sweep levels)
+    bool fuse_restrict = false;  // last pre-sweep + residual + restriction in one kernel (z-sweep levels)
     double* sv[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // solver: b x r z p q (level 0)
     double* sv_scal = nullptr;   // solver scalars
     double* sv_part = nullptr;   // reduction partials
@@ -300,10 +305,89 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
     }
 }
 
+// last pre-sweep + residual + restriction of a fine 7-point z-sweep level (mgmc_zsweepres.hpp, opt-in
+// MGMC_FUSE_RESTRICT):
+// 32 x 8 coarse points (64 x 16 fine output vertices) per workgroup, 384 threads, 53 KB of LDS -> 2
+// workgroups per CU; kz = 16 coarse planes per chunk (32 output planes)
+constexpr int ZR_CX = 32, ZR_CY = 8, ZR_NT = 384, ZR_KZ = 16;
+bool zsweepres_eligible(const Level& lf, const Level& lc) {
+    return lf.zsweep && lf.spec.dim == 3 && lf.spec.npoints == 7 && lf.lr.m == 0 && lc.L.nx >= 32 &&
+           lf.L.nx % (2 * ZR_CX) == 0 && 2 * lc.L.nx == lf.L.nx && 2 * lc.L.ny == lf.L.ny && 2 * lc.L.nz == lf.L.nz;
+}
+void launch_zsweepres(const Level& lv, const Level& lc, const double* xin, double* xout, const GibbsArg& g0,
+                      int direction, hipStream_t s) {
+    ZSweepResArgs a;
+    a.L = lv.L;
+    a.Lc = lc.L;
+    a.xin = xin;
+    a.xout = xout;
+    a.f = lv.f;
+    a.fc = lc.f;
+    a.xc = lc.x;
+    a.S = lv.S;
+    a.G = g0;
+    a.G.colour = (direction == MGMC_FORWARD) ? 0 : 1;
+    const char* kz = getenv("MGMC_ZSR_KZ");
+    a.kz = std::max(1, kz ? atoi(kz) : ZR_KZ);
+    a.ntx = (lc.L.nx - 1 + ZR_CX - 1) / ZR_CX;
+    a.nty = (lc.L.ny - 1 + ZR_CY - 1) / ZR_CY;
+    if (!kz)  // shallower chunks until the grid has >= 512 tiles (2 per CU)
+        while (a.kz > 2 && (long long)a.ntx * a.nty * ((lc.L.nz - 1 + a.kz - 1) / a.kz) < 512) a.kz /= 2;
+    a.ntz = (lc.L.nz - 1 + a.kz - 1) / a.kz;
+    const int ntiles = a.ntx * a.nty * a.ntz;
+    const int nb = (ntiles + 7) / 8 * 8;
+    hipLaunchKernelGGL((k_zsweep_res7<ZR_CX, ZR_CY, ZR_NT>), dim3(nb), dim3(ZR_NT), zsweepres_lds_bytes(ZR_CX, ZR_CY),
+                       s, a);
+}
+
 // colour-pair passes of a Galerkin 9/27-point level (in place): forward colours (0,1), (2,3), ...,
 // backward (7,6), (5,4), ... -- 2^(d-1) passes per sweep
 bool pairs_eligible(const LevelSpec& sp, const Layout& L) {
     return (sp.npoints == 27 || sp.npoints == 9) && L.nx / 2 >= 1 && L.nx / 2 <= 256 && L.nx % 2 == 0;
+}
+
+// both colour pairs of a k-parity half per launch (k_sweep_quads, opt-in MGMC_QUADS): rows of up to
+// 128 pairs, so that a workgroup holds >= 7 full rows (<= 1 recomputed row in 7).  Bitwise equal to
+// the pair passes but slower at 512^3 (level 1: 2 x 105 us against 4 x 40 us per sweep):
+// the second pair's loads wait for the first pair's rows, and 512-thread workgroups hide less latency
+bool quads_eligible(const LevelSpec& sp, const Layout& L) {
+    return pairs_eligible(sp, L) && L.nx / 2 <= 128 && getenv("MGMC_QUADS") != nullptr;
+}
+
+void launch_quads(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
+                  hipStream_t s) {
+    QuadPassArgs a;
+    a.L = lv.L;
+    a.x0 = xin;
+    a.xout = xout;
+    a.f = f;
+    a.S = lv.S;
+    a.G = g;
+    const int dim = lv.spec.dim;
+    const int npair = lv.L.nx / 2;
+    // T+1 thread rows of npair threads (<= 512 threads: 2 workgroups per CU)
+    a.T = std::max(1, 512 / npair - 1);
+    a.nblk_y = (lv.L.ny - 1 + 2 * a.T - 1) / (2 * a.T);
+    const int nt = npair * (a.T + 1);
+    const size_t lds = (size_t)(2 * a.T + 1) * (lv.L.nx + 2) * sizeof(double);
+    const bool fwd = direction == MGMC_FORWARD;
+    a.jp1 = fwd ? 0 : 1;  // first pair: colours (0,1) / (4,5) forward, (7,6) / (3,2) backward
+    const int nhalf = dim == 3 ? 2 : 1;
+    for (int h = 0; h < nhalf; ++h) {
+        a.kp = fwd ? h : 1 - h;
+        a.xz = h == 0 ? xin : xout;  // the second half reads the first half's new planes
+        const int first = 2 - a.kp;
+        const int nk = dim == 3 ? (first > lv.L.nz - 1 ? 0 : (lv.L.nz - 1 - first) / 2 + 1) : 1;
+        if (nk == 0) continue;
+        const int nb = a.nblk_y * nk;
+        if (dim == 3) {
+            if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false>), dim3(nb), dim3(nt), lds, s, a);
+            else hipLaunchKernelGGL((k_sweep_quads<3, true>), dim3(nb), dim3(nt), lds, s, a);
+        } else {
+            if (fwd) hipLaunchKernelGGL((k_sweep_quads<2, false>), dim3(nb), dim3(nt), lds, s, a);
+            else hipLaunchKernelGGL((k_sweep_quads<2, true>), dim3(nb), dim3(nt), lds, s, a);
+        }
+    }
 }
 
 void launch_pairs(const Level& lv, double* x, const double* f, const GibbsArg& g, int direction, hipStream_t s) {
@@ -344,14 +428,19 @@ void launch_pairs(const Level& lv, double* x, const double* f, const GibbsArg& g
 void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStream_t s) {
     const int dim = lv.spec.dim, np = lv.spec.npoints, nc = lv.spec.ncolours;
     dim3 block(1024), grid(1);
+    // precomputed right hand sides (k_coarse_ssor_lds) when they fit next to x and f
+    const long long ndof = (long long)(lv.L.nx - 1) * (lv.L.ny - 1) * (dim == 3 ? lv.L.nz - 1 : 1);
+    const size_t lds_pre = lv.lds_bytes + (size_t)nsweeps * ndof * sizeof(double);
+    const int pre = lds_pre <= 150 * 1024 && getenv("MGMC_COARSE_NO_PRE") == nullptr;
+    const size_t lds = pre ? lds_pre : lv.lds_bytes;
     if (dim == 3 && np == 27)
-        hipLaunchKernelGGL((k_coarse_ssor_lds<3, 27>), grid, block, lv.lds_bytes, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc);
+        hipLaunchKernelGGL((k_coarse_ssor_lds<3, 27>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc, pre);
     else if (dim == 3 && np == 7)
-        hipLaunchKernelGGL((k_coarse_ssor_lds<3, 7>), grid, block, lv.lds_bytes, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc);
+        hipLaunchKernelGGL((k_coarse_ssor_lds<3, 7>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc, pre);
     else if (dim == 2 && np == 9)
-        hipLaunchKernelGGL((k_coarse_ssor_lds<2, 9>), grid, block, lv.lds_bytes, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc);
+        hipLaunchKernelGGL((k_coarse_ssor_lds<2, 9>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc, pre);
     else
-        hipLaunchKernelGGL((k_coarse_ssor_lds<2, 5>), grid, block, lv.lds_bytes, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc);
+        hipLaunchKernelGGL((k_coarse_ssor_lds<2, 5>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc, pre);
 }
 
 template <int NPTS, int CX, int CY, int NT>
@@ -371,7 +460,7 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
     // (512^3 level 1 -> 2: kz 4, 103 us against 116 / 146 us with 2 / 8)
     const char* kz = getenv("MGMC_ZR_KZ");
     const long long work = (long long)a.ntx * a.nty * (lc.L.nz - 1);
-    a.kz = kz ? atoi(kz) : (work >= 8 * 1024 ? 8 : (work >= 4 * 1024 ? 4 : 2));
+    a.kz = kz ? atoi(kz) : (work >= 8 * 1024 ? 8 : (work >= 4 * 1024 ? 4 : (work >= 512 ? 2 : 1)));
     a.ntz = (lc.L.nz - 1 + a.kz - 1) / a.kz;
     const int nt = a.ntx * a.nty * a.ntz;
     const int nb = (nt + 7) / 8 * 8;
@@ -380,15 +469,23 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
 
 void launch_residual_restrict(const Level& lf, const Level& lc, const double* x, const double* f, double* fc,
                               double* xc, int zero_xc, hipStream_t s) {
-    if (lf.spec.dim == 3 && zero_xc && getenv("MGMC_NO_ZRESTRICT") == nullptr && lc.L.nx >= 32) {
+    // z-marching kernel on every 3D level with coarse n >= 8: 64 x 4 coarse points per workgroup from
+    // coarse n = ZR_SMALL_NX up, 16 x 4 points (one wavefront) below, where the wide tiles would leave
+    // most of the chip idle (the 27-point gather kernel took 24 us per launch on the 15^3 / 7^3 levels)
+    const char* zsn = getenv("MGMC_ZR_SMALL_NX");
+    const int small_nx = zsn ? atoi(zsn) : 32;
+    if (lf.spec.dim == 3 && zero_xc && getenv("MGMC_NO_ZRESTRICT") == nullptr && lc.L.nx >= 8) {
         const int v = getenv("MGMC_ZR_VARIANT") ? atoi(getenv("MGMC_ZR_VARIANT")) : 0;
+        const bool small = lc.L.nx < small_nx;
         if (lf.spec.npoints == 7) {
             if (v == 1) launch_zresrestrict_t<7, 32, 4, 128>(lf, lc, x, f, fc, xc, s);
             else if (v == 3) launch_zresrestrict_t<7, 32, 8, 256>(lf, lc, x, f, fc, xc, s);
+            else if (small) launch_zresrestrict_t<7, 16, 4, 64>(lf, lc, x, f, fc, xc, s);
             else launch_zresrestrict_t<7, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
         } else {
             if (v == 1) launch_zresrestrict_t<27, 32, 4, 128>(lf, lc, x, f, fc, xc, s);
             else if (v == 3) launch_zresrestrict_t<27, 32, 8, 256>(lf, lc, x, f, fc, xc, s);
+            else if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s);
             else launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
         }
         return;
@@ -603,10 +700,8 @@ void build_ops_level(mgmc_handle* h, int level, uint32_t& tag, std::vector<int>&
             tag += 2 * c.ncoarsesmooth;
         } else {
             for (int t = 0; t < c.ncoarsesmooth; ++t) {
-                Op fw{OP_SWEEP, level, MGMC_FORWARD, tag++, 1};
-                Op bw{OP_SWEEP, level, MGMC_BACKWARD, tag++, 1};
-                h->ops.push_back(fw);
-                h->ops.push_back(bw);
+                push_sweep(h, cur, level, MGMC_FORWARD, tag, none);
+                push_sweep(h, cur, level, MGMC_BACKWARD, tag, none);
             }
         }
         return;
@@ -669,6 +764,17 @@ void build_ops(mgmc_handle* h) {
     }
     h->ops.push_back({OP_QOI, 0, 0, 0, 0});
     if (h->levels.size() == 1) h->seg_end_pre = h->seg_begin_post = h->seg_end_post = 0;
+    // the last pre-sweep of a fine 7-point z-sweep level takes over the residual + restriction
+    if (h->fuse_restrict)
+        for (size_t q = 0; q + 1 < h->ops.size(); ++q) {
+            Op& op = h->ops[q];
+            Op& nx = h->ops[q + 1];
+            if (op.kind == OP_SWEEP && nx.kind == OP_RESIDUAL_RESTRICT && op.level == nx.level && !op.prolong &&
+                nx.src == 1 - op.src && zsweepres_eligible(h->levels[op.level], h->levels[op.level + 1])) {
+                op.restrict_fused = 1;
+                nx.restrict_fused = 1;
+            }
+        }
     // small low-rank levels: the kernel after a sweep also patches f for the level's next op
     for (size_t q = 0; q + 1 < h->ops.size(); ++q) {
         Op& op = h->ops[q];
@@ -696,11 +802,17 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 const bool lr = lv.lr.m > 0;
                 if (lr && !op.lr_skip_patch) lr_patch(h, lv, LR_PATCH_NOISE, lv.f, op.tag, sample, s);
                 double* xo = lv.x;
-                if (lv.zsweep) {
+                if (op.restrict_fused) {
+                    xo = lv.buf(1 - op.src);
+                    launch_zsweepres(lv, h->levels[op.level + 1], lv.buf(op.src), xo, g, op.direction, s);
+                } else if (lv.zsweep) {
                     const Level* lc = op.prolong ? &h->levels[op.level + 1] : nullptr;
                     xo = lv.buf(1 - op.src);
                     launch_zsweep(lv, lv.buf(op.src), xo, lv.f, g, op.direction, lc, lc ? lc->x : nullptr,
                                   h->cfg.coarse_scaling, s);
+                } else if (lv.quads) {
+                    xo = lv.buf(1 - op.src);
+                    launch_quads(lv, lv.buf(op.src), xo, lv.f, g, op.direction, s);
                 } else if (lv.pairs) {
                     launch_pairs(lv, lv.x, lv.f, g, op.direction, s);
                 } else {
@@ -722,6 +834,7 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 break;
             }
             case OP_RESIDUAL_RESTRICT: {
+                if (op.restrict_fused) break;  // done by the previous sweep's kernel
                 Level& lc = h->levels[op.level + 1];
                 const bool lr = lv.lr.m > 0;
                 if (lr && !op.lr_skip_patch) {  // r = (f - B Sigma^{-1} B^T x) - A x
@@ -987,6 +1100,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         lv.zsweep = cfg->dim == 3 && lv.spec.npoints == 7 && symmetric && l + 1 < specs.size() &&
                     (lv.L.nx % (2 * zsweep_xp())) == 0 && getenv("MGMC_NO_ZSWEEP") == nullptr;
         lv.pairs = pairs_eligible(lv.spec, lv.L) && getenv("MGMC_NO_PAIRS") == nullptr;
+        lv.quads = lv.pairs && quads_eligible(lv.spec, lv.L);
         if (lv.pingpong()) {
             if (hipMalloc(&lv.x2, bytes) != hipSuccess) {
                 h->levels.push_back(lv);
@@ -1009,6 +1123,10 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         return bail(rc);
     // op sequence of one sample
     h->fuse_prolong = getenv("MGMC_NO_FUSE_PROLONG") == nullptr;  // default: fused (A/B in DESIGN.md)
+    // opt-in: the fused pre-sweep + residual + restriction is correct (bitwise) but slower at 512^3
+    // (1.98 ms against 0.70 + 0.56 ms): its two-vertex recomputed halo and 2 workgroups
+    // per CU leave it latency / VALU bound
+    h->fuse_restrict = getenv("MGMC_FUSE_RESTRICT") != nullptr;
     build_ops(h);
     if ((rc = ensure_series(h, 1024)) != MGMC_OK) return bail(rc);
     if (hipStreamSynchronize(h->stream) != hipSuccess) {
@@ -1224,6 +1342,9 @@ static int sweep_component(mgmc_handle* h, int level, int direction, int nsweeps
         if (noise && lv.zsweep) {  // the fused z-marching kernel of the V-cycle (out of place)
             launch_zsweep(lv, lv.scratch[cur], lv.scratch[3 - cur], lv.scratch[0], g, direction, nullptr, nullptr, 0.0,
                           h->stream);
+            cur = 3 - cur;
+        } else if (noise && lv.quads) {  // two colour pairs per launch (out of place)
+            launch_quads(lv, lv.scratch[cur], lv.scratch[3 - cur], lv.scratch[0], g, direction, h->stream);
             cur = 3 - cur;
         } else if (noise && lv.pairs) {  // the colour-pair passes of the V-cycle (in place)
             launch_pairs(lv, lv.scratch[cur], lv.scratch[0], g, direction, h->stream);

@@ -206,14 +206,18 @@ __device__ __forceinline__ int colour_of(int i, int j, int k) {
 
 // ---- whole coarse-level SSOR sampler in one workgroup, state in LDS ----
 // nsweeps sweeps alternating forward/backward (SSORSampler::apply, ssor_sampler.cc:9-15),
-// sweep s uses tag0 + s.
+// sweep s uses tag0 + s.  precompute: every right hand side c = fma(sd, xi, f) of every sweep is
+// evaluated up front by all threads at once (f does not change during the sampler), so a colour pass
+// is only the stencil and the update -- one Philox + Box-Muller latency for the whole sampler instead
+// of one per colour pass.  The same operations as gibbs_point, so the same bits.
 template <int DIM, int NPTS>
 __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __restrict__ xg,
                                                           const double* __restrict__ fg, StencilArg S, GibbsArg G,
-                                                          int nsweeps, int ncolours) {
+                                                          int nsweeps, int ncolours, int precompute) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* xs = smem;
     double* fs = smem + L.nstore;
+    double* cs = fs + L.nstore;  // [nsweeps][ndof] right hand sides (precompute)
     for (long long q = threadIdx.x; q < L.nstore; q += blockDim.x) {
         xs[q] = xg[q];
         fs[q] = fg[q];
@@ -222,18 +226,62 @@ __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __re
     const uint64_t sample = *G.sample;
     const int nxi = L.nx - 1, nyi = L.ny - 1;
     const long long ndof = (long long)nxi * nyi * (DIM == 3 ? (L.nz - 1) : 1);
+    if (precompute) {
+        for (long long t = threadIdx.x; t < nsweeps * ndof; t += blockDim.x) {
+            const long long q = t % ndof;
+            const int sw = (int)(t / ndof);
+            const int i = (int)(q % nxi) + 1;
+            const int j = (int)((q / nxi) % nyi) + 1;
+            const int k = (DIM == 3) ? (int)(q / ((long long)nxi * nyi)) + 1 : 0;
+            const double xi = point_normal(G.key, pair_id<DIM>(L, i, j, k), (i & 1) != 0, G.tag + (uint32_t)sw, sample);
+            cs[t] = fma(G.sd, xi, fs[L.at(i, j, k)]);
+        }
+        __syncthreads();
+    }
+    // up to MAXV vertices per thread: coordinates, offset and colour computed once (the colour passes
+    // then do no index arithmetic); larger levels take the generic loop
+    constexpr int MAXV = 4;
+    const bool cached = ndof <= MAXV * (long long)blockDim.x;
+    int vi[MAXV], vj[MAXV], vk[MAXV], vp[MAXV], vc[MAXV];
+#pragma unroll
+    for (int u = 0; u < MAXV; ++u) {
+        const int q = (int)threadIdx.x + u * (int)blockDim.x;
+        vc[u] = -1;
+        vi[u] = vj[u] = vk[u] = vp[u] = 0;
+        if (cached && q < ndof) {
+            vi[u] = q % nxi + 1;
+            vj[u] = (q / nxi) % nyi + 1;
+            vk[u] = (DIM == 3) ? q / (nxi * nyi) + 1 : 0;
+            vp[u] = (int)L.at(vi[u], vj[u], vk[u]);
+            vc[u] = colour_of<DIM, NPTS>(vi[u], vj[u], vk[u]);
+        }
+    }
     GibbsArg g = G;
+    auto update = [&](int s, long long q, int i, int j, int k, long long p) {
+        if (precompute) {
+            const double res = stencil_fma<DIM, NPTS>(xs, p, L, S);
+            xs[p] = fma(g.wd, cs[s * ndof + q] - res, xs[p]);
+        } else {
+            gibbs_point<DIM, NPTS, true>(xs, fs, p, L, S, g, sample, i, j, k);
+        }
+    };
     for (int s = 0; s < nsweeps; ++s) {
         g.tag = G.tag + (uint32_t)s;
         const bool backward = (s & 1) != 0;
         for (int cc = 0; cc < ncolours; ++cc) {
             const int colour = backward ? ncolours - 1 - cc : cc;
-            for (long long q = threadIdx.x; q < ndof; q += blockDim.x) {
-                const int i = (int)(q % nxi) + 1;
-                const int j = (int)((q / nxi) % nyi) + 1;
-                const int k = (DIM == 3) ? (int)(q / ((long long)nxi * nyi)) + 1 : 0;
-                if (colour_of<DIM, NPTS>(i, j, k) != colour) continue;
-                gibbs_point<DIM, NPTS, true>(xs, fs, L.at(i, j, k), L, S, g, sample, i, j, k);
+            if (cached) {
+#pragma unroll
+                for (int u = 0; u < MAXV; ++u)
+                    if (vc[u] == colour) update(s, (int)threadIdx.x + u * (int)blockDim.x, vi[u], vj[u], vk[u], vp[u]);
+            } else {
+                for (long long q = threadIdx.x; q < ndof; q += blockDim.x) {
+                    const int i = (int)(q % nxi) + 1;
+                    const int j = (int)((q / nxi) % nyi) + 1;
+                    const int k = (DIM == 3) ? (int)(q / ((long long)nxi * nyi)) + 1 : 0;
+                    if (colour_of<DIM, NPTS>(i, j, k) != colour) continue;
+                    update(s, q, i, j, k, L.at(i, j, k));
+                }
             }
             __syncthreads();
         }

@@ -57,6 +57,11 @@ CONFIGS = {
     # level 1 -> level 2, partial tiles in y and z
     "3d_zres7": ((256, 40, 48), dict(nlevel=2)),
     "3d_zres27": ((512, 16, 24), dict(nlevel=3)),
+    # (with MGMC_FUSE_RESTRICT, test_variant_cycles_bitwise) last pre-sweep fused with residual +
+    # restriction (k_zsweep_res7): coarse rows / planes ending exactly at a tile / chunk boundary (the
+    # last tile owns the extra fine row / plane), SSOR pre-sampler
+    "3d_zsr_edges": ((128, 34, 18), dict(nlevel=2)),
+    "3d_zsr_ssor_W": ((128, 64, 64), dict(nlevel=3, cycle=2, smoother="SSOR", npresmooth=2, omega=0.9)),
     # dense Cholesky coarse sampler (CholeskySampler, x = G f + U xi on the coarsest level)
     "2d64_chol_W": ((64, 64), dict(nlevel=4, cycle=2, coarse_solver="Cholesky")),
     "3d32_chol_ssor": ((32, 32, 32), dict(nlevel=3, smoother="SSOR", coarse_solver="Cholesky")),
@@ -167,11 +172,25 @@ def test_zsweep_tile_variants_bitwise(hip_device, monkeypatch, variant):
     s.close()
 
 
-@pytest.mark.parametrize("name", ["3d128_zsweep", "3d_aniso_zsweep_ssor", "3d128_zsweep_odd"])
-def test_unfused_prolongation_cycles_bitwise(hip_device, monkeypatch, name):
+@pytest.mark.parametrize("env,name", [("MGMC_NO_FUSE_PROLONG", "3d128_zsweep"),
+                                      ("MGMC_NO_FUSE_PROLONG", "3d_aniso_zsweep_ssor"),
+                                      ("MGMC_NO_FUSE_PROLONG", "3d128_zsweep_odd"),
+                                      ("MGMC_FUSE_RESTRICT", "3d128_zsweep"),
+                                      ("MGMC_FUSE_RESTRICT", "3d_zsr_edges"),
+                                      ("MGMC_FUSE_RESTRICT", "3d_zsr_ssor_W"),
+                                      ("MGMC_FUSE_RESTRICT", "3d_zres7"),
+                                      ("MGMC_FUSE_RESTRICT", "3d128_zsweep_odd"),
+                                      ("MGMC_QUADS", "3d64_4lvl"),
+                                      ("MGMC_QUADS", "3d_zres7"),
+                                      ("MGMC_QUADS", "3d32_W_ssor"),
+                                      ("MGMC_QUADS", "2d64_template_W")])
+def test_variant_cycles_bitwise(hip_device, monkeypatch, env, name):
     """MGMC_NO_FUSE_PROLONG: the separate prolongate-add pass (instead of the default fold into the
-    first post-sweep's plane loads) gives the oracle's cycle exactly."""
-    monkeypatch.setenv("MGMC_NO_FUSE_PROLONG", "1")
+    first post-sweep's plane loads); MGMC_FUSE_RESTRICT: the last pre-sweep, the residual and the
+    restriction in one kernel (k_zsweep_res7, opt-in); MGMC_QUADS: both colour pairs of a k-parity
+    half per launch on Galerkin levels, out of place (k_sweep_quads, opt-in).  All give the oracle's
+    cycle exactly."""
+    monkeypatch.setenv(env, "1")
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)
     mc = oracle_for(s, p, lat)
