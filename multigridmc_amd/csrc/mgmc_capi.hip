@@ -66,6 +66,8 @@ struct Op {
                              // OP_RESIDUAL_RESTRICT: done by the previous sweep (no launch)
 };
 
+int g_num_cu = 256;  // compute units of the device (set by mgmc_create; MI355X: 256)
+
 // z-marching sweep tile shape (mgmc_zsweep.hpp)
 // 32 x-pairs x 16 rows, 256 threads (2 core pairs per thread, 19.5 % halo), 38 KB of LDS -> 4
 // workgroups per CU; tuning history in DESIGN.md
@@ -280,12 +282,20 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
     a.S = lv.S;
     a.G = g0;
     a.G.colour = (direction == MGMC_FORWARD) ? 0 : 1;
-    const char* tz = getenv("MGMC_ZS_TZ");
+    const char* tz = getenv(coarse ? "MGMC_ZS_TZP" : "MGMC_ZS_TZ");
     a.tz = std::max(2, (tz ? atoi(tz) : ZS_TZ) & ~1);  // even: chunks start on odd planes (coarse ring schedule)
     if (!tz) {  // shallower z chunks until the grid has >= 1024 tiles (4 per CU): 256^3 -> 16 planes
         const int xp = zsweep_xp(), ty = zsweep_variant() == 0 ? ZS_TY : 16;
         const long long txy = (long long)((lv.L.nx / 2) / xp) * ((lv.L.ny - 1 + ty - 1) / ty);
         while (a.tz > 8 && txy * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 1024) a.tz /= 2;
+        if (coarse && zsweep_variant() == 0) {
+            // fused-prolongation variant (3 workgroups per CU): deeper chunks when two full rounds of
+            // workgroups still fill the chip -- fewer re-read z halo planes (512^3: tz 32 -> 86, 923 ->
+            // 897 us)
+            const long long nchunk = std::max(1LL, (2LL * 3 * g_num_cu + txy - 1) / txy);
+            const int tz2 = (int)(((lv.L.nz - 1 + nchunk - 1) / nchunk + 1) & ~1LL);
+            if (tz2 > a.tz) a.tz = tz2;
+        }
     }
     const bool pr = coarse != nullptr;
     switch (zsweep_variant()) {
@@ -461,6 +471,15 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
     const char* kz = getenv("MGMC_ZR_KZ");
     const long long work = (long long)a.ntx * a.nty * (lc.L.nz - 1);
     a.kz = kz ? atoi(kz) : (work >= 8 * 1024 ? 8 : (work >= 4 * 1024 ? 4 : (work >= 512 ? 2 : 1)));
+    if (!kz && NPTS == 7 && work >= 32 * 1024) {
+        // fine 7-point level: the deepest chunks that still give two full rounds of workgroups (every
+        // chunk re-reads 2 x planes and 1 f plane below / above it: 512^3 kz 8 -> 43 (6 chunks,
+        // 1536 tiles on 256 CUs x 3 workgroups): 561 -> 451 us)
+        const long long slots = 3LL * g_num_cu;
+        const long long per_chunk = (long long)a.ntx * a.nty;
+        const long long nchunk = std::max(1LL, (2 * slots + per_chunk - 1) / per_chunk);
+        a.kz = std::max(8, (int)((lc.L.nz - 1 + nchunk - 1) / nchunk));
+    }
     a.ntz = (lc.L.nz - 1 + a.kz - 1) / a.kz;
     const int nt = a.ntx * a.nty * a.ntz;
     const int nb = (nt + 7) / 8 * 8;
@@ -1065,6 +1084,11 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     h->seed = seed;
     h->chain = chain_id;
     h->key = make_key(seed, chain_id);
+    {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+            g_num_cu = ncu;
+    }
     if (hipSetDevice(device) != hipSuccess) {
         delete h;
         return fail(nullptr, MGMC_E_HIP, "hipSetDevice failed");
