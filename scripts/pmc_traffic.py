@@ -10,7 +10,7 @@ import json
 import sys
 
 KERNEL = "k_zsweep_rb7"
-PLAIN = ", false,"  # the plain sweep instance (PROLONG = false): the fine pre-sweep of the V-cycle
+PLAIN = ", 256, 0, "  # the plain sweep instance (PROLONG = 0): the fine pre-sweep of the V-cycle
 
 
 def per_launch(path):
