@@ -50,7 +50,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--n", type=int, default=512, help="cells per direction (3D)")
+    ap.add_argument("--n", type=int, default=512, help="cells per direction")
+    ap.add_argument("--dim", type=int, default=3, choices=(2, 3),
+                    help="2: BASELINE config 2 (2D n^2 lattice, e.g. --dim 2 --n 1024 --nlevel 5); not the headline line")
     ap.add_argument("--nlevel", type=int, default=7)
     ap.add_argument("--cpu-samples", type=int, default=1, help="V-cycles timed for the CPU baseline (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -76,7 +78,7 @@ def cpu_info():
     return model
 
 
-def cpu_baseline(n, nlevel, nsamples, posterior=None):
+def cpu_baseline(n, nlevel, nsamples, posterior=None, dim=3):
     """FAITHFUL oracle (reference algorithm: lexicographic SOR Gibbs sweeps, mt19937_64 +
     normal_distribution, CSR operators; with a posterior operator the reference's dense
     lexicographic B_bar fix) on the same hierarchy, 1 thread."""
@@ -84,7 +86,7 @@ def cpu_baseline(n, nlevel, nsamples, posterior=None):
     p = mg.MultigridParameters(nlevel=nlevel, smoother="SOR", coarse_solver="SSOR", npresmooth=1, npostsmooth=1,
                                ncoarsesmooth=1, omega=1.0, cycle=1, coarse_scaling=1.0)
     t0 = time.perf_counter()
-    o = O.Oracle.fd((n, n, n), p, kappa_sq=25.0, mode=O.FAITHFUL, seed=SEED, galerkin=1)
+    o = O.Oracle.fd((n,) * dim, p, kappa_sq=25.0, mode=O.FAITHFUL, seed=SEED, galerkin=1)
     if posterior is not None:
         o.set_lowrank(posterior.get_B())
         o.time_samples(1)  # B_bar setup of every smoother happens on first use: keep it out of the timing
@@ -96,7 +98,7 @@ def cpu_baseline(n, nlevel, nsamples, posterior=None):
         "unit": "samples/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{nsamples} V-cycles of the same 3D {n}^3 {nlevel}-level hierarchy after a {setup:.0f} s setup "
+        "sample": f"{nsamples} V-cycles of the same {dim}D {n}^{dim} {nlevel}-level hierarchy after a {setup:.0f} s setup "
                   f"(oracle/refcpu.cpp FAITHFUL mode: lexicographic SOR Gibbs, mt19937_64, CSR; g++ -O2, 1 thread); "
                   f"{secs:.1f} s timed; host CPU: {cpu_info()}",
     }
@@ -184,7 +186,7 @@ def main():
         n = 256
     if args.posterior and "--nlevel" not in sys.argv:
         nlevel = 6
-    lat = mg.Lattice3d(n, n, n)
+    lat = mg.Lattice3d(n, n, n) if args.dim == 3 else mg.Lattice2d(n, n)
     op = mg.ShiftedLaplaceFDOperator(lat, kappa_sq=1.0 / 0.2 ** 2)  # Lambda = 0.2 (parameters_template.cfg)
     if args.posterior:
         op = posterior_operator(op, args.posterior, args.radius, args.measure_global)
@@ -195,7 +197,7 @@ def main():
     device = int(os.environ.get("MGMC_BENCH_DEVICE", local_rank))
     sampler = mg.MultigridMCSampler(op, SEED, params, device=device, chain_id=rank)
     t_setup = time.perf_counter() - t_setup
-    qoi = mg.measurement_vector_index(lat, [0.5, 0.5, 0.5])
+    qoi = mg.measurement_vector_index(lat, [0.5] * args.dim)
     n0 = lat.Nvertex
 
     coll = Collectives(sampler, rank, world)
@@ -231,7 +233,7 @@ def main():
             if os.path.exists(args.traffic_file):
                 try:
                     tj = json.load(open(args.traffic_file))
-                    if tj.get("n") == n:
+                    if tj.get("n") == n and args.dim == 3:
                         traffic = tj.get("fine_sweep_hbm_bytes_per_launch")
                 except (OSError, ValueError):
                     traffic = None
@@ -241,7 +243,7 @@ def main():
                     "bytes_per_launch": bytes_sweep, "avg_launch_ms": round(t_sweep * 1e3, 4)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.cpu_samples > 0:
-            cpu = cpu_baseline(n, nlevel, args.cpu_samples, op if args.posterior else None)
+            cpu = cpu_baseline(n, nlevel, args.cpu_samples, op if args.posterior else None, args.dim)
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -255,15 +257,18 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: prior (f = 0), x0 = 0, Philox4x32-10 counter-based Gaussian noise",
-            "config": {"workload": f"3D {n}^3 shifted-Laplace FD prior (kappa^2 = 25), {nlevel}-level V-cycle, "
-                                   f"SOR Gibbs 1/1, SSOR coarse 1, omega 1, one independent chain per GPU",
-                       "lattice": [n, n, n], "unknowns": n0, "nlevel": nlevel, "chains": world,
+            "config": {"workload": f"{args.dim}D {n}^{args.dim} shifted-Laplace FD prior (kappa^2 = 25), "
+                                   f"{nlevel}-level V-cycle, SOR Gibbs 1/1, SSOR coarse 1, omega 1, "
+                                   f"one independent chain per GPU",
+                       "lattice": [n] * args.dim, "unknowns": n0, "nlevel": nlevel, "chains": world,
                        "parallelism": f"chains{world} (independent MCMC chains, 1 per GPU; "
                                       f"{'RCCL' if coll.rccl or world == 1 else 'gloo'} all-gather of QoI moments)"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "qoi": {"index": qoi, "samples": nq, "mean": mean, "variance": m2 / nq if nq else None, "chains": len(parts)},
         }
+        if args.dim == 2:
+            line["metric"] = "MGMC V-cycle samples/sec, 2D (BASELINE config 2)"
         if args.posterior:
             m = op.get_m_lowrank()
             rows = [sampler.lowrank_info(lv, mg.FORWARD)[1] for lv in range(nlevel)]
