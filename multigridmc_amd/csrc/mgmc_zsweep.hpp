@@ -97,9 +97,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     }
     for (int q = threadIdx.x; q < 130; q += NT) tab[192 + q] = SINCOS_TAB[q];
     // PROLONG: ring of two coarse planes (slot K & 1) over the tile's coarse footprint, coarse
-    // columns [q0-2, q0+XP+3] x rows [(j0-3)/2, (j0+TY+1)/2]
-    constexpr int CW = XP + 6, CR = TY / 2 + 3, CPS = CR * CW;
-    constexpr int NLC = PROLONG ? (CPS + NT - 1) / NT : 1;
+    // columns [q0-3, q0+XP+4] (starting on an even storage index: 16-byte pair loads) x rows
+    // [(j0-3)/2, (j0+TY+1)/2]
+    constexpr int CW = XP + 8, CWP = CW / 2, CR = TY / 2 + 3, CPS = CR * CW;
+    constexpr int NLC = PROLONG ? (CR * CWP + NT - 1) / NT : 1;
     double* cring = tab + 322;
 
     const Layout& L = a.L;
@@ -196,26 +197,29 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     const Layout& Lc = a.Lc;
     const int Jst = (j0 - 2) >> 1;  // first coarse row of the footprint
     int coff[NLC], clds[NLC];
-    double pcv[NLC];
+    double2 pcv[NLC];
 #pragma unroll
     for (int u = 0; u < NLC; ++u) {
         const int it = tid + u * NT;
-        clds[u] = (PROLONG && it < CPS) ? it : -1;
-        const int r = it / CW, c = it % CW;
+        clds[u] = (PROLONG && it < CR * CWP) ? 2 * it : -1;  // pair it: row it / CWP, columns 2 (it % CWP) + {0, 1}
+        const int r = it / CWP, c = 2 * (it % CWP);
         const int jr = Jst + r;
         const int jc = jr < 0 ? 0 : (jr > Lc.ny ? Lc.ny : jr);
-        coff[u] = clds[u] >= 0 ? (int)((long long)jc * Lc.sx + (q0 - 2 + c) + Lc.off) : Lc.off - 1;
+        coff[u] = clds[u] >= 0 ? (int)((long long)jc * Lc.sx + (q0 - 3 + c) + Lc.off) : Lc.off + 1;
     }
     auto issue_c = [&](int K) {
         const double* base = a.xc + (long long)(K < 0 ? 0 : (K > Lc.nz ? Lc.nz : K)) * Lc.sp;
 #pragma unroll
-        for (int u = 0; u < NLC; ++u) pcv[u] = base[coff[u]];
+        for (int u = 0; u < NLC; ++u) pcv[u] = *reinterpret_cast<const double2*>(base + coff[u]);
     };
     auto deposit_c = [&](int K) {
         double* dst = cring + (K & 1) * CPS;
 #pragma unroll
         for (int u = 0; u < NLC; ++u)
-            if (clds[u] >= 0) dst[clds[u]] = pcv[u];
+            if (clds[u] >= 0) {
+                dst[clds[u]] = pcv[u].x;
+                dst[clds[u] + 1] = pcv[u].y;
+            }
     };
     // x_old + alpha P x_c at the fine pair (i odd, i+1) of row j, plane k, from the coarse ring.  The
     // same terms in the same order as k_prolongate_pairs: coarse parents in ascending (kk, jj, ii),
@@ -263,7 +267,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     for (int u = 0; u < NLX; ++u) {
         const int c2 = xlds[u] < 0 ? 0 : xlds[u] % RS, j = xlds[u] < 0 ? j0 : j0 - 2 + xlds[u] / RS;
         pjodd[u] = j & 1;
-        pcro[u] = c2 + ((j >> 1) - Jst) * CW;
+        pcro[u] = c2 + 1 + ((j >> 1) - Jst) * CW;  // ring column of coarse q0-2+c2
     }
 
     // ---- global <-> LDS / registers ----
@@ -451,7 +455,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
 #endif
 inline size_t zsweep_lds_bytes(int XP, int TY, bool prolong) {
     const int RS = 2 * (XP + 4) + 2, R = TY + 4;
-    const int coarse = prolong ? 2 * (TY / 2 + 3) * (XP + 6) : 0;
+    const int coarse = prolong ? 2 * (TY / 2 + 3) * (XP + 8) : 0;
     return (size_t)(3 * R * RS + 3 * 64 + 130 + coarse) * sizeof(double) + (prolong ? 0 : MGMC_ZS_LDS_EXTRA);
 }
 
