@@ -443,14 +443,20 @@ void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStrea
     const size_t lds_pre = lv.lds_bytes + (size_t)nsweeps * ndof * sizeof(double);
     const int pre = lds_pre <= 150 * 1024 && getenv("MGMC_COARSE_NO_PRE") == nullptr;
     const size_t lds = pre ? lds_pre : lv.lds_bytes;
-    if (dim == 3 && np == 27)
-        hipLaunchKernelGGL((k_coarse_ssor_lds<3, 27>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc, pre);
-    else if (dim == 3 && np == 7)
-        hipLaunchKernelGGL((k_coarse_ssor_lds<3, 7>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc, pre);
-    else if (dim == 2 && np == 9)
-        hipLaunchKernelGGL((k_coarse_ssor_lds<2, 9>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc, pre);
-    else
-        hipLaunchKernelGGL((k_coarse_ssor_lds<2, 5>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g, nsweeps, nc, pre);
+#define MGMC_COARSE_LAUNCH(D, P)                                                                                 \
+    do {                                                                                                           \
+        if (pre)                                                                                                   \
+            hipLaunchKernelGGL((k_coarse_ssor_lds<D, P, true>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g,   \
+                               nsweeps, nc);                                                                       \
+        else                                                                                                       \
+            hipLaunchKernelGGL((k_coarse_ssor_lds<D, P, false>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g,  \
+                               nsweeps, nc);                                                                       \
+    } while (0)
+    if (dim == 3 && np == 27) MGMC_COARSE_LAUNCH(3, 27);
+    else if (dim == 3 && np == 7) MGMC_COARSE_LAUNCH(3, 7);
+    else if (dim == 2 && np == 9) MGMC_COARSE_LAUNCH(2, 9);
+    else MGMC_COARSE_LAUNCH(2, 5);
+#undef MGMC_COARSE_LAUNCH
 }
 
 template <int NPTS, int CX, int CY, int NT>

@@ -206,14 +206,15 @@ __device__ __forceinline__ int colour_of(int i, int j, int k) {
 
 // ---- whole coarse-level SSOR sampler in one workgroup, state in LDS ----
 // nsweeps sweeps alternating forward/backward (SSORSampler::apply, ssor_sampler.cc:9-15),
-// sweep s uses tag0 + s.  precompute: every right hand side c = fma(sd, xi, f) of every sweep is
+// sweep s uses tag0 + s.  PRE: every right hand side c = fma(sd, xi, f) of every sweep is
 // evaluated up front by all threads at once (f does not change during the sampler), so a colour pass
 // is only the stencil and the update -- one Philox + Box-Muller latency for the whole sampler instead
 // of one per colour pass.  The same operations as gibbs_point, so the same bits.
-template <int DIM, int NPTS>
+template <int DIM, int NPTS, bool PRE>
 __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __restrict__ xg,
                                                           const double* __restrict__ fg, StencilArg S, GibbsArg G,
-                                                          int nsweeps, int ncolours, int precompute) {
+                                                          int nsweeps, int ncolours) {
+    constexpr bool precompute = PRE;  // a template parameter: the colour passes carry no Philox code
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* xs = smem;
     double* fs = smem + L.nstore;
@@ -226,7 +227,7 @@ __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __re
     const uint64_t sample = *G.sample;
     const int nxi = L.nx - 1, nyi = L.ny - 1;
     const long long ndof = (long long)nxi * nyi * (DIM == 3 ? (L.nz - 1) : 1);
-    if (precompute) {
+    if constexpr (precompute) {
         for (long long t = threadIdx.x; t < nsweeps * ndof; t += blockDim.x) {
             const long long q = t % ndof;
             const int sw = (int)(t / ndof);
@@ -258,7 +259,7 @@ __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __re
     }
     GibbsArg g = G;
     auto update = [&](int s, long long q, int i, int j, int k, long long p) {
-        if (precompute) {
+        if constexpr (precompute) {
             const double res = stencil_fma<DIM, NPTS>(xs, p, L, S);
             xs[p] = fma(g.wd, cs[s * ndof + q] - res, xs[p]);
         } else {
