@@ -182,12 +182,11 @@ int mgmc_normals(mgmc_handle* h, uint64_t pair0, size_t n, uint32_t sweep_tag, u
  * Run `nsweeps` noisy fine-level (level 0) Gibbs sweeps on the device state, bracketed by
  * HIP events recorded on the handle's own stream; *ms = elapsed milliseconds. */
 int mgmc_time_fine_sweeps(mgmc_handle* h, int nsweeps, float* ms);
-/* Same as mgmc_sample_async + synchronize, but each cycle is replayed as four graph segments
- * [fine pre-sampler | coarse-grid correction | fine post-sampler | QoI] with HIP events recorded
+/* Same as mgmc_sample_async + synchronize, but each cycle is replayed as two graph segments
+ * [fine pre-sampler | coarse-grid correction, fine post-sampler, QoI] with HIP events recorded
  * between them on the handle's stream.  *total_ms = first-to-last event time of the nsteps
  * cycles, *fine_ms = summed time of the fine-level (level 0) pre-sampler segments (plain Gibbs
- * sweeps; the first post-sweep also carries the fused prolongation), *nfine = number of fine-level
- * sweeps they contain. */
+ * sweeps), *nfine = number of fine-level sweeps they contain. */
 int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* fine_ms,
                       int* nfine);
 

@@ -5,7 +5,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import multigridmc_amd as mg  # noqa: E402
 n = int(os.environ.get("N", "512"))
 lat = mg.Lattice3d(n, n, n) if os.environ.get("DIM", "3") == "3" else mg.Lattice2d(n, n)
-s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 1, mg.MultigridParameters(nlevel=int(os.environ.get("NLEVEL", "7"))))
+s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 1, mg.MultigridParameters(nlevel=int(os.environ.get("NLEVEL", "7")),
+                                                                                   ncoarsesmooth=int(os.environ.get("NCS", "1"))))
 s.sample(3)
 tot, fine, nfine = s.sample_timed(int(os.environ.get("K", "10")))
 print("vcycle ms", tot / int(os.environ.get("K", "10")))
