@@ -24,6 +24,7 @@
 #include "mgmc_zsweep.hpp"
 #include "mgmc_zrestrict.hpp"
 #include "mgmc_zsweepres.hpp"
+#include "mgmc_tail.hpp"
 #include "mgmc_gsweep.hpp"
 #include "mgmc_lowrank.hpp"
 #include "mgmc_solver.hpp"
@@ -48,7 +49,8 @@ enum OpKind {
     OP_COARSE_LDS = 3,
     OP_QOI = 4,
     OP_COPY = 5,
-    OP_COARSE_CHOL = 6
+    OP_COARSE_CHOL = 6,
+    OP_TAIL = 7      // the sub-cycle of the coarsest levels in one workgroup (mgmc_tail.hpp)
 };
 
 struct Op {
@@ -62,6 +64,7 @@ struct Op {
     int lr_next = 0;       // sweep on a small low-rank level: the patch of the next op, fused (LR_NEXT_*)
     uint32_t lr_next_tag = 0;
     int lr_skip_patch = 0;  // this op's low-rank patch was done by the previous sweep's kernel
+    int tail = -1;           // OP_TAIL: index into mgmc_handle::tail_args
     int restrict_fused = 0;  // OP_SWEEP: also does the following residual + restriction (k_zsweep_res7);
                              // OP_RESIDUAL_RESTRICT: done by the previous sweep (no launch)
 };
@@ -150,6 +153,8 @@ struct mgmc_handle {
     double* comm_buf = nullptr;  // device scratch for collectives
     bool fuse_prolong = false;   // prolongate-add fused into the first post-sweep (z-sweep levels)
     bool fuse_restrict = false;  // last pre-sweep + residual + restriction in one kernel (z-sweep levels)
+    std::vector<TailArgs*> tail_args;  // device copies, one per OP_TAIL
+    std::vector<size_t> tail_lds;      // dynamic LDS bytes per OP_TAIL
     double* sv[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // solver: b x r z p q (level 0)
     double* sv_scal = nullptr;   // solver scalars
     double* sv_part = nullptr;   // reduction partials
@@ -816,6 +821,130 @@ void build_ops(mgmc_handle* h) {
     }
 }
 
+// ---- the coarsest levels' sub-cycle in one workgroup (k_tail) ----
+constexpr size_t TAIL_LDS_LIMIT = 150 * 1024;
+
+Layout tail_layout(const Layout& L) {
+    Layout G = L;
+    G.off = 0;
+    G.sx = L.nx + 1;
+    G.sp = G.sx * (L.ny + 1);
+    G.nstore = L.dim == 3 ? G.sp * (L.nz + 1) : G.sp;
+    return G;
+}
+
+// smallest level lt >= 1 whose levels lt .. L-1 all fit one workgroup's LDS (x, f per level + one
+// scratch of the largest): Galerkin levels, no low-rank part, ordinary (in-place) sweeps, SSOR coarse
+// sampler; -1 if none or only the coarsest level fits (the coarse LDS kernel covers that)
+int tail_level(const mgmc_handle* h) {
+    if (getenv("MGMC_NO_TAIL") != nullptr || h->cfg.coarse_solver != MGMC_COARSE_SSOR) return -1;
+    const int L = (int)h->levels.size();
+    for (int lt = 1; lt + 1 < L; ++lt) {
+        bool ok = true;
+        size_t tot = 0, vmax = 0;
+        for (int l = lt; l < L && ok; ++l) {
+            const Level& lv = h->levels[l];
+            ok = lv.lr.m == 0 && !lv.pingpong() && lv.spec.npoints == (lv.spec.dim == 3 ? 27 : 9);
+            const size_t v = (size_t)tail_layout(lv.L).nstore;
+            tot += 2 * v;
+            vmax = std::max(vmax, v);
+        }
+        if (ok && (tot + vmax) * sizeof(double) <= TAIL_LDS_LIMIT) return lt;
+    }
+    return -1;
+}
+
+void free_tails(mgmc_handle* h) {
+    for (auto p : h->tail_args)
+        if (p) hipFree(p);
+    h->tail_args.clear();
+    h->tail_lds.clear();
+}
+
+// replace every maximal run of ops on levels >= lt (one call of build_ops_level(lt)) by one OP_TAIL
+int build_tails(mgmc_handle* h) {
+    free_tails(h);
+    const int lt = tail_level(h);
+    if (lt < 0) return MGMC_OK;
+    const int L = (int)h->levels.size();
+    std::vector<Op> out;
+    size_t removed_before_pre = 0;
+    const size_t pre_end = h->seg_end_pre;
+    for (size_t q = 0; q < h->ops.size();) {
+        if (h->ops[q].level < lt || h->ops[q].kind == OP_QOI) {
+            out.push_back(h->ops[q++]);
+            continue;
+        }
+        TailArgs A;
+        memset(&A, 0, sizeof(A));
+        size_t r = q;
+        bool ok = true;
+        for (; r < h->ops.size() && h->ops[r].level >= lt && h->ops[r].kind != OP_QOI; ++r) {
+            const Op& op = h->ops[r];
+            if (A.nops >= TAIL_MAX_OPS) { ok = false; break; }
+            TailOp& t = A.ops[A.nops++];
+            t.level = op.level - lt;
+            t.dir = op.direction;
+            t.tag = op.tag;
+            t.nsweeps = op.nsweeps;
+            switch (op.kind) {
+                case OP_SWEEP: t.kind = TAIL_SWEEP; break;
+                case OP_RESIDUAL_RESTRICT: t.kind = TAIL_RESTRICT; break;
+                case OP_PROLONGATE: t.kind = TAIL_PROLONG; break;
+                case OP_COARSE_LDS: t.kind = TAIL_COARSE; break;
+                default: ok = false;
+            }
+        }
+        if (!ok) {  // leave the ops as they are
+            for (size_t u = q; u < r; ++u) out.push_back(h->ops[u]);
+            q = r;
+            continue;
+        }
+        A.nlev = L - lt;
+        int off = 0;
+        for (int l = lt; l < L; ++l) {
+            TailLevel& tl = A.lv[l - lt];
+            const Level& lv = h->levels[l];
+            tl.G = tail_layout(lv.L);
+            tl.ox = off;
+            off += (int)tl.G.nstore;
+            tl.of = off;
+            off += (int)tl.G.nstore;
+            tl.ncolours = lv.spec.ncolours;
+            const GibbsArg g = make_gibbs(h, lv, 0, 0, h->ctrl);
+            tl.sd = g.sd;
+            tl.wd = g.wd;
+            tl.S = lv.S;
+        }
+        int vmax = 0;
+        for (int l = 0; l < A.nlev; ++l) vmax = std::max(vmax, (int)A.lv[l].G.nstore);
+        A.oscr = off;
+        A.lds_doubles = off + vmax;
+        A.alpha = h->cfg.coarse_scaling;
+        A.key = h->key;
+        A.sample = h->ctrl;
+        A.xg = h->levels[lt].x;
+        A.fg = h->levels[lt].f;
+        A.Lg = h->levels[lt].L;
+        TailArgs* d = nullptr;
+        HIPCHK(h, hipMalloc(&d, sizeof(TailArgs)));
+        HIPCHK(h, hipMemcpy(d, &A, sizeof(TailArgs), hipMemcpyHostToDevice));
+        Op t{OP_TAIL, lt, 0, 0, 0};
+        t.tail = (int)h->tail_args.size();
+        h->tail_args.push_back(d);
+        h->tail_lds.push_back((size_t)A.lds_doubles * sizeof(double));
+        out.push_back(t);
+        if (r <= pre_end) removed_before_pre += r - q - 1;
+        q = r;
+    }
+    const size_t removed = h->ops.size() - out.size();
+    h->ops.swap(out);
+    h->seg_end_pre -= removed_before_pre;
+    h->seg_begin_post = h->seg_begin_post >= removed ? h->seg_begin_post - removed : 0;
+    h->seg_end_post = h->seg_end_post >= removed ? h->seg_end_post - removed : 0;
+    return MGMC_OK;
+}
+
 void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
     const uint64_t* sample = h->ctrl;  // ctrl[0]
     for (size_t q = begin; q < end; ++q) {
@@ -877,6 +1006,14 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
             }
             case OP_COPY: {
                 hipMemcpyAsync(lv.x, lv.buf(op.src), lv.L.nstore * sizeof(double), hipMemcpyDeviceToDevice, s);
+                break;
+            }
+            case OP_TAIL: {
+                const size_t lds = h->tail_lds[op.tail];
+                if (lv.spec.dim == 3)
+                    hipLaunchKernelGGL(k_tail<3>, dim3(1), dim3(1024), lds, s, (const TailArgs*)h->tail_args[op.tail]);
+                else
+                    hipLaunchKernelGGL(k_tail<2>, dim3(1), dim3(1024), lds, s, (const TailArgs*)h->tail_args[op.tail]);
                 break;
             }
             case OP_QOI: {
@@ -1160,6 +1297,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     // per CU leave it latency / VALU bound
     h->fuse_restrict = getenv("MGMC_FUSE_RESTRICT") != nullptr;
     build_ops(h);
+    if ((rc = build_tails(h)) != MGMC_OK) return bail(rc);
     if ((rc = ensure_series(h, 1024)) != MGMC_OK) return bail(rc);
     if (hipStreamSynchronize(h->stream) != hipSuccess) {
         h->last_error = "stream sync failed after setup";
@@ -1181,6 +1319,7 @@ int mgmc_destroy(mgmc_handle* h) {
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
     destroy_graphs(h);
+    free_tails(h);
     for (auto& lv : h->levels) {
         free_lowrank(lv.lr);
         if (lv.x) hipFree(lv.x);
@@ -1930,7 +2069,8 @@ int mgmc_set_lowrank(mgmc_handle* h, int m, const int64_t* colptr, const int64_t
         rc = build_coarse_chol(h, m > 0 ? &cols : nullptr, sigma, m);
     HIPCHK(h, hipStreamSynchronize(h->stream));
     build_ops(h);
-    const int rc2 = build_graphs(h);
+    int rc2 = build_tails(h);
+    if (!rc2) rc2 = build_graphs(h);
     return rc ? rc : rc2;
 }
 

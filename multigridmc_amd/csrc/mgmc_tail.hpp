@@ -1,0 +1,225 @@
+// mgmc_tail.hpp -- the coarsest levels' whole sub-cycle in one workgroup, every level in LDS.
+//
+// Below a certain size a level's kernels are launch-bound: at 512^3 the 15^3 and 7^3 levels took 20
+// launches of 4.8-24 us per cycle (pre-sweep colour-pair passes, residual + restriction, coarse SSOR
+// sampler, prolongation, post-sweep passes) for 3,718 unknowns; the floor of one launch in the cycle
+// graph is ~3.6 us (k_qoi_record, one wavefront).  k_tail replays that stretch of the cycle's op list
+// -- every op of one call of build_ops_level(lt), i.e. MultigridMCSampler::apply's recursion from
+// level lt down (sampler/multigridmc_sampler.cc:103-138) -- inside one 1024-thread workgroup with x and
+// f of every level resident in LDS, __syncthreads between phases instead of kernel boundaries.
+//
+// Each op does exactly the arithmetic of the kernel it replaces, so the cycle is bitwise the same:
+//  * Gibbs sweep (k_sweep_pairs / k_sweep_mc / k_coarse_ssor_lds): colours in order (forward
+//    0..2^d-1, backward reversed); c = fma(sd, xi, f) with xi the cos / sin branch of the Philox pair
+//    (odd i, i+1) of the sweep's tag; x = fma(omega/diag, c - S, x), S the stencil fma chain in
+//    ascending column order.  The right hand sides of a sweep are evaluated first, one Box-Muller per
+//    pair for all colours at once (f does not change during a sweep), then the colour passes;
+//  * residual + restriction (k_zresrestrict / k_residual_restrict): r = f - (0 + sum a x ascending)
+//    at every fine vertex, then f_c = sum over (sz, sy, sx) of (1 w1(sx) w1(sy) w1(sz)) r, x_c = 0;
+//  * prolongate-add (k_prolongate_pairs): x += (alpha w) x_c over the interior parents in ascending
+//    coarse order.
+// LDS layout per level: the (nx+1)(ny+1)(nz+1) vertices including the zero boundary, x fastest, no
+// padding; one scratch array (right hand sides / residuals) of the largest tail level.
+#pragma once
+#include "mgmc_kernels.hpp"
+
+namespace mgmc {
+
+enum TailKind { TAIL_SWEEP = 0, TAIL_RESTRICT = 1, TAIL_PROLONG = 2, TAIL_COARSE = 3 };
+constexpr int TAIL_MAX_LEVELS = 4;
+constexpr int TAIL_MAX_OPS = 96;
+
+struct TailOp {
+    int kind;
+    int level;     // index into TailArgs::lv (0 = level lt)
+    int dir;       // sweeps: 1 forward, 2 backward (MGMC_FORWARD / MGMC_BACKWARD)
+    uint32_t tag;  // first sweep tag
+    int nsweeps;   // TAIL_COARSE: forward/backward sweeps, tags tag, tag+1, ...
+};
+
+struct TailLevel {
+    Layout G;      // LDS layout (off 0, sx = nx+1, sp = sx (ny+1))
+    int ox, of;    // LDS offsets (doubles) of x and f
+    int ncolours;
+    double sd, wd; // sqrt(diag (2-omega)/omega), omega/diag
+    StencilArg S;
+};
+
+struct TailArgs {
+    int nlev, nops, oscr, lds_doubles;
+    double alpha;          // coarse_scaling
+    RngKey key;
+    const uint64_t* sample;
+    double* xg;            // level lt in HBM (its padded layout Lg)
+    const double* fg;
+    Layout Lg;
+    TailLevel lv[TAIL_MAX_LEVELS];
+    TailOp ops[TAIL_MAX_OPS];
+};
+
+template <int DIM>
+__global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
+    constexpr int NPTS = DIM == 3 ? 27 : 9;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int ntot = A->lds_doubles;
+    for (int q = tid; q < ntot; q += nt) lds[q] = 0.0;
+    __syncthreads();
+    const uint64_t sample = *A->sample;
+    const uint32_t s_lo = (uint32_t)sample, s_hi = (uint32_t)(sample >> 32);
+    double* scr = lds + A->oscr;
+
+    // interior vertex q of a level -> (i, j, k)
+    auto coords = [](const Layout& G, int q, int& i, int& j, int& k) {
+        const int nxi = G.nx - 1, nyi = G.ny - 1;
+        i = q % nxi + 1;
+        const int r = q / nxi;
+        j = r % nyi + 1;
+        k = DIM == 3 ? r / nyi + 1 : 0;
+    };
+    auto ndof_of = [](const Layout& G) { return (G.nx - 1) * (G.ny - 1) * (DIM == 3 ? G.nz - 1 : 1); };
+
+    {  // level lt from HBM (boundary entries stay 0)
+        const TailLevel& t0 = A->lv[0];
+        const int nd = ndof_of(t0.G);
+        for (int q = tid; q < nd; q += nt) {
+            int i, j, k;
+            coords(t0.G, q, i, j, k);
+            lds[t0.ox + (int)t0.G.at(i, j, k)] = A->xg[A->Lg.at(i, j, k)];
+            lds[t0.of + (int)t0.G.at(i, j, k)] = A->fg[A->Lg.at(i, j, k)];
+        }
+    }
+    __syncthreads();
+
+    // one Gibbs sweep of level t: right hand sides of every vertex, then the colour passes
+    auto sweep = [&](const TailLevel& t, int dir, uint32_t tag) {
+        const Layout& G = t.G;
+        double* x = lds + t.ox;
+        const double* f = lds + t.of;
+        const int npair = G.nx / 2;
+        const int nrow = (G.ny - 1) * (DIM == 3 ? G.nz - 1 : 1);
+        for (int q = tid; q < npair * nrow; q += nt) {
+            const int m = q % npair, row = q / npair;
+            const int j = row % (G.ny - 1) + 1, k = DIM == 3 ? row / (G.ny - 1) + 1 : 0;
+            const int i0 = 2 * m + 1;
+            if (i0 > G.nx - 1) continue;
+            const Philox4 rnd = philox4x32_10(pair_id<DIM>(G, i0, j, k), tag, s_lo, s_hi, A->key.k0, A->key.k1);
+            double z0, z1;
+            normal_pair(rnd, &z0, &z1);
+            const int p = (int)G.at(i0, j, k);
+            scr[p] = fma(t.sd, z0, f[p]);
+            if (i0 + 1 <= G.nx - 1) scr[p + 1] = fma(t.sd, z1, f[p + 1]);
+        }
+        __syncthreads();
+        const int nc = t.ncolours;
+        for (int cc = 0; cc < nc; ++cc) {
+            const int c = dir == 1 ? cc : nc - 1 - cc;
+            // vertices of colour c: coordinate d = 2 - bit_d(c) + 2 t_d
+            const int fi = 2 - (c & 1), fj = 2 - ((c >> 1) & 1), fk = DIM == 3 ? 2 - ((c >> 2) & 1) : 0;
+            const int ci = fi > G.nx - 1 ? 0 : (G.nx - 1 - fi) / 2 + 1;
+            const int cj = fj > G.ny - 1 ? 0 : (G.ny - 1 - fj) / 2 + 1;
+            const int ck = DIM == 3 ? (fk > G.nz - 1 ? 0 : (G.nz - 1 - fk) / 2 + 1) : 1;
+            for (int q = tid; q < ci * cj * ck; q += nt) {
+                const int i = fi + 2 * (q % ci), r = q / ci;
+                const int j = fj + 2 * (r % cj), k = DIM == 3 ? fk + 2 * (r / cj) : 0;
+                const long long p = G.at(i, j, k);
+                const double res = stencil_fma<DIM, NPTS>(x, p, G, t.S);
+                x[p] = fma(t.wd, scr[p] - res, x[p]);
+            }
+            __syncthreads();
+        }
+    };
+
+    for (int o = 0; o < A->nops; ++o) {
+        const TailOp op = A->ops[o];
+        const TailLevel& t = A->lv[op.level];
+        if (op.kind == TAIL_SWEEP) {
+            sweep(t, op.dir, op.tag);
+        } else if (op.kind == TAIL_COARSE) {
+            for (int s = 0; s < op.nsweeps; ++s) sweep(t, (s & 1) ? 2 : 1, op.tag + (uint32_t)s);
+        } else if (op.kind == TAIL_RESTRICT) {
+            const TailLevel& c = A->lv[op.level + 1];
+            const Layout& G = t.G;
+            const double* x = lds + t.ox;
+            const double* f = lds + t.of;
+            const int nd = ndof_of(G);
+            for (int q = tid; q < nd; q += nt) {
+                int i, j, k;
+                coords(G, q, i, j, k);
+                const long long p = G.at(i, j, k);
+                scr[p] = f[p] - stencil_sum<DIM, NPTS>(x, p, G, t.S);
+            }
+            __syncthreads();
+            const Layout& Gc = c.G;
+            const int ndc = ndof_of(Gc);
+            for (int q = tid; q < ndc; q += nt) {
+                int I, J, K;
+                coords(Gc, q, I, J, K);
+                const long long pf = G.at(2 * I, 2 * J, 2 * K);
+                double result = 0.0;
+                const int zr = DIM == 3 ? 1 : 0;
+                for (int sz = -zr; sz <= zr; ++sz)
+                    for (int sy = -1; sy <= 1; ++sy)
+                        for (int sx = -1; sx <= 1; ++sx) {
+                            double w = 1.0;
+                            w *= w1(sx);
+                            w *= w1(sy);
+                            if (DIM == 3) w *= w1(sz);
+                            result += w * scr[pf + sz * G.sp + sy * G.sx + sx];
+                        }
+                const long long pc = Gc.at(I, J, K);
+                lds[c.of + pc] = result;
+                lds[c.ox + pc] = 0.0;
+            }
+            __syncthreads();
+        } else {  // TAIL_PROLONG: x_l += alpha P x_{l+1}
+            const TailLevel& c = A->lv[op.level + 1];
+            const Layout& G = t.G;
+            const Layout& Gc = c.G;
+            double* x = lds + t.ox;
+            const double* xc = lds + c.ox;
+            const int nd = ndof_of(G);
+            const double alpha = A->alpha;
+            for (int q = tid; q < nd; q += nt) {
+                int i, j, k;
+                coords(G, q, i, j, k);
+                const long long p = G.at(i, j, k);
+                double v = x[p];
+                const int k0 = k >> 1, nk = (DIM == 3 && (k & 1)) ? 2 : 1;
+                const int j0 = j >> 1, nj = (j & 1) ? 2 : 1;
+                const int i0 = i >> 1, ni = (i & 1) ? 2 : 1;
+                for (int aa = 0; aa < nk; ++aa) {
+                    const int kk = k0 + aa;
+                    if (DIM == 3 && (kk < 1 || kk > Gc.nz - 1)) continue;
+                    for (int bb = 0; bb < nj; ++bb) {
+                        const int jj = j0 + bb;
+                        if (jj < 1 || jj > Gc.ny - 1) continue;
+                        for (int cc = 0; cc < ni; ++cc) {
+                            const int ii = i0 + cc;
+                            if (ii < 1 || ii > Gc.nx - 1) continue;
+                            double w = 1.0;
+                            w *= w1(i - 2 * ii);
+                            w *= w1(j - 2 * jj);
+                            if (DIM == 3) w *= w1(k - 2 * kk);
+                            v += alpha * w * xc[Gc.at(ii, jj, DIM == 3 ? kk : 0)];
+                        }
+                    }
+                }
+                x[p] = v;
+            }
+            __syncthreads();
+        }
+    }
+
+    {  // level lt back to HBM
+        const TailLevel& t0 = A->lv[0];
+        const int nd = ndof_of(t0.G);
+        for (int q = tid; q < nd; q += nt) {
+            int i, j, k;
+            coords(t0.G, q, i, j, k);
+            A->xg[A->Lg.at(i, j, k)] = lds[t0.ox + (int)t0.G.at(i, j, k)];
+        }
+    }
+}
+
+}  // namespace mgmc
