@@ -269,7 +269,7 @@ int zsweep_variant() {
 int zsweep_xp() {
     switch (zsweep_variant()) {
         case 1: case 2: case 3: case 4: case 7: case 11: case 13: return 64;
-        case 5: case 6: case 8: case 9: case 12: return 32;
+        case 5: case 6: case 8: case 9: case 12: case 14: return 32;
         default: return ZS_XP;
     }
 }
@@ -294,15 +294,20 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
         const long long txy = (long long)((lv.L.nx / 2) / xp) * ((lv.L.ny - 1 + ty - 1) / ty);
         while (a.tz > 8 && txy * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 1024) a.tz /= 2;
         if (coarse && zsweep_variant() == 0) {
-            // fused-prolongation variant (3 workgroups per CU): deeper chunks when two full rounds of
-            // workgroups still fill the chip -- fewer re-read z halo planes (512^3: tz 32 -> 86, 923 ->
-            // 897 us)
-            const long long nchunk = std::max(1LL, (2LL * 3 * g_num_cu + txy - 1) / txy);
-            const int tz2 = (int)(((lv.L.nz - 1 + nchunk - 1) / nchunk + 1) & ~1LL);
-            if (tz2 > a.tz) a.tz = tz2;
+            // fused-prolongation sweep: 512-thread workgroups (one core pair per thread: 127 VGPRs,
+            // 2 workgroups = 16 waves per CU against 3 x 4 waves with 256 threads, which the 6.7 KB
+            // coarse ring and 161 VGPRs allowed) and chunks up to 64 planes deep as long as the grid
+            // keeps two rounds of workgroups (512^3: tz 64, 2,048 tiles, 906-911 -> 841-851 us;
+            // 256^3: tz 16, 142 -> 118 us; interleaved A/B)
+            a.tz = 64;
+            while (a.tz > 8 && txy * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 2LL * 2 * g_num_cu) a.tz /= 2;
         }
     }
     const bool pr = coarse != nullptr;
+    if (pr && zsweep_variant() == 0 && getenv("MGMC_ZS_PROLONG256") == nullptr) {
+        launch_zsweep_t<32, 16, 512, 4>(lv, a, pr, s);
+        return;
+    }
     switch (zsweep_variant()) {
         case 1: launch_zsweep_t<64, 4, 256>(lv, a, pr, s); break;
         case 2: launch_zsweep_t<64, 8, 512>(lv, a, pr, s); break;
@@ -316,6 +321,7 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
         case 11: launch_zsweep_t<64, 16, 512, 4>(lv, a, pr, s); break;
         case 12: launch_zsweep_t<32, 32, 512, 4>(lv, a, pr, s); break;
         case 13: launch_zsweep_t<64, 32, 1024, 4>(lv, a, pr, s); break;
+        case 14: launch_zsweep_t<32, 16, 512, 4>(lv, a, pr, s); break;  // one core pair per thread
         default: launch_zsweep_t<ZS_XP, ZS_TY, ZS_NT, ZS_MINW>(lv, a, pr, s); break;
     }
 }
