@@ -488,11 +488,11 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
     const char* kz = getenv("MGMC_ZR_KZ");
     const long long work = (long long)a.ntx * a.nty * (lc.L.nz - 1);
     a.kz = kz ? atoi(kz) : (work >= 8 * 1024 ? 8 : (work >= 4 * 1024 ? 4 : (work >= 512 ? 2 : 1)));
-    if (!kz && NPTS == 7 && work >= 32 * 1024) {
+    if (!kz && NPTS == 7 && work >= 16 * 1024) {
         // fine 7-point level: the deepest chunks that still give two full rounds of workgroups (every
-        // chunk re-reads 2 x planes and 1 f plane below / above it: 512^3 kz 8 -> 43 (6 chunks,
-        // 1536 tiles on 256 CUs x 3 workgroups): 561 -> 451 us)
-        const long long slots = 3LL * g_num_cu;
+        // chunk re-reads 2 x planes and 1 f plane below / above it: 512^3 with 64 x 4 tiles kz 8 -> 43
+        // (6 chunks, 1536 tiles on 256 CUs x 3 workgroups): 561 -> 451 us; with 64 x 8 tiles kz 32)
+        const long long slots = (NT >= 512 ? 2LL : 3LL) * g_num_cu;  // workgroups per CU (LDS, VGPRs)
         const long long per_chunk = (long long)a.ntx * a.nty;
         const long long nchunk = std::max(1LL, (2 * slots + per_chunk - 1) / per_chunk);
         a.kz = std::max(8, (int)((lc.L.nz - 1 + nchunk - 1) / nchunk));
@@ -516,7 +516,14 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
         if (lf.spec.npoints == 7) {
             if (v == 1) launch_zresrestrict_t<7, 32, 4, 128>(lf, lc, x, f, fc, xc, s);
             else if (v == 3) launch_zresrestrict_t<7, 32, 8, 256>(lf, lc, x, f, fc, xc, s);
+            else if (v == 2) launch_zresrestrict_t<7, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
+            else if (v == 5) launch_zresrestrict_t<7, 64, 4, 512>(lf, lc, x, f, fc, xc, s);
             else if (small) launch_zresrestrict_t<7, 16, 4, 64>(lf, lc, x, f, fc, xc, s);
+            // 64 x 8 coarse points, 512 threads, 80 KB of LDS (2 workgroups per CU): half the y halo
+            // of 64 x 4 (19 x planes rows per 16 fine rows instead of 11 per 8); 512^3 with kz 32:
+            // 505-525 -> 488-502 us (interleaved A/B); at 256^3 too few tiles (73 against 66 us)
+            else if ((long long)((lc.L.nx + 62) / 64) * ((lc.L.ny + 6) / 8) * (lc.L.nz - 1) >= 16 * 1024)
+                launch_zresrestrict_t<7, 64, 8, 512>(lf, lc, x, f, fc, xc, s);
             else launch_zresrestrict_t<7, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
         } else {
             if (v == 1) launch_zresrestrict_t<27, 32, 4, 128>(lf, lc, x, f, fc, xc, s);

@@ -187,15 +187,22 @@ def test_zsweep_tile_variants_bitwise(hip_device, monkeypatch, variant):
                                       ("MGMC_NO_TAIL", "3d16"),
                                       ("MGMC_NO_TAIL", "3d64_4lvl"),
                                       ("MGMC_NO_TAIL", "2d64_template_W"),
-                                      ("MGMC_NO_TAIL", "3d32_W_ssor")])
+                                      ("MGMC_NO_TAIL", "3d32_W_ssor"),
+                                      ("MGMC_ZR_VARIANT=2", "3d_zres7"),
+                                      ("MGMC_ZR_VARIANT=5", "3d_zres7"),
+                                      ("MGMC_ZS_PROLONG256", "3d128_zsweep"),
+                                      ("MGMC_ZS_PROLONG256", "3d_aniso_zsweep_ssor")])
 def test_variant_cycles_bitwise(hip_device, monkeypatch, env, name):
     """MGMC_NO_FUSE_PROLONG: the separate prolongate-add pass (instead of the default fold into the
     first post-sweep's plane loads); MGMC_FUSE_RESTRICT: the last pre-sweep, the residual and the
     restriction in one kernel (k_zsweep_res7, opt-in); MGMC_QUADS: both colour pairs of a k-parity
     half per launch on Galerkin levels, out of place (k_sweep_quads, opt-in); MGMC_NO_TAIL: the
     coarsest levels' sub-cycle as separate launches instead of one workgroup (k_tail, the default
-    wherever the levels fit its LDS).  All give the oracle's cycle exactly."""
-    monkeypatch.setenv(env, "1")
+    wherever the levels fit its LDS); MGMC_ZR_VARIANT=2 / 5: the 64 x 4 fine residual + restriction
+    tiles with 256 / 512 threads; MGMC_ZS_PROLONG256: the 256-thread fused-prolongation sweep.  All
+    give the oracle's cycle exactly."""
+    var, _, val = env.partition("=")
+    monkeypatch.setenv(var, val or "1")
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)
     mc = oracle_for(s, p, lat)
