@@ -142,6 +142,10 @@ int mgmc_qoi_moments(mgmc_handle* h, double out[3]);
 int mgmc_reset_moments(mgmc_handle* h);
 int mgmc_set_sample_index(mgmc_handle* h, uint64_t index);
 int mgmc_get_sample_index(mgmc_handle* h, uint64_t* index);
+/* Copy the QoI series recorded by the last mgmc_sample / mgmc_sample_async call (n values; waits
+ * for the handle's stream).  With mgmc_sample_async on several handles this collects the series of
+ * chains that ran concurrently (measure_convergence's batched chains, driver_mgmc.cc:188-314). */
+int mgmc_get_series(mgmc_handle* h, double* out, size_t n);
 /* HIP stream (hipStream_t) the handle enqueues on */
 int mgmc_get_stream(mgmc_handle* h, void** stream);
 

@@ -76,6 +76,7 @@ SIGNATURES = [
     ("mgmc_reset_moments", c_int, [_H]),
     ("mgmc_set_sample_index", c_int, [_H, c_uint64]),
     ("mgmc_get_sample_index", c_int, [_H, POINTER(c_uint64)]),
+    ("mgmc_get_series", c_int, [_H, POINTER(c_double), c_size_t]),
     ("mgmc_get_stream", c_int, [_H, POINTER(c_void_p)]),
     ("mgmc_operator_apply", c_int, [_H, c_int, _DP, _DP]),
     ("mgmc_smoother_apply", c_int, [_H, c_int, c_int, c_int, _DP, _DP]),

@@ -1477,6 +1477,15 @@ int mgmc_set_sample_index(mgmc_handle* h, uint64_t index) {
     return MGMC_OK;
 }
 
+int mgmc_get_series(mgmc_handle* h, double* out, size_t n) {
+    if (!h || (!out && n > 0)) return fail(h, MGMC_E_INVALID, "null argument");
+    if (n > h->series_cap) return fail(h, MGMC_E_INVALID, "more values than the series holds");
+    HIPCHK(h, hipSetDevice(h->device));
+    if (n > 0) HIPCHK(h, hipMemcpyAsync(out, h->series, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return MGMC_OK;
+}
+
 int mgmc_get_sample_index(mgmc_handle* h, uint64_t* index) {
     if (!h || !index) return fail(h, MGMC_E_INVALID, "null argument");
     HIPCHK(h, hipSetDevice(h->device));

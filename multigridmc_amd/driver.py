@@ -118,9 +118,44 @@ def measure_sampling_time(sampler, exact: ExactTargets, sampling_params: Samplin
     return data, (mean_exact, variance_exact)
 
 
+def convergence_series(sampler, nsamples: int, nsteps: int, rows, vals, batch: int = 1) -> np.ndarray:
+    """QoI series z[k, j] of nsamples chains from x = 0, nsteps cycles each (driver_mgmc.cc:236-254).
+    Chain k draws sample indices s0 + k nsteps .. s0 + (k+1) nsteps - 1, exactly as one handle running
+    the chains one after the other.  batch > 1 (radius-0 QoI) runs that many chains at a time on
+    clones of the handle, each on its own HIP stream, with those sample indices: the same draws, so
+    the same series bit for bit, with the small lattices' idle GPU filled by the concurrent chains."""
+    x0 = np.zeros(sampler.ndof)
+    z = np.empty((nsamples, nsteps))
+    if batch <= 1 or not (len(rows) == 1 and vals[0] == 1.0):
+        for k in range(nsamples):
+            sampler.set_state(x0)
+            z[k] = _qoi_series(sampler, nsteps, rows, vals)
+        return z
+    s0 = sampler.get_sample_index()
+    handles = [sampler] + [sampler.clone() for _ in range(min(batch, nsamples) - 1)]
+    try:
+        if sampler._fixed_rhs is not None:
+            for h in handles[1:]:
+                h.fix_rhs(sampler._fixed_rhs)
+        for k0 in range(0, nsamples, len(handles)):
+            ks = list(range(k0, min(k0 + len(handles), nsamples)))
+            for h, k in zip(handles, ks):
+                h.set_sample_index(s0 + k * nsteps)
+                h.set_state(x0)
+                h.sample_async(nsteps, int(rows[0]))
+            for h, k in zip(handles, ks):
+                z[k] = h.get_series(nsteps)
+        sampler.set_sample_index(s0 + nsamples * nsteps)
+    finally:
+        for h in handles[1:]:
+            h.close()
+    return z
+
+
 def measure_convergence(sampler, exact: ExactTargets, sampling_params: SamplingParameters,
-                        measurement_params: MeasurementParameters, filename: str):
-    """driver_mgmc.cc:188-314: nsamplesconvergence independent chains from x = 0."""
+                        measurement_params: MeasurementParameters, filename: str, batch: int = 1):
+    """driver_mgmc.cc:188-314: nsamplesconvergence independent chains from x = 0 (batch: chains run
+    concurrently, convergence_series)."""
     op = sampler.get_linear_operator()
     y = _measured_values(measurement_params)
     mean_x_exact = exact.posterior_mean(y) if op.get_m_lowrank() > 0 else np.zeros(op.get_ndof())
@@ -129,10 +164,9 @@ def measure_convergence(sampler, exact: ExactTargets, sampling_params: SamplingP
     nsteps = sampling_params.nstepsconvergence
     nsamples = sampling_params.nsamplesconvergence
     avg = np.zeros((4, nsteps + 1))
-    x0 = np.zeros(op.get_ndof())
+    zs = convergence_series(sampler, nsamples, nsteps, rows, vals, batch)
     for k in range(nsamples):
-        sampler.set_state(x0)
-        z = _qoi_series(sampler, nsteps, rows, vals)
+        z = zs[k]
         for j in range(1, nsteps + 1):
             for a in range(4):
                 avg[a, j] += (z[j - 1] ** (a + 1) - avg[a, j]) / (k + 1.0)
@@ -162,9 +196,13 @@ def measure_convergence(sampler, exact: ExactTargets, sampling_params: SamplingP
 
 
 def main(argv=None) -> int:
-    argv = sys.argv[1:] if argv is None else argv
+    argv = list(sys.argv[1:] if argv is None else argv)
+    batch = 1
+    if len(argv) == 3 and argv[0] == "--convergence-batch":  # concurrent measure_convergence chains
+        batch = int(argv[1])
+        argv = argv[2:]
     if len(argv) != 1:
-        print(f"Usage: {sys.argv[0]} CONFIGURATIONFILE")
+        print(f"Usage: {sys.argv[0]} [--convergence-batch N] CONFIGURATIONFILE")
         return -1
     t_start = time.time()
     print("\n+--------------------------------+")
@@ -219,7 +257,8 @@ def main(argv=None) -> int:
         print("**** Multigrid MC ****")
         measure_sampling_time(sampler, exact, sampling_params, measurement_params, "MGMC",
                               "timeseries_multigridmc.txt")
-        measure_convergence(sampler, exact, sampling_params, measurement_params, "convergence_multigridmc.txt")
+        measure_convergence(sampler, exact, sampling_params, measurement_params, "convergence_multigridmc.txt",
+                            batch)
         if general.save_posterior_statistics:
             print("  posterior_statistics (VTK output) is not on the device path: skipped")
         print()

@@ -172,6 +172,7 @@ class MultigridMCSampler:
                  device: int = 0, chain_id: int = 0):
         self.linear_operator = linear_operator
         self.params = params
+        self.seed, self.device, self.chain_id = int(seed), int(device), int(chain_id)
         self.config = make_config(linear_operator, params)
         self.lib = load_library()
         h = ctypes.c_void_p()
@@ -290,6 +291,18 @@ class MultigridMCSampler:
 
     def reset_moments(self):
         self._chk(self.lib.mgmc_reset_moments(self.handle))
+
+    def get_series(self, n: int) -> np.ndarray:
+        """The QoI series of the last sample / sample_async call (waits for this handle's stream)."""
+        out = np.empty(max(int(n), 0))
+        self._chk(self.lib.mgmc_get_series(self.handle, _dp(out), out.size))
+        return out
+
+    def clone(self) -> "MultigridMCSampler":
+        """A second handle of the same chain: same operator, parameters, device and Philox key
+        (seed, chain_id), its own state, right hand side and HIP stream.  With disjoint sample
+        indices it reproduces the draws this handle would make there (batched chains)."""
+        return MultigridMCSampler(self.linear_operator, self.seed, self.params, self.device, self.chain_id)
 
     def set_sample_index(self, index: int):
         self._chk(self.lib.mgmc_set_sample_index(self.handle, int(index)))

@@ -355,3 +355,25 @@ def test_cpp_host_side_sample_matches_python_path(hip_device, tmp_path):
     zp = s.sample(6, 7 * 15 * 15 + 7 * 15 + 7)
     s.close()
     assert np.array_equal(zc, zp)
+
+
+@pytest.mark.parametrize("shape,nlevel,batch", [((64, 64), 4, 3), ((32, 32, 32), 3, 4)])
+def test_convergence_chains_batched_equal_sequential(hip_device, shape, nlevel, batch):
+    """measure_convergence's chains (driver_mgmc.cc:236-254) run `batch` at a time on cloned handles
+    with the sequential loop's sample indices: the same QoI series bit for bit."""
+    from multigridmc_amd.driver import convergence_series
+    lat = mg.Lattice(*shape)
+    op = mg.ShiftedLaplaceFDOperator(lat, 25.0)
+    p = mg.MultigridParameters(nlevel=nlevel)
+    q = mg.measurement_vector_index(lat, [0.5] * lat.dim)
+    f = np.random.default_rng(3).standard_normal(lat.Nvertex)
+    a = mg.MultigridMCSampler(op, SEED, p)
+    b = mg.MultigridMCSampler(op, SEED, p)
+    a.fix_rhs(f)
+    b.fix_rhs(f)
+    za = convergence_series(a, 7, 5, [q], [1.0], batch=1)
+    zb = convergence_series(b, 7, 5, [q], [1.0], batch=batch)
+    assert np.all(np.isfinite(za)) and np.array_equal(za, zb)
+    assert a.get_sample_index() == b.get_sample_index() == 35
+    a.close()
+    b.close()
