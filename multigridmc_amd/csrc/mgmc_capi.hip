@@ -371,8 +371,13 @@ bool pairs_eligible(const LevelSpec& sp, const Layout& L) {
 // 128 pairs, so that a workgroup holds >= 7 full rows (<= 1 recomputed row in 7).  Bitwise equal to
 // the pair passes but slower at 512^3 (level 1: 2 x 105 us against 4 x 40 us per sweep):
 // the second pair's loads wait for the first pair's rows, and 512-thread workgroups hide less latency
+// default (small levels): rows of <= 32 pairs, where each pass is launch-latency bound and halving the
+// launches pays (256^3: 63^3 level 4 x 5.0 -> 2 x 7.6 us, 31^3 level 4 x 4.8 -> 2 x 6.3 us per sweep);
+// MGMC_QUADS: every level with rows of <= 128 pairs (slower on the large levels, tests); MGMC_NO_QUADS:
+// none.  Levels that k_tail will run are left to it (caller).
 bool quads_eligible(const LevelSpec& sp, const Layout& L) {
-    return pairs_eligible(sp, L) && L.nx / 2 <= 128 && getenv("MGMC_QUADS") != nullptr;
+    if (!pairs_eligible(sp, L) || getenv("MGMC_NO_QUADS") != nullptr) return false;
+    return L.nx / 2 <= (getenv("MGMC_QUADS") != nullptr ? 128 : 32);
 }
 
 void launch_quads(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
@@ -846,6 +851,25 @@ Layout tail_layout(const Layout& L) {
     return G;
 }
 
+// the same choice from the level shapes alone (at creation time, before any level is allocated)
+int tail_start_by_size(const std::vector<LevelSpec>& specs, const mgmc_config& cfg) {
+    if (getenv("MGMC_NO_TAIL") != nullptr || cfg.coarse_solver != MGMC_COARSE_SSOR) return -1;
+    const int L = (int)specs.size();
+    for (int lt = 1; lt + 1 < L; ++lt) {
+        bool ok = true;
+        size_t tot = 0, vmax = 0;
+        for (int l = lt; l < L && ok; ++l) {
+            const LevelSpec& sp = specs[l];
+            ok = sp.npoints == (sp.dim == 3 ? 27 : 9);
+            const size_t v = (size_t)(sp.n[0] + 1) * (sp.n[1] + 1) * (sp.dim == 3 ? sp.n[2] + 1 : 1);
+            tot += 2 * v;
+            vmax = std::max(vmax, v);
+        }
+        if (ok && (tot + vmax) * sizeof(double) <= TAIL_LDS_LIMIT) return lt;
+    }
+    return -1;
+}
+
 // smallest level lt >= 1 whose levels lt .. L-1 all fit one workgroup's LDS (x, f per level + one
 // scratch of the largest): Galerkin levels, no low-rank part, ordinary (in-place) sweeps, SSOR coarse
 // sampler; -1 if none or only the coarsest level fits (the coarse LDS kernel covers that)
@@ -1262,6 +1286,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         return bail(MGMC_E_HIP);
     }
     const std::vector<LevelSpec> specs = build_hierarchy(*cfg);
+    const int tail0 = tail_start_by_size(specs, *cfg);  // levels k_tail can take (no quads there)
     size_t lds_limit = 150 * 1024;
     for (size_t l = 0; l < specs.size(); ++l) {
         Level lv;
@@ -1282,7 +1307,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         lv.zsweep = cfg->dim == 3 && lv.spec.npoints == 7 && symmetric && l + 1 < specs.size() &&
                     (lv.L.nx % (2 * zsweep_xp())) == 0 && getenv("MGMC_NO_ZSWEEP") == nullptr;
         lv.pairs = pairs_eligible(lv.spec, lv.L) && getenv("MGMC_NO_PAIRS") == nullptr;
-        lv.quads = lv.pairs && quads_eligible(lv.spec, lv.L);
+        lv.quads = lv.pairs && quads_eligible(lv.spec, lv.L) && (tail0 < 0 || (int)l < tail0);
         if (lv.pingpong()) {
             if (hipMalloc(&lv.x2, bytes) != hipSuccess) {
                 h->levels.push_back(lv);
