@@ -119,12 +119,26 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             const int ci = fi > G.nx - 1 ? 0 : (G.nx - 1 - fi) / 2 + 1;
             const int cj = fj > G.ny - 1 ? 0 : (G.ny - 1 - fj) / 2 + 1;
             const int ck = DIM == 3 ? (fk > G.nz - 1 ? 0 : (G.nz - 1 - fk) / 2 + 1) : 1;
-            for (int q = tid; q < ci * cj * ck; q += nt) {
-                const int i = fi + 2 * (q % ci), r = q / ci;
-                const int j = fj + 2 * (r % cj), k = DIM == 3 ? fk + 2 * (r / cj) : 0;
-                const long long p = G.at(i, j, k);
-                const double res = stencil_fma<DIM, NPTS>(x, p, G, t.S);
-                x[p] = fma(t.wd, scr[p] - res, x[p]);
+            // small classes (<= 8 x 8 x 16, 2D 32 x 32 vertices): thread bits are the class
+            // coordinates, no index division on the pass's critical path
+            const bool fast = DIM == 3 ? (ci <= 8 && cj <= 8 && ck <= 16 && nt >= 1024) : (ci <= 32 && cj <= 32 && nt >= 1024);
+            if (fast) {
+                const int ti = DIM == 3 ? (tid & 7) : (tid & 31);
+                const int tj = DIM == 3 ? ((tid >> 3) & 7) : (tid >> 5);
+                const int tk = DIM == 3 ? (tid >> 6) : 0;
+                if (ti < ci && tj < cj && tk < ck) {
+                    const int p = (int)G.at(fi + 2 * ti, fj + 2 * tj, DIM == 3 ? fk + 2 * tk : 0);
+                    const double res = stencil_fma<DIM, NPTS>(x, p, G, t.S);
+                    x[p] = fma(t.wd, scr[p] - res, x[p]);
+                }
+            } else {
+                for (int q = tid; q < ci * cj * ck; q += nt) {
+                    const int i = fi + 2 * (q % ci), r = q / ci;
+                    const int j = fj + 2 * (r % cj), k = DIM == 3 ? fk + 2 * (r / cj) : 0;
+                    const long long p = G.at(i, j, k);
+                    const double res = stencil_fma<DIM, NPTS>(x, p, G, t.S);
+                    x[p] = fma(t.wd, scr[p] - res, x[p]);
+                }
             }
             __syncthreads();
         }
