@@ -63,7 +63,11 @@ struct Op {
     int prolong = 0;  // z-sweep with fused prolongate-add of the coarser level's x
     int lr_next = 0;       // sweep on a small low-rank level: the patch of the next op, fused (LR_NEXT_*)
     uint32_t lr_next_tag = 0;
-    int lr_skip_patch = 0;  // this op's low-rank patch was done by the previous sweep's kernel
+    int lr_skip_patch = 0;  // this op's low-rank patch was done by an earlier op's kernel
+    int lr_post_patch = 0;  // OP_RESIDUAL_RESTRICT: the restore of f also patches the level's first post-sweep
+    uint32_t lr_post_tag = 0;
+    int lr_coarse_patch = 0;  // OP_RESIDUAL_RESTRICT: ... and the coarse level's first pre-sweep
+    uint32_t lr_coarse_tag = 0;
     int tail = -1;           // OP_TAIL: index into mgmc_handle::tail_args
     int restrict_fused = 0;  // OP_SWEEP: also does the following residual + restriction (k_zsweep_res7);
                              // OP_RESIDUAL_RESTRICT: done by the previous sweep (no launch)
@@ -663,6 +667,38 @@ void lr_small(const mgmc_handle* h, const Level& lv, double* x, int direction, i
     hipLaunchKernelGGL(k_lr_small, dim3(1), dim3(1024), 0, s, a);
 }
 
+LRJob lr_job(const Level& lv, int restore, int noise, uint32_t tag) {
+    const LowRankDev& r = lv.lr;
+    LRJob j;
+    j.m = r.m;
+    j.nrows = r.nrows;
+    j.off = r.rows_off;
+    j.coef = r.rows_coef;
+    j.mask = r.rows_mask;
+    j.sq = r.sq;
+    j.tag = tag;
+    j.f = lv.f;
+    j.save = r.save;
+    j.restore = restore;
+    j.noise = noise;
+    return j;
+}
+
+// after a residual + restriction of a low-rank level: restore f (+ the patch of the first
+// post-sweep) and the coarse level's first pre-sweep patch in one launch (k_lr_restore_patch)
+void lr_restore_patch(const mgmc_handle* h, const Op& op, const Level& lv, const Level& lc, const uint64_t* sample,
+                      hipStream_t s) {
+    LRRestorePatchArgs a;
+    a.job[0] = lr_job(lv, 1, op.lr_post_patch, op.lr_post_tag);
+    a.job[1] = op.lr_coarse_patch ? lr_job(lc, 0, 1, op.lr_coarse_tag) : lr_job(lc, 0, 0, 0);
+    if (!op.lr_coarse_patch) a.job[1].nrows = 0;
+    a.nb0 = (a.job[0].nrows + 255) / 256;
+    const int nb = a.nb0 + (a.job[1].nrows + 255) / 256;
+    a.key = h->key;
+    a.sample = sample;
+    if (nb > 0) hipLaunchKernelGGL(k_lr_restore_patch, dim3(nb), dim3(256), 0, s, a);
+}
+
 void lr_restore(const Level& lv, double* f, hipStream_t s) {
     const LowRankDev& r = lv.lr;
     if (r.nrows == 0) return;
@@ -837,6 +873,34 @@ void build_ops(mgmc_handle* h) {
             nx.lr_skip_patch = 1;
         }
     }
+    // low-rank levels: the restore after a residual + restriction also patches f for the level's
+    // first post-sweep (nothing writes f in between: the ops of coarser levels and this level's
+    // prolongation touch only coarser f and this level's x) and for the coarse level's first
+    // pre-sweep -- one launch instead of three
+    if (getenv("MGMC_LR_NO_MERGE") == nullptr)
+        for (size_t q = 0; q < h->ops.size(); ++q) {
+            Op& op = h->ops[q];
+            const int l = op.level;
+            if (op.kind != OP_RESIDUAL_RESTRICT || op.restrict_fused || h->levels[l].lr.m == 0) continue;
+            if (q + 1 < h->ops.size()) {
+                Op& nx = h->ops[q + 1];
+                if (nx.kind == OP_SWEEP && nx.level == l + 1 && h->levels[l + 1].lr.m > 0 && !nx.lr_skip_patch) {
+                    op.lr_coarse_patch = 1;
+                    op.lr_coarse_tag = nx.tag;
+                    nx.lr_skip_patch = 1;
+                }
+            }
+            for (size_t r = q + 1; r < h->ops.size(); ++r) {
+                Op& o = h->ops[r];
+                if (o.level > l || (o.kind == OP_PROLONGATE && o.level == l)) continue;
+                if (o.kind == OP_SWEEP && o.level == l && !o.lr_skip_patch) {
+                    op.lr_post_patch = 1;
+                    op.lr_post_tag = o.tag;
+                    o.lr_skip_patch = 1;
+                }
+                break;
+            }
+        }
 }
 
 // ---- the coarsest levels' sub-cycle in one workgroup (k_tail) ----
@@ -1033,7 +1097,10 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                     lr_patch(h, lv, LR_PATCH_RESIDUAL, lv.f, 0, sample, s);
                 }
                 launch_residual_restrict(lv, lc, lv.buf(op.src), lv.f, lc.f, lc.x, 1, s);
-                if (lr) lr_restore(lv, lv.f, s);
+                if (lr && (op.lr_post_patch || op.lr_coarse_patch))
+                    lr_restore_patch(h, op, lv, lc, sample, s);
+                else if (lr)
+                    lr_restore(lv, lv.f, s);
                 break;
             }
             case OP_PROLONGATE: {

@@ -183,6 +183,72 @@ __global__ void __launch_bounds__(256) k_lr_restore(int n, const long long* __re
     if (u < n) f[off[u]] = save[u];
 }
 
+// ---- after a residual + restriction: every f update until the level's next sweeps, one launch ----
+// Job 0 (the fine level of the restriction): restore f, and with `noise` set patch it at once with
+// the noise of its first post-sweep -- f is not touched again before that sweep (the coarse-grid
+// correction writes only coarser f and this level's x), and save[] already holds the true f, so
+// the patched values equal the separate restore + k_lr_patch bit for bit.  Job 1 (the coarse level):
+// the noise patch of its first pre-sweep (k_lr_patch, LR_PATCH_NOISE).  Blocks [0, nb0) run job 0.
+struct LRJob {
+    int m, nrows;
+    const long long* off;
+    const double* coef;
+    const uint64_t* mask;
+    const double* sq;
+    uint32_t tag;
+    double* f;
+    double* save;
+    int restore;  // 1: f = save (+ noise)
+    int noise;    // 1: + B Sigma^{-1/2} xi'
+};
+
+struct LRRestorePatchArgs {
+    LRJob job[2];
+    int nb0;
+    RngKey key;
+    const uint64_t* sample;
+};
+
+__global__ void __launch_bounds__(256) k_lr_restore_patch(LRRestorePatchArgs a) {
+    __shared__ double s[LR_MAX_M];
+    const bool second = (int)blockIdx.x >= a.nb0;
+    const LRJob& j = a.job[second ? 1 : 0];
+    const int u = (second ? (int)blockIdx.x - a.nb0 : (int)blockIdx.x) * blockDim.x + threadIdx.x;
+    if (j.noise) {
+        const int t = threadIdx.x;
+        if (2 * t < j.m) {
+            const uint64_t sample = *a.sample;
+            const Philox4 r =
+                philox4x32_10(LR_PAIR0 + (uint32_t)t, j.tag, (uint32_t)sample, (uint32_t)(sample >> 32), a.key.k0,
+                              a.key.k1);
+            double z0, z1;
+            normal_pair(r, &z0, &z1);
+            s[2 * t] = j.sq[2 * t] * z0;
+            if (2 * t + 1 < j.m) s[2 * t + 1] = j.sq[2 * t + 1] * z1;
+        }
+        __syncthreads();
+    }
+    if (u >= j.nrows) return;
+    const long long p = j.off[u];
+    if (!j.noise) {
+        j.f[p] = j.save[u];
+        return;
+    }
+    const uint64_t msk = j.mask[u];
+    const double* cf = j.coef + (long long)u * j.m;
+    double e = 0.0;
+    for (int k = 0; k < j.m; ++k)
+        if ((msk >> k) & 1) e = e + cf[k] * s[k];
+    double y;
+    if (j.restore) {
+        y = j.save[u];
+    } else {
+        y = j.f[p];
+        j.save[u] = y;
+    }
+    j.f[p] = y + e;
+}
+
 // ---- one workgroup for everything between two sweeps of a level with a small low-rank part ----
 // (every column sparse with <= LR_BLK entries, few B_bar rows): the fix after a sweep, the restore
 // of f, and the patch the next op of the level needs (noise of the next sweep, or the posterior
