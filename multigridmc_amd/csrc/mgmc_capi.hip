@@ -106,6 +106,9 @@ struct LowRankDev {
     double* part = nullptr;        // block partials
     double* w = nullptr;           // m-vector of dots
     bool small = false;            // k_lr_small path (sparse columns, one block each, few rows)
+    int* t_ent_off = nullptr;      // the same offsets in k_tail's LDS layout (small levels)
+    int* t_rows_off = nullptr;
+    int* t_bar_off[2] = {nullptr, nullptr};
     std::vector<void*> allocs;
 };
 
@@ -935,8 +938,9 @@ int tail_start_by_size(const std::vector<LevelSpec>& specs, const mgmc_config& c
 }
 
 // smallest level lt >= 1 whose levels lt .. L-1 all fit one workgroup's LDS (x, f per level + one
-// scratch of the largest): Galerkin levels, no low-rank part, ordinary (in-place) sweeps, SSOR coarse
-// sampler; -1 if none or only the coarsest level fits (the coarse LDS kernel covers that)
+// scratch of the largest + saved f on the rows of B): Galerkin levels, no low-rank part or a small
+// one (k_lr_small's), ordinary (in-place) sweeps, SSOR coarse sampler; -1 if none or only the
+// coarsest level fits (the coarse LDS kernel covers that)
 int tail_level(const mgmc_handle* h) {
     if (getenv("MGMC_NO_TAIL") != nullptr || h->cfg.coarse_solver != MGMC_COARSE_SSOR) return -1;
     const int L = (int)h->levels.size();
@@ -945,9 +949,9 @@ int tail_level(const mgmc_handle* h) {
         size_t tot = 0, vmax = 0;
         for (int l = lt; l < L && ok; ++l) {
             const Level& lv = h->levels[l];
-            ok = lv.lr.m == 0 && !lv.pingpong() && lv.spec.npoints == (lv.spec.dim == 3 ? 27 : 9);
+            ok = (lv.lr.m == 0 || lv.lr.small) && !lv.pingpong() && lv.spec.npoints == (lv.spec.dim == 3 ? 27 : 9);
             const size_t v = (size_t)tail_layout(lv.L).nstore;
-            tot += 2 * v;
+            tot += 2 * v + (size_t)lv.lr.nrows;
             vmax = std::max(vmax, v);
         }
         if (ok && (tot + vmax) * sizeof(double) <= TAIL_LDS_LIMIT) return lt;
@@ -1016,11 +1020,37 @@ int build_tails(mgmc_handle* h) {
             tl.sd = g.sd;
             tl.wd = g.wd;
             tl.S = lv.S;
+            const LowRankDev& r = lv.lr;
+            tl.m = r.m;
+            if (r.m > 0) {
+                tl.nrows = r.nrows;
+                tl.meta = r.meta;
+                tl.ent_off = r.t_ent_off;
+                tl.ent_val = r.ent_val;
+                tl.sc_one = r.sc_one;
+                tl.sc_inv = r.sc_inv;
+                tl.sq = r.sq;
+                for (int d = 0; d < 2; ++d) {
+                    tl.nbar[d] = r.nbar[d];
+                    tl.bar_off[d] = r.t_bar_off[d];
+                    tl.bar_val[d] = r.bar_val[d];
+                }
+                tl.rows_off = r.t_rows_off;
+                tl.coef = r.rows_coef;
+                tl.mask = r.rows_mask;
+            }
         }
         int vmax = 0;
         for (int l = 0; l < A.nlev; ++l) vmax = std::max(vmax, (int)A.lv[l].G.nstore);
         A.oscr = off;
-        A.lds_doubles = off + vmax;
+        off += vmax;
+        for (int l = 0; l < A.nlev; ++l) {
+            A.lv[l].osave = off;
+            off += A.lv[l].m > 0 ? A.lv[l].nrows : 0;
+        }
+        A.lds_doubles = off;
+        // the tail patches level lt's f itself: the restriction before it must not
+        if (!out.empty() && out.back().kind == OP_RESIDUAL_RESTRICT) out.back().lr_coarse_patch = 0;
         A.alpha = h->cfg.coarse_scaling;
         A.key = h->key;
         A.sample = h->ctrl;
@@ -1952,14 +1982,16 @@ int mgmc_solve(mgmc_handle* h, int method, const double* b, double* x, double rt
 
 namespace {
 
-long long ref_to_padded(const Level& lv, long long row) {
+long long ref_to_layout(const Level& lv, const Layout& L, long long row) {
     const long long nxi = lv.L.nx - 1, nyi = lv.L.ny - 1;
     const int i = (int)(row % nxi) + 1;
     const long long r = row / nxi;
     const int j = (int)(r % nyi) + 1;
     const int k = lv.spec.dim == 3 ? (int)(r / nyi) + 1 : 0;
-    return lv.L.at(i, j, k);
+    return L.at(i, j, k);
 }
+long long ref_to_padded(const Level& lv, long long row) { return ref_to_layout(lv, lv.L, row); }
+int ref_to_tail(const Level& lv, long long row) { return (int)ref_to_layout(lv, tail_layout(lv.L), row); }
 
 template <class T>
 int lr_to_device(mgmc_handle* h, LowRankDev& r, T** dst, const std::vector<T>& src) {
@@ -2015,6 +2047,7 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
     std::vector<LRColMeta> meta(m);
     std::vector<int> blk_col;
     std::vector<long long> ent_off;
+    std::vector<int> t_ent_off;
     std::vector<double> ent_val;
     int ndense = 0;
     for (int k = 0; k < m; ++k) {
@@ -2033,13 +2066,15 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
             mt.ent0 = (long long)ent_off.size();
             for (const auto& e : c.ent) {
                 ent_off.push_back(ref_to_padded(lv, e.first));
+                t_ent_off.push_back(ref_to_tail(lv, e.first));
                 ent_val.push_back(e.second);
             }
         }
     }
     r.nblk = (int)blk_col.size();
     if ((rc = lr_to_device(h, r, &r.meta, meta)) || (rc = lr_to_device(h, r, &r.blk_col, blk_col)) ||
-        (rc = lr_to_device(h, r, &r.ent_off, ent_off)) || (rc = lr_to_device(h, r, &r.ent_val, ent_val)))
+        (rc = lr_to_device(h, r, &r.ent_off, ent_off)) || (rc = lr_to_device(h, r, &r.ent_val, ent_val)) ||
+        (rc = lr_to_device(h, r, &r.t_ent_off, t_ent_off)))
         return rc;
     if (ndense > 0) {
         const size_t bytes = (size_t)ndense * lv.L.nstore * sizeof(double);
@@ -2060,10 +2095,12 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
         for (const auto& e : c.ent) slot[e.first] = 0;
     int nrows = 0;
     std::vector<long long> rows_off;
+    std::vector<int> t_rows_off;
     for (long long i = 0; i < N; ++i)
         if (slot[i] == 0) {
             slot[i] = nrows++;
             rows_off.push_back(ref_to_padded(lv, i));
+            t_rows_off.push_back(ref_to_tail(lv, i));
         }
     std::vector<double> coef((size_t)nrows * m, 0.0);
     std::vector<uint64_t> mask(nrows, 0);
@@ -2082,7 +2119,7 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
     if ((rc = lr_to_device(h, r, &r.rows_off, rows_off)) || (rc = lr_to_device(h, r, &r.rows_coef, coef)) ||
         (rc = lr_to_device(h, r, &r.rows_mask, mask)) || (rc = lr_to_device(h, r, &r.save, zeros)) ||
         (rc = lr_to_device(h, r, &r.sc_one, sc_one)) || (rc = lr_to_device(h, r, &r.sc_inv, sc_inv)) ||
-        (rc = lr_to_device(h, r, &r.sq, sq)))
+        (rc = lr_to_device(h, r, &r.sq, sq)) || (rc = lr_to_device(h, r, &r.t_rows_off, t_rows_off)))
         return rc;
     std::vector<double> partz(std::max(r.nblk, 1), 0.0), wz(m, 0.0);
     if ((rc = lr_to_device(h, r, &r.part, partz)) || (rc = lr_to_device(h, r, &r.w, wz))) return rc;
@@ -2112,6 +2149,7 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
         if (!lr_small_inverse(M, m, Minv))
             return fail(h, MGMC_E_INVALID, "Sigma + B^T (L + D/omega)^{-1} B is singular");
         std::vector<long long> boff;
+        std::vector<int> t_boff;
         std::vector<double> bval;
         for (long long i = 0; i < N; ++i) {
             const double* yi = &Y[(size_t)i * m];
@@ -2119,6 +2157,7 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
             for (int l = 0; l < m; ++l) nz = nz || yi[l] != 0.0;
             if (!nz) continue;  // B_bar row is exactly zero: x - 0 = x
             boff.push_back(ref_to_padded(lv, i));
+            t_boff.push_back(ref_to_tail(lv, i));
             for (int k = 0; k < m; ++k) {
                 double u = 0.0;
                 for (int l = 0; l < m; ++l) u = std::fma(yi[l], Minv[(size_t)l * m + k], u);
@@ -2126,7 +2165,9 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
             }
         }
         r.nbar[d] = (int)boff.size();
-        if ((rc = lr_to_device(h, r, &r.bar_off[d], boff)) || (rc = lr_to_device(h, r, &r.bar_val[d], bval))) return rc;
+        if ((rc = lr_to_device(h, r, &r.bar_off[d], boff)) || (rc = lr_to_device(h, r, &r.bar_val[d], bval)) ||
+            (rc = lr_to_device(h, r, &r.t_bar_off[d], t_boff)))
+            return rc;
     }
     bool small = getenv("MGMC_LR_NO_SMALL") == nullptr && ndense == 0 && r.nrows <= (1 << 16) &&
                  r.nbar[0] <= (1 << 16) && r.nbar[1] <= (1 << 16);

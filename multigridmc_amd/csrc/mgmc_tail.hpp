@@ -18,10 +18,17 @@
 //    at every fine vertex, then f_c = sum over (sz, sy, sx) of (1 w1(sx) w1(sy) w1(sz)) r, x_c = 0;
 //  * prolongate-add (k_prolongate_pairs): x += (alpha w) x_c over the interior parents in ascending
 //    coarse order.
+//  * low-rank levels (posterior Q = A + B Sigma^{-1} B^T with small sparse columns, the k_lr_small
+//    path): before a sweep f += B Sigma^{-1/2} xi' on the rows of B (k_lr_patch / k_lr_small noise),
+//    after it w = B^T x by one wavefront per column (lr_wave_dot's order) and x -= B_bar w, f restored;
+//    before a residual f -= B (Sigma^{-1} B^T x), restored after the restriction
+//    (sor_sampler.cc:48-56, sor_smoother.cc:41-53, linear_operator.hh:66-76).
 // LDS layout per level: the (nx+1)(ny+1)(nz+1) vertices including the zero boundary, x fastest, no
-// padding; one scratch array (right hand sides / residuals) of the largest tail level.
+// padding; one scratch array (right hand sides / residuals) of the largest tail level; the saved f
+// on the rows of B of every low-rank level.
 #pragma once
 #include "mgmc_kernels.hpp"
+#include "mgmc_lowrank.hpp"
 
 namespace mgmc {
 
@@ -43,6 +50,20 @@ struct TailLevel {
     int ncolours;
     double sd, wd; // sqrt(diag (2-omega)/omega), omega/diag
     StencilArg S;
+    // low-rank part (m = 0: none); every offset in the LDS layout G
+    int m, nrows, osave;
+    int nbar[2];
+    const LRColMeta* meta;
+    const int* ent_off;
+    const double* ent_val;
+    const double* sc_one;
+    const double* sc_inv;
+    const double* sq;
+    const int* bar_off[2];
+    const double* bar_val[2];
+    const int* rows_off;
+    const double* coef;
+    const uint64_t* mask;
 };
 
 struct TailArgs {
@@ -68,6 +89,46 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
     const uint64_t sample = *A->sample;
     const uint32_t s_lo = (uint32_t)sample, s_hi = (uint32_t)(sample >> 32);
     double* scr = lds + A->oscr;
+
+    __shared__ double lr_s[LR_MAX_M];
+    const int wave = tid >> 6, lane = tid & 63, nwave = nt >> 6;
+    // w_k = sc_k (B^T x)_k, one wavefront per column (lr_wave_dot with LDS offsets)
+    auto lr_dots = [&](const TailLevel& t, const double* sc, const double* x) {
+        for (int k = wave; k < t.m; k += nwave) {
+            const LRColMeta c = t.meta[k];
+            const double sk = sc[k];
+            double acc = 0.0;
+            for (int e = lane; e < (int)c.n; e += 64) {
+                const long long q = c.ent0 + e;
+                acc = acc + (sk * t.ent_val[q]) * x[t.ent_off[q]];
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+            double tot = lane == 0 ? 0.0 + acc : 0.0;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) tot = tot + __shfl_xor(tot, off, 64);
+            if (lane == 0) lr_s[k] = tot;
+        }
+    };
+    // f on the rows of B: save it, then f + B s (sign +1) or f - B s (sign -1), s = lr_s
+    auto lr_patch_rows = [&](const TailLevel& t, double* f, int sign) {
+        double* save = lds + t.osave;
+        for (int u = tid; u < t.nrows; u += nt) {
+            const int p = t.rows_off[u];
+            const uint64_t msk = t.mask[u];
+            const double* cf = t.coef + (long long)u * t.m;
+            double e = 0.0;
+            for (int k = 0; k < t.m; ++k)
+                if ((msk >> k) & 1) e = e + cf[k] * lr_s[k];
+            const double y = f[p];
+            save[u] = y;
+            f[p] = sign > 0 ? y + e : y - e;
+        }
+    };
+    auto lr_restore_rows = [&](const TailLevel& t, double* f) {
+        const double* save = lds + t.osave;
+        for (int u = tid; u < t.nrows; u += nt) f[t.rows_off[u]] = save[u];
+    };
 
     // interior vertex q of a level -> (i, j, k)
     auto coords = [](const Layout& G, int q, int& i, int& j, int& k) {
@@ -95,7 +156,19 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
     auto sweep = [&](const TailLevel& t, int dir, uint32_t tag) {
         const Layout& G = t.G;
         double* x = lds + t.ox;
-        const double* f = lds + t.of;
+        double* f = lds + t.of;
+        if (t.m > 0) {  // f += B Sigma^{-1/2} xi' (the sweep's m extra normals)
+            if (2 * tid < t.m) {
+                const Philox4 r = philox4x32_10(LR_PAIR0 + (uint32_t)tid, tag, s_lo, s_hi, A->key.k0, A->key.k1);
+                double z0, z1;
+                normal_pair(r, &z0, &z1);
+                lr_s[2 * tid] = t.sq[2 * tid] * z0;
+                if (2 * tid + 1 < t.m) lr_s[2 * tid + 1] = t.sq[2 * tid + 1] * z1;
+            }
+            __syncthreads();
+            lr_patch_rows(t, f, 1);
+            __syncthreads();
+        }
         const int npair = G.nx / 2;
         const int nrow = (G.ny - 1) * (DIM == 3 ? G.nz - 1 : 1);
         for (int q = tid; q < npair * nrow; q += nt) {
@@ -142,6 +215,22 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             }
             __syncthreads();
         }
+        if (t.m > 0) {  // x -= B_bar (B^T x), f restored
+            lr_dots(t, t.sc_one, x);
+            lr_restore_rows(t, f);
+            __syncthreads();
+            const int d = dir == 1 ? 0 : 1;
+            const int* boff = t.bar_off[d];
+            const double* bval = t.bar_val[d];
+            for (int u = tid; u < t.nbar[d]; u += nt) {
+                const double* bv = bval + (long long)u * t.m;
+                double acc = 0.0;
+                for (int k = 0; k < t.m; ++k) acc = fma(bv[k], lr_s[k], acc);
+                const int p = boff[u];
+                x[p] = x[p] - acc;
+            }
+            __syncthreads();
+        }
     };
 
     for (int o = 0; o < A->nops; ++o) {
@@ -155,8 +244,14 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             const TailLevel& c = A->lv[op.level + 1];
             const Layout& G = t.G;
             const double* x = lds + t.ox;
-            const double* f = lds + t.of;
+            double* f = lds + t.of;
             const int nd = ndof_of(G);
+            if (t.m > 0) {  // r = (f - B Sigma^{-1} B^T x) - A x
+                lr_dots(t, t.sc_inv, x);
+                __syncthreads();
+                lr_patch_rows(t, f, -1);
+                __syncthreads();
+            }
             for (int q = tid; q < nd; q += nt) {
                 int i, j, k;
                 coords(G, q, i, j, k);
@@ -185,6 +280,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
                 lds[c.of + pc] = result;
                 lds[c.ox + pc] = 0.0;
             }
+            if (t.m > 0) lr_restore_rows(t, f);
             __syncthreads();
         } else {  // TAIL_PROLONG: x_l += alpha P x_{l+1}
             const TailLevel& c = A->lv[op.level + 1];

@@ -27,7 +27,12 @@ CONFIGS = {
     "3d_aniso_zres_points": ((256, 40, 48), dict(nlevel=2, omega=1.1), (0.0, 5, False)),
     "2d32_point_global_chol": ((32, 32), dict(nlevel=3, coarse_solver="Cholesky"), (0.0, 3, True)),
     "3d32_ball_chol_ssor": ((32, 32, 32), dict(nlevel=3, smoother="SSOR", coarse_solver="Cholesky"), (0.1, 2, False)),
+    # levels whose sub-cycle runs in one k_tail workgroup, low-rank part included
+    "3d32_points_tail_W": ((32, 32, 32), dict(nlevel=4, cycle=2, ncoarsesmooth=2), (0.0, 6, False)),
+    "3d48_ball_tail_ssor": ((48, 48, 48), dict(nlevel=4, smoother="SSOR"), (0.1, 3, False)),
+    "2d128_points_tail": ((128, 128), dict(nlevel=5), (0.0, 4, False)),
 }
+TAIL_CONFIGS = ["2d64_ball_ssor_W", "3d32_points_tail_W", "3d48_ball_tail_ssor", "2d128_points_tail"]
 
 
 def measured(shape, kappa_sq, radius, nmeas, glob, seed=1212417, scale=1e-3):
@@ -167,3 +172,23 @@ def test_posterior_statistics_vs_exact_covariance(hip_device, shape, kw, glob, n
     assert np.max(np.abs(ex - mu)) < 2 * tol * scale
     assert np.max(np.abs(cov - Qinv)) < tol * scale
     s.close()
+
+
+@pytest.mark.parametrize("name", TAIL_CONFIGS)
+def test_lowrank_tail_matches_separate_kernels(hip_device, name, monkeypatch):
+    """The coarse levels' sub-cycle in k_tail (low-rank patches, fix and residual in LDS) against the
+    oracle with the tail switched off and on: both bitwise."""
+    out = []
+    for env in ("MGMC_NO_TAIL", None):
+        if env:
+            monkeypatch.setenv(env, "1")
+        else:
+            monkeypatch.delenv("MGMC_NO_TAIL", raising=False)
+        s, mc, p, lat, op = make(name)
+        qoi = mg.measurement_vector_index(lat, [0.5] * lat.dim)
+        z = s.sample(5, qoi)
+        assert np.array_equal(z, mc.sample(5, qoi))
+        out.append(s.get_state())
+        assert np.array_equal(out[-1], mc.get_state())
+        s.close()
+    assert np.array_equal(out[0], out[1])
