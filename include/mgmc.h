@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MGMC_ABI_VERSION 1
+#define MGMC_ABI_VERSION 2
 
 /* error codes */
 #define MGMC_OK 0
@@ -53,16 +53,24 @@ extern "C" {
 
 /* coarse solvers (MultigridParameters::coarse_solver) */
 #define MGMC_COARSE_SSOR 0
-#define MGMC_COARSE_CHOLESKY 1 /* not on the device path yet -> MGMC_E_UNSUPPORTED */
+#define MGMC_COARSE_CHOLESKY 1 /* dense Cholesky factors of the coarsest level (cholesky_sampler.hh:50-66) */
+
+/* fine-level operators (driver_mgmc.cc:414-425, PriorParameters::pde_model) */
+#define MGMC_OPERATOR_FD 0  /* ShiftedLaplaceFDOperator: 5/7-point (shiftedlaplace_fd_operator.cc:9-57) */
+#define MGMC_OPERATOR_FEM 1 /* ShiftedLaplaceFEMOperator: Q1 elements, 9/27-point
+                               (shiftedlaplace_fem_operator.cc:9-145) */
 
 /* sweep directions (smoother/sor_smoother.hh:14-18) */
 #define MGMC_FORWARD 1
 #define MGMC_BACKWARD 2
 
 /* Plain-old-data configuration; mirrors the MultigridParameters / LatticeParameters /
- * ConstantCorrelationLengthModelParameters fields of auxilliary/parameters.hh that reach the
- * hot path.  The fine operator is ShiftedLaplaceFDOperator with constant kappa^2 = 1/Lambda^2
- * (linear_operator/shiftedlaplace_fd_operator.cc:9-57, correlationlength_model.hh:45-66). */
+ * ConstantCorrelationLengthModelParameters / PriorParameters fields of auxilliary/parameters.hh
+ * that reach the hot path.  The fine operator is ShiftedLaplaceFDOperator or
+ * ShiftedLaplaceFEMOperator with constant kappa^2 = 1/Lambda^2
+ * (linear_operator/shiftedlaplace_fd_operator.cc:9-57, shiftedlaplace_fem_operator.cc:9-145,
+ * correlationlength_model.hh:45-66).  Zero-initialise and set the fields: 0 in fine_operator is
+ * the FD operator. */
 typedef struct mgmc_config {
     int dim;            /* 2 or 3 */
     int nx, ny, nz;     /* cells per direction (nz ignored for dim=2) */
@@ -77,13 +85,15 @@ typedef struct mgmc_config {
     double omega;          /* overrelaxation factor of the Gibbs samplers */
     double coarse_scaling; /* factor on the prolongated coarse correction */
     double kappa_sq;       /* 1/Lambda^2 */
+    int fine_operator;     /* MGMC_OPERATOR_* (ABI 2) */
+    int pad_;
 } mgmc_config;
 
 /* Host-side description of one multigrid level (no device needed). */
 typedef struct mgmc_level_desc {
     int nx, ny, nz;       /* cells per direction on this level (nz = 0 for 2D) */
-    int npoints;          /* stencil points: 5/7 (fine FD) or 9/27 (Galerkin) */
-    int ncolours;         /* colours of the Gibbs sweep: 2 (fine) or 2^dim */
+    int npoints;          /* stencil points: 5/7 (fine FD) or 9/27 (fine FEM, Galerkin) */
+    int ncolours;         /* colours of the Gibbs sweep: 2 (5/7-point) or 2^dim (9/27-point) */
     int pad_;
     uint64_t ndof;        /* number of interior unknowns */
     /* stencil coefficients indexed by offset (dz+1)*9 + (dy+1)*3 + (dx+1) (3D) or

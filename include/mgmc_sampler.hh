@@ -46,8 +46,11 @@ struct MultigridParameters {
     int verbose = 0;
 };
 
-inline mgmc_config make_config(int dim, int nx, int ny, int nz, double kappa_sq, const MultigridParameters& p) {
+// fine_operator: MGMC_OPERATOR_FD (pdemodel "shiftedlaplace_fd") or MGMC_OPERATOR_FEM ("shiftedlaplace_fem")
+inline mgmc_config make_config(int dim, int nx, int ny, int nz, double kappa_sq, const MultigridParameters& p,
+                               int fine_operator = MGMC_OPERATOR_FD) {
     mgmc_config c{};
+    c.fine_operator = fine_operator;
     c.dim = dim;
     c.nx = nx;
     c.ny = ny;

@@ -17,6 +17,7 @@ from .sampler import (  # noqa: F401
     Lattice3d,
     MultigridMCSampler,
     ShiftedLaplaceFDOperator,
+    ShiftedLaplaceFEMOperator,
     comm_unique_id,
     describe,
     make_config,

@@ -22,6 +22,9 @@ SMOOTHER_SOR = 0
 SMOOTHER_SSOR = 1
 COARSE_SSOR = 0
 COARSE_CHOLESKY = 1
+OPERATOR_FD = 0
+OPERATOR_FEM = 1
+ABI_VERSION = 2
 SOLVER_LOOP = 0
 SOLVER_CG = 1
 FORWARD = 1
@@ -35,6 +38,7 @@ class MgmcConfig(ctypes.Structure):
         ("npresmooth", c_int), ("npostsmooth", c_int), ("ncoarsesmooth", c_int),
         ("smoother", c_int), ("coarse_solver", c_int), ("verbose", c_int),
         ("omega", c_double), ("coarse_scaling", c_double), ("kappa_sq", c_double),
+        ("fine_operator", c_int), ("pad_", c_int),
     ]
 
 
@@ -113,6 +117,8 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.mgmc_abi_version() != ABI_VERSION:  # the config struct layout changes with the ABI
+        raise ImportError(f"{p}: ABI {lib.mgmc_abi_version()}, this package needs {ABI_VERSION} (rebuild)")
     if path is None:
         _lib = lib
     return lib

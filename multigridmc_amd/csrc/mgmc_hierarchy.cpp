@@ -17,6 +17,93 @@ inline int sidx(int dim, int dx, int dy, int dz) {
     return dim == 3 ? (dz + 1) * 9 + (dy + 1) * 3 + (dx + 1) : (dy + 1) * 3 + (dx + 1);
 }
 
+// Q1 shape functions on the reference cell (shiftedlaplace_fem_operator.cc:148-187): a[j] = 0 is the
+// factor (1 - xhat_j), a[j] = 1 is xhat_j; products from 1.0 in dimension order
+double fem_phi(int dim, const int* a, const double* xh) {
+    double v = 1.0;
+    for (int j = 0; j < dim; ++j) v *= (a[j] == 0) ? (1.0 - xh[j]) : xh[j];
+    return v;
+}
+void fem_grad_phi(int dim, const int* a, const double* xh, double* g) {
+    for (int k = 0; k < dim; ++k) {
+        double v = 1.0;
+        for (int j = 0; j < dim; ++j) {
+            if (j == k)
+                v *= (a[j] == 0) ? -1.0 : +1.0;
+            else
+                v *= (a[j] == 0) ? (1.0 - xh[j]) : xh[j];
+        }
+        g[k] = v;
+    }
+}
+
+// Interior stencil of ShiftedLaplaceFEMOperator with constant kappa^2 (shiftedlaplace_fem_operator.cc
+// :9-145).  The reference assembles cell by cell (cells ascending, x fastest; basis pairs (alpha,
+// beta) in cartesian-product order, last dimension fastest), each entry starting from 0.0 and adding
+// local(alpha, beta) * cell_volume, local = sum_q (kappa^2 phi_a phi_b + grad phi_a . (h^-2 grad
+// phi_b)) w_q over the order-1 Gauss-Legendre points (quadrature.cc:11-55).  With constant kappa^2
+// every interior row receives the same terms in the same order, so one row (entry v -> v + s, the
+// cells c in {v-1, v}^d containing v + s, ascending) gives every row bit for bit; rows next to the
+// boundary are this stencil truncated (the columns of boundary vertices are never created).
+void fem_stencil(int dim, const int* n, double kappa_sq, double* st) {
+    double h[3] = {1, 1, 1}, hinv2[3] = {0, 0, 0};
+    double cell_volume = 1.0;
+    for (int d = 0; d < dim; ++d) {
+        h[d] = 1. / double(n[d]);
+        hinv2[d] = 1. / (h[d] * h[d]);
+        cell_volume *= h[d];
+    }
+    // quadrature: 2 points per dimension, cartesian product with the last dimension fastest
+    const double p1[2] = {-1.0 / sqrt(3.0), +1.0 / sqrt(3.0)};
+    const int nq = 1 << dim;
+    double qp[8][3], qw[8];
+    for (int q = 0; q < nq; ++q) {
+        double w = 1.0;
+        for (int j = 0; j < dim; ++j) {
+            const int b = (q >> (dim - 1 - j)) & 1;
+            w *= 0.5 * 1.0;
+            qp[q][j] = 0.5 * (p1[b] + 1.0);
+        }
+        qw[q] = w;
+    }
+    auto local = [&](const int* a, const int* b) {
+        double v = 0.0;
+        for (int q = 0; q < nq; ++q) {
+            const double pp = fem_phi(dim, a, qp[q]) * fem_phi(dim, b, qp[q]);
+            double ga[3] = {0, 0, 0}, gb[3] = {0, 0, 0};
+            fem_grad_phi(dim, a, qp[q], ga);
+            fem_grad_phi(dim, b, qp[q], gb);
+            double gg = ga[0] * (hinv2[0] * gb[0]);  // Eigen dot: ((t0 + t1) + t2)
+            for (int k = 1; k < dim; ++k) gg = gg + ga[k] * (hinv2[k] * gb[k]);
+            v += (kappa_sq * pp + gg) * qw[q];
+        }
+        return v;
+    };
+    for (int k = 0; k < 27; ++k) st[k] = 0.0;
+    const int zr = dim == 3 ? 1 : 0;
+    for (int sz = -zr; sz <= zr; ++sz)
+        for (int sy = -1; sy <= 1; ++sy)
+            for (int sx = -1; sx <= 1; ++sx) {
+                const int s[3] = {sx, sy, sz};
+                double acc = 0.0;
+                // cells c = v - alpha, alpha in {0,1}^d, ascending cell index (x fastest)
+                for (int cz = zr; cz >= 0; --cz)
+                    for (int cy = 1; cy >= 0; --cy)
+                        for (int cx = 1; cx >= 0; --cx) {
+                            const int alpha[3] = {cx, cy, cz};  // v - c
+                            int beta[3] = {0, 0, 0};
+                            bool ok = true;
+                            for (int d = 0; d < dim; ++d) {
+                                beta[d] = alpha[d] + s[d];
+                                ok = ok && beta[d] >= 0 && beta[d] <= 1;
+                            }
+                            if (!ok) continue;
+                            acc += local(alpha, beta) * cell_volume;
+                        }
+                st[sidx(dim, sx, sy, sz)] = acc;
+            }
+}
+
 }  // namespace
 
 std::string validate_config(const mgmc_config& c) {
@@ -41,6 +128,10 @@ std::string validate_config(const mgmc_config& c) {
     }
     if (!(c.omega > 0.0 && c.omega < 2.0)) return "omega must lie in (0,2)";
     if (!(c.kappa_sq >= 0.0)) return "kappa_sq must be >= 0";
+    if (c.fine_operator != MGMC_OPERATOR_FD && c.fine_operator != MGMC_OPERATOR_FEM) {
+        err << "Error: invalid prior '" << c.fine_operator << "'";  // driver_mgmc.cc:426-429
+        return err.str();
+    }
     int n[3] = {c.nx, c.ny, c.dim == 3 ? c.nz : 2};
     for (int d = 0; d < c.dim; ++d)
         if (n[d] < 2) return "every lattice extent must be >= 2";
@@ -138,6 +229,12 @@ std::vector<LevelSpec> build_hierarchy(const mgmc_config& c) {
     L.st[sidx(c.dim, 0, 0, 0)] = diagonal;
     L.npoints = 2 * c.dim + 1;
     L.ncolours = 2;
+    if (c.fine_operator == MGMC_OPERATOR_FEM) {
+        memset(L.st, 0, sizeof(L.st));
+        fem_stencil(c.dim, L.n, c.kappa_sq, L.st);
+        L.npoints = (c.dim == 3) ? 27 : 9;
+        L.ncolours = 1 << c.dim;
+    }
     for (int level = 0; level < c.nlevel; ++level) {
         L.ndof = 1;
         for (int d = 0; d < c.dim; ++d) L.ndof *= (uint64_t)(L.n[d] - 1);

@@ -15,8 +15,10 @@ a sparse Cholesky factorisation.  As in the reference, the "exact" observed stat
 refer to the measured (posterior) operator built on top of the chosen operator.
 
 Out of scope (not the device hot path): the Cholesky and SSOR samplers of the whole lattice
-(do_cholesky / do_ssor are reported and skipped), FEM / periodic-kappa priors and the VTK output
-of posterior_statistics.
+(do_cholesky / do_ssor are reported and skipped), the periodic-kappa correlation length model and
+the squared_shiftedlaplace_fd prior (neither is a constant 3^d-point stencil), and the VTK output of
+posterior_statistics.  pdemodel = "shiftedlaplace_fd" and "shiftedlaplace_fem" are both on the
+device path.
 """
 from __future__ import annotations
 
@@ -31,7 +33,7 @@ from .measured import MeasuredOperator, measurement_vector
 from .parameters import (ConstantCorrelationLengthModelParameters, GeneralParameters, LatticeParameters,
                          MeasurementParameters, MultigridParameters, PriorParameters, SamplingParameters,
                          read_config)
-from .sampler import Lattice, MultigridMCSampler, ShiftedLaplaceFDOperator
+from .sampler import Lattice, MultigridMCSampler, ShiftedLaplaceFDOperator, ShiftedLaplaceFEMOperator
 
 SEED = 5418513  # driver_mgmc.cc:448
 
@@ -232,11 +234,13 @@ def main(argv=None) -> int:
     if prior_params.correlationlength_model != "constant":
         print(f"Error: correlationlengthmodel '{prior_params.correlationlength_model}' is not on the device path")
         return -1
-    if prior_params.pde_model != "shiftedlaplace_fd":
+    # driver_mgmc.cc:414-429
+    prior_classes = {"shiftedlaplace_fd": ShiftedLaplaceFDOperator, "shiftedlaplace_fem": ShiftedLaplaceFEMOperator}
+    if prior_params.pde_model not in prior_classes:
         print(f"Error: prior '{prior_params.pde_model}' is not on the device path")
         return -1
     kappa_sq = ConstantCorrelationLengthModelParameters.from_config(cfg).kappa_sq
-    prior = ShiftedLaplaceFDOperator(lattice, kappa_sq)
+    prior = prior_classes[prior_params.pde_model](lattice, kappa_sq)
     posterior = MeasuredOperator(prior, measurement_params)
     if general.operator_name == "prior":
         linear_operator = prior

@@ -104,6 +104,17 @@ class ShiftedLaplaceFDOperator:
     def get_m_lowrank(self) -> int:
         return 0
 
+    fine_operator = _native.OPERATOR_FD
+
+
+class ShiftedLaplaceFEMOperator(ShiftedLaplaceFDOperator):
+    """Fine-level precision operator: Q1 finite elements for -div grad + kappa^2 with constant
+    kappa^2 (shiftedlaplace_fem_operator.cc:9-145).  Its interior stencil has 3^d points, so the
+    fine level is swept in 2^d colours like the Galerkin levels; R A_h R^T of it is the FEM
+    operator of the coarse lattice (test_intergrid.hh:179-206)."""
+
+    fine_operator = _native.OPERATOR_FEM
+
 
 def measurement_vector_index(lattice: Lattice, x0, radius: float = 0.0) -> int:
     """Index of the radius-0 measurement vector (measured_operator.cc:74-91): the interior vertex
@@ -142,6 +153,8 @@ def make_config(linear_operator: ShiftedLaplaceFDOperator, params: MultigridPara
     c.omega = params.omega
     c.coarse_scaling = params.coarse_scaling
     c.kappa_sq = linear_operator.kappa_sq
+    base = getattr(linear_operator, "base_operator", linear_operator)
+    c.fine_operator = getattr(base, "fine_operator", _native.OPERATOR_FD)
     return c
 
 

@@ -36,6 +36,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -234,6 +235,127 @@ static CSR fd_operator(const Lattice& lat, double kappa_sq) {
             A.val.push_back(e.second);
         }
         A.rowptr[ell + 1] = (int64_t)A.col.size();
+    }
+    return A;
+}
+
+// ShiftedLaplaceFEMOperator with constant kappa^2 (shiftedlaplace_fem_operator.cc:9-145): sparsity
+// of every valid 3^d shift (STEP 1, entries 0.0), then the cell loop (STEP 2): cells ascending (x
+// fastest), basis pairs (alpha, beta) in cartesian_product order (common.hh:29-50: last dimension
+// fastest), each entry += local * cell_volume with local = sum_q (kappa^2 phi_a phi_b + grad phi_a .
+// (h^-2 grad phi_b)) w_q over GaussLegendreQuadrature(dim, 1) (quadrature.cc:11-55).
+static CSR fem_operator(const Lattice& lat, double kappa_sq) {
+    const int dim = lat.dim;
+    double h[3] = {1, 1, 1}, hinv2[3] = {0, 0, 0};
+    double cell_volume = 1.0;
+    for (int d = 0; d < dim; ++d) {
+        h[d] = 1. / double(lat.n[d]);
+        hinv2[d] = 1. / (h[d] * h[d]);
+        cell_volume *= h[d];
+    }
+    const int nb = 1 << dim;  // basis functions / quadrature points per cell
+    // cartesian products, last dimension fastest
+    auto bits = [&](int q, int* b) {
+        for (int j = 0; j < dim; ++j) b[j] = (q >> (dim - 1 - j)) & 1;
+    };
+    const double p1[2] = {-1.0 / sqrt(3.0), +1.0 / sqrt(3.0)};
+    std::vector<double> qw(nb), qp((size_t)nb * 3, 0.0);
+    for (int q = 0; q < nb; ++q) {
+        int b[3];
+        bits(q, b);
+        double w = 1.0;
+        for (int j = 0; j < dim; ++j) {
+            w *= 0.5 * 1.0;
+            qp[(size_t)q * 3 + j] = 0.5 * (p1[b[j]] + 1.0);
+        }
+        qw[q] = w;
+    }
+    auto phi = [&](const int* a, const double* x) {
+        double v = 1.0;
+        for (int j = 0; j < dim; ++j) v *= (a[j] == 0) ? (1.0 - x[j]) : x[j];
+        return v;
+    };
+    auto grad = [&](const int* a, const double* x, double* g) {
+        for (int k = 0; k < dim; ++k) {
+            double v = 1.0;
+            for (int j = 0; j < dim; ++j) v *= (j == k) ? ((a[j] == 0) ? -1.0 : +1.0) : ((a[j] == 0) ? (1.0 - x[j]) : x[j]);
+            g[k] = v;
+        }
+    };
+    // phi_phi / gradphi_gradphi tables in the reference's (alpha, beta, q) order
+    std::vector<double> pp, gg;
+    for (int ia = 0; ia < nb; ++ia)
+        for (int ib = 0; ib < nb; ++ib)
+            for (int q = 0; q < nb; ++q) {
+                int a[3] = {0, 0, 0}, b[3] = {0, 0, 0};
+                bits(ia, a);
+                bits(ib, b);
+                const double* x = &qp[(size_t)q * 3];
+                pp.push_back(phi(a, x) * phi(b, x));
+                double ga[3] = {0, 0, 0}, gb[3] = {0, 0, 0};
+                grad(a, x, ga);
+                grad(b, x, gb);
+                double t = ga[0] * (hinv2[0] * gb[0]);
+                for (int k = 1; k < dim; ++k) t = t + ga[k] * (hinv2[k] * gb[k]);
+                gg.push_back(t);
+            }
+    // STEP 1: sparsity, columns ascending
+    CSR A;
+    const int64_t nrow = lat.nvertex();
+    A.nrow = A.ncol = nrow;
+    A.rowptr.assign(nrow + 1, 0);
+    const int zr = dim == 3 ? 1 : 0;
+    for (int64_t ell = 0; ell < nrow; ++ell) {
+        for (int sz = -zr; sz <= zr; ++sz)
+            for (int sy = (dim >= 2 ? -1 : 0); sy <= (dim >= 2 ? 1 : 0); ++sy)
+                for (int sx = -1; sx <= 1; ++sx) {
+                    const int sh[3] = {sx, sy, sz};
+                    int64_t e;
+                    if (lat.shifted(ell, sh, e)) {
+                        A.col.push_back((int32_t)e);
+                        A.val.push_back(0.0);
+                    }
+                }
+        A.rowptr[ell + 1] = (int64_t)A.col.size();
+    }
+    auto entry = [&](int64_t r, int64_t c) -> double& {
+        for (int64_t k = A.rowptr[r]; k < A.rowptr[r + 1]; ++k)
+            if (A.col[k] == c) return A.val[k];
+        fprintf(stderr, "fem_operator: missing entry\n");
+        abort();
+    };
+    // STEP 2: cells ascending, cell coordinate x fastest (lattice3d.hh:83-91)
+    int64_t ncell = 1;
+    for (int d = 0; d < dim; ++d) ncell *= lat.n[d];
+    for (int64_t cell = 0; cell < ncell; ++cell) {
+        int cc[3] = {0, 0, 0};
+        int64_t r = cell;
+        for (int d = 0; d < dim; ++d) {
+            cc[d] = (int)(r % lat.n[d]);
+            r /= lat.n[d];
+        }
+        int count = 0;
+        for (int ia = 0; ia < nb; ++ia)
+            for (int ib = 0; ib < nb; ++ib) {
+                int a[3] = {0, 0, 0}, b[3] = {0, 0, 0};
+                bits(ia, a);
+                bits(ib, b);
+                int va[3] = {0, 0, 0}, vb[3] = {0, 0, 0};
+                for (int d = 0; d < dim; ++d) {
+                    va[d] = cc[d] + a[d];
+                    vb[d] = cc[d] + b[d];
+                }
+                if (lat.interior(va) && lat.interior(vb)) {
+                    double local = 0.0;
+                    for (int q = 0; q < nb; ++q) {
+                        local += (kappa_sq * pp[count] + gg[count]) * qw[q];
+                        count++;
+                    }
+                    entry(lat.euc2lin(va), lat.euc2lin(vb)) += local * cell_volume;
+                } else {
+                    count += nb;
+                }
+            }
     }
     return A;
 }
@@ -505,6 +627,12 @@ struct Ctx {
     uint64_t sample = 0;  // multicolour: sample index of the current cycle
     uint32_t tag = 0;     // multicolour: running sweep tag within the current cycle
 };
+
+static int64_t max_row_nnz(const CSR& A) {
+    int64_t m = 0;
+    for (int64_t r = 0; r < A.nrow; ++r) m = std::max(m, A.rowptr[r + 1] - A.rowptr[r]);
+    return m;
+}
 
 static void init_colouring(Level& L, bool fd_level) {
     const int64_t n = L.lat.nvertex();
@@ -958,7 +1086,8 @@ struct MGMC : Sampler {
             std::unique_ptr<Level> L(new Level());
             L->lat = lattice;
             L->A = A;
-            if (lattice.dim >= 2) init_colouring(*L, level == 0);
+            // 2 colours for a 5/7-point fine level (FD), 2^d for 3^d-point levels (FEM, Galerkin)
+            if (lattice.dim >= 2) init_colouring(*L, level == 0 && max_row_nnz(L->A) <= 2 * lattice.dim + 1);
             x_ell.emplace_back(L->A.nrow, 0.0);
             f_ell.emplace_back(L->A.nrow, 0.0);
             r_ell.emplace_back(L->A.nrow, 0.0);
@@ -1079,6 +1208,23 @@ orc_handle* orc_create_fd(const orc_params* q, int mode, uint64_t seed, uint64_t
     const Lattice lat = make_lattice(q);
     CSR A = fd_operator(lat, q->kappa_sq);
     h->mg.reset(new MGMC(&h->ctx, to_params(q), lat, std::move(A), override_st));
+    h->f.assign(h->mg->x_ell[0].size(), 0.0);
+    h->x.assign(h->mg->x_ell[0].size(), 0.0);
+    return h;
+}
+
+// FEM shifted-Laplace prior (constant kappa^2); override_st as for orc_create_fd
+orc_handle* orc_create_fem(const orc_params* q, int mode, uint64_t seed, uint64_t chain, const double* override_st) {
+    orc_handle* h = new orc_handle();
+    h->ctx.mode = (Mode)mode;
+    h->ctx.rng.seed(seed);
+    h->ctx.seed = seed;
+    h->ctx.chain = chain;
+    const Lattice lat = make_lattice(q);
+    CSR A = fem_operator(lat, q->kappa_sq);
+    Params p = to_params(q);
+    p.galerkin = 0;
+    h->mg.reset(new MGMC(&h->ctx, p, lat, std::move(A), override_st));
     h->f.assign(h->mg->x_ell[0].size(), 0.0);
     h->x.assign(h->mg->x_ell[0].size(), 0.0);
     return h;

@@ -39,6 +39,7 @@ def lib():
         L = ctypes.CDLL(LIB)
         sigs = {
             "orc_create_fd": (c_void_p, [POINTER(OrcParams), c_int, c_uint64, c_uint64, _DP]),
+            "orc_create_fem": (c_void_p, [POINTER(OrcParams), c_int, c_uint64, c_uint64, _DP]),
             "orc_create_csr": (c_void_p, [POINTER(OrcParams), c_int, c_uint64, c_int64, POINTER(c_int64),
                                           POINTER(c_int32), _DP]),
             "orc_destroy": (None, [c_void_p]),
@@ -128,6 +129,20 @@ class Oracle:
             st = dp(override_stencils)
         h = lib().orc_create_fd(ctypes.byref(p), mode, seed, chain, st)
         return cls(h, p)
+
+    @classmethod
+    def fem(cls, shape, mg, kappa_sq, mode=FAITHFUL, seed=5418513, chain=0, override_stencils=None):
+        """ShiftedLaplaceFEMOperator prior (constant kappa^2); override_stencils replaces the
+        Galerkin stencils of levels >= 1 (multicolour replay of a device hierarchy)."""
+        p = params_struct(shape, mg, kappa_sq, 0)
+        st = None
+        if override_stencils is not None:
+            override_stencils = np.ascontiguousarray(override_stencils, dtype=np.float64)
+            st = dp(override_stencils)
+        h = lib().orc_create_fem(ctypes.byref(p), mode, seed, chain, st)
+        o = cls(h, p)
+        o._st = override_stencils  # keep the buffer alive
+        return o
 
     @classmethod
     def csr(cls, shape, mg, rowptr, col, val, mode=FAITHFUL, seed=0):

@@ -128,7 +128,8 @@ def test_posterior_qoi_mean_and_variance_at_128_cubed(hip_device):
     s.close()
 
 
-def test_driver_posterior_template_run(hip_device, tmp_path, monkeypatch):
+@pytest.mark.parametrize("pde", ["shiftedlaplace_fd", "shiftedlaplace_fem"])
+def test_driver_posterior_template_run(hip_device, tmp_path, monkeypatch, pde):
     """multigridmc_amd.driver on the reference's parameters_template.cfg / measurements_template.cfg
     (config 1: 2D posterior, 8 measurements, W-cycle), lattice 64^2 and shortened sampling: the
     timeseries and convergence files are written in the reference's formats, and the sample mean
@@ -142,6 +143,8 @@ def test_driver_posterior_template_run(hip_device, tmp_path, monkeypatch):
     text = re.sub(r"ny = 32;", "ny = 64;", text)
     text = re.sub(r"nsamples = 10000;", "nsamples = 20000;", text)
     text = re.sub(r"nsamples = 1000;", "nsamples = 200;", text)
+    text = re.sub(r'pdemodel = "shiftedlaplace_fd";', f'pdemodel = "{pde}";', text)
+    assert f'pdemodel = "{pde}";' in text
     (tmp_path / "parameters.cfg").write_text(text)
     (tmp_path / "measurements_template.cfg").write_text(open(os.path.join(gold, "measurements_template.cfg")).read())
     monkeypatch.chdir(tmp_path)
@@ -157,7 +160,8 @@ def test_driver_posterior_template_run(hip_device, tmp_path, monkeypatch):
     cfg = read_config(str(tmp_path / "parameters.cfg"))
     mp = MeasurementParameters.from_config(cfg, str(tmp_path))
     lat = mg.Lattice(64, 64)
-    op = mg.MeasuredOperator(mg.ShiftedLaplaceFDOperator(lat, 25.0), mp)
+    prior_cls = mg.ShiftedLaplaceFEMOperator if pde == "shiftedlaplace_fem" else mg.ShiftedLaplaceFDOperator
+    op = mg.MeasuredOperator(prior_cls(lat, 25.0), mp)
     s = mg.MultigridMCSampler(op, SEED, MultigridParameters.from_config(cfg))
     rows, vals = mg.measurement_vector(lat, mp.sample_location, mp.radius)
     mean_exact, var_exact = ExactTargets(s).observed_mean_and_variance(_measured_values(mp), rows, vals)
