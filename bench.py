@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--posterior", type=int, default=0, metavar="M",
                     help="BASELINE config 5: posterior operator with M point measurements (default lattice 256^3, "
                          "6 levels); not the headline line")
+    ap.add_argument("--fem", action="store_true",
+                    help="ShiftedLaplaceFEMOperator prior (27/9-point fine level); no CPU baseline")
     ap.add_argument("--radius", type=float, default=0.0, help="measurement radius (--posterior)")
     ap.add_argument("--measure-global", action="store_true", help="add the global average measurement (--posterior)")
     return ap.parse_args()
@@ -187,7 +189,8 @@ def main():
     if args.posterior and "--nlevel" not in sys.argv:
         nlevel = 6
     lat = mg.Lattice3d(n, n, n) if args.dim == 3 else mg.Lattice2d(n, n)
-    op = mg.ShiftedLaplaceFDOperator(lat, kappa_sq=1.0 / 0.2 ** 2)  # Lambda = 0.2 (parameters_template.cfg)
+    prior_cls = mg.ShiftedLaplaceFEMOperator if args.fem else mg.ShiftedLaplaceFDOperator
+    op = prior_cls(lat, kappa_sq=1.0 / 0.2 ** 2)  # Lambda = 0.2 (parameters_template.cfg)
     if args.posterior:
         op = posterior_operator(op, args.posterior, args.radius, args.measure_global)
     params = mg.MultigridParameters(nlevel=nlevel, smoother="SOR", coarse_solver="SSOR", npresmooth=1, npostsmooth=1,
@@ -233,7 +236,7 @@ def main():
             if os.path.exists(args.traffic_file):
                 try:
                     tj = json.load(open(args.traffic_file))
-                    if tj.get("n") == n and args.dim == 3:
+                    if tj.get("n") == n and args.dim == 3 and not args.fem:
                         traffic = tj.get("fine_sweep_hbm_bytes_per_launch")
                 except (OSError, ValueError):
                     traffic = None
@@ -242,7 +245,7 @@ def main():
                     "kernel": "fine-level (level 0) multicolour Gibbs sweep",
                     "bytes_per_launch": bytes_sweep, "avg_launch_ms": round(t_sweep * 1e3, 4)}
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and args.cpu_samples > 0:
+        if world == 1 and not args.no_cpu_baseline and args.cpu_samples > 0 and not args.fem:
             cpu = cpu_baseline(n, nlevel, args.cpu_samples, op if args.posterior else None, args.dim)
         line = {
             "metric": METRIC,
@@ -257,7 +260,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic: prior (f = 0), x0 = 0, Philox4x32-10 counter-based Gaussian noise",
-            "config": {"workload": f"{args.dim}D {n}^{args.dim} shifted-Laplace FD prior (kappa^2 = 25), "
+            "config": {"workload": f"{args.dim}D {n}^{args.dim} shifted-Laplace {'FEM' if args.fem else 'FD'} "
+                                   f"prior (kappa^2 = 25), "
                                    f"{nlevel}-level V-cycle, SOR Gibbs 1/1, SSOR coarse 1, omega 1, "
                                    f"one independent chain per GPU",
                        "lattice": [n] * args.dim, "unknowns": n0, "nlevel": nlevel, "chains": world,
