@@ -106,6 +106,7 @@ struct LowRankDev {
     double* part = nullptr;        // block partials
     double* w = nullptr;           // m-vector of dots
     bool small = false;            // k_lr_small path (sparse columns, one block each, few rows)
+    long long max_col_n = 0;       // most entries of one column
     int* t_ent_off = nullptr;      // the same offsets in k_tail's LDS layout (small levels)
     int* t_rows_off = nullptr;
     int* t_bar_off[2] = {nullptr, nullptr};
@@ -667,7 +668,11 @@ void lr_small(const mgmc_handle* h, const Level& lv, double* x, int direction, i
     a.key = h->key;
     a.tag = next_tag;
     a.sample = sample;
-    hipLaunchKernelGGL(k_lr_small, dim3(1), dim3(1024), 0, s, a);
+    // k_lr_small_pf: one entry per lane, <= 8 columns, <= 2 rows of B_bar and of B per thread
+    if (r.m <= 8 && r.max_col_n <= 64 && a.nbar <= 2048 && a.nrows <= 2048 && getenv("MGMC_LR_NO_PF") == nullptr)
+        hipLaunchKernelGGL((k_lr_small_pf<8, 2>), dim3(1), dim3(1024), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_lr_small, dim3(1), dim3(1024), 0, s, a);
 }
 
 LRJob lr_job(const Level& lv, int restore, int noise, uint32_t tag) {
@@ -2054,6 +2059,7 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
         const LRColumn& c = cols[k];
         LRColMeta& mt = meta[k];
         mt.n = (long long)c.ent.size();
+        r.max_col_n = std::max(r.max_col_n, mt.n);
         mt.blk0 = (int)blk_col.size();
         mt.nblk = (int)((mt.n + LR_BLK - 1) / LR_BLK);
         mt.pad_ = 0;

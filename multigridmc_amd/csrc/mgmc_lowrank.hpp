@@ -351,6 +351,128 @@ __global__ void __launch_bounds__(1024) k_lr_small(LRSmallArgs a) {
     }
 }
 
+// ---- k_lr_small with its independent loads issued up front ----
+// k_lr_small is a chain of dependent global round trips (column metadata -> entries -> x, then
+// B_bar rows, the second dot's metadata and entries, the rows of B), each ~1 us.  When every column
+// has <= 64 entries (one per lane), m <= M and each thread owns <= PR rows of B_bar and of B, all of
+// those loads do not depend on anything this kernel writes and go first; what is left is entries ->
+// x, the fix's read-modify-write of x, (the residual's second read of x), the write of f.  Same
+// arithmetic: one entry per lane is the lane sum 0.0 + (sc B_ek) x_e, the fix is the fma chain over
+// k ascending, the patch the masked mul+add chain.
+template <int M, int PR>
+__global__ void __launch_bounds__(1024) k_lr_small_pf(LRSmallArgs a) {
+    __shared__ double ws[LR_MAX_M], ts[LR_MAX_M];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nt = blockDim.x;
+    const int m = a.m;
+    // 0. independent loads
+    long long eoff = 0;
+    double evs = 0.0, evi = 0.0;
+    bool have_e = false;
+    if (wave < m) {
+        const LRColMeta c = a.meta[wave];
+        if (lane < c.n) {
+            const long long q = c.ent0 + lane;
+            const double v = a.ent_val[q];
+            eoff = a.ent_off[q];
+            evs = a.sc_one[wave] * v;
+            evi = a.sc_inv[wave] * v;
+            have_e = true;
+        }
+    }
+    double bv[PR][M];
+    long long boff[PR];
+    double cf[PR][M];
+    uint64_t msk[PR];
+    long long roff[PR];
+    double base[PR];
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+        const int u = tid + r * nt;
+        boff[r] = 0;
+        roff[r] = 0;
+        msk[r] = 0;
+        base[r] = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k) bv[r][k] = cf[r][k] = 0.0;
+        if (u < a.nbar) {
+            boff[r] = a.bar_off[u];
+#pragma unroll
+            for (int k = 0; k < M; ++k)
+                if (k < m) bv[r][k] = a.bar_val[(long long)u * m + k];
+        }
+        if (u < a.nrows) {
+            roff[r] = a.rows_off[u];
+            msk[r] = a.mask[u];
+#pragma unroll
+            for (int k = 0; k < M; ++k)
+                if (k < m) cf[r][k] = a.coef[(long long)u * m + k];
+            base[r] = a.restore ? a.save[u] : a.f[roff[r]];
+        }
+    }
+    auto wave_total = [&](double acc) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+        double tot = lane == 0 ? 0.0 + acc : 0.0;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) tot = tot + __shfl_xor(tot, off, 64);
+        return tot;
+    };
+    // 1. w = B^T x
+    if (wave < m) {
+        const double acc = have_e ? 0.0 + evs * a.x[eoff] : 0.0;
+        const double t = wave_total(acc);
+        if (lane == 0) ws[wave] = t;
+    }
+    __syncthreads();
+    // 2. x -= B_bar w
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+        const int u = tid + r * nt;
+        if (u < a.nbar) {
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < M; ++k)
+                if (k < m) acc = fma(bv[r][k], ws[k], acc);
+            a.x[boff[r]] = a.x[boff[r]] - acc;
+        }
+    }
+    // 3. the next op's vector
+    if (a.next == LR_NEXT_RESIDUAL) {
+        __syncthreads();
+        if (wave < m) {
+            const double acc = have_e ? 0.0 + evi * a.x[eoff] : 0.0;
+            const double t = wave_total(acc);
+            if (lane == 0) ts[wave] = t;
+        }
+    } else if (a.next == LR_NEXT_NOISE && 2 * tid < m) {
+        const uint64_t sample = *a.sample;
+        const Philox4 rr = philox4x32_10(LR_PAIR0 + (uint32_t)tid, a.tag, (uint32_t)sample, (uint32_t)(sample >> 32),
+                                         a.key.k0, a.key.k1);
+        double z0, z1;
+        normal_pair(rr, &z0, &z1);
+        ts[2 * tid] = a.sq[2 * tid] * z0;
+        if (2 * tid + 1 < m) ts[2 * tid + 1] = a.sq[2 * tid + 1] * z1;
+    }
+    __syncthreads();
+    // 4. f on the rows of B
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+        const int u = tid + r * nt;
+        if (u >= a.nrows) continue;
+        if (a.next == LR_NEXT_NONE) {
+            if (a.restore) a.f[roff[r]] = base[r];
+            continue;
+        }
+        double e = 0.0;
+#pragma unroll
+        for (int k = 0; k < M; ++k)
+            if (k < m && ((msk[r] >> k) & 1)) e = e + cf[r][k] * ts[k];
+        if (!a.restore) a.save[u] = base[r];
+        a.f[roff[r]] = a.next == LR_NEXT_NOISE ? base[r] + e : base[r] - e;
+    }
+}
+
 // ============================================================================================
 // host side: the same orders, for the B_bar setup (M = Sigma + B^T Y needs the dots of Y)
 // ============================================================================================
