@@ -26,6 +26,7 @@
 #include "mgmc_zsweepres.hpp"
 #include "mgmc_tail.hpp"
 #include "mgmc_gsweep.hpp"
+#include "mgmc_rb2d.hpp"
 #include "mgmc_lowrank.hpp"
 #include "mgmc_solver.hpp"
 #include "mgmc_cholesky.hpp"
@@ -125,7 +126,8 @@ struct Level {
     bool zsweep = false;   // fused z-marching red-black sweep available
     bool pairs = false;    // Galerkin level swept in colour-pair passes (mgmc_gsweep.hpp)
     bool quads = false;    // ... two pairs per launch, out of place (k_sweep_quads)
-    bool pingpong() const { return zsweep || quads; }  // out-of-place sweeps: x <-> x2
+    bool rb2d = false;     // 2D 5-point level: one-launch red-black sweep, out of place (k_rb2d)
+    bool pingpong() const { return zsweep || quads || rb2d; }  // out-of-place sweeps: x <-> x2
     double* buf(int i) const { return i == 0 ? x : x2; }
     LowRankDev lr;
 };
@@ -160,6 +162,7 @@ struct mgmc_handle {
     int nranks = 1, rank = 0;
     double* comm_buf = nullptr;  // device scratch for collectives
     bool fuse_prolong = false;   // prolongate-add fused into the first post-sweep (z-sweep levels)
+    bool rb2d_prolong = false;   // ... also on 2D red-black levels (opt-in MGMC_RB2D_PROLONG)
     bool fuse_restrict = false;  // last pre-sweep + residual + restriction in one kernel (z-sweep levels)
     std::vector<TailArgs*> tail_args;  // device copies, one per OP_TAIL
     std::vector<size_t> tail_lds;      // dynamic LDS bytes per OP_TAIL
@@ -382,10 +385,33 @@ bool pairs_eligible(const LevelSpec& sp, const Layout& L) {
 // default (small levels): rows of <= 32 pairs, where each pass is launch-latency bound and halving the
 // launches pays (256^3: 63^3 level 4 x 5.0 -> 2 x 7.6 us, 31^3 level 4 x 4.8 -> 2 x 6.3 us per sweep);
 // MGMC_QUADS: every level with rows of <= 128 pairs (slower on the large levels, tests); MGMC_NO_QUADS:
-// none.  Levels that k_tail will run are left to it (caller).
+// none; MGMC_QUADS_MAXPAIR=n: rows of <= n pairs.  2D: every pair-pass level.  Levels that k_tail will
+// run are left to it (caller).
 bool quads_eligible(const LevelSpec& sp, const Layout& L) {
     if (!pairs_eligible(sp, L) || getenv("MGMC_NO_QUADS") != nullptr) return false;
+    if (const char* mp = getenv("MGMC_QUADS_MAXPAIR")) return L.nx / 2 <= atoi(mp);
+    // 2D levels are launch-bound at every size of the benchmark configs: one launch per sweep instead
+    // of two (2D 1024^2 FD cycle 0.135 -> 0.129 ms, FEM 0.147 -> 0.139 ms, A/B in one box call)
+    if (sp.dim == 2) return true;
     return L.nx / 2 <= (getenv("MGMC_QUADS") != nullptr ? 128 : 32);
+}
+
+// one red-black sweep of a 2D 5-point level, xin -> xout (mgmc_rb2d.hpp)
+// lc: the coarse level whose x is prolongated into the staged state first (fused first post-sweep)
+void launch_rb2d(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
+                 bool noise, hipStream_t s, const Level* lc = nullptr, double alpha = 0.0) {
+    const int ntx = (lv.L.nx - 1 + RB2_TW - 1) / RB2_TW, nty = (lv.L.ny - 1 + RB2_TH - 1) / RB2_TH;
+    const int c1 = direction == MGMC_FORWARD ? 0 : 1;
+    const Layout Lc = lc ? lc->L : lv.L;
+    const double* xc = lc ? lc->x : nullptr;
+    const dim3 grid(ntx * nty), block(RB2_NT);
+    if (lc && noise)
+        hipLaunchKernelGGL((k_rb2d<true, true>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx, Lc, xc, alpha);
+    else if (noise)
+        hipLaunchKernelGGL((k_rb2d<true, false>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx, Lc, xc, alpha);
+    else
+        hipLaunchKernelGGL((k_rb2d<false, false>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx, Lc, xc,
+                           alpha);
 }
 
 void launch_quads(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
@@ -760,7 +786,11 @@ void launch_coarse_chol(const mgmc_handle* h, const Level& lv, const double* f, 
 void push_sweep(mgmc_handle* h, std::vector<int>& cur, int level, int direction, uint32_t& tag, int& pending_prolong) {
     Op op{OP_SWEEP, level, direction, tag++, 1};
     const Level& lv = h->levels[level];
-    if (lv.pingpong() && pending_prolong && !(lv.zsweep && h->fuse_prolong)) {
+    // fused prolongation: z-sweep levels by default; the 2D red-black kernel only with
+    // MGMC_RB2D_PROLONG (bitwise, but its staging becomes a longer latency chain: 2D 1024^2 cycle
+    // 0.1292-0.1305 -> 0.1306-0.1316 ms against the separate k_prolongate_pairs launch)
+    const bool fold = lv.zsweep || (lv.rb2d && h->rb2d_prolong);
+    if (lv.pingpong() && pending_prolong && !(fold && h->fuse_prolong)) {
         h->ops.push_back({OP_PROLONGATE, level, 0, 0, 0});
         h->ops.back().src = cur[level];
         pending_prolong = 0;
@@ -1103,6 +1133,10 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 } else if (lv.quads) {
                     xo = lv.buf(1 - op.src);
                     launch_quads(lv, lv.buf(op.src), xo, lv.f, g, op.direction, s);
+                } else if (lv.rb2d) {
+                    xo = lv.buf(1 - op.src);
+                    const Level* lc = op.prolong ? &h->levels[op.level + 1] : nullptr;
+                    launch_rb2d(lv, lv.buf(op.src), xo, lv.f, g, op.direction, true, s, lc, h->cfg.coarse_scaling);
                 } else if (lv.pairs) {
                     launch_pairs(lv, lv.x, lv.f, g, op.direction, s);
                 } else {
@@ -1409,6 +1443,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         lv.zsweep = cfg->dim == 3 && lv.spec.npoints == 7 && symmetric && l + 1 < specs.size() &&
                     (lv.L.nx % (2 * zsweep_xp())) == 0 && getenv("MGMC_NO_ZSWEEP") == nullptr;
         lv.pairs = pairs_eligible(lv.spec, lv.L) && getenv("MGMC_NO_PAIRS") == nullptr;
+        lv.rb2d = cfg->dim == 2 && lv.spec.npoints == 5 && l + 1 < specs.size() && getenv("MGMC_NO_RB2D") == nullptr;
         lv.quads = lv.pairs && quads_eligible(lv.spec, lv.L) && (tail0 < 0 || (int)l < tail0);
         if (lv.pingpong()) {
             if (hipMalloc(&lv.x2, bytes) != hipSuccess) {
@@ -1432,6 +1467,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         return bail(rc);
     // op sequence of one sample
     h->fuse_prolong = getenv("MGMC_NO_FUSE_PROLONG") == nullptr;  // default: fused (A/B in DESIGN.md)
+    h->rb2d_prolong = getenv("MGMC_RB2D_PROLONG") != nullptr;
     // opt-in: the fused pre-sweep + residual + restriction is correct (bitwise) but slower at 512^3
     // (1.98 ms against 0.70 + 0.56 ms): its two-vertex recomputed halo and 2 workgroups
     // per CU leave it latency / VALU bound
@@ -1666,6 +1702,9 @@ static int sweep_component(mgmc_handle* h, int level, int direction, int nsweeps
         } else if (noise && lv.quads) {  // two colour pairs per launch (out of place)
             launch_quads(lv, lv.scratch[cur], lv.scratch[3 - cur], lv.scratch[0], g, direction, h->stream);
             cur = 3 - cur;
+        } else if (noise && lv.rb2d) {  // one-launch 2D red-black sweep (out of place)
+            launch_rb2d(lv, lv.scratch[cur], lv.scratch[3 - cur], lv.scratch[0], g, direction, true, h->stream);
+            cur = 3 - cur;
         } else if (noise && lv.pairs) {  // the colour-pair passes of the V-cycle (in place)
             launch_pairs(lv, lv.scratch[cur], lv.scratch[0], g, direction, h->stream);
         } else {
@@ -1776,6 +1815,9 @@ int mgmc_time_fine_sweeps(mgmc_handle* h, int nsweeps, float* ms) {
         const int dir = (s & 1) ? MGMC_BACKWARD : MGMC_FORWARD;
         if (lv.zsweep) {
             launch_zsweep(lv, lv.scratch[cur], lv.scratch[3 - cur], lv.f, g, dir, nullptr, nullptr, 0.0, h->stream);
+            cur = 3 - cur;
+        } else if (lv.rb2d) {
+            launch_rb2d(lv, lv.scratch[cur], lv.scratch[3 - cur], lv.f, g, dir, true, h->stream);
             cur = 3 - cur;
         } else {
             launch_sweep(lv, lv.scratch[cur], lv.f, g, dir, true, h->stream);

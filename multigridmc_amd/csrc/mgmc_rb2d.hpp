@@ -1,0 +1,125 @@
+// mgmc_rb2d.hpp -- one launch per red-black Gibbs sweep of a 2D 5-point (FD) level.
+//
+// sampler/sor_sampler.cc:37-59 + smoother/sor_smoother.cc:56-78 under the red-black splitting: the
+// first colour is updated from the old second colour, then the second from the new first.  The 2D
+// fine level (1023^2 unknowns at BASELINE config 2) is launch-bound: two colour passes of ~6.5 us.
+// Here a workgroup stages a 128 x 16 tile of the old state with a 2-vertex halo in LDS, updates the
+// first colour on the tile plus a 1-vertex ring (the ring's values are the neighbouring tiles' own
+// results: same inputs, same arithmetic), then the second colour on the tile, and writes the tile to
+// the other buffer (out of place: neighbouring workgroups still read the old values).  Each update is
+// gibbs_point's arithmetic: c = fma(sd, xi, f) with xi the cos / sin branch of the Philox pair
+// (odd i, i+1) of the sweep's tag, x = fma(omega/diag, c - S, x), S the stencil fma chain.
+#pragma once
+#include "mgmc_kernels.hpp"
+
+namespace mgmc {
+
+constexpr int RB2_TW = 128, RB2_TH = 16;                 // tile columns, rows
+constexpr int RB2_W = RB2_TW + 4, RB2_H = RB2_TH + 4;    // staged region: 2-vertex halo
+constexpr int RB2_NT = 1024;                            // threads: about one item per thread per phase
+
+// PROLONG: the first post-sweep also adds alpha P x_c (intergrid_operator.hh:106-120) to every staged
+// vertex first, with k_prolongate_pairs' terms in its order (coarse rows ascending; an odd i takes
+// parents q, q+1 with weight 1/2, an even i parent q+1 with weight 1; w = 1 * w_x * w_y, then
+// v += (alpha w) x_c), so the separate prolongation launch goes away.
+template <bool NOISE, bool PROLONG>
+__global__ void __launch_bounds__(RB2_NT) k_rb2d(Layout L, const double* __restrict__ xin, double* __restrict__ xout,
+                                              const double* __restrict__ f, StencilArg S, GibbsArg G, int c1,
+                                              int ntx, Layout Lc, const double* __restrict__ xc, double alpha) {
+    __shared__ double xs[RB2_H * RB2_W];
+    __shared__ double cs[RB2_H * RB2_W];  // right hand sides c = fma(sd, xi, f) of the updated vertices
+    const int tid = threadIdx.x;
+    const int tx = (int)blockIdx.x % ntx, ty = (int)blockIdx.x / ntx;
+    const int i0 = 1 + tx * RB2_TW, j0 = 1 + ty * RB2_TH;
+    const int ib = i0 - 2, jb = j0 - 2;  // lattice coordinates of LDS (0, 0)
+    const uint64_t sample = NOISE ? *G.sample : 0;
+    for (int q = tid; q < RB2_H * RB2_W; q += RB2_NT) {
+        const int r = q / RB2_W, c = q - r * RB2_W;
+        const int i = ib + c, j = jb + r;
+        double v = (i >= 0 && i <= L.nx && j >= 0 && j <= L.ny) ? xin[L.at(i, j, 0)] : 0.0;
+        if (PROLONG && i >= 1 && i <= L.nx - 1 && j >= 1 && j <= L.ny - 1) {
+            const int qp = (i - 1) >> 1;  // the pair (2qp+1, 2qp+2)
+            const int j0c = j >> 1, nj = (j & 1) ? 2 : 1;
+            for (int bb = 0; bb < nj; ++bb) {
+                const int jj = j0c + bb;
+                if (jj < 1 || jj > Lc.ny - 1) continue;
+                const double* row = xc + Lc.at(0, jj, 0);
+                const double wy = w1(j - 2 * jj);
+                if (i & 1) {
+                    if (qp >= 1) {
+                        double w = 1.0;
+                        w *= 0.5;
+                        w *= wy;
+                        v += alpha * w * row[qp];
+                    }
+                    if (qp + 1 <= Lc.nx - 1) {
+                        double w = 1.0;
+                        w *= 0.5;
+                        w *= wy;
+                        v += alpha * w * row[qp + 1];
+                    }
+                } else if (qp + 1 <= Lc.nx - 1) {
+                    double w = 1.0;
+                    w *= 1.0;
+                    w *= wy;
+                    v += alpha * w * row[qp + 1];
+                }
+            }
+        }
+        xs[q] = v;
+    }
+    // right hand sides of every vertex the two passes update (rows [j0-1, j0+TH], columns [i0-1,
+    // i0+TW]): f does not change during the sweep, so they are evaluated up front, one Box-Muller per
+    // pair (odd i, i+1) -- the values point_normal gives each vertex
+    {
+        constexpr int NP = RB2_TW / 2 + 2;  // pairs with odd i from i0-2 to i0+TW
+        for (int q = tid; q < NP * (RB2_TH + 2); q += RB2_NT) {
+            const int r = q / NP, m = q - r * NP;
+            const int j = j0 - 1 + r, io = i0 - 2 + 2 * m;
+            if (j < 1 || j > L.ny - 1) continue;
+            double z0 = 0.0, z1 = 0.0;
+            if (NOISE && io >= 1 && io <= L.nx - 1) {
+                const Philox4 rnd =
+                    philox4x32_10(pair_id<2>(L, io, j, 0), G.tag, (uint32_t)sample, (uint32_t)(sample >> 32), G.key.k0,
+                                  G.key.k1);
+                normal_pair(rnd, &z0, &z1);
+            }
+            const int pl = (j - jb) * RB2_W + (io - ib);
+            if (io >= 1 && io <= L.nx - 1 && io >= i0 - 1) {
+                const double fv = f[L.at(io, j, 0)];
+                cs[pl] = NOISE ? fma(G.sd, z0, fv) : fv;
+            }
+            if (io + 1 >= 1 && io + 1 <= L.nx - 1 && io + 1 <= i0 + RB2_TW) {
+                const double fv = f[L.at(io + 1, j, 0)];
+                cs[pl + 1] = NOISE ? fma(G.sd, z1, fv) : fv;
+            }
+        }
+    }
+    Layout Ls = L;  // the LDS region as a layout: stencil offsets +-1, +-RB2_W
+    Ls.sx = RB2_W;
+    __syncthreads();
+    // one colour on columns [ia, ia + w) x rows [ja, ja + h) (interior vertices only)
+    auto colour_pass = [&](int colour, int ia, int ja, int w, int h) {
+        const int per_row = (w + 1) / 2;
+        for (int q = tid; q < per_row * h; q += RB2_NT) {
+            const int r = q / per_row, k = q - r * per_row;
+            const int j = ja + r;
+            const int i = ia + (((ia + j) & 1) != colour ? 1 : 0) + 2 * k;
+            if (i >= ia + w || i < 1 || i > L.nx - 1 || j < 1 || j > L.ny - 1) continue;
+            const int p = (j - jb) * RB2_W + (i - ib);
+            const double res = stencil_fma<2, 5>(xs, p, Ls, S);
+            xs[p] = fma(G.wd, cs[p] - res, xs[p]);
+        }
+    };
+    colour_pass(c1, i0 - 1, j0 - 1, RB2_TW + 2, RB2_TH + 2);
+    __syncthreads();
+    colour_pass(1 - c1, i0, j0, RB2_TW, RB2_TH);
+    __syncthreads();
+    for (int q = tid; q < RB2_TW * RB2_TH; q += RB2_NT) {
+        const int r = q / RB2_TW, c = q - r * RB2_TW;
+        const int i = i0 + c, j = j0 + r;
+        if (i <= L.nx - 1 && j <= L.ny - 1) xout[L.at(i, j, 0)] = xs[(r + 2) * RB2_W + (c + 2)];
+    }
+}
+
+}  // namespace mgmc

@@ -190,6 +190,12 @@ def test_zsweep_tile_variants_bitwise(hip_device, monkeypatch, variant):
                                       ("MGMC_NO_TAIL", "3d32_W_ssor"),
                                       ("MGMC_NO_QUADS", "3d64_4lvl"),
                                       ("MGMC_NO_QUADS", "3d_zres27"),
+                                      ("MGMC_NO_QUADS", "2d256_global_coarse"),
+                                      ("MGMC_NO_QUADS", "2d_aniso_ssor"),
+                                      ("MGMC_NO_RB2D", "2d64_template_W"),
+                                      ("MGMC_NO_RB2D", "2d_aniso_ssor"),
+                                      ("MGMC_RB2D_PROLONG", "2d64_template_W"),
+                                      ("MGMC_RB2D_PROLONG", "2d_aniso_ssor"),
                                       ("MGMC_ZR_VARIANT=2", "3d_zres7"),
                                       ("MGMC_ZR_VARIANT=5", "3d_zres7"),
                                       ("MGMC_ZS_PROLONG256", "3d128_zsweep"),
