@@ -17,6 +17,12 @@ namespace mgmc {
 constexpr int RB2_TW = 128, RB2_TH = 16;                 // tile columns, rows
 constexpr int RB2_W = RB2_TW + 4, RB2_H = RB2_TH + 4;    // staged region: 2-vertex halo
 constexpr int RB2_NT = 1024;                            // threads: about one item per thread per phase
+constexpr int RB2_HW = RB2_W / 2;                       // LDS rows are colour-split: [even c | odd c]
+
+// LDS index of region row r, column c: the vertices of one colour in a row are consecutive doubles,
+// so a colour pass reads without bank conflicts (the natural layout's stride 2 was 44% conflict
+// cycles, PMC)
+__device__ __forceinline__ int rb2_lidx(int r, int c) { return r * RB2_W + (c & 1) * RB2_HW + (c >> 1); }
 
 // PROLONG: the first post-sweep also adds alpha P x_c (intergrid_operator.hh:106-120) to every staged
 // vertex first, with k_prolongate_pairs' terms in its order (coarse rows ascending; an odd i takes
@@ -66,7 +72,7 @@ __global__ void __launch_bounds__(RB2_NT) k_rb2d(Layout L, const double* __restr
                 }
             }
         }
-        xs[q] = v;
+        xs[rb2_lidx(r, c)] = v;
     }
     // right hand sides of every vertex the two passes update (rows [j0-1, j0+TH], columns [i0-1,
     // i0+TW]): f does not change during the sweep, so they are evaluated up front, one Box-Muller per
@@ -84,19 +90,16 @@ __global__ void __launch_bounds__(RB2_NT) k_rb2d(Layout L, const double* __restr
                                   G.key.k1);
                 normal_pair(rnd, &z0, &z1);
             }
-            const int pl = (j - jb) * RB2_W + (io - ib);
             if (io >= 1 && io <= L.nx - 1 && io >= i0 - 1) {
                 const double fv = f[L.at(io, j, 0)];
-                cs[pl] = NOISE ? fma(G.sd, z0, fv) : fv;
+                cs[rb2_lidx(j - jb, io - ib)] = NOISE ? fma(G.sd, z0, fv) : fv;
             }
             if (io + 1 >= 1 && io + 1 <= L.nx - 1 && io + 1 <= i0 + RB2_TW) {
                 const double fv = f[L.at(io + 1, j, 0)];
-                cs[pl + 1] = NOISE ? fma(G.sd, z1, fv) : fv;
+                cs[rb2_lidx(j - jb, io + 1 - ib)] = NOISE ? fma(G.sd, z1, fv) : fv;
             }
         }
     }
-    Layout Ls = L;  // the LDS region as a layout: stencil offsets +-1, +-RB2_W
-    Ls.sx = RB2_W;
     __syncthreads();
     // one colour on columns [ia, ia + w) x rows [ja, ja + h) (interior vertices only)
     auto colour_pass = [&](int colour, int ia, int ja, int w, int h) {
@@ -106,8 +109,14 @@ __global__ void __launch_bounds__(RB2_NT) k_rb2d(Layout L, const double* __restr
             const int j = ja + r;
             const int i = ia + (((ia + j) & 1) != colour ? 1 : 0) + 2 * k;
             if (i >= ia + w || i < 1 || i > L.nx - 1 || j < 1 || j > L.ny - 1) continue;
-            const int p = (j - jb) * RB2_W + (i - ib);
-            const double res = stencil_fma<2, 5>(xs, p, Ls, S);
+            const int r2 = j - jb, c2 = i - ib;
+            const int p = rb2_lidx(r2, c2);
+            // stencil_fma<2, 5>'s chain: south, west, centre, east, north
+            double res = S.a[1] * xs[p - RB2_W];
+            res = fma(S.a[3], xs[rb2_lidx(r2, c2 - 1)], res);
+            res = fma(S.a[4], xs[p], res);
+            res = fma(S.a[5], xs[rb2_lidx(r2, c2 + 1)], res);
+            res = fma(S.a[7], xs[p + RB2_W], res);
             xs[p] = fma(G.wd, cs[p] - res, xs[p]);
         }
     };
@@ -118,7 +127,7 @@ __global__ void __launch_bounds__(RB2_NT) k_rb2d(Layout L, const double* __restr
     for (int q = tid; q < RB2_TW * RB2_TH; q += RB2_NT) {
         const int r = q / RB2_TW, c = q - r * RB2_TW;
         const int i = i0 + c, j = j0 + r;
-        if (i <= L.nx - 1 && j <= L.ny - 1) xout[L.at(i, j, 0)] = xs[(r + 2) * RB2_W + (c + 2)];
+        if (i <= L.nx - 1 && j <= L.ny - 1) xout[L.at(i, j, 0)] = xs[rb2_lidx(r + 2, c + 2)];
     }
 }
 
