@@ -155,6 +155,8 @@ struct mgmc_handle {
     std::vector<Op> ops;            // one sample
     size_t seg_end_pre = 0, seg_begin_post = 0, seg_end_post = 0;  // fine-sweep segments
     hipGraphExec_t graph_all = nullptr;
+    hipGraphExec_t graph_unroll = nullptr;  // unroll copies of the cycle in one graph (sample loops)
+    int unroll = 1;
     hipGraphExec_t graph_seg[4] = {nullptr, nullptr, nullptr, nullptr};
     int64_t qoi_store_index = -1;
     std::string last_error;
@@ -1211,6 +1213,8 @@ int capture(mgmc_handle* h, size_t begin, size_t end, hipGraphExec_t* out) {
 void destroy_graphs(mgmc_handle* h) {
     if (h->graph_all) hipGraphExecDestroy(h->graph_all);
     h->graph_all = nullptr;
+    if (h->graph_unroll) hipGraphExecDestroy(h->graph_unroll);
+    h->graph_unroll = nullptr;
     for (auto& g : h->graph_seg) {
         if (g) hipGraphExecDestroy(g);
         g = nullptr;
@@ -1222,6 +1226,20 @@ int build_graphs(mgmc_handle* h) {
     destroy_graphs(h);
     int rc = capture(h, 0, h->ops.size(), &h->graph_all);
     if (rc) return rc;
+    // small lattices: one hipGraphLaunch costs about as much host time as a 2D 1024^2 cycle takes on
+    // the GPU, so the sample loops replay `unroll` cycles per launch (the sample index lives on the
+    // device: the copies are identical)
+    const uint64_t n0 = h->levels[0].spec.ndof;
+    h->unroll = n0 <= (1u << 22) ? 8 : (n0 <= (1u << 25) ? 2 : 1);
+    if (const char* u = getenv("MGMC_GRAPH_UNROLL")) h->unroll = std::max(1, std::min(64, atoi(u)));
+    if (h->unroll > 1) {
+        hipGraph_t g = nullptr;
+        HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+        for (int u = 0; u < h->unroll; ++u) enqueue_ops(h, 0, h->ops.size(), h->stream);
+        HIPCHK(h, hipStreamEndCapture(h->stream, &g));
+        HIPCHK(h, hipGraphInstantiate(&h->graph_unroll, g, nullptr, nullptr, 0));
+        HIPCHK(h, hipGraphDestroy(g));
+    }
     if (h->levels.size() > 1) {
         // two segments per cycle: [fine pre-sampler | the rest] (each segment boundary costs ~12 us
         // of graph launch between HIP events; four segments cost 0.85% of the 512^3 cycle)
@@ -1592,7 +1610,10 @@ int mgmc_sample_async(mgmc_handle* h, int nsteps, int64_t qoi_index) {
     // series restarts at 0 for each call
     HIPCHK(h, hipMemsetAsync(h->ctrl + 1, 0, sizeof(uint64_t), h->stream));
     if ((rc = ensure_series(h, (uint64_t)std::max(nsteps, 1)))) return rc;
-    for (int s = 0; s < nsteps; ++s) HIPCHK(h, hipGraphLaunch(h->graph_all, h->stream));
+    int s = 0;
+    if (h->graph_unroll)
+        for (; s + h->unroll <= nsteps; s += h->unroll) HIPCHK(h, hipGraphLaunch(h->graph_unroll, h->stream));
+    for (; s < nsteps; ++s) HIPCHK(h, hipGraphLaunch(h->graph_all, h->stream));
     return MGMC_OK;
 }
 

@@ -385,3 +385,26 @@ def test_convergence_chains_batched_equal_sequential(hip_device, shape, nlevel, 
     assert a.get_sample_index() == b.get_sample_index() == 35
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("name,unroll", [("2d64_template_W", None), ("3d32_W_ssor", "3"), ("3d16", "1")])
+def test_unrolled_sample_loop_bitwise(hip_device, monkeypatch, name, unroll):
+    """The sample loop replays `unroll` cycles per graph launch (8 on small lattices by default,
+    MGMC_GRAPH_UNROLL): 19 cycles = whole unrolled launches + single-cycle launches, QoI series and
+    state equal to the oracle's sequential cycles."""
+    if unroll is not None:
+        monkeypatch.setenv("MGMC_GRAPH_UNROLL", unroll)
+    shape, kw = CONFIGS[name]
+    s, p, lat = make(shape, **kw)
+    mc = oracle_for(s, p, lat)
+    f = np.random.default_rng(3).standard_normal(lat.Nvertex)
+    qoi = mg.measurement_vector_index(lat, [0.5] * lat.dim)
+    s.fix_rhs(f)
+    s.set_state(np.zeros(lat.Nvertex))
+    mc.set_rhs(f)
+    mc.set_state(np.zeros(lat.Nvertex))
+    for nsteps in (19, 8, 5):
+        assert np.array_equal(s.sample(nsteps, qoi), mc.sample(nsteps, qoi))
+    assert np.array_equal(s.get_state(), mc.get_state())
+    assert s.get_sample_index() == 32
+    s.close()
