@@ -1,5 +1,6 @@
 """Throughput of C independent chains per GPU, each handle on its own HIP stream (graph replays
-overlap across streams).  python scripts/multichain_bench.py N NLEVEL K C1 C2 ..."""
+overlap across streams).  python scripts/multichain_bench.py N NLEVEL K C1 C2 ...
+THREADS=1: one host thread per chain."""
 import os
 import sys
 import time
@@ -15,10 +16,17 @@ for C in [int(c) for c in sys.argv[4:]]:
     for s in ss:
         s.sample(5, q)
     t0 = time.perf_counter()
-    for s in ss:
-        s.sample_async(K, q)
-    for s in ss:
-        s.synchronize()
+    if os.environ.get("THREADS") == "1":
+        # one host thread per chain: the graph launches (host-side AQL packets, a few us per kernel
+        # node) of different chains are enqueued concurrently; ctypes releases the GIL
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(len(ss)) as ex:
+            list(ex.map(lambda s: (s.sample_async(K, q), s.synchronize()), ss))
+    else:
+        for s in ss:
+            s.sample_async(K, q)
+        for s in ss:
+            s.synchronize()
     dt = time.perf_counter() - t0
     print(f"lattice {lat.shape} chains {C}: {C * K / dt:10.1f} samples/s  ({dt / K * 1e3:.3f} ms per round)", flush=True)
     for s in ss:
