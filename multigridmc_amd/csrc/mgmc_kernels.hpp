@@ -270,6 +270,29 @@ __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __re
             vc[u] = colour_of<DIM, NPTS>(vi[u], vj[u], vk[u]);
         }
     }
+    // 2^d-colour levels with right-hand sides precomputed: thread t takes the t-th vertex of each
+    // colour class, so every colour pass runs on full wavefronts (with the per-thread vertex cache a
+    // pass ran each of its MAXV slots with about 1/ncolours of the lanes active)
+    constexpr int NCMAX = DIM == 3 ? 8 : 4;
+    const bool bycolour = precompute && (NPTS == 9 || NPTS == 27) && ncolours == NCMAX;
+    int cp[NCMAX], cq[NCMAX];
+    bool all_fit = true;
+#pragma unroll
+    for (int c = 0; c < NCMAX; ++c) {
+        cp[c] = -1;
+        cq[c] = 0;
+        const int fi = 2 - (c & 1), fj = 2 - ((c >> 1) & 1), fk = DIM == 3 ? 2 - ((c >> 2) & 1) : 0;
+        const int ci = fi > nxi ? 0 : (nxi - fi) / 2 + 1;
+        const int cj = fj > nyi ? 0 : (nyi - fj) / 2 + 1;
+        const int ck = DIM == 3 ? (fk > L.nz - 1 ? 0 : (L.nz - 1 - fk) / 2 + 1) : 1;
+        all_fit = all_fit && ci * cj * ck <= (int)blockDim.x;
+        const int t = threadIdx.x;
+        if (bycolour && t < ci * cj * ck) {
+            const int i = fi + 2 * (t % ci), j = fj + 2 * ((t / ci) % cj), k = DIM == 3 ? fk + 2 * (t / (ci * cj)) : 0;
+            cp[c] = (int)L.at(i, j, k);
+            cq[c] = (DIM == 3 ? (k - 1) * nxi * nyi : 0) + (j - 1) * nxi + (i - 1);
+        }
+    }
     GibbsArg g = G;
     auto update = [&](int s, long long q, int i, int j, int k, long long p) {
         if constexpr (precompute) {
@@ -284,7 +307,11 @@ __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __re
         const bool backward = (s & 1) != 0;
         for (int cc = 0; cc < ncolours; ++cc) {
             const int colour = backward ? ncolours - 1 - cc : cc;
-            if (cached) {
+            if (bycolour && all_fit) {
+#pragma unroll
+                for (int c = 0; c < NCMAX; ++c)
+                    if (c == colour && cp[c] >= 0) update(s, cq[c], 0, 0, 0, cp[c]);
+            } else if (cached) {
 #pragma unroll
                 for (int u = 0; u < MAXV; ++u)
                     if (vc[u] == colour) update(s, (int)threadIdx.x + u * (int)blockDim.x, vi[u], vj[u], vk[u], vp[u]);
