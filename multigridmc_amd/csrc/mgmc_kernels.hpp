@@ -230,22 +230,23 @@ __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __re
     if constexpr (precompute) {
         // one Philox block and Box-Muller per pair (odd i, i+1) and sweep: cos -> odd, sin -> even,
         // the values point_normal gives each vertex
+        // 32-bit index arithmetic: an LDS-resident level has far fewer than 2^31 items
         const int npair = L.nx / 2;
-        const long long nrow = (long long)nyi * (DIM == 3 ? (L.nz - 1) : 1);
-        for (long long t = threadIdx.x; t < nsweeps * nrow * npair; t += blockDim.x) {
-            const int m = (int)(t % npair);
-            const long long rt = t / npair;
-            const long long row = rt % nrow;
-            const int sw = (int)(rt / nrow);
+        const int nrow = nyi * (DIM == 3 ? (L.nz - 1) : 1);
+        for (int t = threadIdx.x; t < nsweeps * nrow * npair; t += blockDim.x) {
+            const int m = t % npair;
+            const int rt = t / npair;
+            const int row = rt % nrow;
+            const int sw = rt / nrow;
             const int i0 = 2 * m + 1;
             if (i0 > nxi) continue;
-            const int j = (int)(row % nyi) + 1;
-            const int k = (DIM == 3) ? (int)(row / nyi) + 1 : 0;
+            const int j = row % nyi + 1;
+            const int k = (DIM == 3) ? row / nyi + 1 : 0;
             const Philox4 rnd = philox4x32_10(pair_id<DIM>(L, i0, j, k), G.tag + (uint32_t)sw, (uint32_t)sample,
                                               (uint32_t)(sample >> 32), G.key.k0, G.key.k1);
             double z0, z1;
             normal_pair(rnd, &z0, &z1);
-            const long long q = (long long)sw * ndof + row * nxi + (i0 - 1);
+            const long long q = (long long)sw * ndof + (long long)row * nxi + (i0 - 1);
             const long long p = L.at(i0, j, k);
             cs[q] = fma(G.sd, z0, fs[p]);
             if (i0 + 1 <= nxi) cs[q + 1] = fma(G.sd, z1, fs[p + 1]);
