@@ -165,6 +165,7 @@ struct mgmc_handle {
     double* comm_buf = nullptr;  // device scratch for collectives
     bool fuse_prolong = false;   // prolongate-add fused into the first post-sweep (z-sweep levels)
     bool rb2d_prolong = false;   // ... also on 2D red-black levels (opt-in MGMC_RB2D_PROLONG)
+    int tail_nt = 1024;          // k_tail workgroup size (MGMC_TAIL_NT)
     bool fuse_restrict = false;  // last pre-sweep + residual + restriction in one kernel (z-sweep levels)
     std::vector<TailArgs*> tail_args;  // device copies, one per OP_TAIL
     std::vector<size_t> tail_lds;      // dynamic LDS bytes per OP_TAIL
@@ -1186,9 +1187,9 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
             case OP_TAIL: {
                 const size_t lds = h->tail_lds[op.tail];
                 if (lv.spec.dim == 3)
-                    hipLaunchKernelGGL(k_tail<3>, dim3(1), dim3(1024), lds, s, (const TailArgs*)h->tail_args[op.tail]);
+                    hipLaunchKernelGGL(k_tail<3>, dim3(1), dim3(h->tail_nt), lds, s, (const TailArgs*)h->tail_args[op.tail]);
                 else
-                    hipLaunchKernelGGL(k_tail<2>, dim3(1), dim3(1024), lds, s, (const TailArgs*)h->tail_args[op.tail]);
+                    hipLaunchKernelGGL(k_tail<2>, dim3(1), dim3(h->tail_nt), lds, s, (const TailArgs*)h->tail_args[op.tail]);
                 break;
             }
             case OP_QOI: {
@@ -1486,6 +1487,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     // op sequence of one sample
     h->fuse_prolong = getenv("MGMC_NO_FUSE_PROLONG") == nullptr;  // default: fused (A/B in DESIGN.md)
     h->rb2d_prolong = getenv("MGMC_RB2D_PROLONG") != nullptr;
+    if (const char* t = getenv("MGMC_TAIL_NT")) h->tail_nt = std::max(64, std::min(1024, atoi(t) / 64 * 64));
     // opt-in: the fused pre-sweep + residual + restriction is correct (bitwise) but slower at 512^3
     // (1.98 ms against 0.70 + 0.56 ms): its two-vertex recomputed halo and 2 workgroups
     // per CU leave it latency / VALU bound

@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             const int ck = DIM == 3 ? (fk > G.nz - 1 ? 0 : (G.nz - 1 - fk) / 2 + 1) : 1;
             // small classes (<= 8 x 8 x 16, 2D 32 x 32 vertices): thread bits are the class
             // coordinates, no index division on the pass's critical path
-            const bool fast = DIM == 3 ? (ci <= 8 && cj <= 8 && ck <= 16 && nt >= 1024) : (ci <= 32 && cj <= 32 && nt >= 1024);
+            const bool fast = DIM == 3 ? (ci <= 8 && cj <= 8 && ck * 64 <= nt) : (ci <= 32 && cj * 32 <= nt);
             if (fast) {
                 const int ti = DIM == 3 ? (tid & 7) : (tid & 31);
                 const int tj = DIM == 3 ? ((tid >> 3) & 7) : (tid >> 5);
