@@ -17,12 +17,18 @@ both sides and the max over ranks is used.
 
 Rank 0 prints ONE JSON line.  Field notes:
   value      = chains x K / max-over-ranks time (whole job, samples/s)
-  roofline   = fine-level (level 0) Gibbs sweep: algorithmic 24 B/unknown (read x, read f,
-               write x) x N0 / average sweep time, measured with HIP events on the library's
-               stream around the fine pre-sampler graph segment (plain sweep kernel) inside the
-               timed region
+  roofline   = the dominant fine-level kernel (the longer of the two level-0 Gibbs sweeps of a cycle);
+               roofline.per_kernel holds both:
+                 pre_sweep : algorithmic 24 B/unknown (read x, read f, write x) x N0 / average time,
+                 post_sweep: 24 B x N0 + 8 B x N1 (the fused prolongation reads x_1) / average time,
+               each timed with HIP events on the library's stream around its graph segment of the
+               timed cycles (mgmc_sample_timed); `traffic` = rocprofv3 PMC bytes per launch from the
+               committed profiles/pmc_traffic.json (a stored figure; `traffic_source` names it)
+  config.collectives / rccl_ranks = what the final all-gather ran on and how many ranks the RCCL
+               communicator spans (ncclCommCount); a failed communicator exits non-zero
   cpu_baseline = the CPU oracle (oracle/refcpu.cpp, FAITHFUL mode = the reference algorithm,
-               1 thread) timed on a bounded sample of the same workload on rank 0 at N=1
+               g++ -O3) run as a child process (oracle/baseline.py) on rank 0 at N=1: 1 core
+               (3 warm-up + 5 timed cycles) and the all-cores aggregate
 """
 from __future__ import annotations
 
@@ -54,7 +60,8 @@ def parse():
     ap.add_argument("--dim", type=int, default=3, choices=(2, 3),
                     help="2: BASELINE config 2 (2D n^2 lattice, e.g. --dim 2 --n 1024 --nlevel 5); not the headline line")
     ap.add_argument("--nlevel", type=int, default=7)
-    ap.add_argument("--cpu-samples", type=int, default=1, help="V-cycles timed for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-samples", type=int, default=5, help="V-cycles timed for the 1-core CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-warmup", type=int, default=3, help="untimed V-cycles before them")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--plain", action="store_true", help="time the single-graph loop instead of the segmented one")
@@ -68,113 +75,142 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_info():
-    model = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    return model
-
-
-def cpu_baseline(n, nlevel, nsamples, posterior=None, dim=3):
-    """FAITHFUL oracle (reference algorithm: lexicographic SOR Gibbs sweeps, mt19937_64 +
-    normal_distribution, CSR operators; with a posterior operator the reference's dense
-    lexicographic B_bar fix) on the same hierarchy, 1 thread."""
-    from tests import oracle_lib as O
-    p = mg.MultigridParameters(nlevel=nlevel, smoother="SOR", coarse_solver="SSOR", npresmooth=1, npostsmooth=1,
-                               ncoarsesmooth=1, omega=1.0, cycle=1, coarse_scaling=1.0)
-    t0 = time.perf_counter()
-    o = O.Oracle.fd((n,) * dim, p, kappa_sq=25.0, mode=O.FAITHFUL, seed=SEED, galerkin=1)
-    if posterior is not None:
-        o.set_lowrank(posterior.get_B())
-        o.time_samples(1)  # B_bar setup of every smoother happens on first use: keep it out of the timing
-    setup = time.perf_counter() - t0
-    secs = o.time_samples(nsamples)
-    del o
-    return {
-        "value": nsamples / secs,
+def cpu_baseline(dim, n, nlevel, warmup, samples, posterior_args=None):
+    """The CPU oracle in FAITHFUL mode (the reference algorithm, oracle/refcpu.cpp, g++ -O3) on the same
+    hierarchy, run as a GPU-free child process (oracle/baseline.py): one core (warmup + samples
+    timed applications after the setup) and the all-cores aggregate (one forked chain per core of
+    this process's CPU share, all timed together)."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(ROOT, "oracle", "baseline.py"), "--dim", str(dim), "--n", str(n),
+           "--nlevel", str(nlevel), "--warmup", str(warmup), "--samples", str(samples)]
+    if posterior_args:
+        cmd += posterior_args
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=1500)
+    if r.returncode != 0:
+        raise RuntimeError(f"CPU baseline failed (rc {r.returncode}): {r.stderr[-800:]}")
+    b = json.loads(r.stdout.strip().splitlines()[-1])
+    agg = ""
+    if "cores_aggregate" in b:
+        agg = (f"; all cores: {b['cores_aggregate']} chains forked after the setup (shared CSR operators, own "
+               f"state and mt19937_64 stream each), {b['aggregate_warmup']} warm-up + {b['aggregate_samples']} "
+               f"timed cycles each, aggregate = chains x cycles / slowest chain ({b['aggregate_timed_s_max']} s)")
+    out = {
+        "value": b["value"],
         "unit": "samples/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"{nsamples} V-cycles of the same {dim}D {n}^{dim} {nlevel}-level hierarchy after a {setup:.0f} s setup "
-                  f"(oracle/refcpu.cpp FAITHFUL mode: lexicographic SOR Gibbs, mt19937_64, CSR; g++ -O2, 1 thread); "
-                  f"{secs:.1f} s timed; host CPU: {cpu_info()}",
+        "sample": f"{dim}D {n}^{dim} {nlevel}-level hierarchy, oracle/refcpu.cpp FAITHFUL mode (reference algorithm: "
+                  f"lexicographic SOR Gibbs, mt19937_64 + normal_distribution, CSR; g++ -O3); setup {b['setup_s']} s "
+                  f"excluded; 1 core: {b['warmup']} warm-up + {b['samples']} timed cycles ({b['timed_s']} s){agg}; "
+                  f"host CPU: {b['cpu_model']}",
     }
+    if "cores_aggregate" in b:
+        out["cores_aggregate"] = b["cores_aggregate"]
+        out["value_aggregate"] = b["value_aggregate"]
+    return out
+
+
+class CommError(RuntimeError):
+    pass
 
 
 class Collectives:
-    """The bench's three collectives (barrier, max of the timed interval, all-gather of the per-chain
-    QoI moments -- 24 B per chain).  N > 1: RCCL on the library's stream, with the unique id shipped
-    by torch.distributed gloo on the CPU; if the RCCL communicator cannot be created (e.g. ranks
-    sharing one device), the same three host-side collectives run on gloo."""
+    """The bench's three collectives: barrier, max of the timed interval, all-gather of the per-chain
+    QoI moments (24 B per chain).  N > 1 on distinct devices: RCCL on the library's stream (the
+    unique id is shipped by torch.distributed gloo on the CPU); a communicator that cannot be
+    created, or one that does not span every rank, is an error (exit non-zero), never a silent
+    fallback.  Ranks that share one device (MGMC_BENCH_DEVICE, a rehearsal of the N > 1 path on a
+    1-GPU box, where RCCL cannot run) use gloo collectives, and the line says so."""
 
     def __init__(self, sampler, rank, world):
-        self.s, self.rank, self.world, self.rccl = sampler, rank, world, False
+        self.s, self.rank, self.world = sampler, rank, world
+        self.kind, self.rccl_ranks = "none", 0
         if world == 1:
             return
+        import threading
         import torch.distributed as dist
         self.dist = dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
+        buses = [None] * world
+        dist.all_gather_object(buses, sampler.comm_info()["pci_bus_id"])
+        if len(set(buses)) < world:
+            if os.environ.get("MGMC_BENCH_DEVICE") is None:
+                raise CommError(f"ranks share GPUs (PCI bus ids {buses}): RCCL cannot run and the line would "
+                                f"claim {world} GPUs; set MGMC_BENCH_DEVICE only to rehearse the N > 1 host path")
+            self.kind = "gloo"
+            return
         obj = [None]
         if rank == 0:
             try:
                 obj[0] = mg.comm_unique_id()
             except mg.MgmcError as e:
-                print(f"rank 0: no RCCL unique id ({e})", file=sys.stderr)
+                obj[0] = f"rank 0: no RCCL unique id ({e})"
         dist.broadcast_object_list(obj, src=0)
+        if not isinstance(obj[0], bytes):
+            raise CommError(str(obj[0]))
+        # ncclCommInitRank is collective: if another rank failed before reaching it, this one would
+        # wait forever -- a watchdog turns that into a non-zero exit
+        done = threading.Event()
+
+        def watchdog():
+            if not done.wait(float(os.environ.get("MGMC_COMM_INIT_TIMEOUT", "300"))):
+                print(f"rank {rank}: ncclCommInitRank did not return; exiting", file=sys.stderr, flush=True)
+                os._exit(3)
+        threading.Thread(target=watchdog, daemon=True).start()
         try:
-            if obj[0] is None:
-                raise mg.MgmcError(-2, "no RCCL unique id")
             sampler.comm_init(world, rank, obj[0])
-            ok = 1
-        except mg.MgmcError as e:
-            print(f"rank {rank}: RCCL communicator unavailable ({e}); host collectives on gloo", file=sys.stderr)
-            ok = 0
-        flags = [None] * world
-        dist.all_gather_object(flags, ok)
-        self.rccl = all(f == 1 for f in flags)
-        if not self.rccl and ok:
-            sampler.comm_destroy()
+        finally:
+            done.set()
+        info = sampler.comm_info()
+        if info["rccl_ranks"] != world or info["rccl_rank"] != rank:
+            raise CommError(f"rank {rank}: the RCCL communicator spans {info['rccl_ranks']} ranks (rank "
+                            f"{info['rccl_rank']}), expected {world}")
+        counts = [None] * world
+        dist.all_gather_object(counts, info["rccl_ranks"])
+        self.kind, self.rccl_ranks = "rccl", min(counts)
 
     def barrier(self):
-        if self.rccl or self.world == 1:
-            self.s.comm_barrier()  # RCCL all-reduce + device synchronisation
-        else:
+        if self.kind == "gloo":
             self.s.synchronize()
             self.dist.barrier()
+        else:
+            self.s.comm_barrier()  # RCCL all-reduce + device synchronisation (world 1: synchronisation)
 
     def max(self, v):
-        if self.rccl or self.world == 1:
-            return self.s.comm_allreduce_max(v)
-        out = [None] * self.world
-        self.dist.all_gather_object(out, v)
-        return max(out)
+        if self.kind == "gloo":
+            out = [None] * self.world
+            self.dist.all_gather_object(out, v)
+            return max(out)
+        return self.s.comm_allreduce_max(v)
 
     def allgather_moments(self):
-        if self.rccl or self.world == 1:
-            return self.s.comm_allgather_moments(self.world)
-        import numpy as np
-        out = [None] * self.world
-        self.dist.all_gather_object(out, list(self.s.qoi_moments()))
-        return np.array(out)
+        if self.kind == "gloo":
+            import numpy as np
+            out = [None] * self.world
+            self.dist.all_gather_object(out, list(self.s.qoi_moments()))
+            return np.array(out)
+        return self.s.comm_allgather_moments(self.world)
 
 
-def posterior_operator(prior, m, radius, measure_global):
-    """BASELINE config 5: m measurements at fixed pseudo-random interior locations with the
-    variances of measurements_template.cfg's scale (~1e-6), optional global average
-    (parameters_template.cfg: variance_global 0.01)."""
-    import numpy as np
-    from multigridmc_amd.parameters import MeasurementParameters
-    rng = np.random.default_rng(20250219)
-    mp = MeasurementParameters(radius=radius, variance_scaling=1.0, measure_global=measure_global,
-                               variance_global=0.01)
-    mp.measurement_locations = [list(rng.uniform(0.1, 0.9, 3)) for _ in range(m)]
-    mp.variance = list(1e-6 * (1.0 + rng.random(m)))
-    return mg.MeasuredOperator(prior, mp)
+def stored_traffic(path, n, key):
+    """Per-launch HBM bytes of one fine-sweep kernel from a committed rocprofv3 PMC summary
+    (scripts/pmc_traffic.py): a stored figure, with its provenance, not a measurement of this run."""
+    try:
+        tj = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    if tj.get("n") != n or key not in tj:
+        return None, None
+    return tj[key]["hbm_bytes_per_launch"], {"file": os.path.relpath(path, ROOT), "head": tj.get("head"),
+                                              "date": tj.get("date"), "method": tj.get("correction")}
+
+
+def sweep_roofline(ms, nsweeps, bytes_sweep, traffic, provenance, kernel):
+    t = ms / nsweeps * 1e-3
+    achieved = bytes_sweep / t / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": provenance,
+            "kernel": kernel, "bytes_per_launch": bytes_sweep, "avg_launch_ms": round(t * 1e3, 4)}
 
 
 def main():
@@ -192,18 +228,23 @@ def main():
     prior_cls = mg.ShiftedLaplaceFEMOperator if args.fem else mg.ShiftedLaplaceFDOperator
     op = prior_cls(lat, kappa_sq=1.0 / 0.2 ** 2)  # Lambda = 0.2 (parameters_template.cfg)
     if args.posterior:
-        op = posterior_operator(op, args.posterior, args.radius, args.measure_global)
+        op = mg.synthetic_posterior(op, args.posterior, args.radius, args.measure_global)
     params = mg.MultigridParameters(nlevel=nlevel, smoother="SOR", coarse_solver="SSOR", npresmooth=1, npostsmooth=1,
                                     ncoarsesmooth=1, omega=1.0, cycle=1, coarse_scaling=1.0)
     t_setup = time.perf_counter()
-    # MGMC_BENCH_DEVICE pins every rank to one device (rehearsing the N>1 path on a 1-GPU box)
+    # MGMC_BENCH_DEVICE pins every rank to one device (rehearsing the N>1 host path on a 1-GPU box)
     device = int(os.environ.get("MGMC_BENCH_DEVICE", local_rank))
     sampler = mg.MultigridMCSampler(op, SEED, params, device=device, chain_id=rank)
     t_setup = time.perf_counter() - t_setup
     qoi = mg.measurement_vector_index(lat, [0.5] * args.dim)
     n0 = lat.Nvertex
 
-    coll = Collectives(sampler, rank, world)
+    try:
+        coll = Collectives(sampler, rank, world)
+    except (CommError, mg.MgmcError) as e:
+        print(f"rank {rank}: {e}", file=sys.stderr, flush=True)
+        sampler.close()
+        sys.exit(2)
 
     # warmup (prior: f = 0, x0 = 0 -- driver_mgmc.cc:61-69 with mean_x_exact = xbar = 0)
     sampler.sample(args.warmup, qoi)
@@ -213,9 +254,9 @@ def main():
     if args.plain:
         sampler.sample_async(args.steps, qoi)
         sampler.synchronize()
-        fine_ms, nfine = float("nan"), 0
+        timed = None
     else:
-        _, fine_ms, nfine = sampler.sample_timed(args.steps, qoi)
+        timed = sampler.sample_timed(args.steps, qoi)
     sampler.synchronize()
     t1 = time.perf_counter()
     coll.barrier()
@@ -227,26 +268,34 @@ def main():
 
     if rank == 0:
         value = world * args.steps / elapsed
-        roof = None
-        if nfine > 0:
-            t_sweep = fine_ms / nfine * 1e-3
-            bytes_sweep = 24.0 * n0
-            achieved = bytes_sweep / t_sweep / 1e9
-            traffic = None
-            if os.path.exists(args.traffic_file):
-                try:
-                    tj = json.load(open(args.traffic_file))
-                    if tj.get("n") == n and args.dim == 3 and not args.fem:
-                        traffic = tj.get("fine_sweep_hbm_bytes_per_launch")
-                except (OSError, ValueError):
-                    traffic = None
-            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "fine-level (level 0) multicolour Gibbs sweep",
-                    "bytes_per_launch": bytes_sweep, "avg_launch_ms": round(t_sweep * 1e3, 4)}
+        roof, per_kernel = None, {}
+        if timed and timed["npre"] > 0:
+            plain3d = args.dim == 3 and not args.fem and not args.posterior
+            tr_pre, prov = stored_traffic(args.traffic_file, n, "pre_sweep") if plain3d else (None, None)
+            tr_post, prov2 = stored_traffic(args.traffic_file, n, "post_sweep") if plain3d else (None, None)
+            pre = sweep_roofline(timed["pre_ms"], timed["npre"], 24.0 * n0, tr_pre, prov,
+                                 "fine pre-sweep k_zsweep_rb7 (one red-black Gibbs sweep of level 0)")
+            per_kernel["pre_sweep"] = pre
+            if timed["npost"] > 0:
+                n1 = mg.Lattice(*((n // 2,) * args.dim)).Nvertex
+                post = sweep_roofline(timed["post_ms"], timed["npost"], 24.0 * n0 + 8.0 * n1, tr_post, prov2,
+                                      "fine post-sweep k_zsweep_rb7<PROLONG> (prolongate-add of level 1 fused, "
+                                      "24 B per fine + 8 B per coarse unknown; segment includes the ~4 us QoI record)")
+                per_kernel["post_sweep"] = post
+            # the dominant kernel (the longer of the two) is the headline roofline
+            roof = dict(max(per_kernel.values(), key=lambda r: r["avg_launch_ms"]))
+            roof["per_kernel"] = per_kernel
+            if args.posterior:
+                for r in (roof, pre):
+                    r["kernel"] += " + low-rank noise patch and B_bar fix (same segment)"
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.cpu_samples > 0 and not args.fem:
-            cpu = cpu_baseline(n, nlevel, args.cpu_samples, op if args.posterior else None, args.dim)
+            pa = None
+            if args.posterior:
+                pa = ["--posterior", str(args.posterior), "--radius", str(args.radius)]
+                if args.measure_global:
+                    pa.append("--measure-global")
+            cpu = cpu_baseline(args.dim, n, nlevel, args.cpu_warmup, args.cpu_samples, pa)
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -265,12 +314,17 @@ def main():
                                    f"{nlevel}-level V-cycle, SOR Gibbs 1/1, SSOR coarse 1, omega 1, "
                                    f"one independent chain per GPU",
                        "lattice": [n] * args.dim, "unknowns": n0, "nlevel": nlevel, "chains": world,
-                       "parallelism": f"chains{world} (independent MCMC chains, 1 per GPU; "
-                                      f"{'RCCL' if coll.rccl or world == 1 else 'gloo'} all-gather of QoI moments)"},
+                       "parallelism": f"chains{world} (independent MCMC chains, 1 per GPU, no data-path "
+                                      f"collective; final QoI-moment all-gather over {coll.kind})",
+                       "collectives": coll.kind, "rccl_ranks": coll.rccl_ranks},
             "roofline": roof,
             "cpu_baseline": cpu,
             "qoi": {"index": qoi, "samples": nq, "mean": mean, "variance": m2 / nq if nq else None, "chains": len(parts)},
         }
+        if timed:
+            line["segments_ms_per_step"] = {"pre": round(timed["pre_ms"] / args.steps, 4),
+                                            "post": round(timed["post_ms"] / args.steps, 4),
+                                            "total": round(timed["total_ms"] / args.steps, 4)}
         if args.dim == 2:
             line["metric"] = "MGMC V-cycle samples/sec, 2D (BASELINE config 2)"
         if args.posterior:
@@ -285,13 +339,10 @@ def main():
             line["config"]["m_lowrank"] = m
             line["config"]["bbar_rows_forward_per_level"] = rows
             line["config"]["setup_s"] = round(t_setup, 2)
-            if roof:
-                roof["kernel"] = "fine pre-sampler segment: Gibbs sweep + low-rank noise patch + B_bar fix"
         print(json.dumps(line), flush=True)
     if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-        dist.destroy_process_group()
+        coll.dist.barrier()
+        coll.dist.destroy_process_group()
     sampler.close()
 
 

@@ -196,13 +196,14 @@ int mgmc_normals(mgmc_handle* h, uint64_t pair0, size_t n, uint32_t sweep_tag, u
  * Run `nsweeps` noisy fine-level (level 0) Gibbs sweeps on the device state, bracketed by
  * HIP events recorded on the handle's own stream; *ms = elapsed milliseconds. */
 int mgmc_time_fine_sweeps(mgmc_handle* h, int nsweeps, float* ms);
-/* Same as mgmc_sample_async + synchronize, but each cycle is replayed as two graph segments
- * [fine pre-sampler | coarse-grid correction, fine post-sampler, QoI] with HIP events recorded
- * between them on the handle's stream.  *total_ms = first-to-last event time of the nsteps
- * cycles, *fine_ms = summed time of the fine-level (level 0) pre-sampler segments (plain Gibbs
- * sweeps), *nfine = number of fine-level sweeps they contain. */
-int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* fine_ms,
-                      int* nfine);
+/* Same as mgmc_sample_async + synchronize, but each cycle is replayed as three graph segments
+ * [fine pre-sampler | coarse-grid correction | fine post-sampler + QoI record] with HIP events
+ * recorded between them on the handle's stream.  *total_ms = first-to-last event time of the nsteps
+ * cycles; *pre_ms / *post_ms = summed time of the fine-level (level 0) pre- / post-sampler segments
+ * (the post segment holds the sweep with the fused prolongation and the ~4 us QoI record);
+ * *npre / *npost = number of fine-level sweeps they contain. */
+int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* pre_ms, int* npre,
+                      double* post_ms, int* npost);
 
 /* ---- multi-GPU: one chain per rank, RCCL over xGMI for the final QoI reduction ----
  * (the reference is single-process; this is the only collective of the path) */
@@ -217,6 +218,10 @@ int mgmc_comm_allreduce_max(mgmc_handle* h, double* value);
 /* device-side barrier over the communicator, followed by a stream synchronisation */
 int mgmc_comm_barrier(mgmc_handle* h);
 int mgmc_comm_destroy(mgmc_handle* h);
+/* what the communicator really spans: *rccl_ranks = ncclCommCount (0 without a communicator),
+ * *rccl_rank = ncclCommUserRank (-1 without one), *pci_bus_id = PCI bus id of the handle's device
+ * (ranks that report the same id share one GPU, where RCCL cannot run). */
+int mgmc_comm_info(const mgmc_handle* h, int* rccl_ranks, int* rccl_rank, int* pci_bus_id);
 
 #ifdef __cplusplus
 }

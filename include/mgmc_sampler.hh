@@ -84,8 +84,10 @@ class HipMultigridMCSampler {
     size_t get_ndof() const { return ndof_; }
     mgmc_handle* handle() const { return h_.get(); }
 
-    // Sampler::apply(f, x): x in/out on the host (PCIe inclusive).  When the right hand side was
-    // fixed with fix_rhs, f is not re-uploaded (pass f = nullptr or the fixed vector).
+    // Sampler::apply(f, x): x in/out on the host (PCIe inclusive).  Without a fixed rhs, f is uploaded
+    // and used.  After fix_rhs (the promise of Sampler::fix_rhs, sampler/sampler.hh:49-56, kept as
+    // CholeskySampler::apply keeps g_rhs) the fixed rhs is used and f is not read (nullptr is fine).
+    // multigridmc_amd/sampler.py MultigridMCSampler.apply behaves the same.
     void apply(const double* f, double* x) const {
         if (rhs_fixed_) {
             check(mgmc_set_state(h_.get(), x, ndof_), h_.get(), "mgmc_set_state");

@@ -6,7 +6,7 @@ csrc/*.hip behind the C-ABI of include/mgmc.h; this package is the host-side mir
 reference's Sampler / LinearOperator interfaces.
 """
 from ._native import MgmcError, load_library  # noqa: F401
-from .measured import LowRankUpdate, MeasuredOperator, measurement_vector  # noqa: F401
+from .measured import LowRankUpdate, MeasuredOperator, measurement_vector, synthetic_posterior  # noqa: F401
 from .parameters import MultigridParameters, read_config  # noqa: F401
 from .sampler import (  # noqa: F401
     BACKWARD,

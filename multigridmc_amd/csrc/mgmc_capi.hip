@@ -74,7 +74,6 @@ struct Op {
                              // OP_RESIDUAL_RESTRICT: done by the previous sweep (no launch)
 };
 
-int g_num_cu = 256;  // compute units of the device (set by mgmc_create; MI355X: 256)
 
 // z-marching sweep tile shape (mgmc_zsweep.hpp)
 // 32 x-pairs x 16 rows, 256 threads (2 core pairs per thread, 19.5 % halo), 38 KB of LDS -> 4
@@ -123,6 +122,7 @@ struct Level {
     double* f = nullptr;
     double* scratch[3] = {nullptr, nullptr, nullptr};
     size_t lds_bytes = 0;  // >0 if the whole-level LDS kernel can hold x and f
+    int num_cu = 256;      // compute units of the handle's device (grid sizing; MI355X: 256)
     bool zsweep = false;   // fused z-marching red-black sweep available
     bool pairs = false;    // Galerkin level swept in colour-pair passes (mgmc_gsweep.hpp)
     bool quads = false;    // ... two pairs per launch, out of place (k_sweep_quads)
@@ -314,7 +314,7 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
             // keeps two rounds of workgroups (512^3: tz 64, 2,048 tiles, 906-911 -> 841-851 us;
             // 256^3: tz 16, 142 -> 118 us; interleaved A/B)
             a.tz = 64;
-            while (a.tz > 8 && txy * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 2LL * 2 * g_num_cu) a.tz /= 2;
+            while (a.tz > 8 && txy * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 2LL * 2 * lv.num_cu) a.tz /= 2;
         }
     }
     const bool pr = coarse != nullptr;
@@ -534,7 +534,7 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
         // fine 7-point level: the deepest chunks that still give two full rounds of workgroups (every
         // chunk re-reads 2 x planes and 1 f plane below / above it: 512^3 with 64 x 4 tiles kz 8 -> 43
         // (6 chunks, 1536 tiles on 256 CUs x 3 workgroups): 561 -> 451 us; with 64 x 8 tiles kz 32)
-        const long long slots = (NT >= 512 ? 2LL : 3LL) * g_num_cu;  // workgroups per CU (LDS, VGPRs)
+        const long long slots = (NT >= 512 ? 2LL : 3LL) * lf.num_cu;  // workgroups per CU (LDS, VGPRs)
         const long long per_chunk = (long long)a.ntx * a.nty;
         const long long nchunk = std::max(1LL, (2 * slots + per_chunk - 1) / per_chunk);
         a.kz = std::max(8, (int)((lc.L.nz - 1 + nchunk - 1) / nchunk));
@@ -1242,11 +1242,11 @@ int build_graphs(mgmc_handle* h) {
         HIPCHK(h, hipGraphDestroy(g));
     }
     if (h->levels.size() > 1) {
-        // two segments per cycle: [fine pre-sampler | the rest] (each segment boundary costs ~12 us
-        // of graph launch between HIP events; four segments cost 0.85% of the 512^3 cycle)
+        // three segments per cycle: [fine pre-sampler | coarse-grid correction | fine post-sampler and
+        // the QoI record] (each segment boundary costs ~12 us of graph launch between HIP events)
         const size_t n = h->ops.size();
-        const size_t b[3] = {0, h->seg_end_pre, n};
-        for (int s = 0; s < 2; ++s) {
+        const size_t b[4] = {0, h->seg_end_pre, h->seg_begin_post, n};
+        for (int s = 0; s < 3; ++s) {
             rc = capture(h, b[s], b[s + 1], &h->graph_seg[s]);
             if (rc) return rc;
         }
@@ -1421,11 +1421,8 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     h->seed = seed;
     h->chain = chain_id;
     h->key = make_key(seed, chain_id);
-    {
-        int ncu = 0;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
-            g_num_cu = ncu;
-    }
+    int ncu = 0;  // per handle: concurrent mgmc_create calls share no mutable state
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
     if (hipSetDevice(device) != hipSuccess) {
         delete h;
         return fail(nullptr, MGMC_E_HIP, "hipSetDevice failed");
@@ -1445,6 +1442,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     size_t lds_limit = 150 * 1024;
     for (size_t l = 0; l < specs.size(); ++l) {
         Level lv;
+        lv.num_cu = ncu;
         lv.spec = specs[l];
         lv.L = make_layout(cfg->dim, specs[l].n, getenv("MGMC_LAYOUT_A64") == nullptr);  // 128-B rows
         memcpy(lv.S.a, specs[l].st, sizeof(lv.S.a));
@@ -1855,16 +1853,17 @@ int mgmc_time_fine_sweeps(mgmc_handle* h, int nsweeps, float* ms) {
     return MGMC_OK;
 }
 
-int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* fine_ms,
-                      int* nfine) {
-    if (!h || nsteps < 1 || !total_ms || !fine_ms || !nfine) return fail(h, MGMC_E_INVALID, "invalid argument");
+int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* pre_ms, int* npre,
+                      double* post_ms, int* npost) {
+    if (!h || nsteps < 1 || !total_ms || !pre_ms || !npre || !post_ms || !npost)
+        return fail(h, MGMC_E_INVALID, "invalid argument");
     if (h->levels.size() < 2) return fail(h, MGMC_E_UNSUPPORTED, "timed sampling needs nlevel >= 2");
     HIPCHK(h, hipSetDevice(h->device));
     int rc = set_qoi(h, qoi_index);
     if (rc) return rc;
     HIPCHK(h, hipMemsetAsync(h->ctrl + 1, 0, sizeof(uint64_t), h->stream));
     if ((rc = ensure_series(h, (uint64_t)nsteps))) return rc;
-    constexpr int NSEG = 2;
+    constexpr int NSEG = 3;  // [fine pre-sampler | coarse-grid correction | fine post-sampler, QoI]
     std::vector<hipEvent_t> ev(NSEG * (size_t)nsteps + 1);
     for (auto& e : ev) HIPCHK(h, hipEventCreate(&e));
     for (int s = 0; s < nsteps; ++s) {
@@ -1876,18 +1875,25 @@ int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* tot
     HIPCHK(h, hipEventRecord(ev[NSEG * nsteps], h->stream));
     HIPCHK(h, hipEventSynchronize(ev[NSEG * nsteps]));
     float t = 0.f;
-    double fine = 0.0;
-    for (int s = 0; s < nsteps; ++s) {  // pre-sampler segment: plain fine sweeps only
+    double pre = 0.0, post = 0.0;
+    for (int s = 0; s < nsteps; ++s) {
         HIPCHK(h, hipEventElapsedTime(&t, ev[NSEG * s], ev[NSEG * s + 1]));
-        fine += t;
+        pre += t;
+        HIPCHK(h, hipEventElapsedTime(&t, ev[NSEG * s + 2], ev[NSEG * s + 3]));
+        post += t;
     }
     HIPCHK(h, hipEventElapsedTime(&t, ev[0], ev[NSEG * nsteps]));
     *total_ms = t;
-    *fine_ms = fine;
-    int cnt = 0;
-    for (size_t q = 0; q < h->seg_end_pre; ++q)
-        if (h->ops[q].kind == OP_SWEEP && h->ops[q].level == 0) ++cnt;
-    *nfine = cnt * nsteps;
+    *pre_ms = pre;
+    *post_ms = post;
+    int cpre = 0, cpost = 0;
+    for (size_t q = 0; q < h->ops.size(); ++q)
+        if (h->ops[q].kind == OP_SWEEP && h->ops[q].level == 0) {
+            if (q < h->seg_end_pre) ++cpre;
+            else if (q >= h->seg_begin_post) ++cpost;
+        }
+    *npre = cpre * nsteps;
+    *npost = cpost * nsteps;
     for (auto& e : ev) hipEventDestroy(e);
     return MGMC_OK;
 }
@@ -2371,6 +2377,19 @@ int mgmc_comm_barrier(mgmc_handle* h) {
     if (h->comm) NCCLCHK(h, ncclAllReduce(h->comm_buf, h->comm_buf, 1, ncclDouble, ncclSum, h->comm, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipDeviceSynchronize());
+    return MGMC_OK;
+}
+
+int mgmc_comm_info(const mgmc_handle* h, int* rccl_ranks, int* rccl_rank, int* pci_bus_id) {
+    if (!h || !rccl_ranks || !rccl_rank || !pci_bus_id) return fail(nullptr, MGMC_E_INVALID, "null argument");
+    *rccl_ranks = 0;
+    *rccl_rank = -1;
+    if (h->comm) {
+        NCCLCHK(const_cast<mgmc_handle*>(h), ncclCommCount(h->comm, rccl_ranks));
+        NCCLCHK(const_cast<mgmc_handle*>(h), ncclCommUserRank(h->comm, rccl_rank));
+    }
+    if (hipDeviceGetAttribute(pci_bus_id, hipDeviceAttributePciBusId, h->device) != hipSuccess)
+        return fail(const_cast<mgmc_handle*>(h), MGMC_E_HIP, "hipDeviceGetAttribute(PciBusId) failed");
     return MGMC_OK;
 }
 

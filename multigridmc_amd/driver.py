@@ -31,8 +31,8 @@ import numpy as np
 
 from .measured import MeasuredOperator, measurement_vector
 from .parameters import (ConstantCorrelationLengthModelParameters, GeneralParameters, LatticeParameters,
-                         MeasurementParameters, MultigridParameters, PriorParameters, SamplingParameters,
-                         read_config)
+                         MeasurementFileError, MeasurementParameters, MultigridParameters, PriorParameters,
+                         SamplingParameters, read_config)
 from .sampler import Lattice, MultigridMCSampler, ShiftedLaplaceFDOperator, ShiftedLaplaceFEMOperator
 
 SEED = 5418513  # driver_mgmc.cc:448
@@ -136,9 +136,6 @@ def convergence_series(sampler, nsamples: int, nsteps: int, rows, vals, batch: i
     s0 = sampler.get_sample_index()
     handles = [sampler] + [sampler.clone() for _ in range(min(batch, nsamples) - 1)]
     try:
-        if sampler._fixed_rhs is not None:
-            for h in handles[1:]:
-                h.fix_rhs(sampler._fixed_rhs)
         for k0 in range(0, nsamples, len(handles)):
             ks = list(range(k0, min(k0 + len(handles), nsamples)))
             for h, k in zip(handles, ks):
@@ -220,7 +217,11 @@ def main(argv=None) -> int:
     mg_params = MultigridParameters.from_config(cfg)
     sampling_params = SamplingParameters.from_config(cfg)
     prior_params = PriorParameters.from_config(cfg)
-    measurement_params = MeasurementParameters.from_config(cfg, base)
+    try:
+        measurement_params = MeasurementParameters.from_config(cfg, base)
+    except MeasurementFileError as e:  # parameters.cc:273-276: message on stderr, exit(-1)
+        print(str(e), file=sys.stderr)
+        return -1
     if measurement_params.dim != general.dim:
         print("ERROR: dimension of measurement locations differs from problem dimension")
         return -1

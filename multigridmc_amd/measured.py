@@ -205,3 +205,21 @@ class MeasuredOperator:
 
 
 __all__ = ["V_sphere", "gauss_legendre_order1", "measurement_vector", "LowRankUpdate", "MeasuredOperator"]
+
+
+def synthetic_posterior(prior, m: int, radius: float = 0.0, measure_global: bool = False,
+                        seed: int = 20250219) -> MeasuredOperator:
+    """BASELINE config 5's synthetic posterior: m measurements at fixed pseudo-random interior
+    locations (uniform in [0.1, 0.9]^d, numpy PCG64 seeded with `seed`) with variances on the scale of
+    measurements_template.cfg (1e-6 (1 + U)), optionally the global average (variance_global 0.01 as
+    in parameters_template.cfg).  The measured values stay 0 (f = 0 in the bench); bench.py and the
+    CPU baseline build the same operator from these arguments."""
+    rng = np.random.default_rng(seed)
+    dim = prior.get_lattice().dim
+    mp = MeasurementParameters(radius=radius, variance_scaling=1.0, measure_global=measure_global,
+                               variance_global=0.01)
+    mp.dim = dim
+    mp.measurement_locations = [list(rng.uniform(0.1, 0.9, dim)) for _ in range(m)]
+    mp.variance = list(1e-6 * (1.0 + rng.random(m)))
+    mp.n = m
+    return MeasuredOperator(prior, mp)

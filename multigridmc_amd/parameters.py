@@ -27,6 +27,10 @@ class ConfigError(ValueError):
     pass
 
 
+class MeasurementFileError(ConfigError):
+    """The measurements file named by measurements.filename cannot be opened (parameters.cc:273-276)."""
+
+
 def _tokenize(text: str):
     pos = 0
     out = []
@@ -229,21 +233,28 @@ class MeasurementParameters:
     variance: list = field(default_factory=list)
 
     @classmethod
-    def from_config(cls, cfg: dict, base_dir: str = ".") -> "MeasurementParameters":
+    def from_config(cls, cfg: dict, base_dir: str | None = None) -> "MeasurementParameters":
+        """parameters.cc:245-300.  The measurements file is opened as given, i.e. relative to the
+        working directory, like the reference's readFile(filename); only if that fails is it looked
+        up next to the configuration file (base_dir).  A file found in neither place raises
+        MeasurementFileError with the reference's message (parameters.cc:273-276 prints it and
+        exits with -1): a posterior without its measurements is never built silently."""
         import os
         g = _get(cfg, "measurements")
         p = cls(float(g["radius"]), [float(v) for v in g["sample_location"]], float(g["variance_scaling"]),
                 bool(g["measure_global"]), float(g["mean_global"]), float(g["variance_global"]),
                 str(g["filename"]))
-        path = p.filename if os.path.isabs(p.filename) else os.path.join(base_dir, p.filename)
-        if os.path.exists(path):
-            m = read_config(path)
-            p.dim = int(m["dim"])
-            p.n = int(m["n"])
-            loc = [float(v) for v in m["measurement_locations"]]
-            p.measurement_locations = [loc[p.dim * k:p.dim * (k + 1)] for k in range(p.n)]
-            p.mean = [float(v) for v in m["mean"]]
-            p.variance = [float(v) for v in m["variance"]]
-        else:
-            p.dim = len(p.sample_location)
+        candidates = [p.filename]
+        if base_dir is not None and not os.path.isabs(p.filename):
+            candidates.append(os.path.join(base_dir, p.filename))
+        path = next((c for c in candidates if os.path.isfile(c)), None)
+        if path is None:
+            raise MeasurementFileError(f"ERROR opening configuration file with measurements: '{p.filename}'.")
+        m = read_config(path)
+        p.dim = int(m["dim"])
+        p.n = int(m["n"])
+        loc = [float(v) for v in m["measurement_locations"]]
+        p.measurement_locations = [loc[p.dim * k:p.dim * (k + 1)] for k in range(p.n)]
+        p.mean = [float(v) for v in m["mean"]]
+        p.variance = [float(v) for v in m["variance"]]
         return p

@@ -194,7 +194,8 @@ class MultigridMCSampler:
         self.handle = h
         self.ndof = linear_operator.get_ndof()
         self.nlevel = params.nlevel
-        self._fixed_rhs = None
+        self._fixed_rhs = None   # rhs promised by fix_rhs (apply then skips the upload)
+        self._device_rhs = None  # the rhs the device holds (fix_rhs or the last apply); clones copy it
         if linear_operator.get_m_lowrank() > 0:  # MeasuredOperator (measured.py): Q = A + B Sigma^-1 B^T
             self.set_lowrank(linear_operator.get_B())
 
@@ -254,19 +255,32 @@ class MultigridMCSampler:
         return self.linear_operator
 
     def fix_rhs(self, f):
-        f = _as_f64(f, self.ndof, "f")
+        """Upload f once and keep it resident: later apply() calls use it and do not upload their
+        f argument (the promise of Sampler::fix_rhs, sampler.hh:49-56, as CholeskySampler::apply
+        keeps g_rhs; include/mgmc_sampler.hh behaves the same)."""
+        f = _as_f64(f, self.ndof, "f").copy()
         self._chk(self.lib.mgmc_set_rhs(self.handle, _dp(f), self.ndof))
         self._fixed_rhs = f
+        self._device_rhs = f
 
     def unfix_rhs(self):
+        """apply() uploads its f argument again (the device keeps the last rhs until then)."""
         self._fixed_rhs = None
 
     def apply(self, f, x: np.ndarray):
-        """Draw a new sample x (in/out), one MGMC cycle."""
-        f = _as_f64(f, self.ndof, "f")
+        """Draw a new sample x (in/out), one MGMC cycle (MultigridMCSampler::apply,
+        multigridmc_sampler.cc:132-138).  Without a fixed rhs f is uploaded and used; after fix_rhs
+        the fixed rhs is used and f is not read (pass None or the fixed vector)."""
         if not (isinstance(x, np.ndarray) and x.dtype == np.float64 and x.flags.c_contiguous and x.shape == (self.ndof,)):
             raise ValueError("x must be a contiguous float64 array of length ndof")
+        if self._fixed_rhs is not None:
+            self._chk(self.lib.mgmc_set_state(self.handle, _dp(x), self.ndof))
+            self._chk(self.lib.mgmc_sample(self.handle, 1, -1, None))
+            self._chk(self.lib.mgmc_get_state(self.handle, _dp(x), self.ndof))
+            return
+        f = _as_f64(f, self.ndof, "f").copy()
         self._chk(self.lib.mgmc_apply(self.handle, _dp(f), _dp(x), self.ndof))
+        self._device_rhs = f
 
     # -- device-resident chain (driver_mgmc.cc:66-94) --
     def set_state(self, x):
@@ -289,13 +303,16 @@ class MultigridMCSampler:
     def synchronize(self):
         self._chk(self.lib.mgmc_synchronize(self.handle))
 
-    def sample_timed(self, nsteps: int, qoi_index: int = -1):
-        tot = ctypes.c_double()
-        fine = ctypes.c_double()
-        nfine = ctypes.c_int()
+    def sample_timed(self, nsteps: int, qoi_index: int = -1) -> dict:
+        """nsteps cycles replayed as [fine pre-sampler | coarse correction | fine post-sampler + QoI]
+        graph segments with HIP events on the handle's stream (mgmc_sample_timed)."""
+        tot, pre, post = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        npre, npost = ctypes.c_int(), ctypes.c_int()
         self._chk(self.lib.mgmc_sample_timed(self.handle, int(nsteps), int(qoi_index), ctypes.byref(tot),
-                                             ctypes.byref(fine), ctypes.byref(nfine)))
-        return tot.value, fine.value, nfine.value
+                                             ctypes.byref(pre), ctypes.byref(npre), ctypes.byref(post),
+                                             ctypes.byref(npost)))
+        return {"total_ms": tot.value, "pre_ms": pre.value, "npre": npre.value, "post_ms": post.value,
+                "npost": npost.value}
 
     def qoi_moments(self):
         out = np.zeros(3)
@@ -315,7 +332,12 @@ class MultigridMCSampler:
         """A second handle of the same chain: same operator, parameters, device and Philox key
         (seed, chain_id), its own state, right hand side and HIP stream.  With disjoint sample
         indices it reproduces the draws this handle would make there (batched chains)."""
-        return MultigridMCSampler(self.linear_operator, self.seed, self.params, self.device, self.chain_id)
+        c = MultigridMCSampler(self.linear_operator, self.seed, self.params, self.device, self.chain_id)
+        if self._device_rhs is not None:  # the same right hand side as this handle's device copy
+            c.fix_rhs(self._device_rhs)
+            if self._fixed_rhs is None:
+                c.unfix_rhs()
+        return c
 
     def set_sample_index(self, index: int):
         self._chk(self.lib.mgmc_set_sample_index(self.handle, int(index)))
@@ -401,6 +423,12 @@ class MultigridMCSampler:
 
     def comm_barrier(self):
         self._chk(self.lib.mgmc_comm_barrier(self.handle))
+
+    def comm_info(self) -> dict:
+        """{'rccl_ranks': ncclCommCount (0 without a communicator), 'rccl_rank', 'pci_bus_id'}"""
+        n, r, bus = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self._chk(self.lib.mgmc_comm_info(self.handle, ctypes.byref(n), ctypes.byref(r), ctypes.byref(bus)))
+        return {"rccl_ranks": n.value, "rccl_rank": r.value, "pci_bus_id": bus.value}
 
     def comm_destroy(self):
         self._chk(self.lib.mgmc_comm_destroy(self.handle))

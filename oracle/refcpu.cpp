@@ -1268,6 +1268,13 @@ void orc_set_rhs(orc_handle* h, const double* f) { std::copy(f, f + h->f.size(),
 void orc_set_state(orc_handle* h, const double* x) { std::copy(x, x + h->x.size(), h->x.begin()); }
 void orc_get_state(orc_handle* h, double* x) { std::copy(h->x.begin(), h->x.end(), x); }
 void orc_set_sample_index(orc_handle* h, uint64_t s) { h->ctx.sample = s; }
+// independent chains of one hierarchy (the CPU all-cores baseline forks one process per chain after
+// the setup): FAITHFUL re-seeds the shared mt19937_64 (seed + chain), MULTICOLOUR changes the Philox key
+void orc_reseed(orc_handle* h, uint64_t seed, uint64_t chain) {
+    h->ctx.rng.seed(seed + chain);
+    h->ctx.seed = seed;
+    h->ctx.chain = chain;
+}
 
 // Sampler::apply(f, x)
 void orc_apply(orc_handle* h, const double* f, double* x) { h->mg->apply(f, x); }

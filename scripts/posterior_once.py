@@ -9,5 +9,5 @@ lat = mg.Lattice3d(256, 256, 256)
 op = bench.posterior_operator(mg.ShiftedLaplaceFDOperator(lat, 25.0), int(os.environ.get("M", "8")), 0.0, False)
 s = mg.MultigridMCSampler(op, 1, mg.MultigridParameters(nlevel=6))
 s.sample(3)
-tot, fine, nfine = s.sample_timed(10)
+_t = s.sample_timed(10); tot, fine, nfine = _t["total_ms"], _t["pre_ms"], _t["npre"]
 print("vcycle ms", tot / 10)

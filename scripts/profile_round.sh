@@ -1,11 +1,12 @@
-# Round evidence on the GPU box: (optional) gpu tests, bench (with CPU baseline), rocprofv3 stats
-# of the bench command, PMC traffic of the fine sweep inside V-cycles (separate FETCH_SIZE /
-# WRITE_SIZE passes; the plain pre-sweep kernel instance, as timed by bench.py).
-#   RUN_PYTEST=1 bash scripts/profile_round.sh     BENCH_ARGS="--cpu-samples 1"
+# Round evidence on the GPU box: (optional) gpu tests, the default bench (with the CPU baseline),
+# rocprofv3 stats of the bench command, PMC traffic of both fine sweeps inside V-cycles (separate
+# FETCH_SIZE / WRITE_SIZE passes).
+#   RUN_PYTEST=1 bash scripts/profile_round.sh     BENCH_ARGS="--steps 100"
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/round && export TMPDIR=/tmp
 O=gpurun_out/round
+python -c "import os; print('affinity', len(os.sched_getaffinity(0)), 'cpu_count', os.cpu_count(), 'OMP', os.environ.get('OMP_NUM_THREADS'))" > $O/cpu.txt
 if [ -n "$RUN_PYTEST" ]; then
-  timeout -k 10 1100 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1; rc=$?
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
   echo "pytest rc=$rc"; tail -3 $O/pytest_gpu.log
   [ $rc -eq 0 ] || exit $rc
 fi

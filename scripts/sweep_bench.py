@@ -18,7 +18,7 @@ s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 1, mg.Multigri
 s.time_fine_sweeps(2)
 ms = min(s.time_fine_sweeps(10) / 10 for _ in range(3))
 s.sample(3)
-tot, fine, nfine = s.sample_timed(10)
+_t = s.sample_timed(10); tot, fine, nfine = _t["total_ms"], _t["pre_ms"], _t["npre"]
 print(json.dumps({"sweep_ms": ms, "GBps": 24 * lat.Nvertex / ms / 1e6, "vcycle_ms": tot / 10,
                   "fine_in_cycle_ms": fine / nfine}))
 '''

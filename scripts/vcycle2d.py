@@ -9,5 +9,5 @@ cls = mg.ShiftedLaplaceFEMOperator if os.environ.get("FEM") == "1" else mg.Shift
 s = mg.MultigridMCSampler(cls(lat, 25.0), 1, mg.MultigridParameters(nlevel=int(os.environ.get("NLEVEL", "5"))))
 s.sample(3)
 k = int(os.environ.get("K", "10"))
-tot, fine, nfine = s.sample_timed(k)
+_t = s.sample_timed(k); tot, fine, nfine = _t["total_ms"], _t["pre_ms"], _t["npre"]
 print("vcycle ms", tot / k)

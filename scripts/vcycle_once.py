@@ -8,5 +8,5 @@ lat = mg.Lattice3d(n, n, n) if os.environ.get("DIM", "3") == "3" else mg.Lattice
 s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 1, mg.MultigridParameters(nlevel=int(os.environ.get("NLEVEL", "7")),
                                                                                    ncoarsesmooth=int(os.environ.get("NCS", "1"))))
 s.sample(3)
-tot, fine, nfine = s.sample_timed(int(os.environ.get("K", "10")))
+_t = s.sample_timed(int(os.environ.get("K", "10"))); tot, fine, nfine = _t["total_ms"], _t["pre_ms"], _t["npre"]
 print("vcycle ms", tot / int(os.environ.get("K", "10")))

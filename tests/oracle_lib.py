@@ -51,6 +51,7 @@ def lib():
             "orc_set_state": (None, [c_void_p, _DP]),
             "orc_get_state": (None, [c_void_p, _DP]),
             "orc_set_sample_index": (None, [c_void_p, c_uint64]),
+            "orc_reseed": (None, [c_void_p, c_uint64, c_uint64]),
             "orc_apply": (None, [c_void_p, _DP, _DP]),
             "orc_sample": (None, [c_void_p, c_int, c_int64, _DP]),
             "orc_time_samples": (c_double, [c_void_p, c_int]),

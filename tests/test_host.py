@@ -125,6 +125,35 @@ def test_parameters_template_parses():
     assert meas.variance[7] == 1.864273250664901e-06
 
 
+def test_missing_measurements_file_fails_like_the_reference(tmp_path, monkeypatch, capsys):
+    """parameters.cc:268-276: a measurements file that cannot be opened is an error (message, exit -1),
+    never a posterior with zero measurements.  The name is tried relative to the working directory
+    first (the reference's readFile), then next to the configuration file."""
+    from multigridmc_amd import driver
+    from multigridmc_amd.parameters import MeasurementFileError, MeasurementParameters, read_config
+    text = open(os.path.join(GOLDEN, "parameters_template.cfg")).read()
+    cfg_path = tmp_path / "p.cfg"
+    cfg_path.write_text(text.replace('"measurements_template.cfg"', '"no_such_measurements.cfg"'))
+    cfg = read_config(str(cfg_path))
+    with pytest.raises(MeasurementFileError, match="ERROR opening configuration file with measurements"):
+        MeasurementParameters.from_config(cfg, base_dir=str(tmp_path))
+    monkeypatch.chdir(tmp_path)
+    assert driver.main([str(cfg_path)]) == -1
+    assert "no_such_measurements.cfg" in capsys.readouterr().err
+    # working directory first: a file of that name in the cwd wins over the config directory
+    sub = tmp_path / "cfgdir"
+    sub.mkdir()
+    (sub / "p.cfg").write_text(text)
+    other = open(os.path.join(GOLDEN, "measurements_template.cfg")).read().replace("n =  8;", "n =  7;")
+    (tmp_path / "measurements_template.cfg").write_text(other)
+    meas = MeasurementParameters.from_config(read_config(str(sub / "p.cfg")), base_dir=str(sub))
+    assert meas.n == 7
+    (tmp_path / "measurements_template.cfg").unlink()
+    (sub / "measurements_template.cfg").write_text(open(os.path.join(GOLDEN, "measurements_template.cfg")).read())
+    meas = MeasurementParameters.from_config(read_config(str(sub / "p.cfg")), base_dir=str(sub))
+    assert meas.n == 8
+
+
 def test_measurement_vector_index():
     """radius-0 QoI (measured_operator.cc:74-91): 2D 64^2 [0.5,0.5] -> (32,32); 3D 512^3 -> (256,256,256)."""
     lat = mg.Lattice2d(64, 64)
@@ -216,13 +245,25 @@ def test_cpp_host_side_describe_and_loud_failure(tmp_path):
 
 
 class _FakeChain:
-    """Stands in for a device sampler in bench.Collectives: RCCL unavailable, per-rank moments."""
+    """Stands in for a device sampler in bench.Collectives.  mode: "rehearsal" / "shared" = both ranks
+    report one PCI bus id (with / without MGMC_BENCH_DEVICE); "init_fails" = distinct devices, the
+    communicator cannot be created; "short" = it is created but spans one rank; "ok" = it works (its
+    collectives are simulated over the gloo group, like RCCL would compute them)."""
 
-    def __init__(self, rank):
-        self.rank = rank
+    def __init__(self, rank, mode):
+        self.rank, self.mode, self.comm = rank, mode, False
+
+    def comm_info(self):
+        shared = self.mode in ("rehearsal", "shared")
+        n = {"ok": 2, "short": 1}.get(self.mode, 0) if self.comm else 0
+        return {"rccl_ranks": n, "rccl_rank": self.rank if self.comm else -1,
+                "pci_bus_id": 7 if shared else 7 + self.rank}
 
     def comm_init(self, world, rank, uid):
-        raise mg.MgmcError(-2, "RCCL error invalid usage (test)")
+        assert len(uid) == 128
+        if self.mode == "init_fails":
+            raise mg.MgmcError(-2, "RCCL error invalid usage (test)")
+        self.comm = True
 
     def synchronize(self):
         pass
@@ -230,21 +271,51 @@ class _FakeChain:
     def qoi_moments(self):
         return np.array([10.0 + self.rank, 0.5 * self.rank, 2.0])
 
+    def comm_barrier(self):
+        import torch.distributed as dist
+        dist.barrier()
 
-def _bench_coll_worker(rank, world, port, q):
+    def comm_allreduce_max(self, v):
+        import torch.distributed as dist
+        out = [None, None]
+        dist.all_gather_object(out, v)
+        return max(out)
+
+    def comm_allgather_moments(self, world):
+        import torch.distributed as dist
+        out = [None] * world
+        dist.all_gather_object(out, list(self.qoi_moments()))
+        return np.array(out)
+
+
+def _bench_coll_worker(rank, world, port, mode, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    if mode == "rehearsal":
+        os.environ["MGMC_BENCH_DEVICE"] = "0"
+    import torch.distributed as dist
     import bench
-    c = bench.Collectives(_FakeChain(rank), rank, world)
+    bench.mg.comm_unique_id = lambda: bytes(128)
+    try:
+        c = bench.Collectives(_FakeChain(rank, mode), rank, world)
+    except (bench.CommError, mg.MgmcError) as e:
+        q.put((rank, type(e).__name__, str(e), None, None, None))
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     c.barrier()
-    q.put((rank, c.rccl, c.max(1.0 + rank), c.allgather_moments().tolist()))
+    q.put((rank, c.kind, c.rccl_ranks, c.max(1.0 + rank), c.allgather_moments().tolist(), None))
     c.dist.barrier()
     c.dist.destroy_process_group()
 
 
-def test_bench_collectives_fall_back_to_gloo_world2():
-    """bench.py's N > 1 collectives (barrier, max time, per-chain moments) when the RCCL
-    communicator cannot be created: the same values over gloo, identical on every rank."""
+@pytest.mark.parametrize("mode", ["rehearsal", "ok", "shared", "init_fails", "short"])
+def test_bench_collectives_world2(mode):
+    """bench.py's N > 1 collectives (barrier, max time, per-chain moments, world_size 2 on gloo):
+    RCCL on distinct devices reports collectives "rccl" and the communicator's rank count; ranks
+    sharing a device run gloo collectives only as an explicit rehearsal (MGMC_BENCH_DEVICE); a
+    shared device without it, a communicator that fails, or one that spans fewer ranks is an error
+    on every rank (bench.main exits non-zero), never a silent gloo fallback."""
     import socket
 
     import torch.multiprocessing as tmp
@@ -254,7 +325,7 @@ def test_bench_collectives_fall_back_to_gloo_world2():
     s.close()
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_bench_coll_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_bench_coll_worker, args=(r, 2, port, mode, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in procs))
@@ -262,6 +333,16 @@ def test_bench_collectives_fall_back_to_gloo_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     for r in range(2):
-        rccl, tmax, parts = res[r]
-        assert rccl is False and tmax == 2.0
-        assert parts == [[10.0, 0.0, 2.0], [11.0, 0.5, 2.0]]
+        if mode in ("rehearsal", "ok"):
+            kind, nranks, tmax, parts, _ = res[r]
+            assert kind == ("gloo" if mode == "rehearsal" else "rccl")
+            assert nranks == (0 if mode == "rehearsal" else 2)
+            assert tmax == 2.0
+            assert parts == [[10.0, 0.0, 2.0], [11.0, 0.5, 2.0]]
+        else:
+            err, msg = res[r][0], res[r][1]
+            assert err == ("MgmcError" if mode == "init_fails" else "CommError"), (err, msg)
+            if mode == "shared":
+                assert "share GPUs" in msg
+            if mode == "short":
+                assert "spans 1 ranks" in msg
