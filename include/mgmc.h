@@ -46,6 +46,9 @@ extern "C" {
 #define MGMC_E_HIP -2       /* HIP runtime error (incl. no device)        */
 #define MGMC_E_NOMEM -3     /* device allocation failed                   */
 #define MGMC_E_UNSUPPORTED -4 /* feature not (yet) on the device path     */
+#define MGMC_E_NONFINITE -5 /* the chain state became NaN / Inf (guard on the QoI vertex, or the
+                               lattice centre without a QoI, checked after every cycle); the flag
+                               stays set until mgmc_set_state */
 
 /* smoother kinds (parameters.hh:145-174 MultigridParameters::smoother) */
 #define MGMC_SMOOTHER_SOR 0   /* forward SOR pre-sampler, backward SOR post-sampler */

@@ -17,6 +17,7 @@ MGMC_E_INVALID = -1
 MGMC_E_HIP = -2
 MGMC_E_NOMEM = -3
 MGMC_E_UNSUPPORTED = -4
+MGMC_E_NONFINITE = -5
 
 SMOOTHER_SOR = 0
 SMOOTHER_SSOR = 1

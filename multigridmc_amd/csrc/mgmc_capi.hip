@@ -23,7 +23,6 @@
 #include "mgmc_kernels.hpp"
 #include "mgmc_zsweep.hpp"
 #include "mgmc_zrestrict.hpp"
-#include "mgmc_zsweepres.hpp"
 #include "mgmc_tail.hpp"
 #include "mgmc_gsweep.hpp"
 #include "mgmc_rb2d.hpp"
@@ -70,15 +69,73 @@ struct Op {
     int lr_coarse_patch = 0;  // OP_RESIDUAL_RESTRICT: ... and the coarse level's first pre-sweep
     uint32_t lr_coarse_tag = 0;
     int tail = -1;           // OP_TAIL: index into mgmc_handle::tail_args
-    int restrict_fused = 0;  // OP_SWEEP: also does the following residual + restriction (k_zsweep_res7);
                              // OP_RESIDUAL_RESTRICT: done by the previous sweep (no launch)
 };
 
 
+// Kernel-path switches.  Every default fast path has a general fallback (the same arithmetic, bitwise
+// equal); MGMC_DISABLE=<comma list> turns fast paths off at mgmc_create so the variant tests
+// (tests/test_gpu_parity.py test_variant_cycles_bitwise, test_gpu_lowrank.py) can run the fallbacks
+// on shapes where the fast path would be taken.  Read once per handle; unknown tokens are an error.
+enum PathFlag : uint32_t {
+    PATH_NO_TAIL = 1u << 0,               // coarsest levels as separate launches instead of k_tail
+    PATH_NO_FUSE_PROLONG = 1u << 1,       // separate prolongate-add pass before the first post-sweep
+    PATH_NO_QUADS = 1u << 2,              // colour-pair passes instead of two pairs per launch
+    PATH_NO_RB2D = 1u << 3,               // 2D fine level: colour passes instead of k_rb2d
+    PATH_NO_ZSWEEP = 1u << 4,             // 3D fine level: colour passes instead of k_zsweep_rb7
+    PATH_NO_PAIRS = 1u << 5,              // Galerkin levels: per-colour passes instead of pair passes
+    PATH_NO_ZRESTRICT = 1u << 6,          // residual + restriction: per-point gather kernel
+    PATH_NO_LR_SMALL = 1u << 7,           // low-rank fix: generic multi-launch path instead of k_lr_small
+    PATH_NO_LR_MERGE = 1u << 8,           // low-rank: separate restore / patch launches around restriction
+    PATH_NO_LR_PREFETCH = 1u << 9,        // low-rank small fix without the up-front loads
+    PATH_NO_COARSE_PRECOMPUTE = 1u << 10, // coarse SSOR: right-hand sides inside the colour passes
+};
+
+struct PathToken {
+    const char* name;
+    uint32_t flag;
+};
+constexpr PathToken kPathTokens[] = {
+    {"tail", PATH_NO_TAIL},           {"fuse_prolong", PATH_NO_FUSE_PROLONG},
+    {"quads", PATH_NO_QUADS},         {"rb2d", PATH_NO_RB2D},
+    {"zsweep", PATH_NO_ZSWEEP},       {"pairs", PATH_NO_PAIRS},
+    {"zrestrict", PATH_NO_ZRESTRICT}, {"lr_small", PATH_NO_LR_SMALL},
+    {"lr_merge", PATH_NO_LR_MERGE},   {"lr_prefetch", PATH_NO_LR_PREFETCH},
+    {"coarse_precompute", PATH_NO_COARSE_PRECOMPUTE},
+};
+
+// parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
+bool read_path_flags(uint32_t* flags, std::string* bad) {
+    *flags = 0;
+    const char* e = getenv("MGMC_DISABLE");
+    if (!e) return true;
+    std::string list(e);
+    size_t pos = 0;
+    while (pos <= list.size()) {
+        size_t end = list.find(',', pos);
+        if (end == std::string::npos) end = list.size();
+        const std::string tok = list.substr(pos, end - pos);
+        if (!tok.empty()) {
+            bool found = false;
+            for (const PathToken& t : kPathTokens)
+                if (tok == t.name) {
+                    *flags |= t.flag;
+                    found = true;
+                }
+            if (!found) {
+                *bad = tok;
+                return false;
+            }
+        }
+        pos = end + 1;
+    }
+    return true;
+}
+
 // z-marching sweep tile shape (mgmc_zsweep.hpp)
 // 32 x-pairs x 16 rows, 256 threads (2 core pairs per thread, 19.5 % halo), 38 KB of LDS -> 4
 // workgroups per CU; tuning history in DESIGN.md
-constexpr int ZS_XP = 32, ZS_TY = 16, ZS_NT = 256, ZS_MINW = 1, ZS_TZ = 32;
+constexpr int ZS_XP = 32, ZS_TY = 16, ZS_NT = 256, ZS_MINW = 1, ZS_TZ = 32, ZS_TZP = 64;
 #ifndef MGMC_ZS_MINW_PROLONG
 #define MGMC_ZS_MINW_PROLONG 3  // waves/SIMD floor of the fused-prolongation variant (3: 167 VGPRs, no spill; 4 spills)
 #endif
@@ -123,6 +180,7 @@ struct Level {
     double* scratch[3] = {nullptr, nullptr, nullptr};
     size_t lds_bytes = 0;  // >0 if the whole-level LDS kernel can hold x and f
     int num_cu = 256;      // compute units of the handle's device (grid sizing; MI355X: 256)
+    uint32_t paths = 0;    // PathFlag bits of the handle (MGMC_DISABLE)
     bool zsweep = false;   // fused z-marching red-black sweep available
     bool pairs = false;    // Galerkin level swept in colour-pair passes (mgmc_gsweep.hpp)
     bool quads = false;    // ... two pairs per launch, out of place (k_sweep_quads)
@@ -156,17 +214,20 @@ struct mgmc_handle {
     size_t seg_end_pre = 0, seg_begin_post = 0, seg_end_post = 0;  // fine-sweep segments
     hipGraphExec_t graph_all = nullptr;
     hipGraphExec_t graph_unroll = nullptr;  // unroll copies of the cycle in one graph (sample loops)
+    // the cycle with four event-record nodes (before the fine pre-sampler, after it, before the fine
+    // post-sampler, after the QoI record): mgmc_sample_timed points them at per-step events
+    hipGraph_t graph_timed_src = nullptr;
+    hipGraphExec_t graph_timed = nullptr;
+    hipGraphNode_t timed_node[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t timed_ev0[4] = {nullptr, nullptr, nullptr, nullptr};
     int unroll = 1;
-    hipGraphExec_t graph_seg[4] = {nullptr, nullptr, nullptr, nullptr};
     int64_t qoi_store_index = -1;
     std::string last_error;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     double* comm_buf = nullptr;  // device scratch for collectives
-    bool fuse_prolong = false;   // prolongate-add fused into the first post-sweep (z-sweep levels)
-    bool rb2d_prolong = false;   // ... also on 2D red-black levels (opt-in MGMC_RB2D_PROLONG)
-    int tail_nt = 1024;          // k_tail workgroup size (MGMC_TAIL_NT)
-    bool fuse_restrict = false;  // last pre-sweep + residual + restriction in one kernel (z-sweep levels)
+    uint32_t paths = 0;          // PathFlag bits (MGMC_DISABLE)
+    int unroll_override = 0;     // MGMC_GRAPH_UNROLL (cycles per sample-loop graph launch; 0 = by size)
     std::vector<TailArgs*> tail_args;  // device copies, one per OP_TAIL
     std::vector<size_t> tail_lds;      // dynamic LDS bytes per OP_TAIL
     double* sv[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // solver: b x r z p q (level 0)
@@ -273,21 +334,6 @@ void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s)
         hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 0, MINW>), dim3(nb), dim3(NT), lds, s, a);
 }
 
-// tile-shape variant (MGMC_ZS_VARIANT, for tuning experiments; 0 = default)
-int zsweep_variant() {
-    const char* v = getenv("MGMC_ZS_VARIANT");
-    return v ? atoi(v) : 0;
-}
-
-// x-pairs per tile of the selected variant (the fine nx must be a multiple of 2 * xp)
-int zsweep_xp() {
-    switch (zsweep_variant()) {
-        case 1: case 2: case 3: case 4: case 7: case 11: case 13: return 64;
-        case 5: case 6: case 8: case 9: case 12: case 14: return 32;
-        default: return ZS_XP;
-    }
-}
-
 void launch_zsweep(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g0,
                    int direction, const Level* coarse, const double* xc, double alpha, hipStream_t s) {
     ZSweepArgs a;
@@ -301,78 +347,23 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
     a.S = lv.S;
     a.G = g0;
     a.G.colour = (direction == MGMC_FORWARD) ? 0 : 1;
-    const char* tz = getenv(coarse ? "MGMC_ZS_TZP" : "MGMC_ZS_TZ");
-    a.tz = std::max(2, (tz ? atoi(tz) : ZS_TZ) & ~1);  // even: chunks start on odd planes (coarse ring schedule)
-    if (!tz) {  // shallower z chunks until the grid has >= 1024 tiles (4 per CU): 256^3 -> 16 planes
-        const int xp = zsweep_xp(), ty = zsweep_variant() == 0 ? ZS_TY : 16;
-        const long long txy = (long long)((lv.L.nx / 2) / xp) * ((lv.L.ny - 1 + ty - 1) / ty);
-        while (a.tz > 8 && txy * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 1024) a.tz /= 2;
-        if (coarse && zsweep_variant() == 0) {
-            // fused-prolongation sweep: 512-thread workgroups (one core pair per thread: 127 VGPRs,
-            // 2 workgroups = 16 waves per CU against 3 x 4 waves with 256 threads, which the 6.7 KB
-            // coarse ring and 161 VGPRs allowed) and chunks up to 64 planes deep as long as the grid
-            // keeps two rounds of workgroups (512^3: tz 64, 2,048 tiles, 906-911 -> 841-851 us;
-            // 256^3: tz 16, 142 -> 118 us; interleaved A/B)
-            a.tz = 64;
-            while (a.tz > 8 && txy * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 2LL * 2 * lv.num_cu) a.tz /= 2;
-        }
-    }
-    const bool pr = coarse != nullptr;
-    if (pr && zsweep_variant() == 0 && getenv("MGMC_ZS_PROLONG256") == nullptr) {
-        launch_zsweep_t<32, 16, 512, 4>(lv, a, pr, s);
+    const long long txy = (long long)((lv.L.nx / 2) / ZS_XP) * ((lv.L.ny - 1 + ZS_TY - 1) / ZS_TY);
+    if (coarse) {
+        // fused-prolongation sweep: 512-thread workgroups (one core pair per thread: 127 VGPRs,
+        // 2 workgroups = 16 waves per CU against 3 x 4 waves with 256 threads, which the 6.7 KB
+        // coarse ring and 161 VGPRs allowed) and chunks up to 64 planes deep as long as the grid
+        // keeps two rounds of workgroups (512^3: tz 64, 2,048 tiles, 906-911 -> 841-851 us;
+        // 256^3: tz 16, 142 -> 118 us; interleaved A/B).  tz stays even: chunks start on odd planes
+        // (coarse ring schedule)
+        a.tz = ZS_TZP;
+        while (a.tz > 8 && txy * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 2LL * 2 * lv.num_cu) a.tz /= 2;
+        launch_zsweep_t<ZS_XP, ZS_TY, 2 * ZS_NT, 4>(lv, a, true, s);
         return;
     }
-    switch (zsweep_variant()) {
-        case 1: launch_zsweep_t<64, 4, 256>(lv, a, pr, s); break;
-        case 2: launch_zsweep_t<64, 8, 512>(lv, a, pr, s); break;
-        case 3: launch_zsweep_t<64, 8, 256>(lv, a, pr, s); break;
-        case 4: launch_zsweep_t<64, 16, 512>(lv, a, pr, s); break;
-        case 5: launch_zsweep_t<32, 16, 256>(lv, a, pr, s); break;
-        case 6: launch_zsweep_t<32, 24, 384>(lv, a, pr, s); break;
-        case 7: launch_zsweep_t<64, 12, 384>(lv, a, pr, s); break;
-        case 8: launch_zsweep_t<32, 12, 192>(lv, a, pr, s); break;
-        case 9: launch_zsweep_t<32, 8, 256>(lv, a, pr, s); break;
-        case 11: launch_zsweep_t<64, 16, 512, 4>(lv, a, pr, s); break;
-        case 12: launch_zsweep_t<32, 32, 512, 4>(lv, a, pr, s); break;
-        case 13: launch_zsweep_t<64, 32, 1024, 4>(lv, a, pr, s); break;
-        case 14: launch_zsweep_t<32, 16, 512, 4>(lv, a, pr, s); break;  // one core pair per thread
-        default: launch_zsweep_t<ZS_XP, ZS_TY, ZS_NT, ZS_MINW>(lv, a, pr, s); break;
-    }
-}
-
-// last pre-sweep + residual + restriction of a fine 7-point z-sweep level (mgmc_zsweepres.hpp, opt-in
-// MGMC_FUSE_RESTRICT):
-// 32 x 8 coarse points (64 x 16 fine output vertices) per workgroup, 384 threads, 53 KB of LDS -> 2
-// workgroups per CU; kz = 16 coarse planes per chunk (32 output planes)
-constexpr int ZR_CX = 32, ZR_CY = 8, ZR_NT = 384, ZR_KZ = 16;
-bool zsweepres_eligible(const Level& lf, const Level& lc) {
-    return lf.zsweep && lf.spec.dim == 3 && lf.spec.npoints == 7 && lf.lr.m == 0 && lc.L.nx >= 32 &&
-           lf.L.nx % (2 * ZR_CX) == 0 && 2 * lc.L.nx == lf.L.nx && 2 * lc.L.ny == lf.L.ny && 2 * lc.L.nz == lf.L.nz;
-}
-void launch_zsweepres(const Level& lv, const Level& lc, const double* xin, double* xout, const GibbsArg& g0,
-                      int direction, hipStream_t s) {
-    ZSweepResArgs a;
-    a.L = lv.L;
-    a.Lc = lc.L;
-    a.xin = xin;
-    a.xout = xout;
-    a.f = lv.f;
-    a.fc = lc.f;
-    a.xc = lc.x;
-    a.S = lv.S;
-    a.G = g0;
-    a.G.colour = (direction == MGMC_FORWARD) ? 0 : 1;
-    const char* kz = getenv("MGMC_ZSR_KZ");
-    a.kz = std::max(1, kz ? atoi(kz) : ZR_KZ);
-    a.ntx = (lc.L.nx - 1 + ZR_CX - 1) / ZR_CX;
-    a.nty = (lc.L.ny - 1 + ZR_CY - 1) / ZR_CY;
-    if (!kz)  // shallower chunks until the grid has >= 512 tiles (2 per CU)
-        while (a.kz > 2 && (long long)a.ntx * a.nty * ((lc.L.nz - 1 + a.kz - 1) / a.kz) < 512) a.kz /= 2;
-    a.ntz = (lc.L.nz - 1 + a.kz - 1) / a.kz;
-    const int ntiles = a.ntx * a.nty * a.ntz;
-    const int nb = (ntiles + 7) / 8 * 8;
-    hipLaunchKernelGGL((k_zsweep_res7<ZR_CX, ZR_CY, ZR_NT>), dim3(nb), dim3(ZR_NT), zsweepres_lds_bytes(ZR_CX, ZR_CY),
-                       s, a);
+    // shallower z chunks until the grid has >= 1024 tiles (4 per CU): 256^3 -> 16 planes
+    a.tz = ZS_TZ;
+    while (a.tz > 8 && txy * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 1024) a.tz /= 2;
+    launch_zsweep_t<ZS_XP, ZS_TY, ZS_NT, ZS_MINW>(lv, a, false, s);
 }
 
 // colour-pair passes of a Galerkin 9/27-point level (in place): forward colours (0,1), (2,3), ...,
@@ -381,40 +372,27 @@ bool pairs_eligible(const LevelSpec& sp, const Layout& L) {
     return (sp.npoints == 27 || sp.npoints == 9) && L.nx / 2 >= 1 && L.nx / 2 <= 256 && L.nx % 2 == 0;
 }
 
-// both colour pairs of a k-parity half per launch (k_sweep_quads, opt-in MGMC_QUADS): rows of up to
-// 128 pairs, so that a workgroup holds >= 7 full rows (<= 1 recomputed row in 7).  Bitwise equal to
-// the pair passes but slower at 512^3 (level 1: 2 x 105 us against 4 x 40 us per sweep):
-// the second pair's loads wait for the first pair's rows, and 512-thread workgroups hide less latency
-// default (small levels): rows of <= 32 pairs, where each pass is launch-latency bound and halving the
-// launches pays (256^3: 63^3 level 4 x 5.0 -> 2 x 7.6 us, 31^3 level 4 x 4.8 -> 2 x 6.3 us per sweep);
-// MGMC_QUADS: every level with rows of <= 128 pairs (slower on the large levels, tests); MGMC_NO_QUADS:
-// none; MGMC_QUADS_MAXPAIR=n: rows of <= n pairs.  2D: every pair-pass level.  Levels that k_tail will
-// run are left to it (caller).
-bool quads_eligible(const LevelSpec& sp, const Layout& L) {
-    if (!pairs_eligible(sp, L) || getenv("MGMC_NO_QUADS") != nullptr) return false;
-    if (const char* mp = getenv("MGMC_QUADS_MAXPAIR")) return L.nx / 2 <= atoi(mp);
-    // 2D levels are launch-bound at every size of the benchmark configs: one launch per sweep instead
-    // of two (2D 1024^2 FD cycle 0.135 -> 0.129 ms, FEM 0.147 -> 0.139 ms, A/B in one box call)
-    if (sp.dim == 2) return true;
-    return L.nx / 2 <= (getenv("MGMC_QUADS") != nullptr ? 128 : 32);
+// both colour pairs of a k-parity half per launch (k_sweep_quads): on levels with rows of <= 32
+// pairs, where each pair pass is launch-latency bound and halving the launches pays (256^3: 63^3
+// level 4 x 5.0 -> 2 x 7.6 us, 31^3 level 4 x 4.8 -> 2 x 6.3 us per sweep), and on every 2D pair-pass
+// level (2D 1024^2 FD cycle 0.135 -> 0.129 ms, FEM 0.147 -> 0.139 ms; A/B in one box call).  On the
+// large 3D levels it loses (512^3 level 1: 2 x 105 us against 4 x 41 us per sweep): the
+// second pair's loads wait for the first pair's rows.  Levels that k_tail runs are left to it (caller).
+bool quads_eligible(const LevelSpec& sp, const Layout& L, uint32_t paths) {
+    if (!pairs_eligible(sp, L) || (paths & PATH_NO_QUADS)) return false;
+    return sp.dim == 2 || L.nx / 2 <= 32;
 }
 
 // one red-black sweep of a 2D 5-point level, xin -> xout (mgmc_rb2d.hpp)
-// lc: the coarse level whose x is prolongated into the staged state first (fused first post-sweep)
 void launch_rb2d(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
-                 bool noise, hipStream_t s, const Level* lc = nullptr, double alpha = 0.0) {
+                 bool noise, hipStream_t s) {
     const int ntx = (lv.L.nx - 1 + RB2_TW - 1) / RB2_TW, nty = (lv.L.ny - 1 + RB2_TH - 1) / RB2_TH;
     const int c1 = direction == MGMC_FORWARD ? 0 : 1;
-    const Layout Lc = lc ? lc->L : lv.L;
-    const double* xc = lc ? lc->x : nullptr;
     const dim3 grid(ntx * nty), block(RB2_NT);
-    if (lc && noise)
-        hipLaunchKernelGGL((k_rb2d<true, true>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx, Lc, xc, alpha);
-    else if (noise)
-        hipLaunchKernelGGL((k_rb2d<true, false>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx, Lc, xc, alpha);
+    if (noise)
+        hipLaunchKernelGGL((k_rb2d<true>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx);
     else
-        hipLaunchKernelGGL((k_rb2d<false, false>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx, Lc, xc,
-                           alpha);
+        hipLaunchKernelGGL((k_rb2d<false>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx);
 }
 
 void launch_quads(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
@@ -494,7 +472,7 @@ void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStrea
     // precomputed right hand sides (k_coarse_ssor_lds) when they fit next to x and f
     const long long ndof = (long long)(lv.L.nx - 1) * (lv.L.ny - 1) * (dim == 3 ? lv.L.nz - 1 : 1);
     const size_t lds_pre = lv.lds_bytes + (size_t)nsweeps * ndof * sizeof(double);
-    const int pre = lds_pre <= 150 * 1024 && getenv("MGMC_COARSE_NO_PRE") == nullptr;
+    const int pre = lds_pre <= 150 * 1024 && !(lv.paths & PATH_NO_COARSE_PRECOMPUTE);
     const size_t lds = pre ? lds_pre : lv.lds_bytes;
 #define MGMC_COARSE_LAUNCH(D, P)                                                                                 \
     do {                                                                                                           \
@@ -527,10 +505,9 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
     a.nty = (lc.L.ny - 1 + CY - 1) / CY;
     // 8 coarse planes per workgroup, fewer on small levels so the grid still fills the chip
     // (512^3 level 1 -> 2: kz 4, 103 us against 116 / 146 us with 2 / 8)
-    const char* kz = getenv("MGMC_ZR_KZ");
     const long long work = (long long)a.ntx * a.nty * (lc.L.nz - 1);
-    a.kz = kz ? atoi(kz) : (work >= 8 * 1024 ? 8 : (work >= 4 * 1024 ? 4 : (work >= 512 ? 2 : 1)));
-    if (!kz && NPTS == 7 && work >= 16 * 1024) {
+    a.kz = work >= 8 * 1024 ? 8 : (work >= 4 * 1024 ? 4 : (work >= 512 ? 2 : 1));
+    if (NPTS == 7 && work >= 16 * 1024) {
         // fine 7-point level: the deepest chunks that still give two full rounds of workgroups (every
         // chunk re-reads 2 x planes and 1 f plane below / above it: 512^3 with 64 x 4 tiles kz 8 -> 43
         // (6 chunks, 1536 tiles on 256 CUs x 3 workgroups): 561 -> 451 us; with 64 x 8 tiles kz 32)
@@ -550,17 +527,10 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
     // z-marching kernel on every 3D level with coarse n >= 8: 64 x 4 coarse points per workgroup from
     // coarse n = ZR_SMALL_NX up, 16 x 4 points (one wavefront) below, where the wide tiles would leave
     // most of the chip idle (the 27-point gather kernel took 24 us per launch on the 15^3 / 7^3 levels)
-    const char* zsn = getenv("MGMC_ZR_SMALL_NX");
-    const int small_nx = zsn ? atoi(zsn) : 32;
-    if (lf.spec.dim == 3 && zero_xc && getenv("MGMC_NO_ZRESTRICT") == nullptr && lc.L.nx >= 8) {
-        const int v = getenv("MGMC_ZR_VARIANT") ? atoi(getenv("MGMC_ZR_VARIANT")) : 0;
-        const bool small = lc.L.nx < small_nx;
+    if (lf.spec.dim == 3 && zero_xc && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8) {
+        const bool small = lc.L.nx < 32;
         if (lf.spec.npoints == 7) {
-            if (v == 1) launch_zresrestrict_t<7, 32, 4, 128>(lf, lc, x, f, fc, xc, s);
-            else if (v == 3) launch_zresrestrict_t<7, 32, 8, 256>(lf, lc, x, f, fc, xc, s);
-            else if (v == 2) launch_zresrestrict_t<7, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
-            else if (v == 5) launch_zresrestrict_t<7, 64, 4, 512>(lf, lc, x, f, fc, xc, s);
-            else if (small) launch_zresrestrict_t<7, 16, 4, 64>(lf, lc, x, f, fc, xc, s);
+            if (small) launch_zresrestrict_t<7, 16, 4, 64>(lf, lc, x, f, fc, xc, s);
             // 64 x 8 coarse points, 512 threads, 80 KB of LDS (2 workgroups per CU): half the y halo
             // of 64 x 4 (19 x planes rows per 16 fine rows instead of 11 per 8); 512^3 with kz 32:
             // 505-525 -> 488-502 us (interleaved A/B); at 256^3 too few tiles (73 against 66 us)
@@ -568,9 +538,7 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
                 launch_zresrestrict_t<7, 64, 8, 512>(lf, lc, x, f, fc, xc, s);
             else launch_zresrestrict_t<7, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
         } else {
-            if (v == 1) launch_zresrestrict_t<27, 32, 4, 128>(lf, lc, x, f, fc, xc, s);
-            else if (v == 3) launch_zresrestrict_t<27, 32, 8, 256>(lf, lc, x, f, fc, xc, s);
-            else if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s);
+            if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s);
             else launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
         }
         return;
@@ -589,21 +557,12 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
 }
 
 void launch_prolongate(const Level& lf, const Level& lc, double* x, const double* xc, double alpha, hipStream_t s) {
-    if (getenv("MGMC_OLD_PROLONG") == nullptr) {
-        dim3 block(64, 4, 1);
-        dim3 grid = grid3(lf.L.nx / 2, lf.L.ny - 1, lf.spec.dim == 3 ? lf.L.nz - 1 : 1, block);
-        if (lf.spec.dim == 3)
-            hipLaunchKernelGGL((k_prolongate_pairs<3>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha);
-        else
-            hipLaunchKernelGGL((k_prolongate_pairs<2>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha);
-        return;
-    }
     dim3 block(64, 4, 1);
-    dim3 grid = grid3(lf.L.nx - 1, lf.L.ny - 1, lf.spec.dim == 3 ? lf.L.nz - 1 : 1, block);
+    dim3 grid = grid3(lf.L.nx / 2, lf.L.ny - 1, lf.spec.dim == 3 ? lf.L.nz - 1 : 1, block);
     if (lf.spec.dim == 3)
-        hipLaunchKernelGGL((k_prolongate_add<3>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha);
+        hipLaunchKernelGGL((k_prolongate_pairs<3>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha);
     else
-        hipLaunchKernelGGL((k_prolongate_add<2>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha);
+        hipLaunchKernelGGL((k_prolongate_pairs<2>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha);
 }
 
 void launch_pack(const Level& lv, const double* lex, double* pad, bool pack, hipStream_t s) {
@@ -698,7 +657,7 @@ void lr_small(const mgmc_handle* h, const Level& lv, double* x, int direction, i
     a.tag = next_tag;
     a.sample = sample;
     // k_lr_small_pf: one entry per lane, <= 8 columns, <= 2 rows of B_bar and of B per thread
-    if (r.m <= 8 && r.max_col_n <= 64 && a.nbar <= 2048 && a.nrows <= 2048 && getenv("MGMC_LR_NO_PF") == nullptr)
+    if (r.m <= 8 && r.max_col_n <= 64 && a.nbar <= 2048 && a.nrows <= 2048 && !(lv.paths & PATH_NO_LR_PREFETCH))
         hipLaunchKernelGGL((k_lr_small_pf<8, 2>), dim3(1), dim3(1024), 0, s, a);
     else
         hipLaunchKernelGGL(k_lr_small, dim3(1), dim3(1024), 0, s, a);
@@ -789,11 +748,11 @@ void launch_coarse_chol(const mgmc_handle* h, const Level& lv, const double* f, 
 void push_sweep(mgmc_handle* h, std::vector<int>& cur, int level, int direction, uint32_t& tag, int& pending_prolong) {
     Op op{OP_SWEEP, level, direction, tag++, 1};
     const Level& lv = h->levels[level];
-    // fused prolongation: z-sweep levels by default; the 2D red-black kernel only with
-    // MGMC_RB2D_PROLONG (bitwise, but its staging becomes a longer latency chain: 2D 1024^2 cycle
-    // 0.1292-0.1305 -> 0.1306-0.1316 ms against the separate k_prolongate_pairs launch)
-    const bool fold = lv.zsweep || (lv.rb2d && h->rb2d_prolong);
-    if (lv.pingpong() && pending_prolong && !(fold && h->fuse_prolong)) {
+    // fused prolongation on z-sweep levels (the 2D red-black kernel does not fold it: its staging
+    // becomes a longer latency chain, 2D 1024^2 cycle 0.1292-0.1305 -> 0.1306-0.1316 ms against the
+    // separate k_prolongate_pairs launch, measured in round 1)
+    const bool fold = lv.zsweep && !(h->paths & PATH_NO_FUSE_PROLONG);
+    if (lv.pingpong() && pending_prolong && !fold) {
         h->ops.push_back({OP_PROLONGATE, level, 0, 0, 0});
         h->ops.back().src = cur[level];
         pending_prolong = 0;
@@ -889,17 +848,6 @@ void build_ops(mgmc_handle* h) {
     }
     h->ops.push_back({OP_QOI, 0, 0, 0, 0});
     if (h->levels.size() == 1) h->seg_end_pre = h->seg_begin_post = h->seg_end_post = 0;
-    // the last pre-sweep of a fine 7-point z-sweep level takes over the residual + restriction
-    if (h->fuse_restrict)
-        for (size_t q = 0; q + 1 < h->ops.size(); ++q) {
-            Op& op = h->ops[q];
-            Op& nx = h->ops[q + 1];
-            if (op.kind == OP_SWEEP && nx.kind == OP_RESIDUAL_RESTRICT && op.level == nx.level && !op.prolong &&
-                nx.src == 1 - op.src && zsweepres_eligible(h->levels[op.level], h->levels[op.level + 1])) {
-                op.restrict_fused = 1;
-                nx.restrict_fused = 1;
-            }
-        }
     // small low-rank levels: the kernel after a sweep also patches f for the level's next op
     for (size_t q = 0; q + 1 < h->ops.size(); ++q) {
         Op& op = h->ops[q];
@@ -918,11 +866,11 @@ void build_ops(mgmc_handle* h) {
     // first post-sweep (nothing writes f in between: the ops of coarser levels and this level's
     // prolongation touch only coarser f and this level's x) and for the coarse level's first
     // pre-sweep -- one launch instead of three
-    if (getenv("MGMC_LR_NO_MERGE") == nullptr)
+    if (!(h->paths & PATH_NO_LR_MERGE))
         for (size_t q = 0; q < h->ops.size(); ++q) {
             Op& op = h->ops[q];
             const int l = op.level;
-            if (op.kind != OP_RESIDUAL_RESTRICT || op.restrict_fused || h->levels[l].lr.m == 0) continue;
+            if (op.kind != OP_RESIDUAL_RESTRICT || h->levels[l].lr.m == 0) continue;
             if (q + 1 < h->ops.size()) {
                 Op& nx = h->ops[q + 1];
                 if (nx.kind == OP_SWEEP && nx.level == l + 1 && h->levels[l + 1].lr.m > 0 && !nx.lr_skip_patch) {
@@ -946,6 +894,8 @@ void build_ops(mgmc_handle* h) {
 
 // ---- the coarsest levels' sub-cycle in one workgroup (k_tail) ----
 constexpr size_t TAIL_LDS_LIMIT = 150 * 1024;
+// one 1024-thread workgroup (1024 / 512 / 256 threads: 256^3 cycle 0.529 / 0.538 / 0.570 ms, round 1)
+constexpr int TAIL_NT = 1024;
 
 Layout tail_layout(const Layout& L) {
     Layout G = L;
@@ -957,8 +907,8 @@ Layout tail_layout(const Layout& L) {
 }
 
 // the same choice from the level shapes alone (at creation time, before any level is allocated)
-int tail_start_by_size(const std::vector<LevelSpec>& specs, const mgmc_config& cfg) {
-    if (getenv("MGMC_NO_TAIL") != nullptr || cfg.coarse_solver != MGMC_COARSE_SSOR) return -1;
+int tail_start_by_size(const std::vector<LevelSpec>& specs, const mgmc_config& cfg, uint32_t paths) {
+    if ((paths & PATH_NO_TAIL) || cfg.coarse_solver != MGMC_COARSE_SSOR) return -1;
     const int L = (int)specs.size();
     for (int lt = 1; lt + 1 < L; ++lt) {
         bool ok = true;
@@ -980,7 +930,7 @@ int tail_start_by_size(const std::vector<LevelSpec>& specs, const mgmc_config& c
 // one (k_lr_small's), ordinary (in-place) sweeps, SSOR coarse sampler; -1 if none or only the
 // coarsest level fits (the coarse LDS kernel covers that)
 int tail_level(const mgmc_handle* h) {
-    if (getenv("MGMC_NO_TAIL") != nullptr || h->cfg.coarse_solver != MGMC_COARSE_SSOR) return -1;
+    if ((h->paths & PATH_NO_TAIL) || h->cfg.coarse_solver != MGMC_COARSE_SSOR) return -1;
     const int L = (int)h->levels.size();
     for (int lt = 1; lt + 1 < L; ++lt) {
         bool ok = true;
@@ -1125,10 +1075,7 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 const bool lr = lv.lr.m > 0;
                 if (lr && !op.lr_skip_patch) lr_patch(h, lv, LR_PATCH_NOISE, lv.f, op.tag, sample, s);
                 double* xo = lv.x;
-                if (op.restrict_fused) {
-                    xo = lv.buf(1 - op.src);
-                    launch_zsweepres(lv, h->levels[op.level + 1], lv.buf(op.src), xo, g, op.direction, s);
-                } else if (lv.zsweep) {
+                if (lv.zsweep) {
                     const Level* lc = op.prolong ? &h->levels[op.level + 1] : nullptr;
                     xo = lv.buf(1 - op.src);
                     launch_zsweep(lv, lv.buf(op.src), xo, lv.f, g, op.direction, lc, lc ? lc->x : nullptr,
@@ -1138,8 +1085,7 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                     launch_quads(lv, lv.buf(op.src), xo, lv.f, g, op.direction, s);
                 } else if (lv.rb2d) {
                     xo = lv.buf(1 - op.src);
-                    const Level* lc = op.prolong ? &h->levels[op.level + 1] : nullptr;
-                    launch_rb2d(lv, lv.buf(op.src), xo, lv.f, g, op.direction, true, s, lc, h->cfg.coarse_scaling);
+                    launch_rb2d(lv, lv.buf(op.src), xo, lv.f, g, op.direction, true, s);
                 } else if (lv.pairs) {
                     launch_pairs(lv, lv.x, lv.f, g, op.direction, s);
                 } else {
@@ -1161,7 +1107,6 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 break;
             }
             case OP_RESIDUAL_RESTRICT: {
-                if (op.restrict_fused) break;  // done by the previous sweep's kernel
                 Level& lc = h->levels[op.level + 1];
                 const bool lr = lv.lr.m > 0;
                 if (lr && !op.lr_skip_patch) {  // r = (f - B Sigma^{-1} B^T x) - A x
@@ -1187,9 +1132,9 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
             case OP_TAIL: {
                 const size_t lds = h->tail_lds[op.tail];
                 if (lv.spec.dim == 3)
-                    hipLaunchKernelGGL(k_tail<3>, dim3(1), dim3(h->tail_nt), lds, s, (const TailArgs*)h->tail_args[op.tail]);
+                    hipLaunchKernelGGL(k_tail<3>, dim3(1), dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
                 else
-                    hipLaunchKernelGGL(k_tail<2>, dim3(1), dim3(h->tail_nt), lds, s, (const TailArgs*)h->tail_args[op.tail]);
+                    hipLaunchKernelGGL(k_tail<2>, dim3(1), dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
                 break;
             }
             case OP_QOI: {
@@ -1216,10 +1161,41 @@ void destroy_graphs(mgmc_handle* h) {
     h->graph_all = nullptr;
     if (h->graph_unroll) hipGraphExecDestroy(h->graph_unroll);
     h->graph_unroll = nullptr;
-    for (auto& g : h->graph_seg) {
-        if (g) hipGraphExecDestroy(g);
-        g = nullptr;
+    if (h->graph_timed) hipGraphExecDestroy(h->graph_timed);
+    h->graph_timed = nullptr;
+    if (h->graph_timed_src) hipGraphDestroy(h->graph_timed_src);
+    h->graph_timed_src = nullptr;
+}
+
+// the timed cycle: the same ops in one graph with an external event-record node at each of the four
+// segment boundaries (no extra graph launches; mgmc_sample_timed re-targets the nodes per step)
+int capture_timed(mgmc_handle* h) {
+    for (auto& e : h->timed_ev0)
+        if (!e) HIPCHK(h, hipEventCreate(&e));
+    const size_t b[4] = {0, h->seg_end_pre, h->seg_begin_post, h->ops.size()};
+    HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    for (int q = 0; q < 4; ++q) {
+        HIPCHK(h, hipEventRecordWithFlags(h->timed_ev0[q], h->stream, hipEventRecordExternal));
+        if (q < 3) enqueue_ops(h, b[q], b[q + 1], h->stream);
     }
+    HIPCHK(h, hipStreamEndCapture(h->stream, &h->graph_timed_src));
+    size_t nn = 0;
+    HIPCHK(h, hipGraphGetNodes(h->graph_timed_src, nullptr, &nn));
+    std::vector<hipGraphNode_t> nodes(nn);
+    HIPCHK(h, hipGraphGetNodes(h->graph_timed_src, nodes.data(), &nn));
+    for (hipGraphNode_t nd : nodes) {
+        hipGraphNodeType ty;
+        HIPCHK(h, hipGraphNodeGetType(nd, &ty));
+        if (ty != hipGraphNodeTypeEventRecord) continue;
+        hipEvent_t e = nullptr;
+        HIPCHK(h, hipGraphEventRecordNodeGetEvent(nd, &e));
+        for (int q = 0; q < 4; ++q)
+            if (e == h->timed_ev0[q]) h->timed_node[q] = nd;
+    }
+    for (int q = 0; q < 4; ++q)
+        if (!h->timed_node[q]) return fail(h, MGMC_E_HIP, "timed graph: event-record node not captured");
+    HIPCHK(h, hipGraphInstantiate(&h->graph_timed, h->graph_timed_src, nullptr, nullptr, 0));
+    return MGMC_OK;
 }
 
 // (re)capture the graphs; they embed series/series_cap, so recapture when those change
@@ -1232,7 +1208,7 @@ int build_graphs(mgmc_handle* h) {
     // device: the copies are identical)
     const uint64_t n0 = h->levels[0].spec.ndof;
     h->unroll = n0 <= (1u << 22) ? 8 : (n0 <= (1u << 25) ? 2 : 1);
-    if (const char* u = getenv("MGMC_GRAPH_UNROLL")) h->unroll = std::max(1, std::min(64, atoi(u)));
+    if (h->unroll_override > 0) h->unroll = h->unroll_override;
     if (h->unroll > 1) {
         hipGraph_t g = nullptr;
         HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
@@ -1242,14 +1218,8 @@ int build_graphs(mgmc_handle* h) {
         HIPCHK(h, hipGraphDestroy(g));
     }
     if (h->levels.size() > 1) {
-        // three segments per cycle: [fine pre-sampler | coarse-grid correction | fine post-sampler and
-        // the QoI record] (each segment boundary costs ~12 us of graph launch between HIP events)
-        const size_t n = h->ops.size();
-        const size_t b[4] = {0, h->seg_end_pre, h->seg_begin_post, n};
-        for (int s = 0; s < 3; ++s) {
-            rc = capture(h, b[s], b[s + 1], &h->graph_seg[s]);
-            if (rc) return rc;
-        }
+        rc = capture_timed(h);
+        if (rc) return rc;
     }
     return MGMC_OK;
 }
@@ -1412,10 +1382,15 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     *out = nullptr;
     const std::string err = validate_config(*cfg);
     if (!err.empty()) return fail(nullptr, MGMC_E_INVALID, err);
+    uint32_t paths = 0;
+    std::string bad;
+    if (!read_path_flags(&paths, &bad)) return fail(nullptr, MGMC_E_INVALID, "MGMC_DISABLE: unknown path '" + bad + "'");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(nullptr, MGMC_E_HIP, "no HIP device");
     if (device < 0 || device >= ndev) return fail(nullptr, MGMC_E_INVALID, "device index out of range");
     mgmc_handle* h = new mgmc_handle();
+    h->paths = paths;
+    if (const char* u = getenv("MGMC_GRAPH_UNROLL")) h->unroll_override = std::max(1, std::min(64, atoi(u)));
     h->cfg = *cfg;
     h->device = device;
     h->seed = seed;
@@ -1438,13 +1413,14 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         return bail(MGMC_E_HIP);
     }
     const std::vector<LevelSpec> specs = build_hierarchy(*cfg);
-    const int tail0 = tail_start_by_size(specs, *cfg);  // levels k_tail can take (no quads there)
+    const int tail0 = tail_start_by_size(specs, *cfg, h->paths);  // levels k_tail can take (no quads there)
     size_t lds_limit = 150 * 1024;
     for (size_t l = 0; l < specs.size(); ++l) {
         Level lv;
         lv.num_cu = ncu;
         lv.spec = specs[l];
-        lv.L = make_layout(cfg->dim, specs[l].n, getenv("MGMC_LAYOUT_A64") == nullptr);  // 128-B rows
+        lv.paths = h->paths;
+        lv.L = make_layout(cfg->dim, specs[l].n);
         memcpy(lv.S.a, specs[l].st, sizeof(lv.S.a));
         const size_t bytes = lv.L.nstore * sizeof(double);
         if (hipMalloc(&lv.x, bytes) != hipSuccess || hipMalloc(&lv.f, bytes) != hipSuccess) {
@@ -1458,10 +1434,10 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         const double* st = lv.spec.st;  // the z-sweep folds the symmetric FD stencil to 4 coefficients
         const bool symmetric = st[4] == st[22] && st[10] == st[16] && st[12] == st[14];
         lv.zsweep = cfg->dim == 3 && lv.spec.npoints == 7 && symmetric && l + 1 < specs.size() &&
-                    (lv.L.nx % (2 * zsweep_xp())) == 0 && getenv("MGMC_NO_ZSWEEP") == nullptr;
-        lv.pairs = pairs_eligible(lv.spec, lv.L) && getenv("MGMC_NO_PAIRS") == nullptr;
-        lv.rb2d = cfg->dim == 2 && lv.spec.npoints == 5 && l + 1 < specs.size() && getenv("MGMC_NO_RB2D") == nullptr;
-        lv.quads = lv.pairs && quads_eligible(lv.spec, lv.L) && (tail0 < 0 || (int)l < tail0);
+                    (lv.L.nx % (2 * ZS_XP)) == 0 && !(h->paths & PATH_NO_ZSWEEP);
+        lv.pairs = pairs_eligible(lv.spec, lv.L) && !(h->paths & PATH_NO_PAIRS);
+        lv.rb2d = cfg->dim == 2 && lv.spec.npoints == 5 && l + 1 < specs.size() && !(h->paths & PATH_NO_RB2D);
+        lv.quads = lv.pairs && quads_eligible(lv.spec, lv.L, h->paths) && (tail0 < 0 || (int)l < tail0);
         if (lv.pingpong()) {
             if (hipMalloc(&lv.x2, bytes) != hipSuccess) {
                 h->levels.push_back(lv);
@@ -1477,19 +1453,15 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         h->last_error = "device allocation failed";
         return bail(MGMC_E_NOMEM);
     }
-    uint64_t ctrl0[8] = {0, 0, (uint64_t)(int64_t)-1, 0, 0, 0, 0, 0};
+    // ctrl[6]: the vertex the non-finite guard watches when no QoI is recorded (lattice centre)
+    const Level& l0 = h->levels[0];
+    const long long probe = l0.L.at(l0.L.nx / 2, l0.L.ny / 2, cfg->dim == 3 ? l0.L.nz / 2 : 0);
+    uint64_t ctrl0[8] = {0, 0, (uint64_t)(int64_t)-1, 0, 0, 0, (uint64_t)probe, 0};
     hipMemcpyAsync(h->ctrl, ctrl0, sizeof(ctrl0), hipMemcpyHostToDevice, h->stream);
     hipMemsetAsync(h->mom, 0, 4 * sizeof(double), h->stream);
     if (cfg->coarse_solver == MGMC_COARSE_CHOLESKY && (rc = build_coarse_chol(h, nullptr, nullptr, 0)) != MGMC_OK)
         return bail(rc);
     // op sequence of one sample
-    h->fuse_prolong = getenv("MGMC_NO_FUSE_PROLONG") == nullptr;  // default: fused (A/B in DESIGN.md)
-    h->rb2d_prolong = getenv("MGMC_RB2D_PROLONG") != nullptr;
-    if (const char* t = getenv("MGMC_TAIL_NT")) h->tail_nt = std::max(64, std::min(1024, atoi(t) / 64 * 64));
-    // opt-in: the fused pre-sweep + residual + restriction is correct (bitwise) but slower at 512^3
-    // (1.98 ms against 0.70 + 0.56 ms): its two-vertex recomputed halo and 2 workgroups
-    // per CU leave it latency / VALU bound
-    h->fuse_restrict = getenv("MGMC_FUSE_RESTRICT") != nullptr;
     build_ops(h);
     if ((rc = build_tails(h)) != MGMC_OK) return bail(rc);
     if ((rc = ensure_series(h, 1024)) != MGMC_OK) return bail(rc);
@@ -1513,6 +1485,8 @@ int mgmc_destroy(mgmc_handle* h) {
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
     destroy_graphs(h);
+    for (auto e : h->timed_ev0)
+        if (e) hipEventDestroy(e);
     free_tails(h);
     for (auto& lv : h->levels) {
         free_lowrank(lv.lr);
@@ -1562,6 +1536,7 @@ int mgmc_set_state(mgmc_handle* h, const double* x, size_t n) {
     HIPCHK(h, hipSetDevice(h->device));
     int rc = upload(h, 0, x, h->levels[0].x);
     if (rc) return rc;
+    HIPCHK(h, hipMemsetAsync(h->ctrl + 5, 0, sizeof(uint64_t), h->stream));  // a new state: guard cleared
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return MGMC_OK;
 }
@@ -1571,6 +1546,19 @@ int mgmc_get_state(mgmc_handle* h, double* x, size_t n) {
     if (n != h->levels[0].spec.ndof) return fail(h, MGMC_E_INVALID, "state size mismatch");
     HIPCHK(h, hipSetDevice(h->device));
     return download(h, 0, h->levels[0].x, x);
+}
+
+// the device-side non-finite guard (ctrl[5], set by k_qoi_record): MGMC_E_NONFINITE with the sample
+// index and the watched vertex, instead of a chain that silently carries NaN / Inf
+static int check_finite(mgmc_handle* h) {
+    uint64_t flag = 0;
+    HIPCHK(h, hipMemcpyAsync(&flag, h->ctrl + 5, sizeof(flag), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (flag == 0) return MGMC_OK;
+    return fail(h, MGMC_E_NONFINITE,
+                "non-finite chain state: the " + std::string(h->qoi_store_index >= 0 ? "QoI vertex" : "lattice centre") +
+                    " became NaN / Inf in sample " + std::to_string(flag - 1) +
+                    " (check the right-hand side, the low-rank Sigma and omega; mgmc_set_state clears the guard)");
 }
 
 static int set_qoi(mgmc_handle* h, int64_t qoi_index) {
@@ -1599,7 +1587,8 @@ int mgmc_apply(mgmc_handle* h, const double* f, double* x, size_t n) {
     if ((rc = mgmc_set_state(h, x, n))) return rc;
     if ((rc = set_qoi(h, -1))) return rc;
     HIPCHK(h, hipGraphLaunch(h->graph_all, h->stream));
-    return mgmc_get_state(h, x, n);
+    if ((rc = mgmc_get_state(h, x, n))) return rc;
+    return check_finite(h);
 }
 
 int mgmc_sample_async(mgmc_handle* h, int nsteps, int64_t qoi_index) {
@@ -1621,7 +1610,7 @@ int mgmc_synchronize(mgmc_handle* h) {
     if (!h) return fail(nullptr, MGMC_E_INVALID, "null handle");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    return MGMC_OK;
+    return check_finite(h);
 }
 
 int mgmc_sample(mgmc_handle* h, int nsteps, int64_t qoi_index, double* qoi_out) {
@@ -1630,7 +1619,7 @@ int mgmc_sample(mgmc_handle* h, int nsteps, int64_t qoi_index, double* qoi_out) 
     if (qoi_out && nsteps > 0 && qoi_index >= 0)
         HIPCHK(h, hipMemcpyAsync(qoi_out, h->series, nsteps * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    return MGMC_OK;
+    return check_finite(h);
 }
 
 int mgmc_qoi_moments(mgmc_handle* h, double out[3]) {
@@ -1863,17 +1852,18 @@ int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* tot
     if (rc) return rc;
     HIPCHK(h, hipMemsetAsync(h->ctrl + 1, 0, sizeof(uint64_t), h->stream));
     if ((rc = ensure_series(h, (uint64_t)nsteps))) return rc;
-    constexpr int NSEG = 3;  // [fine pre-sampler | coarse-grid correction | fine post-sampler, QoI]
-    std::vector<hipEvent_t> ev(NSEG * (size_t)nsteps + 1);
+    // one graph launch per cycle; its four event-record nodes are re-targeted at this step's events
+    // before the launch (boundaries: fine pre-sampler | coarse-grid correction | fine post-sampler +
+    // QoI record)
+    constexpr int NSEG = 4;
+    std::vector<hipEvent_t> ev(NSEG * (size_t)nsteps);
     for (auto& e : ev) HIPCHK(h, hipEventCreate(&e));
     for (int s = 0; s < nsteps; ++s) {
-        for (int g = 0; g < NSEG; ++g) {
-            HIPCHK(h, hipEventRecord(ev[NSEG * s + g], h->stream));
-            HIPCHK(h, hipGraphLaunch(h->graph_seg[g], h->stream));
-        }
+        for (int q = 0; q < NSEG; ++q)
+            HIPCHK(h, hipGraphExecEventRecordNodeSetEvent(h->graph_timed, h->timed_node[q], ev[NSEG * s + q]));
+        HIPCHK(h, hipGraphLaunch(h->graph_timed, h->stream));
     }
-    HIPCHK(h, hipEventRecord(ev[NSEG * nsteps], h->stream));
-    HIPCHK(h, hipEventSynchronize(ev[NSEG * nsteps]));
+    HIPCHK(h, hipEventSynchronize(ev[NSEG * nsteps - 1]));
     float t = 0.f;
     double pre = 0.0, post = 0.0;
     for (int s = 0; s < nsteps; ++s) {
@@ -1882,7 +1872,7 @@ int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* tot
         HIPCHK(h, hipEventElapsedTime(&t, ev[NSEG * s + 2], ev[NSEG * s + 3]));
         post += t;
     }
-    HIPCHK(h, hipEventElapsedTime(&t, ev[0], ev[NSEG * nsteps]));
+    HIPCHK(h, hipEventElapsedTime(&t, ev[0], ev[NSEG * nsteps - 1]));
     *total_ms = t;
     *pre_ms = pre;
     *post_ms = post;
@@ -1895,7 +1885,7 @@ int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* tot
     *npre = cpre * nsteps;
     *npost = cpost * nsteps;
     for (auto& e : ev) hipEventDestroy(e);
-    return MGMC_OK;
+    return check_finite(h);
 }
 
 // ---------------- exact-statistics engine: multigrid-preconditioned solvers ----------------
@@ -2246,7 +2236,7 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
             (rc = lr_to_device(h, r, &r.t_bar_off[d], t_boff)))
             return rc;
     }
-    bool small = getenv("MGMC_LR_NO_SMALL") == nullptr && ndense == 0 && r.nrows <= (1 << 16) &&
+    bool small = !(h->paths & PATH_NO_LR_SMALL) && ndense == 0 && r.nrows <= (1 << 16) &&
                  r.nbar[0] <= (1 << 16) && r.nbar[1] <= (1 << 16);
     for (int k = 0; k < m; ++k) small = small && meta[k].nblk <= 1;
     r.small = small;

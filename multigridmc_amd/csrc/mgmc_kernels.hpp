@@ -508,13 +508,16 @@ __global__ void __launch_bounds__(256) k_unpack(Layout L, const double* __restri
 }
 
 // ---- QoI record + running moments; advances the sample index (driver_mgmc.cc:72-78, :86-94) ----
-// ctrl[0] = sample index, ctrl[1] = series length, ctrl[2] = QoI storage index (int64, <0 = off)
+// ctrl[0] = sample index, ctrl[1] = series length, ctrl[2] = QoI storage index (int64, <0 = off),
+// ctrl[5] = non-finite guard (0, or 1 + the sample index at which the watched value first was NaN /
+// Inf), ctrl[6] = storage index watched when no QoI is recorded (the lattice centre)
 __global__ void k_qoi_record(const double* __restrict__ x, uint64_t* ctrl, double* series, uint64_t capacity,
                              double* mom) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const long long q = (long long)ctrl[2];
+    const double z = x[q >= 0 ? q : (long long)ctrl[6]];
+    if (!isfinite(z) && ctrl[5] == 0) ctrl[5] = ctrl[0] + 1;
     if (q >= 0) {
-        const double z = x[q];
         const uint64_t n = ctrl[1];
         if (n < capacity) series[n] = z;
         ctrl[1] = n + 1;

@@ -24,14 +24,10 @@ constexpr int RB2_HW = RB2_W / 2;                       // LDS rows are colour-s
 // cycles, PMC)
 __device__ __forceinline__ int rb2_lidx(int r, int c) { return r * RB2_W + (c & 1) * RB2_HW + (c >> 1); }
 
-// PROLONG: the first post-sweep also adds alpha P x_c (intergrid_operator.hh:106-120) to every staged
-// vertex first, with k_prolongate_pairs' terms in its order (coarse rows ascending; an odd i takes
-// parents q, q+1 with weight 1/2, an even i parent q+1 with weight 1; w = 1 * w_x * w_y, then
-// v += (alpha w) x_c), so the separate prolongation launch goes away.
-template <bool NOISE, bool PROLONG>
+template <bool NOISE>
 __global__ void __launch_bounds__(RB2_NT) k_rb2d(Layout L, const double* __restrict__ xin, double* __restrict__ xout,
                                               const double* __restrict__ f, StencilArg S, GibbsArg G, int c1,
-                                              int ntx, Layout Lc, const double* __restrict__ xc, double alpha) {
+                                              int ntx) {
     __shared__ double xs[RB2_H * RB2_W];
     __shared__ double cs[RB2_H * RB2_W];  // right hand sides c = fma(sd, xi, f) of the updated vertices
     const int tid = threadIdx.x;
@@ -42,36 +38,7 @@ __global__ void __launch_bounds__(RB2_NT) k_rb2d(Layout L, const double* __restr
     for (int q = tid; q < RB2_H * RB2_W; q += RB2_NT) {
         const int r = q / RB2_W, c = q - r * RB2_W;
         const int i = ib + c, j = jb + r;
-        double v = (i >= 0 && i <= L.nx && j >= 0 && j <= L.ny) ? xin[L.at(i, j, 0)] : 0.0;
-        if (PROLONG && i >= 1 && i <= L.nx - 1 && j >= 1 && j <= L.ny - 1) {
-            const int qp = (i - 1) >> 1;  // the pair (2qp+1, 2qp+2)
-            const int j0c = j >> 1, nj = (j & 1) ? 2 : 1;
-            for (int bb = 0; bb < nj; ++bb) {
-                const int jj = j0c + bb;
-                if (jj < 1 || jj > Lc.ny - 1) continue;
-                const double* row = xc + Lc.at(0, jj, 0);
-                const double wy = w1(j - 2 * jj);
-                if (i & 1) {
-                    if (qp >= 1) {
-                        double w = 1.0;
-                        w *= 0.5;
-                        w *= wy;
-                        v += alpha * w * row[qp];
-                    }
-                    if (qp + 1 <= Lc.nx - 1) {
-                        double w = 1.0;
-                        w *= 0.5;
-                        w *= wy;
-                        v += alpha * w * row[qp + 1];
-                    }
-                } else if (qp + 1 <= Lc.nx - 1) {
-                    double w = 1.0;
-                    w *= 1.0;
-                    w *= wy;
-                    v += alpha * w * row[qp + 1];
-                }
-            }
-        }
+        const double v = (i >= 0 && i <= L.nx && j >= 0 && j <= L.ny) ? xin[L.at(i, j, 0)] : 0.0;
         xs[rb2_lidx(r, c)] = v;
     }
     // right hand sides of every vertex the two passes update (rows [j0-1, j0+TH], columns [i0-1,

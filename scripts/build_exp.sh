@@ -11,4 +11,5 @@ for n in ${NTEXPS:-}; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off -fPIC -w --offload-arch=gfx950 $d -shared \
     -o ../../build/libmgmc_exp$n.so mgmc_capi.hip mgmc_hierarchy.cpp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib &
 done
+
 wait

@@ -1,5 +1,5 @@
 """Fine-sweep timing of experiment builds (build/libmgmc_exp<N>.so, see scripts/build_exp.sh) against the
-product library, for a list of z-sweep variants.  python scripts/exp_bench.py [variants] [exps]"""
+product library.  python scripts/exp_bench.py [exps, 0 = product]"""
 import os
 import subprocess
 import sys
@@ -14,18 +14,12 @@ s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 1, mg.Multigri
 s.time_fine_sweeps(2)
 print(min(s.time_fine_sweeps(10) / 10 for _ in range(3)))
 '''
-variants = sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "5", "11"]
-exps = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1", "2", "3", "4"]
+exps = sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "1", "2", "3", "4"]
 names = {"0": "product", "1": "no-BoxMuller", "2": "no-halo", "3": "no-Philox", "4": "no-stencil", "5": "skeleton", "6": "no-barriers", "7": "nt-store", "8": "nt-f", "9": "nt-store+f"}
-tzs = os.environ.get("TZS", "32").split(",")
-aligns = os.environ.get("ALIGNS", "1").split(",")
-for v, x, tz, al in [(v, x, tz, al) for v in variants for x in exps for tz in tzs for al in aligns]:
-    if True:
-        env = dict(os.environ, MGMC_ZS_VARIANT=v, MGMC_ZS_TZ=tz)
-        if al == "0":
-            env["MGMC_LAYOUT_A64"] = "1"
-        if x != "0":
-            env["MGMC_LIBRARY"] = os.path.join(ROOT, "build", f"libmgmc_exp{x}.so")
-        r = subprocess.run([sys.executable, "-c", CHILD % ROOT], env=env, capture_output=True, text=True, timeout=300)
-        out = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else f"FAILED {r.stderr[-300:]}"
-        print(f"v{v} tz{tz} a128={al} {names[x]:14s} {out}", flush=True)
+for x in exps:
+    env = dict(os.environ)
+    if x != "0":
+        env["MGMC_LIBRARY"] = os.path.join(ROOT, "build", f"libmgmc_exp{x}.so")
+    r = subprocess.run([sys.executable, "-c", CHILD % ROOT], env=env, capture_output=True, text=True, timeout=300)
+    out = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else f"FAILED {r.stderr[-300:]}"
+    print(f"{names.get(x, x):14s} {out}", flush=True)

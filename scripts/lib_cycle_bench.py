@@ -1,0 +1,31 @@
+"""In-cycle timing of library builds: for each library (product or build/libmgmc_exp<N>.so), K timed
+512^3 V-cycles (mgmc_sample_timed: fine pre / post sweep segments) in a fresh child process, and the
+plain single-graph replay of the same K cycles.  python scripts/lib_cycle_bench.py [exps, 0 = product]"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = r'''
+import sys, json, time
+sys.path.insert(0, %r)
+import multigridmc_amd as mg
+lat = mg.Lattice3d(512, 512, 512)
+s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 1, mg.MultigridParameters(nlevel=7))
+s.sample(5)
+best = None
+for _ in range(3):
+    t = s.sample_timed(30)
+    s.synchronize(); t0 = time.perf_counter(); s.sample_async(30); s.synchronize(); plain = (time.perf_counter() - t0) / 30 * 1e3
+    r = {"pre_ms": t["pre_ms"] / t["npre"], "post_ms": t["post_ms"] / t["npost"], "timed_cycle_ms": t["total_ms"] / 30,
+         "plain_cycle_ms": plain}
+    best = r if best is None or r["timed_cycle_ms"] < best["timed_cycle_ms"] else best
+print(json.dumps(best))
+'''
+for x in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["0"]):
+    env = dict(os.environ)
+    if x != "0":
+        env["MGMC_LIBRARY"] = os.path.join(ROOT, "build", f"libmgmc_exp{x}.so")
+    r = subprocess.run([sys.executable, "-c", CHILD % ROOT], env=env, capture_output=True, text=True, timeout=300)
+    print(x, r.stdout.strip().splitlines()[-1] if r.returncode == 0 else f"FAILED {r.stderr[-400:]}", flush=True)

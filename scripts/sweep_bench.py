@@ -1,5 +1,5 @@
-"""Micro-benchmark of the fine-level sweep kernel variants and of the whole V-cycle (GPU box).
-Usage: python scripts/sweep_bench.py [n] [nlevel] [zsweep variants, comma separated]"""
+"""Micro-benchmark of the fine-level sweep and of the whole V-cycle (GPU box), default paths and with
+fast paths switched off (MGMC_DISABLE).  Usage: python scripts/sweep_bench.py [n] [nlevel]"""
 import json
 import os
 import subprocess
@@ -25,11 +25,7 @@ print(json.dumps({"sweep_ms": ms, "GBps": 24 * lat.Nvertex / ms / 1e6, "vcycle_m
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 nlevel = int(sys.argv[2]) if len(sys.argv) > 2 else 7
-variants = []
-for v in (sys.argv[3].split(",") if len(sys.argv) > 3 else ["0"]):
-    variants.append((f"zsweep-v{v}", {"MGMC_ZS_VARIANT": v}))
-variants.append(("zrestrict-v3-32x8", {"MGMC_ZR_VARIANT": "3"}))
-variants.append(("no-fuse-prolong", {"MGMC_NO_FUSE_PROLONG": "1"}))
+variants = [("default", {}), ("no-fuse-prolong", {"MGMC_DISABLE": "fuse_prolong"})]
 for name, env in variants:
     e = dict(os.environ)
     e.update(env)

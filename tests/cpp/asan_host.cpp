@@ -1,0 +1,206 @@
+// AddressSanitizer / UBSan harness for the host code (TEST INFRASTRUCTURE, `make -C oracle asan`):
+//  * the product's host-side hierarchy setup (multigridmc_amd/csrc/mgmc_hierarchy.cpp:
+//    validate_config, build_hierarchy, galerkin_stencil) over valid and invalid configurations;
+//  * the CPU oracle (oracle/refcpu.cpp) C API in both modes: FD / FEM / CSR hierarchies, cycles,
+//    component operators, the low-rank part (sparse and dense columns), the dense Cholesky coarse
+//    sampler, lattice maps and the RNG helpers.
+// Built with -fsanitize=address,undefined; any report aborts with a non-zero exit code.
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../multigridmc_amd/csrc/mgmc_hierarchy.hpp"
+
+extern "C" {
+typedef struct orc_params {
+    int dim, nx, ny, nz;
+    int nlevel, cycle, npresmooth, npostsmooth, ncoarsesmooth;
+    int smoother, coarse_solver, galerkin;
+    double omega, coarse_scaling, kappa_sq;
+} orc_params;
+struct orc_handle;
+orc_handle* orc_create_fd(const orc_params* q, int mode, uint64_t seed, uint64_t chain, const double* override_st);
+orc_handle* orc_create_fem(const orc_params* q, int mode, uint64_t seed, uint64_t chain, const double* override_st);
+orc_handle* orc_create_csr(const orc_params* q, int mode, uint64_t seed, int64_t nrow, const int64_t* rowptr,
+                           const int32_t* col, const double* val);
+void orc_destroy(orc_handle* h);
+int64_t orc_ndof(orc_handle* h, int level);
+int orc_nlevel(orc_handle* h);
+int64_t orc_nnz(orc_handle* h, int level);
+void orc_get_csr(orc_handle* h, int level, int64_t* rowptr, int32_t* col, double* val);
+void orc_set_rhs(orc_handle* h, const double* f);
+void orc_set_state(orc_handle* h, const double* x);
+void orc_get_state(orc_handle* h, double* x);
+void orc_apply(orc_handle* h, const double* f, double* x);
+void orc_sample(orc_handle* h, int nsteps, int64_t qoi, double* qoi_out);
+void orc_operator_apply(orc_handle* h, int level, const double* x, double* y);
+void orc_set_lowrank(orc_handle* h, int m, const int64_t* colptr, const int64_t* rows, const double* vals,
+                     const double* sigma);
+void orc_smoother_apply(orc_handle* h, int level, int direction, int nsweeps, const double* b, double* x);
+void orc_sor_sampler_apply(orc_handle* h, int level, int direction, uint32_t tag, uint64_t sample, const double* f,
+                           double* x);
+void orc_restrict(orc_handle* h, int level, const double* r, double* rc);
+void orc_prolongate_add(orc_handle* h, int level, double alpha, const double* xc, double* x);
+void orc_residual_restrict(orc_handle* h, int level, const double* f, const double* x, double* fc);
+void orc_philox_normals(uint64_t seed, uint64_t chain, uint64_t pair0, int64_t n, uint32_t tag, uint64_t sample,
+                        double* out);
+void orc_mt_normals(uint64_t seed, int64_t n, double* out);
+int64_t orc_lattice_fine_vertex_idx(int dim, const int* n, int64_t ell);
+}
+
+static int failures = 0;
+#define EXPECT(c)                                                        \
+    do {                                                                 \
+        if (!(c)) {                                                      \
+            std::fprintf(stderr, "%s:%d: EXPECT(%s)\n", __FILE__, __LINE__, #c); \
+            ++failures;                                                  \
+        }                                                                \
+    } while (0)
+
+static void hierarchy_checks() {
+    const int shapes[][4] = {{2, 16, 16, 0}, {2, 64, 32, 0}, {3, 16, 16, 16}, {3, 32, 16, 8},
+                             {3, 64, 64, 64}, {2, 6, 6, 0}, {3, 15, 16, 16}, {3, 8, 8, 8}};
+    for (const auto& sh : shapes)
+        for (int nlevel = 1; nlevel <= 5; ++nlevel)
+            for (int op = 0; op <= 1; ++op) {
+                mgmc_config c;
+                std::memset(&c, 0, sizeof(c));
+                c.dim = sh[0];
+                c.nx = sh[1];
+                c.ny = sh[2];
+                c.nz = sh[3];
+                c.nlevel = nlevel;
+                c.cycle = 1;
+                c.npresmooth = c.npostsmooth = c.ncoarsesmooth = 1;
+                c.omega = 1.0;
+                c.coarse_scaling = 1.0;
+                c.kappa_sq = 25.0;
+                c.fine_operator = op;
+                if (!mgmc::validate_config(c).empty()) continue;
+                const std::vector<mgmc::LevelSpec> lv = mgmc::build_hierarchy(c);
+                EXPECT((int)lv.size() == nlevel);
+                for (const auto& s : lv) EXPECT(std::isfinite(s.diag()) && s.diag() > 0.0);
+            }
+    double fine[27] = {0}, coarse[27];
+    fine[13] = 6.0;
+    fine[4] = fine[22] = fine[10] = fine[16] = fine[12] = fine[14] = -1.0;
+    mgmc::galerkin_stencil(3, fine, coarse);
+    EXPECT(std::isfinite(coarse[13]));
+}
+
+static orc_params params(int dim, int n, int nlevel, int cycle, int smoother, int coarse) {
+    orc_params p;
+    p.dim = dim;
+    p.nx = p.ny = n;
+    p.nz = dim == 3 ? n : 0;
+    p.nlevel = nlevel;
+    p.cycle = cycle;
+    p.npresmooth = 1;
+    p.npostsmooth = 2;
+    p.ncoarsesmooth = 2;
+    p.smoother = smoother;
+    p.coarse_solver = coarse;
+    p.galerkin = 0;
+    p.omega = 1.1;
+    p.coarse_scaling = 1.0;
+    p.kappa_sq = 25.0;
+    return p;
+}
+
+static void exercise(orc_handle* h, bool lowrank) {
+    const int nl = orc_nlevel(h);
+    const int64_t n = orc_ndof(h, 0);
+    std::vector<double> f(n), x(n, 0.0), y(n);
+    for (int64_t i = 0; i < n; ++i) f[i] = std::sin(0.37 * (double)i);
+    if (lowrank) {  // two point columns, one ball-like column and the dense global column
+        std::vector<int64_t> colptr = {0, 1, 2, 5, 5 + n};
+        std::vector<int64_t> rows = {n / 3, n / 2, n / 4, n / 4 + 1, n / 4 + 2};
+        std::vector<double> vals = {1.0, 1.0, 0.3, 0.4, 0.3};
+        for (int64_t i = 0; i < n; ++i) {
+            rows.push_back(i);
+            vals.push_back(1.0 / (double)n);
+        }
+        const double sigma[4] = {1e-3, 2e-3, 5e-3, 1e-2};
+        orc_set_lowrank(h, 4, colptr.data(), rows.data(), vals.data(), sigma);
+    }
+    orc_apply(h, f.data(), x.data());
+    orc_set_rhs(h, f.data());
+    orc_set_state(h, x.data());
+    std::vector<double> q(3);
+    orc_sample(h, 3, n / 2, q.data());
+    for (double v : q) EXPECT(std::isfinite(v));
+    orc_get_state(h, x.data());
+    for (int l = 0; l < nl; ++l) {
+        const int64_t m = orc_ndof(h, l);
+        std::vector<double> a(m, 0.5), b(m);
+        orc_operator_apply(h, l, a.data(), b.data());
+        orc_smoother_apply(h, l, 1, 1, a.data(), b.data());
+        orc_smoother_apply(h, l, 2, 2, a.data(), b.data());
+        orc_sor_sampler_apply(h, l, 1, 3, 7, a.data(), b.data());
+        std::vector<int64_t> rp(m + 1);
+        std::vector<int32_t> col(orc_nnz(h, l));
+        std::vector<double> val(orc_nnz(h, l));
+        orc_get_csr(h, l, rp.data(), col.data(), val.data());
+        if (l + 1 < nl) {
+            std::vector<double> c(orc_ndof(h, l + 1), 0.25);
+            orc_restrict(h, l, a.data(), c.data());
+            orc_prolongate_add(h, l, 1.0, c.data(), b.data());
+            orc_residual_restrict(h, l, a.data(), b.data(), c.data());
+        }
+    }
+}
+
+int main() {
+    hierarchy_checks();
+    for (int mode = 0; mode <= 1; ++mode) {
+        for (int coarse = 0; coarse <= 1; ++coarse) {
+            const orc_params p2 = params(2, 32, 3, 2, 0, coarse), p3 = params(3, 16, 3, 1, 1, coarse);
+            for (int lr = 0; lr <= 1; ++lr) {
+                orc_handle* h = orc_create_fd(&p2, mode, 5418513ull, 1, nullptr);
+                exercise(h, lr);
+                orc_destroy(h);
+                h = orc_create_fd(&p3, mode, 5418513ull, 2, nullptr);
+                exercise(h, lr);
+                orc_destroy(h);
+            }
+            orc_handle* h = orc_create_fem(&p3, mode, 11ull, 0, nullptr);
+            exercise(h, false);
+            orc_destroy(h);
+        }
+        // a CSR operator (2D 16^2 5-point Laplacian + shift) through orc_create_csr
+        const int n = 15;
+        std::vector<int64_t> rp = {0};
+        std::vector<int32_t> col;
+        std::vector<double> val;
+        for (int j = 0; j < n; ++j)
+            for (int i = 0; i < n; ++i) {
+                const int r = j * n + i;
+                if (j > 0) { col.push_back(r - n); val.push_back(-1.0); }
+                if (i > 0) { col.push_back(r - 1); val.push_back(-1.0); }
+                col.push_back(r); val.push_back(4.1);
+                if (i + 1 < n) { col.push_back(r + 1); val.push_back(-1.0); }
+                if (j + 1 < n) { col.push_back(r + n); val.push_back(-1.0); }
+                rp.push_back((int64_t)col.size());
+            }
+        orc_params pc = params(2, 16, 3, 1, 0, 0);
+        orc_handle* h = orc_create_csr(&pc, mode, 3ull, n * n, rp.data(), col.data(), val.data());
+        if (h) {
+            exercise(h, false);
+            orc_destroy(h);
+        }
+    }
+    std::vector<double> z(64);
+    orc_philox_normals(5418513ull, 3, 0, 32, 7, 11, z.data());
+    orc_mt_normals(5418513ull, 64, z.data());
+    for (double v : z) EXPECT(std::isfinite(v));
+    const int nn[3] = {16, 16, 16};
+    EXPECT(orc_lattice_fine_vertex_idx(3, nn, 0) >= 0);
+    if (failures) {
+        std::fprintf(stderr, "asan_host: %d expectation(s) failed\n", failures);
+        return 1;
+    }
+    std::printf("asan_host OK\n");
+    return 0;
+}

@@ -6,10 +6,14 @@ import subprocess
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def build_client(tmpdir):
-    exe = os.path.join(str(tmpdir), "abi_client")
+def build_client(tmpdir, asan=False):
+    """asan: the client (include/mgmc_sampler.hh and its caller) with AddressSanitizer + UBSan; the
+    library itself stays uninstrumented (no device sanitizers on this pool)."""
+    exe = os.path.join(str(tmpdir), "abi_client_asan" if asan else "abi_client")
     libdir = os.path.join(ROOT, "multigridmc_amd")
-    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+    san = ["-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"] \
+        if asan else []
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", *san, "-I", os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tests", "cpp", "abi_client.cpp"), "-L", libdir, "-lmgmc_hip",
                     f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
     return exe

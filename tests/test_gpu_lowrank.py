@@ -174,16 +174,21 @@ def test_posterior_statistics_vs_exact_covariance(hip_device, shape, kw, glob, n
     s.close()
 
 
-@pytest.mark.parametrize("name", TAIL_CONFIGS)
-def test_lowrank_tail_matches_separate_kernels(hip_device, name, monkeypatch):
-    """The coarse levels' sub-cycle in k_tail (low-rank patches, fix and residual in LDS) against the
-    oracle with the tail switched off and on: both bitwise."""
+@pytest.mark.parametrize("name,paths", [(n, "tail") for n in TAIL_CONFIGS] +
+                         [(n, q) for n in ("3d32_points_tail_W", "2d32_point_global", "3d_aniso_zres_points")
+                          for q in ("lr_small", "lr_merge", "lr_prefetch", "lr_small,lr_merge,tail")])
+def test_lowrank_paths_match(hip_device, name, paths, monkeypatch):
+    """Low-rank kernel paths switched off (MGMC_DISABLE): tail = the coarse levels' sub-cycle as
+    separate launches instead of k_tail (low-rank patches, fix and residual in LDS); lr_small = the
+    generic fix / patch / restore launches instead of the single-workgroup k_lr_small; lr_merge =
+    separate restore and patch launches around the residual + restriction; lr_prefetch = k_lr_small
+    without its up-front loads.  QoI series and state bitwise against the oracle, on and off."""
     out = []
-    for env in ("MGMC_NO_TAIL", None):
+    for env in (paths, None):
         if env:
-            monkeypatch.setenv(env, "1")
+            monkeypatch.setenv("MGMC_DISABLE", env)
         else:
-            monkeypatch.delenv("MGMC_NO_TAIL", raising=False)
+            monkeypatch.delenv("MGMC_DISABLE", raising=False)
         s, mc, p, lat, op = make(name)
         qoi = mg.measurement_vector_index(lat, [0.5] * lat.dim)
         z = s.sample(5, qoi)

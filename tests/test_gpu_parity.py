@@ -57,9 +57,7 @@ CONFIGS = {
     # level 1 -> level 2, partial tiles in y and z
     "3d_zres7": ((256, 40, 48), dict(nlevel=2)),
     "3d_zres27": ((512, 16, 24), dict(nlevel=3)),
-    # (with MGMC_FUSE_RESTRICT, test_variant_cycles_bitwise) last pre-sweep fused with residual +
-    # restriction (k_zsweep_res7): coarse rows / planes ending exactly at a tile / chunk boundary (the
-    # last tile owns the extra fine row / plane), SSOR pre-sampler
+    # coarse rows / planes ending exactly at a tile / chunk boundary, SSOR pre-sampler
     "3d_zsr_edges": ((128, 34, 18), dict(nlevel=2)),
     "3d_zsr_ssor_W": ((128, 64, 64), dict(nlevel=3, cycle=2, smoother="SSOR", npresmooth=2, omega=0.9)),
     # dense Cholesky coarse sampler (CholeskySampler, x = G f + U xi on the coarsest level)
@@ -154,63 +152,34 @@ def test_mgmc_cycles_bitwise(hip_device, name):
     s.close()
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "3", "4", "5", "6", "7", "8", "9", "11", "12", "13"])
-def test_zsweep_tile_variants_bitwise(hip_device, monkeypatch, variant):
-    """Every z-sweep tile shape (MGMC_ZS_VARIANT: 64x4, 64x8/512, 64x8, 64x16, 32x16, 32x24, 64x12,
-    32x12, 32x8 unconstrained registers, 64x16/512; default 32x8 at 5 waves/SIMD) gives the oracle's multicolour cycle exactly, on a shape whose y/z extents do
-    not divide the tiles."""
-    monkeypatch.setenv("MGMC_ZS_VARIANT", variant)
-    shape, kw = (128, 72, 40), dict(nlevel=2, npresmooth=2, npostsmooth=1)
-    s, p, lat = make(shape, **kw)
-    mc = oracle_for(s, p, lat)
-    f = np.random.default_rng(5).standard_normal(lat.Nvertex)
-    x_dev, x_orc = np.zeros(lat.Nvertex), np.zeros(lat.Nvertex)
-    for _ in range(2):
-        s.apply(f, x_dev)
-        mc.apply(f, x_orc)
-    assert np.array_equal(x_dev, x_orc)
-    s.close()
+# every MGMC_DISABLE token of mgmc_capi.hip (PathFlag), alone and all together, on configurations
+# where the fast path it turns off would run
+ALL_PATHS = "tail,fuse_prolong,quads,rb2d,zsweep,pairs,zrestrict,lr_small,lr_merge,lr_prefetch,coarse_precompute"
+VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_ssor"),
+            ("fuse_prolong", "3d128_zsweep_odd"),
+            ("tail", "3d16"), ("tail", "3d64_4lvl"), ("tail", "2d64_template_W"), ("tail", "3d32_W_ssor"),
+            ("quads", "3d64_4lvl"), ("quads", "3d_zres27"), ("quads", "2d256_global_coarse"),
+            ("quads", "2d_aniso_ssor"),
+            ("rb2d", "2d64_template_W"), ("rb2d", "2d_aniso_ssor"),
+            ("zsweep", "3d128_zsweep"), ("zsweep", "3d_aniso_zsweep_ssor"), ("zsweep", "3d192_zsweep"),
+            ("pairs", "3d64_4lvl"), ("pairs", "2d64_template_W"), ("pairs,quads", "3d32_W_ssor"),
+            ("zrestrict", "3d_zres7"), ("zrestrict", "3d_zres27"), ("zrestrict", "3d128_zsweep"),
+            ("coarse_precompute", "3d16"), ("coarse_precompute", "2d64_template_W"),
+            ("coarse_precompute", "3d32_W_ssor"), ("coarse_precompute,tail", "3d64_4lvl"),
+            (ALL_PATHS, "3d128_zsweep"), (ALL_PATHS, "3d_aniso_zsweep_ssor"), (ALL_PATHS, "2d64_template_W"),
+            (ALL_PATHS, "2d_aniso_ssor"), (ALL_PATHS, "3d_zres27")]
 
 
-@pytest.mark.parametrize("env,name", [("MGMC_NO_FUSE_PROLONG", "3d128_zsweep"),
-                                      ("MGMC_NO_FUSE_PROLONG", "3d_aniso_zsweep_ssor"),
-                                      ("MGMC_NO_FUSE_PROLONG", "3d128_zsweep_odd"),
-                                      ("MGMC_FUSE_RESTRICT", "3d128_zsweep"),
-                                      ("MGMC_FUSE_RESTRICT", "3d_zsr_edges"),
-                                      ("MGMC_FUSE_RESTRICT", "3d_zsr_ssor_W"),
-                                      ("MGMC_FUSE_RESTRICT", "3d_zres7"),
-                                      ("MGMC_FUSE_RESTRICT", "3d128_zsweep_odd"),
-                                      ("MGMC_QUADS", "3d64_4lvl"),
-                                      ("MGMC_QUADS", "3d_zres7"),
-                                      ("MGMC_QUADS", "3d32_W_ssor"),
-                                      ("MGMC_QUADS", "2d64_template_W"),
-                                      ("MGMC_NO_TAIL", "3d16"),
-                                      ("MGMC_NO_TAIL", "3d64_4lvl"),
-                                      ("MGMC_NO_TAIL", "2d64_template_W"),
-                                      ("MGMC_NO_TAIL", "3d32_W_ssor"),
-                                      ("MGMC_NO_QUADS", "3d64_4lvl"),
-                                      ("MGMC_NO_QUADS", "3d_zres27"),
-                                      ("MGMC_NO_QUADS", "2d256_global_coarse"),
-                                      ("MGMC_NO_QUADS", "2d_aniso_ssor"),
-                                      ("MGMC_NO_RB2D", "2d64_template_W"),
-                                      ("MGMC_NO_RB2D", "2d_aniso_ssor"),
-                                      ("MGMC_RB2D_PROLONG", "2d64_template_W"),
-                                      ("MGMC_RB2D_PROLONG", "2d_aniso_ssor"),
-                                      ("MGMC_ZR_VARIANT=2", "3d_zres7"),
-                                      ("MGMC_ZR_VARIANT=5", "3d_zres7"),
-                                      ("MGMC_ZS_PROLONG256", "3d128_zsweep"),
-                                      ("MGMC_ZS_PROLONG256", "3d_aniso_zsweep_ssor")])
-def test_variant_cycles_bitwise(hip_device, monkeypatch, env, name):
-    """MGMC_NO_FUSE_PROLONG: the separate prolongate-add pass (instead of the default fold into the
-    first post-sweep's plane loads); MGMC_FUSE_RESTRICT: the last pre-sweep, the residual and the
-    restriction in one kernel (k_zsweep_res7, opt-in); MGMC_QUADS: both colour pairs of a k-parity
-    half per launch on Galerkin levels, out of place (k_sweep_quads, opt-in); MGMC_NO_TAIL: the
-    coarsest levels' sub-cycle as separate launches instead of one workgroup (k_tail, the default
-    wherever the levels fit its LDS); MGMC_ZR_VARIANT=2 / 5: the 64 x 4 fine residual + restriction
-    tiles with 256 / 512 threads; MGMC_ZS_PROLONG256: the 256-thread fused-prolongation sweep.  All
-    give the oracle's cycle exactly."""
-    var, _, val = env.partition("=")
-    monkeypatch.setenv(var, val or "1")
+@pytest.mark.parametrize("paths,name", VARIANTS)
+def test_variant_cycles_bitwise(hip_device, monkeypatch, paths, name):
+    """MGMC_DISABLE=<paths> turns default fast paths off (mgmc_capi.hip PathFlag): tail = the coarsest
+    levels as separate launches instead of one k_tail workgroup; fuse_prolong = the separate
+    prolongate-add pass instead of the fold into the first post-sweep's plane loads; quads = one
+    colour pair per launch; rb2d / zsweep = the 2D / 3D fine level in colour passes; pairs = one
+    colour per pass on Galerkin levels; zrestrict = the per-point residual + restriction;
+    coarse_precompute = the coarse SSOR sampler's right-hand sides inside its colour passes.  Every
+    combination gives the oracle's cycle exactly."""
+    monkeypatch.setenv("MGMC_DISABLE", paths)
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)
     mc = oracle_for(s, p, lat)
@@ -221,6 +190,39 @@ def test_variant_cycles_bitwise(hip_device, monkeypatch, env, name):
         mc.apply(f, x_orc)
     assert np.array_equal(x_dev, x_orc)
     s.close()
+
+
+@pytest.mark.parametrize("name,qoi", [("3d128_zsweep", True), ("2d64_template_W", False), ("3d16", True)])
+def test_nonfinite_state_fails_loudly(hip_device, name, qoi):
+    """A NaN injected into the state (away from the watched vertex) reaches the QoI vertex / lattice
+    centre within a few cycles: mgmc_sample returns MGMC_E_NONFINITE with the sample index instead of
+    a chain that silently carries NaN; mgmc_set_state clears the guard."""
+    from multigridmc_amd import _native
+    shape, kw = CONFIGS[name]
+    s, p, lat = make(shape, **kw)
+    q = mg.measurement_vector_index(lat, [0.5] * lat.dim) if qoi else -1
+    s.sample(3, q)  # finite chain: no error
+    x = s.get_state()
+    x[1] = np.nan
+    s.set_state(x)
+    with pytest.raises(mg.MgmcError, match="non-finite chain state") as e:
+        s.sample(40, q)
+    assert e.value.code == _native.MGMC_E_NONFINITE
+    with pytest.raises(mg.MgmcError):  # sticky until a new state
+        s.synchronize()
+    s.set_state(np.zeros(lat.Nvertex))
+    s.sample(2, q)
+    f = np.zeros(lat.Nvertex)
+    f[lat.Nvertex // 2] = np.inf
+    with pytest.raises(mg.MgmcError, match="non-finite"):
+        s.apply(f, np.zeros(lat.Nvertex))
+    s.close()
+
+
+def test_unknown_disable_token_rejected(hip_device, monkeypatch):
+    monkeypatch.setenv("MGMC_DISABLE", "tail,no_such_path")
+    with pytest.raises(mg.MgmcError, match="no_such_path"):
+        make((16, 16, 16))
 
 
 def test_mgmc_seed_chain_independence(hip_device):

@@ -81,6 +81,34 @@ def test_create_without_gpu_fails_loudly():
         mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 1, mg.MultigridParameters(nlevel=2))
 
 
+def test_unknown_disable_token_rejected_before_any_device_call(monkeypatch):
+    """MGMC_DISABLE (the kernel-path switches, mgmc_capi.hip PathFlag) is parsed before the device is
+    touched; an unknown token is MGMC_E_INVALID with its name, on any host."""
+    monkeypatch.setenv("MGMC_DISABLE", "tail,bogus_path")
+    lat = mg.Lattice3d(8, 8, 8)
+    with pytest.raises(mg.MgmcError, match="bogus_path") as e:
+        mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 1, mg.MultigridParameters(nlevel=2))
+    assert e.value.code == _native.MGMC_E_INVALID
+
+
+def test_product_reads_only_documented_switches():
+    """The only environment the library reads: MGMC_DISABLE (kernel-path switches, each covered by
+    tests/test_gpu_parity.py VARIANTS / test_gpu_lowrank.py) and MGMC_GRAPH_UNROLL
+    (test_unrolled_sample_loop_bitwise)."""
+    src = ""
+    csrc = os.path.join(ROOT, "multigridmc_amd", "csrc")
+    for fn in os.listdir(csrc):
+        if fn.endswith((".hip", ".hpp", ".cpp", ".h")):
+            src += open(os.path.join(csrc, fn)).read()
+    assert sorted(set(re.findall(r'getenv\("([A-Z_0-9]+)"\)', src))) == ["MGMC_DISABLE", "MGMC_GRAPH_UNROLL"]
+    tokens = re.findall(r'\{"([a-z_0-9]+)", PATH_NO_', src)
+    assert len(tokens) == 11
+    tested = open(os.path.join(ROOT, "tests", "test_gpu_parity.py")).read() + \
+        open(os.path.join(ROOT, "tests", "test_gpu_lowrank.py")).read()
+    for t in tokens:
+        assert re.search(rf'["(,]{t}[",)]', tested), f"MGMC_DISABLE token {t} has no variant test"
+
+
 @pytest.mark.parametrize("shape", [(16, 16), (64, 32), (16, 16, 16), (32, 16, 16), (64, 64, 64)])
 def test_stencils_match_oracle_spgemm_bitwise(shape):
     nlevel = 3
@@ -221,14 +249,17 @@ def test_pooled_statistics_gloo_world2():
         assert res[r]["variance"] == pytest.approx(allv.var(), rel=1e-12)
 
 
-def test_cpp_host_side_describe_and_loud_failure(tmp_path):
-    """include/mgmc_sampler.hh compiles with g++ against the C-ABI library; the host-only path matches
-    mgmc_describe through ctypes, and on a host without a GPU constructing the sampler prints the
-    library error and exits with -1 (the reference's error convention, multigridmc_sampler.cc:47-49)."""
+@pytest.mark.parametrize("asan", [False, True])
+def test_cpp_host_side_describe_and_loud_failure(tmp_path, asan):
+    """include/mgmc_sampler.hh compiles with g++ against the C-ABI library (also with AddressSanitizer
+    and UBSan on the client); the host-only path matches mgmc_describe through ctypes, and on a host
+    without a GPU constructing the sampler prints the library error and exits with -1 (the
+    reference's error convention, multigridmc_sampler.cc:47-49)."""
     import subprocess
     from tests.cpp_client import build_client
-    exe = build_client(tmp_path)
-    out = subprocess.run([exe, "describe"], capture_output=True, text=True, check=True).stdout.split("\n")
+    exe = build_client(tmp_path, asan=asan)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    out = subprocess.run([exe, "describe"], capture_output=True, text=True, check=True, env=env).stdout.split("\n")
     assert out[0] == "abi 2"
     cfg_levels = mg.describe(mg.make_config(mg.ShiftedLaplaceFDOperator(mg.Lattice3d(64, 64, 64), 25.0),
                                             mg.MultigridParameters(nlevel=4)))
@@ -240,7 +271,7 @@ def test_cpp_host_side_describe_and_loud_failure(tmp_path):
     n = ctypes.c_int(0)
     if hip.hipGetDeviceCount(ctypes.byref(n)) == 0 and n.value > 0:
         return
-    r = subprocess.run([exe, "sample", "2"], capture_output=True, text=True)
+    r = subprocess.run([exe, "sample", "2"], capture_output=True, text=True, env=env)
     assert r.returncode == 255 and "ERROR: mgmc_create failed" in r.stderr
 
 

@@ -288,3 +288,16 @@ def test_mgmc_3d_fd_statistics(mode):
     # infinity norm over 343^2 covariance entries of a 20000-sample estimate: ~4 sigma of
     # sqrt(2/n) * max|Q^-1| * sqrt(IACT) ~ 0.04-0.05 relative; tolerance 0.07
     assert em < 0.05 * scale and ec < 0.07 * scale
+
+
+def test_host_code_clean_under_address_sanitizer():
+    """`make -C oracle asan`: the product's host-side hierarchy setup (mgmc_hierarchy.cpp) and the
+    whole oracle C API (both modes, FD / FEM / CSR, low-rank sparse and dense columns, dense
+    Cholesky coarse sampler) under AddressSanitizer + UBSan, no report."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle"), "asan"], check=True)
+    r = subprocess.run([os.path.join(root, "oracle", "build", "asan_host")], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "asan_host OK" in r.stdout
