@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MGMC_ABI_VERSION 2
+#define MGMC_ABI_VERSION 3
 
 /* error codes */
 #define MGMC_OK 0
@@ -62,6 +62,13 @@ extern "C" {
 #define MGMC_OPERATOR_FD 0  /* ShiftedLaplaceFDOperator: 5/7-point (shiftedlaplace_fd_operator.cc:9-57) */
 #define MGMC_OPERATOR_FEM 1 /* ShiftedLaplaceFEMOperator: Q1 elements, 9/27-point
                                (shiftedlaplace_fem_operator.cc:9-145) */
+#define MGMC_OPERATOR_SQUARED_FD 2 /* SquaredShiftedLaplaceFDOperator, 2D 13-point
+                                      (squared_shiftedlaplace_fd_operator.cc:9-96); CSR path only */
+
+/* correlation-length models (linear_operator/correlationlength_model.hh:45-112) */
+#define MGMC_KAPPA_CONSTANT 0 /* kappa^2 = 1 / Lambda^2 */
+#define MGMC_KAPPA_PERIODIC 1 /* Lambda(x) = L1 + L2 prod_d cos(pi x_d), L1/2 = (Lambda_max +/- Lambda_min)/2 */
+#define MGMC_KAPPA_GIVEN 2    /* constant kappa^2 given directly (mgmc_config.kappa_sq's convention) */
 
 /* sweep directions (smoother/sor_smoother.hh:14-18) */
 #define MGMC_FORWARD 1
@@ -97,7 +104,7 @@ typedef struct mgmc_level_desc {
     int nx, ny, nz;       /* cells per direction on this level (nz = 0 for 2D) */
     int npoints;          /* stencil points: 5/7 (fine FD) or 9/27 (fine FEM, Galerkin) */
     int ncolours;         /* colours of the Gibbs sweep: 2 (5/7-point) or 2^dim (9/27-point) */
-    int pad_;
+    int varcoef;          /* 1: per-vertex coefficients (mgmc_create_csr); stencil = the centre row */
     uint64_t ndof;        /* number of interior unknowns */
     /* stencil coefficients indexed by offset (dz+1)*9 + (dy+1)*3 + (dx+1) (3D) or
      * (dy+1)*3 + (dx+1) (2D); entries outside the stencil are 0 */
@@ -113,8 +120,36 @@ int mgmc_abi_version(void);
 int mgmc_describe(const mgmc_config* cfg, mgmc_level_desc* out, int max_levels);
 const char* mgmc_last_error(const mgmc_handle* h);
 
+/* ---- fine operators as matrices (ABI 3; host only, no GPU touched) ----
+ * The reference's LinearOperator subclasses with any correlation-length model
+ * (ShiftedLaplaceFDOperator shiftedlaplace_fd_operator.cc:9-57, ShiftedLaplaceFEMOperator
+ * shiftedlaplace_fem_operator.cc:9-145, SquaredShiftedLaplaceFDOperator
+ * squared_shiftedlaplace_fd_operator.cc:9-96; PeriodicCorrelationLengthModel
+ * correlationlength_model.hh:68-112) assembled as their A_sparse: CSR, rows = interior vertices in
+ * the lattice order (x fastest), columns ascending, entries summed as the reference sums them. */
+typedef struct mgmc_operator_desc {
+    int dim, nx, ny, nz;       /* lattice (nz ignored for dim = 2) */
+    int pde;                   /* MGMC_OPERATOR_FD / _FEM / _SQUARED_FD */
+    int kappa_model;           /* MGMC_KAPPA_CONSTANT / _PERIODIC */
+    double Lambda;             /* constant model */
+    double Lambda_min, Lambda_max; /* periodic model */
+    double kappa_sq;           /* MGMC_KAPPA_GIVEN */
+} mgmc_operator_desc;
+/* rows and stored entries of the assembled matrix */
+int mgmc_operator_csr_size(const mgmc_operator_desc* d, int64_t* nrow, int64_t* nnz);
+/* fill rowptr[nrow + 1], col[nnz], val[nnz] */
+int mgmc_operator_csr(const mgmc_operator_desc* d, int64_t* rowptr, int32_t* col, double* val);
+
 /* ---- lifetime ---- */
 int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chain_id, mgmc_handle** out);
+/* A sampler on a fine operator given as a matrix (LinearOperator::A_sparse, linear_operator.hh:187):
+ * CSR on cfg's lattice (rows = interior vertices, columns strictly ascending, a positive diagonal,
+ * couplings at most 2 vertices apart per direction).  Every coarse level is the Galerkin product
+ * R A R^T (linear_operator.cc:10-23) formed on the host; every level is swept with its own per-vertex
+ * coefficients (2 colours for a 5/7-point fine level, 2^d for reach-1 levels, 3^d for reach-2
+ * levels such as the squared FD operator's).  cfg.kappa_sq and cfg.fine_operator are ignored. */
+int mgmc_create_csr(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr, const int32_t* col,
+                    const double* val, int device, uint64_t seed, uint64_t chain_id, mgmc_handle** out);
 int mgmc_destroy(mgmc_handle* h);
 int mgmc_level_desc_get(const mgmc_handle* h, int level, mgmc_level_desc* out);
 

@@ -18,6 +18,9 @@ from .sampler import (  # noqa: F401
     MultigridMCSampler,
     ShiftedLaplaceFDOperator,
     ShiftedLaplaceFEMOperator,
+    SquaredShiftedLaplaceFDOperator,
+    ConstantCorrelationLengthModel,
+    PeriodicCorrelationLengthModel,
     comm_unique_id,
     describe,
     make_config,

@@ -25,7 +25,11 @@ COARSE_SSOR = 0
 COARSE_CHOLESKY = 1
 OPERATOR_FD = 0
 OPERATOR_FEM = 1
-ABI_VERSION = 2
+OPERATOR_SQUARED_FD = 2
+KAPPA_CONSTANT = 0
+KAPPA_PERIODIC = 1
+KAPPA_GIVEN = 2
+ABI_VERSION = 3
 SOLVER_LOOP = 0
 SOLVER_CG = 1
 FORWARD = 1
@@ -46,9 +50,17 @@ class MgmcConfig(ctypes.Structure):
 class MgmcLevelDesc(ctypes.Structure):
     _fields_ = [
         ("nx", c_int), ("ny", c_int), ("nz", c_int),
-        ("npoints", c_int), ("ncolours", c_int), ("pad_", c_int),
+        ("npoints", c_int), ("ncolours", c_int), ("varcoef", c_int),
         ("ndof", c_uint64),
         ("stencil", c_double * 27),
+    ]
+
+
+class MgmcOperatorDesc(ctypes.Structure):
+    _fields_ = [
+        ("dim", c_int), ("nx", c_int), ("ny", c_int), ("nz", c_int),
+        ("pde", c_int), ("kappa_model", c_int),
+        ("Lambda", c_double), ("Lambda_min", c_double), ("Lambda_max", c_double), ("kappa_sq", c_double),
     ]
 
 
@@ -66,6 +78,10 @@ SIGNATURES = [
     ("mgmc_describe", c_int, [POINTER(MgmcConfig), POINTER(MgmcLevelDesc), c_int]),
     ("mgmc_last_error", c_char_p, [_H]),
     ("mgmc_create", c_int, [POINTER(MgmcConfig), c_int, c_uint64, c_uint64, POINTER(c_void_p)]),
+    ("mgmc_create_csr", c_int, [POINTER(MgmcConfig), c_int64, POINTER(c_int64), POINTER(ctypes.c_int32), _DP, c_int,
+                                c_uint64, c_uint64, POINTER(c_void_p)]),
+    ("mgmc_operator_csr_size", c_int, [POINTER(MgmcOperatorDesc), POINTER(c_int64), POINTER(c_int64)]),
+    ("mgmc_operator_csr", c_int, [POINTER(MgmcOperatorDesc), POINTER(c_int64), POINTER(ctypes.c_int32), _DP]),
     ("mgmc_destroy", c_int, [_H]),
     ("mgmc_level_desc_get", c_int, [_H, c_int, POINTER(MgmcLevelDesc)]),
     ("mgmc_set_lowrank", c_int, [_H, c_int, POINTER(c_int64), POINTER(c_int64), _DP, _DP]),

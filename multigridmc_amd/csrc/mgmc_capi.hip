@@ -29,6 +29,8 @@
 #include "mgmc_lowrank.hpp"
 #include "mgmc_solver.hpp"
 #include "mgmc_cholesky.hpp"
+#include "mgmc_field.hpp"
+#include "mgmc_operators.hpp"
 
 using namespace mgmc;
 
@@ -185,6 +187,9 @@ struct Level {
     bool pairs = false;    // Galerkin level swept in colour-pair passes (mgmc_gsweep.hpp)
     bool quads = false;    // ... two pairs per launch, out of place (k_sweep_quads)
     bool rb2d = false;     // 2D 5-point level: one-launch red-black sweep, out of place (k_rb2d)
+    bool field = false;    // per-vertex coefficients (mgmc_create_csr, mgmc_field.hpp)
+    FieldArg F;            // ... their device field, pattern and colouring
+    double* rbuf = nullptr;  // ... residual scratch (padded layout, zero boundary)
     bool pingpong() const { return zsweep || quads || rb2d; }  // out-of-place sweeps: x <-> x2
     double* buf(int i) const { return i == 0 ? x : x2; }
     LowRankDev lr;
@@ -235,6 +240,8 @@ struct mgmc_handle {
     double* sv_part = nullptr;   // reduction partials
     std::vector<LRColumn> lr_cols;  // low-rank columns of the coarsest level, and Sigma (for the factors)
     std::vector<double> lr_sigma;
+    bool field_mode = false;     // hierarchy built from a matrix (mgmc_create_csr)
+    CsrHost coarse_csr;          // ... and its coarsest level (dense Cholesky factors)
     int chol_n = 0;              // dense Cholesky factors of the coarsest level (mgmc_cholesky.hpp)
     double* chol_G = nullptr;
     double* chol_Li = nullptr;
@@ -299,8 +306,35 @@ void launch_sweep_t(const Level& lv, double* x, const double* f, const GibbsArg&
     }
 }
 
+// colour passes of a field level (mgmc_field.hpp): colours ascending forward, descending backward
+void launch_fsweep(const Level& lv, double* x, const double* f, const GibbsArg& g0, int direction, bool noise,
+                   hipStream_t s) {
+    const Layout& L = lv.L;
+    const int nc = lv.F.scheme, dim = lv.spec.dim;
+    const int st = nc == 9 || nc == 27 ? 3 : 2;  // vertices of one colour are st apart per direction
+    dim3 block(64, 4, 1);
+    dim3 grid = nc == 2 ? grid3(L.nx / 2, L.ny - 1, dim == 3 ? L.nz - 1 : 1, block)
+                        : grid3((L.nx - 1 + st - 1) / st, (L.ny - 1 + st - 1) / st,
+                                dim == 3 ? (L.nz - 1 + st - 1) / st : 1, block);
+    for (int cc = 0; cc < nc; ++cc) {
+        GibbsArg g = g0;
+        g.colour = (direction == MGMC_FORWARD) ? cc : nc - 1 - cc;
+        if (dim == 3) {
+            if (noise) hipLaunchKernelGGL((k_fsweep<3, true>), grid, block, 0, s, L, x, f, lv.F, g);
+            else hipLaunchKernelGGL((k_fsweep<3, false>), grid, block, 0, s, L, x, f, lv.F, g);
+        } else {
+            if (noise) hipLaunchKernelGGL((k_fsweep<2, true>), grid, block, 0, s, L, x, f, lv.F, g);
+            else hipLaunchKernelGGL((k_fsweep<2, false>), grid, block, 0, s, L, x, f, lv.F, g);
+        }
+    }
+}
+
 void launch_sweep(const Level& lv, double* x, const double* f, const GibbsArg& g, int direction, bool noise,
                   hipStream_t s) {
+    if (lv.field) {
+        launch_fsweep(lv, x, f, g, direction, noise, s);
+        return;
+    }
     const int dim = lv.spec.dim, np = lv.spec.npoints;
 #define DISPATCH(D, P)                                                       \
     if (dim == D && np == P) {                                               \
@@ -524,6 +558,20 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
 
 void launch_residual_restrict(const Level& lf, const Level& lc, const double* x, const double* f, double* fc,
                               double* xc, int zero_xc, hipStream_t s) {
+    if (lf.field) {  // r = f - A x into the level's scratch, then fc = R r (and x_c = 0)
+        dim3 block(64, 4, 1);
+        dim3 grid = grid3(lf.L.nx - 1, lf.L.ny - 1, lf.spec.dim == 3 ? lf.L.nz - 1 : 1, block);
+        dim3 gc = grid3(lc.L.nx - 1, lc.L.ny - 1, lf.spec.dim == 3 ? lc.L.nz - 1 : 1, block);
+        if (lf.spec.dim == 3) {
+            hipLaunchKernelGGL((k_fresidual<3>), grid, block, 0, s, lf.L, x, f, lf.F, lf.rbuf);
+            hipLaunchKernelGGL((k_restrict<3>), gc, block, 0, s, lf.L, lc.L, (const double*)lf.rbuf, fc);
+        } else {
+            hipLaunchKernelGGL((k_fresidual<2>), grid, block, 0, s, lf.L, x, f, lf.F, lf.rbuf);
+            hipLaunchKernelGGL((k_restrict<2>), gc, block, 0, s, lf.L, lc.L, (const double*)lf.rbuf, fc);
+        }
+        if (zero_xc) hipMemsetAsync(xc, 0, lc.L.nstore * sizeof(double), s);
+        return;
+    }
     // z-marching kernel on every 3D level with coarse n >= 8: 64 x 4 coarse points per workgroup from
     // coarse n = ZR_SMALL_NX up, 16 x 4 points (one wavefront) below, where the wide tiles would leave
     // most of the chip idle (the 27-point gather kernel took 24 us per launch on the 15^3 / 7^3 levels)
@@ -707,7 +755,11 @@ void launch_operator_apply(const mgmc_handle* h, const Level& lv, const double* 
     dim3 block(64, 4, 1);
     dim3 grid = grid3(lv.L.nx - 1, lv.L.ny - 1, lv.spec.dim == 3 ? lv.L.nz - 1 : 1, block);
     const int dim = lv.spec.dim, np = lv.spec.npoints;
-    if (dim == 3 && np == 7)
+    if (lv.field && dim == 3)
+        hipLaunchKernelGGL((k_fapply<3>), grid, block, 0, s, lv.L, xs, lv.F, ys);
+    else if (lv.field)
+        hipLaunchKernelGGL((k_fapply<2>), grid, block, 0, s, lv.L, xs, lv.F, ys);
+    else if (dim == 3 && np == 7)
         hipLaunchKernelGGL((k_operator_apply<3, 7>), grid, block, 0, s, lv.L, xs, ys, lv.S);
     else if (dim == 3)
         hipLaunchKernelGGL((k_operator_apply<3, 27>), grid, block, 0, s, lv.L, xs, ys, lv.S);
@@ -907,8 +959,8 @@ Layout tail_layout(const Layout& L) {
 }
 
 // the same choice from the level shapes alone (at creation time, before any level is allocated)
-int tail_start_by_size(const std::vector<LevelSpec>& specs, const mgmc_config& cfg, uint32_t paths) {
-    if ((paths & PATH_NO_TAIL) || cfg.coarse_solver != MGMC_COARSE_SSOR) return -1;
+int tail_start_by_size(const std::vector<LevelSpec>& specs, const mgmc_config& cfg, uint32_t paths, bool field) {
+    if ((paths & PATH_NO_TAIL) || field || cfg.coarse_solver != MGMC_COARSE_SSOR) return -1;
     const int L = (int)specs.size();
     for (int lt = 1; lt + 1 < L; ++lt) {
         bool ok = true;
@@ -930,7 +982,7 @@ int tail_start_by_size(const std::vector<LevelSpec>& specs, const mgmc_config& c
 // one (k_lr_small's), ordinary (in-place) sweeps, SSOR coarse sampler; -1 if none or only the
 // coarsest level fits (the coarse LDS kernel covers that)
 int tail_level(const mgmc_handle* h) {
-    if ((h->paths & PATH_NO_TAIL) || h->cfg.coarse_solver != MGMC_COARSE_SSOR) return -1;
+    if ((h->paths & PATH_NO_TAIL) || h->field_mode || h->cfg.coarse_solver != MGMC_COARSE_SSOR) return -1;
     const int L = (int)h->levels.size();
     for (int lt = 1; lt + 1 < L; ++lt) {
         bool ok = true;
@@ -1297,7 +1349,12 @@ int build_coarse_chol(mgmc_handle* h, const std::vector<LRColumn>* cols, const d
     const int dim = lv.spec.dim;
     const int nx = lv.spec.n[0], ny = lv.spec.n[1], nz = dim == 3 ? lv.spec.n[2] : 2;
     std::vector<double> Q((size_t)n * n, 0.0);
-    for (long long r = 0; r < n; ++r) {
+    if (h->field_mode) {  // the coarsest Galerkin matrix itself
+        const CsrHost& A = h->coarse_csr;
+        for (long long r = 0; r < n; ++r)
+            for (int64_t q = A.rowptr[r]; q < A.rowptr[r + 1]; ++q) Q[(size_t)r * n + A.col[q]] = A.val[q];
+    }
+    for (long long r = 0; r < (h->field_mode ? 0 : n); ++r) {
         const int i = (int)(r % (nx - 1)) + 1, j = (int)((r / (nx - 1)) % (ny - 1)) + 1;
         const int k = dim == 3 ? (int)(r / ((long long)(nx - 1) * (ny - 1))) + 1 : 1;
         for (int dz = (dim == 3 ? -1 : 0); dz <= (dim == 3 ? 1 : 0); ++dz)
@@ -1338,8 +1395,9 @@ int build_coarse_chol(mgmc_handle* h, const std::vector<LRColumn>* cols, const d
     return MGMC_OK;
 }
 
-void fill_desc(const LevelSpec& s, mgmc_level_desc* d) {
+void fill_desc(const LevelSpec& s, mgmc_level_desc* d, bool varcoef = false) {
     memset(d, 0, sizeof(*d));
+    d->varcoef = varcoef ? 1 : 0;
     d->nx = s.n[0];
     d->ny = s.n[1];
     d->nz = s.dim == 3 ? s.n[2] : 0;
@@ -1347,6 +1405,73 @@ void fill_desc(const LevelSpec& s, mgmc_level_desc* d) {
     d->ncolours = s.ncolours;
     d->ndof = s.ndof;
     memcpy(d->stencil, s.st, sizeof(d->stencil));
+}
+
+// a level's coefficient field from its matrix (mgmc_field.hpp): the union of the rows' offsets in
+// ascending column order, every row's entries at their offsets (zeros elsewhere); the colouring of
+// the oracle's multicolour mode: red-black for a fine level of at most 2d+1 entries per row and reach
+// 1, coordinates mod 3 for reach 2, parities otherwise
+struct FieldHost {
+    int np = 0, diag = -1, scheme = 0;
+    int d[FIELD_MAXNP][3];
+    std::vector<double> coef;
+    double centre[27];
+};
+
+FieldHost make_field(const CsrHost& A, int dim, const int* n, int level) {
+    FieldHost F;
+    const int64_t nxi = n[0] - 1, nyi = n[1] - 1;
+    auto euc = [&](int64_t e, int* idx) {
+        idx[0] = (int)(e % nxi) + 1;
+        idx[1] = (int)((e / nxi) % nyi) + 1;
+        idx[2] = dim == 3 ? (int)(e / (nxi * nyi)) + 1 : 0;
+    };
+    auto key = [](int dx, int dy, int dz) { return (dz + 2) * 25 + (dy + 2) * 5 + (dx + 2); };
+    bool present[125] = {false};
+    int reach = 0;
+    int64_t maxnnz = 0;
+    for (int64_t r = 0; r < A.nrow; ++r) {
+        int a[3], b[3];
+        euc(r, a);
+        maxnnz = std::max(maxnnz, A.rowptr[r + 1] - A.rowptr[r]);
+        for (int64_t q = A.rowptr[r]; q < A.rowptr[r + 1]; ++q) {
+            euc(A.col[q], b);
+            const int dx = b[0] - a[0], dy = b[1] - a[1], dz = b[2] - a[2];
+            reach = std::max(reach, std::max(std::abs(dx), std::max(std::abs(dy), std::abs(dz))));
+            present[key(dx, dy, dz)] = true;
+        }
+    }
+    int slot[125];
+    for (int k = 0; k < 125; ++k) {
+        slot[k] = -1;
+        if (!present[k]) continue;
+        slot[k] = F.np;
+        F.d[F.np][0] = k % 5 - 2;
+        F.d[F.np][1] = (k / 5) % 5 - 2;
+        F.d[F.np][2] = k / 25 - 2;
+        if (k == key(0, 0, 0)) F.diag = F.np;
+        ++F.np;
+    }
+    F.scheme = reach >= 2 ? (dim == 3 ? 27 : 9) : ((level == 0 && maxnnz <= 2 * dim + 1) ? 2 : (1 << dim));
+    F.coef.assign((size_t)A.nrow * F.np, 0.0);
+    for (int64_t r = 0; r < A.nrow; ++r) {
+        int a[3], b[3];
+        euc(r, a);
+        for (int64_t q = A.rowptr[r]; q < A.rowptr[r + 1]; ++q) {
+            euc(A.col[q], b);
+            F.coef[(size_t)r * F.np + slot[key(b[0] - a[0], b[1] - a[1], b[2] - a[2])]] = A.val[q];
+        }
+    }
+    // the row of the lattice's centre vertex, for mgmc_level_desc (3^d box)
+    for (double& v : F.centre) v = 0.0;
+    const int64_t rc = ((int64_t)(dim == 3 ? (n[2] / 2 - 1) : 0) * nyi + (n[1] / 2 - 1)) * nxi + (n[0] / 2 - 1);
+    for (int p = 0; p < F.np; ++p) {
+        const int* o = F.d[p];
+        if (std::abs(o[0]) > 1 || std::abs(o[1]) > 1 || std::abs(o[2]) > 1) continue;
+        const int k = dim == 3 ? (o[2] + 1) * 9 + (o[1] + 1) * 3 + (o[0] + 1) : (o[1] + 1) * 3 + (o[0] + 1);
+        F.centre[k] = F.coef[(size_t)rc * F.np + p];
+    }
+    return F;
 }
 
 }  // namespace
@@ -1377,11 +1502,26 @@ int mgmc_describe(const mgmc_config* cfg, mgmc_level_desc* out, int max_levels) 
     return (int)lv.size();
 }
 
-int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chain_id, mgmc_handle** out) {
+// mgmc_create / mgmc_create_csr: csr = the fine operator's matrix (null: the constant-coefficient
+// hierarchy of cfg), every level then built from matrices
+static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, uint64_t seed, uint64_t chain_id,
+                       mgmc_handle** out) {
     if (!cfg || !out) return fail(nullptr, MGMC_E_INVALID, "null argument");
     *out = nullptr;
     const std::string err = validate_config(*cfg);
     if (!err.empty()) return fail(nullptr, MGMC_E_INVALID, err);
+    std::vector<CsrHost> mats;  // per level (matrix path)
+    if (csr) {
+        const int n0[3] = {cfg->nx, cfg->ny, cfg->dim == 3 ? cfg->nz : 1};
+        const std::string e = check_lattice_csr(cfg->dim, n0, *csr);
+        if (!e.empty()) return fail(nullptr, MGMC_E_INVALID, "mgmc_create_csr: " + e);
+        mats.push_back(*csr);
+        int n[3] = {n0[0], n0[1], n0[2]};
+        for (int l = 1; l < cfg->nlevel; ++l) {
+            mats.push_back(galerkin_csr(mats.back(), cfg->dim, n));
+            for (int d = 0; d < cfg->dim; ++d) n[d] /= 2;
+        }
+    }
     uint32_t paths = 0;
     std::string bad;
     if (!read_path_flags(&paths, &bad)) return fail(nullptr, MGMC_E_INVALID, "MGMC_DISABLE: unknown path '" + bad + "'");
@@ -1412,8 +1552,17 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         h->last_error = "hipStreamCreate failed";
         return bail(MGMC_E_HIP);
     }
-    const std::vector<LevelSpec> specs = build_hierarchy(*cfg);
-    const int tail0 = tail_start_by_size(specs, *cfg, h->paths);  // levels k_tail can take (no quads there)
+    std::vector<LevelSpec> specs = build_hierarchy(*cfg);
+    h->field_mode = csr != nullptr;
+    std::vector<FieldHost> fields;
+    for (size_t l = 0; l < mats.size(); ++l) {
+        fields.push_back(make_field(mats[l], cfg->dim, specs[l].n, (int)l));
+        specs[l].npoints = fields.back().np;
+        specs[l].ncolours = fields.back().scheme;
+        memcpy(specs[l].st, fields.back().centre, sizeof(specs[l].st));
+    }
+    if (!mats.empty()) h->coarse_csr = mats.back();
+    const int tail0 = tail_start_by_size(specs, *cfg, h->paths, h->field_mode);  // levels k_tail can take (no quads there)
     size_t lds_limit = 150 * 1024;
     for (size_t l = 0; l < specs.size(); ++l) {
         Level lv;
@@ -1430,13 +1579,38 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
         }
         hipMemsetAsync(lv.x, 0, bytes, h->stream);
         hipMemsetAsync(lv.f, 0, bytes, h->stream);
+        if (h->field_mode) {  // per-vertex coefficients and a residual scratch
+            const FieldHost& fh = fields[l];
+            lv.field = true;
+            memset(&lv.F, 0, sizeof(lv.F));
+            lv.F.np = fh.np;
+            lv.F.diag = fh.diag;
+            lv.F.nxi = lv.L.nx - 1;
+            lv.F.nyi = lv.L.ny - 1;
+            lv.F.scheme = fh.scheme;
+            lv.F.omega = cfg->omega;
+            for (int q = 0; q < fh.np; ++q)
+                lv.F.off[q] = (int)(fh.d[q][2] * lv.L.sp + fh.d[q][1] * lv.L.sx + fh.d[q][0]);
+            double* coef = nullptr;
+            if (hipMalloc(&coef, fh.coef.size() * sizeof(double)) != hipSuccess ||
+                hipMalloc(&lv.rbuf, bytes) != hipSuccess) {
+                lv.F.coef = coef;
+                h->levels.push_back(lv);
+                h->last_error = "device allocation failed (coefficient field)";
+                return bail(MGMC_E_NOMEM);
+            }
+            lv.F.coef = coef;
+            hipMemcpyAsync(coef, fh.coef.data(), fh.coef.size() * sizeof(double), hipMemcpyHostToDevice, h->stream);
+            hipMemsetAsync(lv.rbuf, 0, bytes, h->stream);
+        }
         // fused z-marching sweep: fine 3D 7-point levels whose row splits into 64-pair tiles
         const double* st = lv.spec.st;  // the z-sweep folds the symmetric FD stencil to 4 coefficients
         const bool symmetric = st[4] == st[22] && st[10] == st[16] && st[12] == st[14];
-        lv.zsweep = cfg->dim == 3 && lv.spec.npoints == 7 && symmetric && l + 1 < specs.size() &&
+        lv.zsweep = !lv.field && cfg->dim == 3 && lv.spec.npoints == 7 && symmetric && l + 1 < specs.size() &&
                     (lv.L.nx % (2 * ZS_XP)) == 0 && !(h->paths & PATH_NO_ZSWEEP);
-        lv.pairs = pairs_eligible(lv.spec, lv.L) && !(h->paths & PATH_NO_PAIRS);
-        lv.rb2d = cfg->dim == 2 && lv.spec.npoints == 5 && l + 1 < specs.size() && !(h->paths & PATH_NO_RB2D);
+        lv.pairs = !lv.field && pairs_eligible(lv.spec, lv.L) && !(h->paths & PATH_NO_PAIRS);
+        lv.rb2d = !lv.field && cfg->dim == 2 && lv.spec.npoints == 5 && l + 1 < specs.size() &&
+                  !(h->paths & PATH_NO_RB2D);
         lv.quads = lv.pairs && quads_eligible(lv.spec, lv.L, h->paths) && (tail0 < 0 || (int)l < tail0);
         if (lv.pingpong()) {
             if (hipMalloc(&lv.x2, bytes) != hipSuccess) {
@@ -1446,7 +1620,7 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
             }
             hipMemsetAsync(lv.x2, 0, bytes, h->stream);
         }
-        if (l + 1 == specs.size() && 2 * bytes <= lds_limit) lv.lds_bytes = 2 * bytes;
+        if (!lv.field && l + 1 == specs.size() && 2 * bytes <= lds_limit) lv.lds_bytes = 2 * bytes;
         h->levels.push_back(lv);
     }
     if (hipMalloc(&h->ctrl, 8 * sizeof(uint64_t)) != hipSuccess || hipMalloc(&h->mom, 4 * sizeof(double)) != hipSuccess) {
@@ -1480,6 +1654,46 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
     return MGMC_OK;
 }
 
+int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chain_id, mgmc_handle** out) {
+    return create_impl(cfg, nullptr, device, seed, chain_id, out);
+}
+
+int mgmc_create_csr(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr, const int32_t* col,
+                    const double* val, int device, uint64_t seed, uint64_t chain_id, mgmc_handle** out) {
+    if (!cfg || !rowptr || !col || !val || !out || nrow < 1) return fail(nullptr, MGMC_E_INVALID, "null argument");
+    if (rowptr[0] != 0 || rowptr[nrow] < nrow) return fail(nullptr, MGMC_E_INVALID, "mgmc_create_csr: invalid row pointer");
+    mgmc_config c = *cfg;  // the matrix replaces kappa^2 and the fine-operator choice
+    c.kappa_sq = 0.0;
+    c.fine_operator = MGMC_OPERATOR_FD;
+    CsrHost A;
+    A.nrow = nrow;
+    A.rowptr.assign(rowptr, rowptr + nrow + 1);
+    A.col.assign(col, col + rowptr[nrow]);
+    A.val.assign(val, val + rowptr[nrow]);
+    return create_impl(&c, &A, device, seed, chain_id, out);
+}
+
+int mgmc_operator_csr_size(const mgmc_operator_desc* d, int64_t* nrow, int64_t* nnz) {
+    if (!d || !nrow || !nnz) return fail(nullptr, MGMC_E_INVALID, "null argument");
+    const std::string e = validate_operator(*d);
+    if (!e.empty()) return fail(nullptr, MGMC_E_INVALID, e);
+    const CsrHost A = assemble_operator(*d);
+    *nrow = A.nrow;
+    *nnz = (int64_t)A.col.size();
+    return MGMC_OK;
+}
+
+int mgmc_operator_csr(const mgmc_operator_desc* d, int64_t* rowptr, int32_t* col, double* val) {
+    if (!d || !rowptr || !col || !val) return fail(nullptr, MGMC_E_INVALID, "null argument");
+    const std::string e = validate_operator(*d);
+    if (!e.empty()) return fail(nullptr, MGMC_E_INVALID, e);
+    const CsrHost A = assemble_operator(*d);
+    std::copy(A.rowptr.begin(), A.rowptr.end(), rowptr);
+    std::copy(A.col.begin(), A.col.end(), col);
+    std::copy(A.val.begin(), A.val.end(), val);
+    return MGMC_OK;
+}
+
 int mgmc_destroy(mgmc_handle* h) {
     if (!h) return MGMC_OK;
     hipSetDevice(h->device);
@@ -1493,6 +1707,8 @@ int mgmc_destroy(mgmc_handle* h) {
         if (lv.x) hipFree(lv.x);
         if (lv.x2) hipFree(lv.x2);
         if (lv.f) hipFree(lv.f);
+        if (lv.F.coef && lv.field) hipFree((void*)lv.F.coef);
+        if (lv.rbuf) hipFree(lv.rbuf);
         for (auto p : lv.scratch)
             if (p) hipFree(p);
     }
@@ -1516,7 +1732,7 @@ int mgmc_destroy(mgmc_handle* h) {
 int mgmc_level_desc_get(const mgmc_handle* h, int level, mgmc_level_desc* out) {
     if (!h || !out) return fail(nullptr, MGMC_E_INVALID, "null argument");
     if (level < 0 || level >= (int)h->levels.size()) return fail(nullptr, MGMC_E_INVALID, "level out of range");
-    fill_desc(h->levels[level].spec, out);
+    fill_desc(h->levels[level].spec, out, h->levels[level].field);
     return MGMC_OK;
 }
 

@@ -85,15 +85,61 @@ def Lattice3d(nx: int, ny: int, nz: int) -> Lattice:
     return Lattice(nx, ny, nz)
 
 
+class ConstantCorrelationLengthModel:
+    """kappa^2 = 1 / Lambda^2 everywhere (correlationlength_model.hh:45-66)."""
+
+    kind = _native.KAPPA_CONSTANT
+
+    def __init__(self, Lambda: float):
+        self.Lambda = float(Lambda)
+
+    def kappa_sq(self, x=None) -> float:
+        import math
+        return 1.0 / math.pow(self.Lambda, 2)
+
+
+class PeriodicCorrelationLengthModel:
+    """Lambda(x) = Lambda_1 + Lambda_2 prod_d cos(pi x_d), Lambda_1,2 = (Lambda_max +/- Lambda_min) / 2,
+    kappa^2 = 1 / Lambda^2 (correlationlength_model.hh:68-112).  Its operators have per-vertex
+    coefficients: they go to the device as matrices (mgmc_create_csr)."""
+
+    kind = _native.KAPPA_PERIODIC
+
+    def __init__(self, Lambda_min: float, Lambda_max: float):
+        self.Lambda_min, self.Lambda_max = float(Lambda_min), float(Lambda_max)
+
+    def kappa_sq(self, x) -> float:
+        import math
+        lam = 0.5 * (self.Lambda_max - self.Lambda_min)
+        for v in x:
+            lam *= math.cos(math.pi * float(v))
+        lam += 0.5 * (self.Lambda_max + self.Lambda_min)
+        return 1.0 / (lam * lam)
+
+
 class ShiftedLaplaceFDOperator:
-    """Fine-level precision operator: FD shifted Laplacian with constant kappa^2.
+    """Fine-level precision operator: FD shifted Laplacian (shiftedlaplace_fd_operator.cc:9-57).
 
-    The device path consumes the operator's data (the stencil), not its methods, because the
-    reference's LinearOperator::apply is not virtual (linear_operator.hh:66)."""
+    With a constant kappa^2 (a number, or ConstantCorrelationLengthModel) the device consumes the
+    operator's data as a constant stencil per level (the reference's LinearOperator::apply is not
+    virtual, linear_operator.hh:66); with PeriodicCorrelationLengthModel it consumes the assembled
+    matrix (get_csr(), the reference's A_sparse) and builds the Galerkin levels from it."""
 
-    def __init__(self, lattice: Lattice, kappa_sq: float):
+    fine_operator = _native.OPERATOR_FD
+
+    def __init__(self, lattice: Lattice, kappa_sq=None, correlation_model=None):
         self.lattice = lattice
-        self.kappa_sq = float(kappa_sq)
+        if isinstance(kappa_sq, (ConstantCorrelationLengthModel, PeriodicCorrelationLengthModel)):
+            correlation_model, kappa_sq = kappa_sq, None
+        if correlation_model is None:
+            if kappa_sq is None:
+                raise ValueError("need kappa_sq or a correlation-length model")
+            self.correlation_model = None
+            self.kappa_sq = float(kappa_sq)
+        else:
+            self.correlation_model = correlation_model
+            self.kappa_sq = correlation_model.kappa_sq() if correlation_model.kind == _native.KAPPA_CONSTANT else 0.0
+        self._csr = None
 
     def get_lattice(self) -> Lattice:
         return self.lattice
@@ -104,16 +150,81 @@ class ShiftedLaplaceFDOperator:
     def get_m_lowrank(self) -> int:
         return 0
 
-    fine_operator = _native.OPERATOR_FD
+    @property
+    def variable_coefficients(self) -> bool:
+        """True if the device gets the matrix (per-vertex coefficients) instead of a stencil."""
+        return self.correlation_model is not None and self.correlation_model.kind != _native.KAPPA_CONSTANT
+
+    def operator_desc(self) -> "_native.MgmcOperatorDesc":
+        d = _native.MgmcOperatorDesc()
+        lat = self.lattice
+        d.dim = lat.dim
+        d.nx, d.ny = lat.shape[0], lat.shape[1]
+        d.nz = lat.shape[2] if lat.dim == 3 else 0
+        d.pde = self.fine_operator
+        m = self.correlation_model
+        if m is None:
+            d.kappa_model = _native.KAPPA_GIVEN
+            d.kappa_sq = self.kappa_sq
+        elif m.kind == _native.KAPPA_CONSTANT:
+            d.kappa_model = _native.KAPPA_CONSTANT
+            d.Lambda = m.Lambda
+        else:
+            d.kappa_model = _native.KAPPA_PERIODIC
+            d.Lambda_min, d.Lambda_max = m.Lambda_min, m.Lambda_max
+        return d
+
+    def get_csr(self):
+        """A_sparse as (rowptr int64, col int32, val float64), assembled by the library's host code
+        in the reference's arithmetic (mgmc_operator_csr); cached."""
+        if self._csr is None:
+            lib = load_library()
+            d = self.operator_desc()
+            nrow, nnz = ctypes.c_int64(), ctypes.c_int64()
+            check(lib.mgmc_operator_csr_size(ctypes.byref(d), ctypes.byref(nrow), ctypes.byref(nnz)))
+            rowptr = np.empty(nrow.value + 1, dtype=np.int64)
+            col = np.empty(nnz.value, dtype=np.int32)
+            val = np.empty(nnz.value, dtype=np.float64)
+            check(lib.mgmc_operator_csr(ctypes.byref(d), rowptr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                        col.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _dp(val)))
+            self._csr = (rowptr, col, val)
+        return self._csr
+
+    def matrix(self):
+        """A_sparse as a scipy CSR matrix (host)."""
+        import scipy.sparse as sp
+        rowptr, col, val = self.get_csr()
+        n = self.get_ndof()
+        return sp.csr_matrix((val, col, rowptr), shape=(n, n))
 
 
 class ShiftedLaplaceFEMOperator(ShiftedLaplaceFDOperator):
-    """Fine-level precision operator: Q1 finite elements for -div grad + kappa^2 with constant
-    kappa^2 (shiftedlaplace_fem_operator.cc:9-145).  Its interior stencil has 3^d points, so the
-    fine level is swept in 2^d colours like the Galerkin levels; R A_h R^T of it is the FEM
-    operator of the coarse lattice (test_intergrid.hh:179-206)."""
+    """Fine-level precision operator: Q1 finite elements for -div grad + kappa^2
+    (shiftedlaplace_fem_operator.cc:9-145).  With a constant kappa^2 its interior stencil has 3^d
+    points, so the fine level is swept in 2^d colours like the Galerkin levels; R A_h R^T of it is
+    the FEM operator of the coarse lattice (test_intergrid.hh:179-206).  With the periodic model the
+    matrix goes to the device (kappa^2 at the quadrature points of every cell)."""
 
     fine_operator = _native.OPERATOR_FEM
+
+
+class SquaredShiftedLaplaceFDOperator(ShiftedLaplaceFDOperator):
+    """(kappa^2 - Laplace)^2 by finite differences, 2D only (squared_shiftedlaplace_fd_operator.cc:9-96):
+    a 13-point diamond with homogeneous Neumann corrections on the diagonal.  Always a matrix on the
+    device (couplings two vertices apart: the Galerkin levels are 25-point, swept in 3^d colours).
+    With a periodic kappa^2 the reference's matrix is not symmetric (the x / y neighbour entries use
+    the row vertex's kappa^2); the device sweeps with its rows."""
+
+    fine_operator = _native.OPERATOR_SQUARED_FD
+
+    def __init__(self, lattice: Lattice, kappa_sq=None, correlation_model=None):
+        if lattice.dim != 2:
+            raise ValueError("SquaredShiftedLaplaceFDOperator only implemented for d=2")
+        super().__init__(lattice, kappa_sq, correlation_model)
+
+    @property
+    def variable_coefficients(self) -> bool:
+        return True
 
 
 def measurement_vector_index(lattice: Lattice, x0, radius: float = 0.0) -> int:
@@ -189,8 +300,17 @@ class MultigridMCSampler:
         self.config = make_config(linear_operator, params)
         self.lib = load_library()
         h = ctypes.c_void_p()
-        check(self.lib.mgmc_create(ctypes.byref(self.config), int(device), int(seed) & (2**64 - 1),
-                                   int(chain_id) & (2**64 - 1), ctypes.byref(h)))
+        base = getattr(linear_operator, "base_operator", linear_operator)
+        if getattr(base, "variable_coefficients", False):
+            # per-vertex coefficients: the assembled matrix (A_sparse) and a Galerkin hierarchy of matrices
+            rowptr, col, val = base.get_csr()
+            check(self.lib.mgmc_create_csr(ctypes.byref(self.config), len(rowptr) - 1,
+                                           rowptr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                           col.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _dp(val), int(device),
+                                           int(seed) & (2**64 - 1), int(chain_id) & (2**64 - 1), ctypes.byref(h)))
+        else:
+            check(self.lib.mgmc_create(ctypes.byref(self.config), int(device), int(seed) & (2**64 - 1),
+                                       int(chain_id) & (2**64 - 1), ctypes.byref(h)))
         self.handle = h
         self.ndof = linear_operator.get_ndof()
         self.nlevel = params.nlevel
@@ -351,7 +471,7 @@ class MultigridMCSampler:
         d = MgmcLevelDesc()
         self._chk(self.lib.mgmc_level_desc_get(self.handle, int(level), ctypes.byref(d)))
         return {"shape": (d.nx, d.ny, d.nz)[: self.config.dim], "npoints": d.npoints, "ncolours": d.ncolours,
-                "ndof": int(d.ndof), "stencil": np.array(d.stencil[:])}
+                "ndof": int(d.ndof), "stencil": np.array(d.stencil[:]), "varcoef": bool(d.varcoef)}
 
     # -- component operations (reference layout host vectors) --
     def operator_apply(self, level: int, x) -> np.ndarray:
@@ -462,5 +582,6 @@ class HipMulticolourSORSmoother:
 
 __all__ = [
     "Lattice", "Lattice2d", "Lattice3d", "ShiftedLaplaceFDOperator", "MultigridMCSampler",
-    "HipMulticolourSORSmoother", "measurement_vector_index", "comm_unique_id", "make_config", "describe", "FORWARD", "BACKWARD",
+    "HipMulticolourSORSmoother", "measurement_vector_index", "ConstantCorrelationLengthModel",
+    "PeriodicCorrelationLengthModel", "SquaredShiftedLaplaceFDOperator", "comm_unique_id", "make_config", "describe", "FORWARD", "BACKWARD",
 ]

@@ -196,9 +196,37 @@ static CSR transpose(const CSR& A) {
 }
 
 // =============================================================================================
-// Fine operator: ShiftedLaplaceFDOperator with constant kappa^2 (shiftedlaplace_fd_operator.cc)
+// Correlation-length models (correlationlength_model.hh:45-112): kappa^2 at a point
 // =============================================================================================
-static CSR fd_operator(const Lattice& lat, double kappa_sq) {
+struct KappaModel {
+    int periodic = 0;
+    double kappa_sq_const = 0.0;       // constant model: 1 / Lambda^2
+    double Lambda_1 = 0.0, Lambda_2 = 0.0;  // periodic: (Lambda_max +/- Lambda_min) / 2
+    double operator()(const double* x, int dim) const {
+        if (!periodic) return kappa_sq_const;
+        double L = Lambda_2;
+        for (int d = 0; d < dim; ++d) L *= cos(M_PI * x[d]);
+        L += Lambda_1;
+        return 1. / (L * L);
+    }
+    static KappaModel constant(double kappa_sq) {
+        KappaModel k;
+        k.kappa_sq_const = kappa_sq;
+        return k;
+    }
+};
+
+// Lattice::vertex_coordinates (lattice2d.hh:188-195, lattice3d.hh): (0-based index + 1.0) * h
+static void vertex_coords(const Lattice& lat, int64_t ell, double* x) {
+    int idx[3];
+    lat.lin2euc(ell, idx);
+    for (int d = 0; d < lat.dim; ++d) x[d] = ((double)(idx[d] - 1) + 1.0) * (1. / double(lat.n[d]));
+}
+
+// =============================================================================================
+// Fine operator: ShiftedLaplaceFDOperator (shiftedlaplace_fd_operator.cc:9-57)
+// =============================================================================================
+static CSR fd_operator(const Lattice& lat, const KappaModel& kappa) {
     const int dim = lat.dim;
     double hinv2[3] = {0, 0, 0};
     double cell_volume = 1.0;
@@ -216,7 +244,9 @@ static CSR fd_operator(const Lattice& lat, double kappa_sq) {
     std::vector<std::pair<int64_t, double>> row;
     for (int64_t ell = 0; ell < nrow; ++ell) {
         row.clear();
-        double diagonal = cell_volume * kappa_sq;
+        double xv[3] = {0, 0, 0};
+        vertex_coords(lat, ell, xv);
+        double diagonal = cell_volume * kappa(xv, dim);
         for (int d = 0; d < dim; ++d) {
             for (int j = 0; j < 2; ++j) {
                 int s[3] = {0, 0, 0};
@@ -244,7 +274,7 @@ static CSR fd_operator(const Lattice& lat, double kappa_sq) {
 // fastest), basis pairs (alpha, beta) in cartesian_product order (common.hh:29-50: last dimension
 // fastest), each entry += local * cell_volume with local = sum_q (kappa^2 phi_a phi_b + grad phi_a .
 // (h^-2 grad phi_b)) w_q over GaussLegendreQuadrature(dim, 1) (quadrature.cc:11-55).
-static CSR fem_operator(const Lattice& lat, double kappa_sq) {
+static CSR fem_operator(const Lattice& lat, const KappaModel& kappa) {
     const int dim = lat.dim;
     double h[3] = {1, 1, 1}, hinv2[3] = {0, 0, 0};
     double cell_volume = 1.0;
@@ -348,7 +378,10 @@ static CSR fem_operator(const Lattice& lat, double kappa_sq) {
                 if (lat.interior(va) && lat.interior(vb)) {
                     double local = 0.0;
                     for (int q = 0; q < nb; ++q) {
-                        local += (kappa_sq * pp[count] + gg[count]) * qw[q];
+                        // x = h (xhat_q + cell), shiftedlaplace_fem_operator.cc:118-126
+                        double xq[3] = {0, 0, 0};
+                        for (int d = 0; d < dim; ++d) xq[d] = h[d] * (qp[(size_t)q * 3 + d] + (double)cc[d]);
+                        local += (kappa(xq, dim) * pp[count] + gg[count]) * qw[q];
                         count++;
                     }
                     entry(lat.euc2lin(va), lat.euc2lin(vb)) += local * cell_volume;
@@ -356,6 +389,61 @@ static CSR fem_operator(const Lattice& lat, double kappa_sq) {
                     count += nb;
                 }
             }
+    }
+    return A;
+}
+
+// SquaredShiftedLaplaceFDOperator, 2D only (squared_shiftedlaplace_fd_operator.cc:9-96): the 13-point
+// diamond; an offset (+-1, 0) / (0, +-1) whose vertex is on the boundary adds the (+-2, 0) / (0, +-2)
+// entry to the diagonal (homogeneous Neumann)
+static CSR squared_fd_operator(const Lattice& lat, const KappaModel& kappa) {
+    double h0 = 1. / double(lat.n[0]), h1 = 1. / double(lat.n[1]);
+    const double hinv2[2] = {1. / (h0 * h0), 1. / (h1 * h1)};
+    const double cell_volume = h0 * h1;
+    double lap[2][2] = {{0, 0}, {0, 0}}, sq[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+    lap[0][0] = -2 * (hinv2[0] + hinv2[1]);
+    lap[1][0] = hinv2[0];
+    lap[0][1] = hinv2[1];
+    sq[0][0] = 6 * (hinv2[0] * hinv2[0] + hinv2[1] * hinv2[1]) + 8 * hinv2[0] * hinv2[1];
+    sq[1][0] = -4 * hinv2[0] * (hinv2[0] + hinv2[1]);
+    sq[0][1] = -4 * hinv2[1] * (hinv2[0] + hinv2[1]);
+    sq[2][0] = hinv2[0] * hinv2[0];
+    sq[0][2] = hinv2[1] * hinv2[1];
+    sq[1][1] = 2 * hinv2[0] * hinv2[1];
+    CSR A;
+    const int64_t nrow = lat.nvertex();
+    A.nrow = A.ncol = nrow;
+    A.rowptr.assign(nrow + 1, 0);
+    std::vector<std::pair<int64_t, double>> row;
+    for (int64_t ell = 0; ell < nrow; ++ell) {
+        row.clear();
+        double xv[3] = {0, 0, 0};
+        vertex_coords(lat, ell, xv);
+        const double ab = kappa(xv, 2);
+        double diagonal = (ab * ab - 2. * ab * lap[0][0] + sq[0][0]) * cell_volume;
+        for (int j = -2; j <= 2; ++j)
+            for (int k = -2; k <= 2; ++k) {
+                const int aj = j < 0 ? -j : j, ak = k < 0 ? -k : k;
+                if (aj + ak > 2 || (j == 0 && k == 0)) continue;
+                const int sh[3] = {j, k, 0};
+                int64_t e;
+                if (lat.shifted(ell, sh, e)) {
+                    double v = sq[aj][ak];
+                    if (aj + ak == 1) v += -2. * ab * lap[aj][ak];
+                    row.push_back({e, v * cell_volume});
+                } else if (aj + ak == 1) {
+                    diagonal += sq[2 * aj][2 * ak] * cell_volume;
+                }
+            }
+        row.push_back({ell, diagonal});
+        std::sort(row.begin(), row.end(), [](const std::pair<int64_t, double>& a, const std::pair<int64_t, double>& b) {
+            return a.first < b.first;
+        });
+        for (auto& e : row) {
+            A.col.push_back((int32_t)e.first);
+            A.val.push_back(e.second);
+        }
+        A.rowptr[ell + 1] = (int64_t)A.col.size();
     }
     return A;
 }
@@ -634,18 +722,38 @@ static int64_t max_row_nnz(const CSR& A) {
     return m;
 }
 
+// largest coordinate distance between coupled vertices (1 for 3^d-point operators, 2 for the
+// squared FD operator and its Galerkin levels)
+static int coupling_reach(const Level& L) {
+    int reach = 0, a[3], b[3];
+    for (int64_t r = 0; r < L.A.nrow; ++r) {
+        L.lat.lin2euc(r, a);
+        for (int64_t q = L.A.rowptr[r]; q < L.A.rowptr[r + 1]; ++q) {
+            L.lat.lin2euc(L.A.col[q], b);
+            for (int d = 0; d < L.lat.dim; ++d) reach = std::max(reach, std::abs(a[d] - b[d]));
+        }
+    }
+    return reach;
+}
+
+// colour classes of the multicolour sweeps: red-black for a 5/7-point fine level, coordinate parities
+// (2^d colours) for reach-1 levels, coordinates mod 3 (3^d colours) for reach-2 levels
 static void init_colouring(Level& L, bool fd_level) {
     const int64_t n = L.lat.nvertex();
     L.colour.resize(n);
     L.pair.resize(n);
     L.cos_branch.resize(n);
     const int dim = L.lat.dim;
-    L.ncolours = fd_level ? 2 : (1 << dim);
+    const bool mod3 = coupling_reach(L) >= 2;
+    if (mod3) fd_level = false;
+    L.ncolours = fd_level ? 2 : (mod3 ? (dim == 3 ? 27 : 9) : (1 << dim));
     int idx[3];
     for (int64_t e = 0; e < n; ++e) {
         L.lat.lin2euc(e, idx);
         if (fd_level)
             L.colour[e] = (idx[0] + idx[1] + idx[2]) & 1;
+        else if (mod3)
+            L.colour[e] = (idx[0] % 3) + 3 * (idx[1] % 3) + (dim == 3 ? 9 * (idx[2] % 3) : 0);
         else
             L.colour[e] = (idx[0] & 1) | ((idx[1] & 1) << 1) | ((idx[2] & 1) << 2);
         uint64_t row = 0;
@@ -1206,7 +1314,7 @@ orc_handle* orc_create_fd(const orc_params* q, int mode, uint64_t seed, uint64_t
     h->ctx.seed = seed;
     h->ctx.chain = chain;
     const Lattice lat = make_lattice(q);
-    CSR A = fd_operator(lat, q->kappa_sq);
+    CSR A = fd_operator(lat, KappaModel::constant(q->kappa_sq));
     h->mg.reset(new MGMC(&h->ctx, to_params(q), lat, std::move(A), override_st));
     h->f.assign(h->mg->x_ell[0].size(), 0.0);
     h->x.assign(h->mg->x_ell[0].size(), 0.0);
@@ -1221,7 +1329,7 @@ orc_handle* orc_create_fem(const orc_params* q, int mode, uint64_t seed, uint64_
     h->ctx.seed = seed;
     h->ctx.chain = chain;
     const Lattice lat = make_lattice(q);
-    CSR A = fem_operator(lat, q->kappa_sq);
+    CSR A = fem_operator(lat, KappaModel::constant(q->kappa_sq));
     Params p = to_params(q);
     p.galerkin = 0;
     h->mg.reset(new MGMC(&h->ctx, p, lat, std::move(A), override_st));
@@ -1252,6 +1360,39 @@ orc_handle* orc_create_csr(const orc_params* q, int mode, uint64_t seed, int64_t
 }
 
 void orc_destroy(orc_handle* h) { delete h; }
+
+// the reference's fine operators (any correlation-length model) as CSR: pde 0 FD, 1 FEM, 2 squared
+// FD (2D); kmodel 0 constant (kappa^2 = 1 / pow(Lambda, 2)), 1 periodic (Lambda_min, Lambda_max)
+static CSR model_operator(int dim, const int* n, int pde, int kmodel, double Lambda, double Lmin, double Lmax) {
+    Lattice lat;
+    lat.dim = dim;
+    lat.n[0] = n[0];
+    lat.n[1] = dim >= 2 ? n[1] : 1;
+    lat.n[2] = dim == 3 ? n[2] : 1;
+    KappaModel k;
+    if (kmodel == 1) {
+        k.periodic = 1;
+        k.Lambda_1 = 0.5 * (Lmax + Lmin);
+        k.Lambda_2 = 0.5 * (Lmax - Lmin);
+    } else {
+        k.kappa_sq_const = 1. / pow(Lambda, 2);
+    }
+    if (pde == 1) return fem_operator(lat, k);
+    if (pde == 2) return squared_fd_operator(lat, k);
+    return fd_operator(lat, k);
+}
+
+int64_t orc_operator_nnz(int dim, const int* n, int pde, int kmodel, double Lambda, double Lmin, double Lmax) {
+    return (int64_t)model_operator(dim, n, pde, kmodel, Lambda, Lmin, Lmax).col.size();
+}
+
+void orc_operator_csr(int dim, const int* n, int pde, int kmodel, double Lambda, double Lmin, double Lmax,
+                      int64_t* rowptr, int32_t* col, double* val) {
+    const CSR A = model_operator(dim, n, pde, kmodel, Lambda, Lmin, Lmax);
+    std::copy(A.rowptr.begin(), A.rowptr.end(), rowptr);
+    std::copy(A.col.begin(), A.col.end(), col);
+    std::copy(A.val.begin(), A.val.end(), val);
+}
 
 int64_t orc_ndof(orc_handle* h, int level) { return h->mg->levels[level]->A.nrow; }
 int orc_nlevel(orc_handle* h) { return (int)h->mg->levels.size(); }

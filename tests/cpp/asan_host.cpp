@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../multigridmc_amd/csrc/mgmc_hierarchy.hpp"
+#include "../../multigridmc_amd/csrc/mgmc_operators.hpp"
 
 extern "C" {
 typedef struct orc_params {
@@ -90,6 +91,37 @@ static void hierarchy_checks() {
     EXPECT(std::isfinite(coarse[13]));
 }
 
+// the matrix path's host code: assembly of every operator / model, Galerkin products down to the
+// coarsest level, the lattice checks
+static void operator_checks() {
+    const int shapes[][4] = {{2, 8, 8, 0}, {2, 16, 12, 0}, {3, 8, 8, 8}, {3, 8, 4, 6}};
+    for (const auto& sh : shapes)
+        for (int pde = 0; pde <= 2; ++pde)
+            for (int km = 0; km <= 2; ++km) {
+                mgmc_operator_desc d;
+                std::memset(&d, 0, sizeof(d));
+                d.dim = sh[0];
+                d.nx = sh[1];
+                d.ny = sh[2];
+                d.nz = sh[3];
+                d.pde = pde;
+                d.kappa_model = km;
+                d.Lambda = 0.2;
+                d.Lambda_min = 1.2;
+                d.Lambda_max = 2.3;
+                d.kappa_sq = 25.0;
+                if (!mgmc::validate_operator(d).empty()) continue;
+                mgmc::CsrHost A = mgmc::assemble_operator(d);
+                int n[3] = {sh[1], sh[2], sh[0] == 3 ? sh[3] : 1};
+                EXPECT(mgmc::check_lattice_csr(sh[0], n, A).empty());
+                for (int l = 0; l < 2 && n[0] >= 4 && n[1] >= 4; ++l) {
+                    A = mgmc::galerkin_csr(A, sh[0], n);
+                    for (int q = 0; q < sh[0]; ++q) n[q] /= 2;
+                    EXPECT(mgmc::check_lattice_csr(sh[0], n, A).empty());
+                }
+            }
+}
+
 static orc_params params(int dim, int n, int nlevel, int cycle, int smoother, int coarse) {
     orc_params p;
     p.dim = dim;
@@ -154,6 +186,7 @@ static void exercise(orc_handle* h, bool lowrank) {
 
 int main() {
     hierarchy_checks();
+    operator_checks();
     for (int mode = 0; mode <= 1; ++mode) {
         for (int coarse = 0; coarse <= 1; ++coarse) {
             const orc_params p2 = params(2, 32, 3, 2, 0, coarse), p3 = params(3, 16, 3, 1, 1, coarse);

@@ -52,6 +52,9 @@ def lib():
             "orc_get_state": (None, [c_void_p, _DP]),
             "orc_set_sample_index": (None, [c_void_p, c_uint64]),
             "orc_reseed": (None, [c_void_p, c_uint64, c_uint64]),
+            "orc_operator_nnz": (c_int64, [c_int, POINTER(c_int), c_int, c_int, c_double, c_double, c_double]),
+            "orc_operator_csr": (None, [c_int, POINTER(c_int), c_int, c_int, c_double, c_double, c_double,
+                                        POINTER(c_int64), POINTER(c_int32), _DP]),
             "orc_apply": (None, [c_void_p, _DP, _DP]),
             "orc_sample": (None, [c_void_p, c_int, c_int64, _DP]),
             "orc_time_samples": (c_double, [c_void_p, c_int]),
@@ -267,6 +270,21 @@ class Oracle:
         out = np.empty(self.ndof(level + 1))
         self.L.orc_residual_restrict(self.h, level, dp(f), dp(x), dp(out))
         return out
+
+
+def operator_csr(shape, pde, periodic=False, Lambda=0.2, Lambda_min=0.2, Lambda_max=0.4):
+    """The oracle's own assembly of the reference's fine operators (pde 0 FD, 1 FEM, 2 squared FD)
+    with the constant (Lambda) or periodic (Lambda_min, Lambda_max) correlation-length model."""
+    n = (c_int * 3)(*(list(shape) + [0] * (3 - len(shape))))
+    args = (len(shape), n, int(pde), 1 if periodic else 0, float(Lambda), float(Lambda_min), float(Lambda_max))
+    nnz = lib().orc_operator_nnz(*args)
+    nrow = int(np.prod([v - 1 for v in shape]))
+    rowptr = np.empty(nrow + 1, dtype=np.int64)
+    col = np.empty(nnz, dtype=np.int32)
+    val = np.empty(nnz, dtype=np.float64)
+    lib().orc_operator_csr(*args, rowptr.ctypes.data_as(POINTER(c_int64)), col.ctypes.data_as(POINTER(c_int32)),
+                           dp(val))
+    return rowptr, col, val
 
 
 def philox_normals(seed, chain, pair0, n, tag, sample):

@@ -1,0 +1,183 @@
+"""GPU parity of the matrix path (-m gpu): operators with per-vertex coefficients (the periodic
+correlation-length model, correlationlength_model.hh:68-112) and the squared FD operator
+(squared_shiftedlaplace_fd_operator.cc:9-96), built with mgmc_create_csr: the Galerkin hierarchy of
+matrices (linear_operator.cc:10-23) formed on the host, every level swept with its coefficient field.
+
+T2 (bitwise, np.array_equal) against the oracle's MULTICOLOUR replay on the same fine matrix (the
+oracle forms its own Galerkin products): operator, smoothers, samplers, residual + restriction on every
+level, whole cycles (also with a low-rank posterior part and the dense Cholesky coarse sampler).
+T3: the reference's own 2D MGMC sampler test in its configuration (test_sampler.hh:260-323: FEM prior,
+periodic Lambda in [1.2, 2.3], 4 ball measurements, SSOR smoother, Cholesky coarse sampler, 8^2
+lattice, 10,000 samples after 1,000 warm-up) with the reference's tolerance 2e-2 on the mean and the
+covariance (L-infinity, mean_covariance_error, test_sampler.hh:113-153).
+"""
+import numpy as np
+import pytest
+
+import multigridmc_amd as mg
+from multigridmc_amd.parameters import MeasurementParameters
+from tests import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+SEED = 5418513
+PERIODIC = mg.PeriodicCorrelationLengthModel(0.2, 0.4)  # parameters_template.cfg periodiccorrelationlengthmodel
+
+CONFIGS = {
+    "2d_fd_periodic_W": ((64, 64), "fd", PERIODIC, dict(nlevel=4, cycle=2)),
+    "2d_fem_periodic_chol": ((32, 32), "fem", PERIODIC, dict(nlevel=3, smoother="SSOR", coarse_solver="Cholesky")),
+    "3d_fd_periodic": ((32, 32, 32), "fd", PERIODIC, dict(nlevel=3, ncoarsesmooth=2)),
+    "3d_fem_periodic_ssor": ((16, 16, 16), "fem", PERIODIC, dict(nlevel=3, smoother="SSOR", omega=1.1)),
+    "3d_fd_periodic_aniso": ((32, 16, 24), "fd", PERIODIC, dict(nlevel=2, coarse_scaling=0.9)),
+    "2d_squared": ((32, 32), "squared", 25.0, dict(nlevel=3)),
+    "2d_squared_periodic_chol": ((32, 32), "squared", PERIODIC, dict(nlevel=3, coarse_solver="Cholesky")),
+    "2d_squared_ssor_W": ((64, 32), "squared", 25.0, dict(nlevel=3, smoother="SSOR", cycle=2, ncoarsesmooth=2)),
+}
+OPS = {"fd": mg.ShiftedLaplaceFDOperator, "fem": mg.ShiftedLaplaceFEMOperator,
+       "squared": mg.SquaredShiftedLaplaceFDOperator}
+
+
+def make(name, lowrank=False, chain=0):
+    shape, pde, model, kw = CONFIGS[name]
+    p = mg.MultigridParameters(**{"nlevel": 3, "smoother": "SOR", "coarse_solver": "SSOR", **kw})
+    lat = mg.Lattice(*shape)
+    op = OPS[pde](lat, model)
+    if lowrank:
+        rng = np.random.default_rng(3)
+        mp = MeasurementParameters(radius=0.0, variance_scaling=1e-3, measure_global=True, variance_global=0.02)
+        mp.measurement_locations = [list(rng.uniform(0.15, 0.85, lat.dim)) for _ in range(3)]
+        mp.variance = list(1.0 + 2.0 * rng.random(3))
+        op = mg.MeasuredOperator(op, mp)
+    s = mg.MultigridMCSampler(op, SEED, p, device=0, chain_id=chain)
+    base = getattr(op, "base_operator", op)
+    rowptr, col, val = base.get_csr()
+    mc = O.Oracle.csr(shape, p, rowptr, col, val, mode=O.MULTICOLOUR, seed=SEED)
+    if lowrank:
+        mc.set_lowrank(op.get_B())
+    return s, mc, p, lat
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_varcoef_components_bitwise(hip_device, name):
+    s, mc, p, lat = make(name)
+    rng = np.random.default_rng(5)
+    assert s.level_desc(0)["varcoef"]
+    for level in range(p.nlevel):
+        n = s.level_desc(level)["ndof"]
+        assert n == mc.ndof(level)
+        x = rng.standard_normal(n)
+        b = rng.standard_normal(n)
+        assert np.array_equal(s.operator_apply(level, x), mc.operator_apply(level, x)), f"level {level} apply"
+        for direction in (mg.FORWARD, mg.BACKWARD):
+            assert np.array_equal(s.smoother_apply(level, direction, 2, b, x),
+                                  mc.smoother_apply(level, direction, 2, b, x)), f"level {level} smoother"
+            assert np.array_equal(s.sor_sampler_apply(level, direction, 3 + level, 19, b, x),
+                                  mc.sor_sampler_apply(level, direction, 3 + level, 19, b, x)), f"level {level} sampler"
+        if level + 1 < p.nlevel:
+            assert np.array_equal(s.residual_restrict(level, b, x), mc.residual_restrict(level, b, x)), \
+                f"level {level} residual"
+    s.close()
+
+
+@pytest.mark.parametrize("name,lowrank", [(n, False) for n in CONFIGS] +
+                         [("2d_fem_periodic_chol", True), ("3d_fd_periodic", True), ("2d_squared", True)])
+def test_varcoef_cycles_bitwise(hip_device, name, lowrank):
+    s, mc, p, lat = make(name, lowrank)
+    f = np.random.default_rng(7).standard_normal(lat.Nvertex)
+    x_dev, x_orc = np.zeros(lat.Nvertex), np.zeros(lat.Nvertex)
+    for _ in range(2):
+        s.apply(f, x_dev)
+        mc.apply(f, x_orc)
+    assert np.array_equal(x_dev, x_orc)
+    q = mg.measurement_vector_index(lat, [0.5] * lat.dim)
+    s.fix_rhs(f)
+    s.set_state(x_dev)
+    mc.set_rhs(f)
+    mc.set_state(x_orc)
+    assert np.array_equal(s.sample(5, q), mc.sample(5, q))
+    assert np.array_equal(s.get_state(), mc.get_state())
+    s.close()
+
+
+class MT19937_64:
+    """std::mt19937_64 (for the reference test's own inputs: its Sigma and mean vectors come from
+    std::uniform_real_distribution<double>(0, 1) = generate_canonical<double, 53> on this engine,
+    one 64-bit draw scaled by 2^-64)."""
+
+    def __init__(self, seed):
+        self.mt = [0] * 312
+        self.mt[0] = seed & 0xFFFFFFFFFFFFFFFF
+        for i in range(1, 312):
+            self.mt[i] = (6364136223846793005 * (self.mt[i - 1] ^ (self.mt[i - 1] >> 62)) + i) & 0xFFFFFFFFFFFFFFFF
+        self.i = 312
+
+    def __call__(self):
+        if self.i >= 312:
+            for k in range(312):
+                y = (self.mt[k] & 0xFFFFFFFF80000000) | (self.mt[(k + 1) % 312] & 0x7FFFFFFF)
+                v = self.mt[(k + 156) % 312] ^ (y >> 1)
+                if y & 1:
+                    v ^= 0xB5026F5AA96619E9
+                self.mt[k] = v
+            self.i = 0
+        y = self.mt[self.i]
+        self.i += 1
+        y ^= (y >> 29) & 0x5555555555555555
+        y ^= (y << 17) & 0x71D67FFFEDA60000
+        y ^= (y << 37) & 0xFFF7EEE000000000
+        y ^= y >> 43
+        return y & 0xFFFFFFFFFFFFFFFF
+
+    def uniform(self):
+        r = float(self()) / 18446744073709551616.0
+        return r if r < 1.0 else np.nextafter(1.0, 0.0)
+
+
+def test_mt19937_64_known_answer():
+    """The 10000th output of a default-seeded std::mt19937_64 is 9981545732273789042 (C++11 [rand.predef])."""
+    g = MT19937_64(5489)
+    for _ in range(9999):
+        g()
+    assert g() == 9981545732273789042
+
+
+def test_reference_2d_mgmc_sampler_case(hip_device):
+    """test_sampler.hh:260-323 (TestMultigridMCSampler2d) in its own configuration: nx = ny = 8, FEM
+    prior with the periodic model (Lambda_min 1.2, Lambda_max 2.3), MeasuredOperator with 4 ball
+    measurements (radius 0.05, variance 1e-4 (1 + 2 U), U from mt19937_64(1212417)), nlevel 3, SSOR
+    smoother, Cholesky coarse sampler, omega 1, V-cycle; mean_covariance_error with f = Q mean_exact,
+    mean_exact ~ U(0, 1) from mt19937_64(1342517), 1,000 warm-up + 10,000 samples, tolerance 2e-2 on
+    |E x - mean|_inf and |Cov - Q^-1|_inf."""
+    lat = mg.Lattice(8, 8)
+    prior = mg.ShiftedLaplaceFEMOperator(lat, mg.PeriodicCorrelationLengthModel(1.2, 2.3))
+    g = MT19937_64(1212417)
+    mp = MeasurementParameters(radius=0.05, variance_scaling=1e-4, measure_global=False, variance_global=0.0,
+                               mean_global=0.0)
+    mp.measurement_locations = [[0.25, 0.25], [0.25, 0.75], [0.75, 0.25], [0.75, 0.75]]
+    mp.variance = [1.0 + 2.0 * g.uniform() for _ in range(4)]
+    op = mg.MeasuredOperator(prior, mp)
+    p = mg.MultigridParameters(nlevel=3, smoother="SSOR", coarse_solver="Cholesky", npresmooth=1, npostsmooth=1,
+                               ncoarsesmooth=1, omega=1.0, cycle=1, coarse_scaling=1.0)
+    s = mg.MultigridMCSampler(op, 31841287, p)
+    n = lat.Nvertex
+    Q = prior.matrix().toarray() + op.get_B().precision_update()
+    h = MT19937_64(1342517)
+    mean_exact = np.array([h.uniform() for _ in range(n)])
+    f = Q @ mean_exact
+    cov_exact = np.linalg.inv(Q)
+    s.fix_rhs(f)
+    s.set_state(np.zeros(n))
+    s.sample(1000)
+    Ex = np.zeros(n)
+    Exx = np.zeros((n, n))
+    for k in range(10000):
+        s.sample(1)
+        x = s.get_state()
+        Ex += 1.0 / (k + 1) * (x - Ex)
+        Exx += 1.0 / (k + 1) * (np.outer(x, x) - Exx)
+    cov = Exx - np.outer(Ex, Ex)
+    err_mean = np.max(np.abs(Ex - mean_exact))
+    err_cov = np.max(np.abs(cov - cov_exact))
+    assert err_mean < 2e-2, err_mean
+    assert err_cov < 2e-2, err_cov
+    s.close()
