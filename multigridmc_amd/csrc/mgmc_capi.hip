@@ -137,7 +137,17 @@ bool read_path_flags(uint32_t* flags, std::string* bad) {
 // z-marching sweep tile shape (mgmc_zsweep.hpp)
 // 32 x-pairs x 16 rows, 256 threads (2 core pairs per thread, 19.5 % halo), 38 KB of LDS -> 4
 // workgroups per CU; tuning history in DESIGN.md
-constexpr int ZS_XP = 32, ZS_TY = 16, ZS_NT = 256, ZS_MINW = 1, ZS_TZ = 32, ZS_TZP = 64;
+// (MGMC_ZS_SHAPE_* override the shape in timing-experiment builds only, scripts/build_exp.sh)
+#ifndef MGMC_ZS_SHAPE_XP
+#define MGMC_ZS_SHAPE_XP 32
+#define MGMC_ZS_SHAPE_TY 16
+#define MGMC_ZS_SHAPE_NT 256
+#endif
+#ifndef MGMC_ZS_SHAPE_TZ
+#define MGMC_ZS_SHAPE_TZ 32
+#endif
+constexpr int ZS_XP = MGMC_ZS_SHAPE_XP, ZS_TY = MGMC_ZS_SHAPE_TY, ZS_NT = MGMC_ZS_SHAPE_NT, ZS_MINW = 1,
+              ZS_TZ = MGMC_ZS_SHAPE_TZ, ZS_TZP = 64;
 #ifndef MGMC_ZS_MINW_PROLONG
 #define MGMC_ZS_MINW_PROLONG 3  // waves/SIMD floor of the fused-prolongation variant (3: 167 VGPRs, no spill; 4 spills)
 #endif
@@ -1569,7 +1579,9 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
         lv.num_cu = ncu;
         lv.spec = specs[l];
         lv.paths = h->paths;
-        lv.L = make_layout(cfg->dim, specs[l].n);
+        // reach-2 field levels (3^d colourings) read two vertices beyond every interior vertex
+        lv.L = make_layout(cfg->dim, specs[l].n,
+                           h->field_mode && (fields[l].scheme == 9 || fields[l].scheme == 27));
         memcpy(lv.S.a, specs[l].st, sizeof(lv.S.a));
         const size_t bytes = lv.L.nstore * sizeof(double);
         if (hipMalloc(&lv.x, bytes) != hipSuccess || hipMalloc(&lv.f, bytes) != hipSuccess) {

@@ -39,20 +39,23 @@ struct Layout {
     }
 };
 
-// align128: the first interior vertex of every row on a 128-byte line (row stride a multiple of 16
-// doubles, off = 15); otherwise 64-byte rows with off = 7.  off stays odd either way, so interior
-// x-pairs (i odd, i+1) sit on 16-byte boundaries.
-inline Layout make_layout(int dim, const int n[3], bool align128 = false) {
+// The first interior vertex of every row sits on a 128-byte line (row stride a multiple of 16
+// doubles, off = 15, odd, so interior x-pairs (i odd, i+1) sit on 16-byte boundaries).
+// reach2: operators coupling vertices two apart (the squared FD operator's field levels) read one
+// row and one plane beyond the zero boundary on either side; the storage then starts one plane + one
+// row earlier and ends one plane + one row later (zeros), so those reads stay inside the allocation.
+inline Layout make_layout(int dim, const int n[3], bool reach2 = false) {
     Layout L;
     L.dim = dim;
     L.nx = n[0];
     L.ny = n[1];
     L.nz = dim == 3 ? n[2] : 0;
-    L.off = align128 ? 15 : 7;
     L.pad_ = 0;
-    L.sx = align128 ? ((long long)L.nx + 16 + 15) / 16 * 16 : ((long long)L.nx + 8 + 7) / 8 * 8;
+    L.sx = ((long long)L.nx + 16 + 15) / 16 * 16;  // >= nx + 16: columns -2 .. nx + 2 stay in the row
     L.sp = L.sx * (L.ny + 1);
-    L.nstore = (dim == 3 ? L.sp * (L.nz + 1) : L.sp) + 64;
+    const long long margin = reach2 ? (dim == 3 ? L.sp : 0) + L.sx : 0;  // multiple of 16
+    L.off = 15 + (int)margin;
+    L.nstore = (dim == 3 ? L.sp * (L.nz + 1) : L.sp) + 64 + 2 * margin;
     return L;
 }
 

@@ -19,7 +19,7 @@ names = {"0": "product", "1": "no-BoxMuller", "2": "no-halo", "3": "no-Philox", 
 for x in exps:
     env = dict(os.environ)
     if x != "0":
-        env["MGMC_LIBRARY"] = os.path.join(ROOT, "build", f"libmgmc_exp{x}.so")
+        env["MGMC_LIBRARY"] = os.path.join(ROOT, "build", f"libmgmc_exp{x}.so")  # x = N or s<shape>
     r = subprocess.run([sys.executable, "-c", CHILD % ROOT], env=env, capture_output=True, text=True, timeout=300)
     out = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else f"FAILED {r.stderr[-300:]}"
     print(f"{names.get(x, x):14s} {out}", flush=True)
