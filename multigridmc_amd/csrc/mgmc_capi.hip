@@ -134,23 +134,26 @@ bool read_path_flags(uint32_t* flags, std::string* bad) {
     return true;
 }
 
-// z-marching sweep tile shape (mgmc_zsweep.hpp)
-// 32 x-pairs x 16 rows, 256 threads (2 core pairs per thread, 19.5 % halo), 38 KB of LDS -> 4
-// workgroups per CU; tuning history in DESIGN.md
+// z-marching sweep tile shape (mgmc_zsweep.hpp): 32 x-pairs x TY rows, TY/2 core waves + 2 halo
+// waves rounded up to a multiple of four (768 threads for TY 16); two workgroups per CU need <= 80
+// VGPRs (6 waves per SIMD).  Tuning history in DESIGN.md.
 // (MGMC_ZS_SHAPE_* override the shape in timing-experiment builds only, scripts/build_exp.sh)
-#ifndef MGMC_ZS_SHAPE_XP
-#define MGMC_ZS_SHAPE_XP 32
-#define MGMC_ZS_SHAPE_TY 16
-#define MGMC_ZS_SHAPE_NT 256
+#ifndef MGMC_ZS_SHAPE_TY
+#define MGMC_ZS_SHAPE_TY 20
+#endif
+#ifndef MGMC_ZS_SHAPE_MINW
+#define MGMC_ZS_SHAPE_MINW 6
 #endif
 #ifndef MGMC_ZS_SHAPE_TZ
 #define MGMC_ZS_SHAPE_TZ 32
 #endif
-constexpr int ZS_XP = MGMC_ZS_SHAPE_XP, ZS_TY = MGMC_ZS_SHAPE_TY, ZS_NT = MGMC_ZS_SHAPE_NT, ZS_MINW = 1,
-              ZS_TZ = MGMC_ZS_SHAPE_TZ, ZS_TZP = 64;
-#ifndef MGMC_ZS_MINW_PROLONG
-#define MGMC_ZS_MINW_PROLONG 3  // waves/SIMD floor of the fused-prolongation variant (3: 167 VGPRs, no spill; 4 spills)
+#ifndef MGMC_ZS_SHAPE_TYP  // the fused-prolongation (post-)sweep
+#define MGMC_ZS_SHAPE_TYP 16
+#define MGMC_ZS_SHAPE_MINWP 6
 #endif
+constexpr int ZS_XP = 32, ZS_TY = MGMC_ZS_SHAPE_TY, ZS_NT = zs_threads(ZS_TY), ZS_MINW = MGMC_ZS_SHAPE_MINW,
+              ZS_TZ = MGMC_ZS_SHAPE_TZ, ZS_TYP = MGMC_ZS_SHAPE_TYP, ZS_NTP = zs_threads(ZS_TYP),
+              ZS_MINWP = MGMC_ZS_SHAPE_MINWP, ZS_TZP = 64;
 
 // device copy of a level's low-rank part (mgmc_lowrank.hpp); one allocation list, freed together
 struct LowRankDev {
@@ -366,14 +369,13 @@ void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s)
     const int ntiles = a.ntx * a.nty * a.ntz;
     const int nb = (ntiles + 7) / 8 * 8;
     const size_t lds = zsweep_lds_bytes(XP, TY, prolong);
-    constexpr int MINWP = MINW > MGMC_ZS_MINW_PROLONG ? MINW : MGMC_ZS_MINW_PROLONG;
     // alpha a power of two (coarse_scaling 1): fma prolongation terms, same bits (mgmc_zsweep.hpp)
     int ex;
     const bool pow2 = std::isnormal(a.alpha) && std::frexp(std::fabs(a.alpha), &ex) == 0.5 && ex > -900 && ex < 900;
     if (prolong && pow2)
-        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 2, MINWP>), dim3(nb), dim3(NT), lds, s, a);
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 2, MINW>), dim3(nb), dim3(NT), lds, s, a);
     else if (prolong)
-        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 1, MINWP>), dim3(nb), dim3(NT), lds, s, a);
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 1, MINW>), dim3(nb), dim3(NT), lds, s, a);
     else
         hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 0, MINW>), dim3(nb), dim3(NT), lds, s, a);
 }
@@ -392,6 +394,7 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
     a.G = g0;
     a.G.colour = (direction == MGMC_FORWARD) ? 0 : 1;
     const long long txy = (long long)((lv.L.nx / 2) / ZS_XP) * ((lv.L.ny - 1 + ZS_TY - 1) / ZS_TY);
+    const long long txyp = (long long)((lv.L.nx / 2) / ZS_XP) * ((lv.L.ny - 1 + ZS_TYP - 1) / ZS_TYP);
     if (coarse) {
         // fused-prolongation sweep: 512-thread workgroups (one core pair per thread: 127 VGPRs,
         // 2 workgroups = 16 waves per CU against 3 x 4 waves with 256 threads, which the 6.7 KB
@@ -400,8 +403,8 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
         // 256^3: tz 16, 142 -> 118 us; interleaved A/B).  tz stays even: chunks start on odd planes
         // (coarse ring schedule)
         a.tz = ZS_TZP;
-        while (a.tz > 8 && txy * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 2LL * 2 * lv.num_cu) a.tz /= 2;
-        launch_zsweep_t<ZS_XP, ZS_TY, 2 * ZS_NT, 4>(lv, a, true, s);
+        while (a.tz > 8 && txyp * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 2LL * 2 * lv.num_cu) a.tz /= 2;
+        launch_zsweep_t<ZS_XP, ZS_TYP, ZS_NTP, ZS_MINWP>(lv, a, true, s);
         return;
     }
     // shallower z chunks until the grid has >= 1024 tiles (4 per CU): 256^3 -> 16 planes

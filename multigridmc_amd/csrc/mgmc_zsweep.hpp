@@ -12,17 +12,28 @@
 //    the second colour on plane p-1 (tile only), which then is final and is stored.  A red update
 //    on plane p only reads black values of planes p-1..p+1 (still old), a black update on p-1 only
 //    reads red values of planes p-2..p (already new): this is exactly the two-pass result.
-//  * Planes live in a 3-slot LDS ring (p-1, p, p+1) in a colour-split row layout; global traffic is
+//  * Planes live in a 4-slot LDS ring (p-2 .. p+1) in a colour-split row layout; global traffic is
 //    16-byte pair loads and stores, one pass over x_in, f and x_out (+ halo re-reads that hit L2 /
 //    Infinity Cache).  Second-colour results never return to LDS (no update reads them), they go
-//    straight to the store; the z-below values of the second colour come from registers.
+//    straight to the store; the z-below values of the second colour come from registers.  With four
+//    slots the deposit of plane p+2 never touches a plane the second colour still reads, so a step
+//    needs two barriers.
 //  * The two vertices of an x-pair share one Philox block: the first-colour update consumes one
-//    Box-Muller branch and parks the other in LDS for the second-colour update one step later.
+//    Box-Muller branch and keeps the other's right-hand side in a register for the second-colour
+//    update one step later.  The noise of plane p+1 is drawn in the second-colour phase of step p
+//    (it depends on no data), which evens the arithmetic out over the phases between barriers.
+//  * One pair item per thread: TY/2 core waves (rows of one parity per wave, so which element of a
+//    pair takes the first colour is a wave-uniform branch, not a per-lane select), two waves for the
+//    first-colour halo ring (row j0-1 with the columns of the odd core rows, row j0+TY with those of
+//    the even ones), idle waves up to a multiple of four (the dispatcher places a workgroup's waves
+//    round-robin over the four SIMDs: other sizes strand wave slots).
 //  * Optional fused prolongate-add on the input: x_old = x_in + alpha P x_c, evaluated exactly as
 //    k_prolongate_add (so the post-sampler needs no separate prolongation pass).
 // Per-vertex arithmetic is that of mgmc_kernels.hpp (fused Gibbs update); results are bitwise
 // equal to the two colour passes.
 #pragma once
+#include <type_traits>
+
 #include "mgmc_kernels.hpp"
 
 namespace mgmc {
@@ -44,7 +55,7 @@ struct ZSweepArgs {
 // One pair item of a tile: LDS offset, plane-independent global offset, Philox pair base,
 // position parity and interior flags, all computed once per workgroup.
 struct ZItem {
-    long long goff;  // j*sx + i + off  (add k*sp for plane k)
+    int goff;        // j*sx + i + off  (add k*sp for plane k; a plane is < 2^31 doubles)
     uint32_t pbase;  // (j-1)*(nx/2) + (i-1)/2
     int lds;         // r*RS + c2 (odd element; even element at +WP)
     int flags;       // bit0 row interior, bit1 i interior, bit2 i+1 interior, bit3 parity (i+j)&1
@@ -59,9 +70,6 @@ struct ZItem {
 #ifndef MGMC_ZS_NT_STORE
 #define MGMC_ZS_NT_STORE 1
 #endif
-#ifndef MGMC_ZS_NT_F
-#define MGMC_ZS_NT_F 0
-#endif
 #if MGMC_ZS_EXP == 6
 #define ZS_STEP_SYNC() ((void)0)
 #else
@@ -71,25 +79,30 @@ struct ZItem {
 // v = fma(alpha w, x_c, v), selected when alpha is a power of two: alpha w x_c is then exact, so the
 // fma rounds once like the separate add and the bits are the same.
 // MINW: minimum waves per SIMD the register allocation must allow (1 = unconstrained)
+struct RunE0 {
+    int value;
+};
+
+// threads of a TY-row tile: TY/2 core waves + 2 halo waves, rounded up to a multiple of 4 waves
+constexpr int zs_threads(int TY) { return 256 * ((TY / 2 + 2 + 3) / 4); }
+
+// XP must be 32 (a wave = two rows of 32 pairs); TY a multiple of 4, <= 32
 template <int XP, int TY, int NT, int PROLONG, int MINW>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW))) k_zsweep_rb7(ZSweepArgs a) {
+    static_assert(XP == 32 && TY % 4 == 0 && TY <= 32 && NT == zs_threads(TY), "tile shape");
     constexpr int WP = XP + 4;     // pairs per LDS row: positions [2*q0-3, 2*q0+2*XP+4]
     // LDS row = [odd positions of the WP pairs | even positions | 2 pad]: lanes owning consecutive
     // pairs read consecutive doubles (conflict-free); the row stride (2XP+10 doubles = 20 mod 64 banks)
-    // spreads the column
-    // accesses of the x-halo items over the banks
+    // spreads the column accesses of the x-halo items over the banks
     constexpr int RS = 2 * WP + 2;
-    constexpr int PS = (TY + 4) * RS;  // LDS plane
     constexpr int R = TY + 4;      // rows j0-2 .. j0+TY+1
-    constexpr int NCORE = TY * XP;                 // core pairs (both colours)
-    constexpr int NHALO = 2 * (XP + 2) + 2 * TY;   // first-colour halo ring pairs
-    static_assert(NCORE % NT == 0, "core pairs must divide evenly over the workgroup");
-    constexpr int NC = NCORE / NT;                 // core pairs per thread
-    constexpr int NH = (NHALO + NT - 1) / NT;      // halo pairs per thread
+    constexpr int PS = R * RS;     // LDS plane
+    constexpr int NSLOT = 4;
+    constexpr int NCW = TY / 2;    // core waves
     constexpr int NLX = (R * WP + NT - 1) / NT;    // pair loads of one x plane per thread
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* xs = smem;                 // [3][R][RS] ring of x planes (p-1 .. p+1)
-    double* tab = xs + 3 * PS;      // [3][64] log reduction table (rc, hi, lo) + [130] cos/sin table
+    double* xs = smem;                  // [4][R][RS] ring of x planes
+    double* tab = xs + NSLOT * PS;      // [3][64] log reduction table (rc, hi, lo) + [130] cos/sin table
     for (int q = threadIdx.x; q < 64; q += NT) {
         tab[q] = LOGTAB_RC[q];
         tab[64 + q] = LOGTAB_HI[q];
@@ -110,8 +123,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     const int per = nb >> 3;
     const int tile = (nb & 7) ? b : (b & 7) * per + (b >> 3);
     // x fastest: a workgroup's x neighbours run next to it on the same XCD and share the partial
-    // 128-B lines of the x halo through L2 (y fastest: 1.49x algorithmic traffic against 1.21x,
-    // 0.77 against 0.69 ms; 2 x 2 tile groups: unchanged -- round-2 experiments)
+    // 128-B lines of the x halo through L2 (y fastest: 1.49x algorithmic traffic against 1.21x)
     const int txi = tile % a.ntx;
     const int tyi = (tile / a.ntx) % a.nty;
     const int tzi = tile / (a.ntx * a.nty);
@@ -127,8 +139,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     const uint32_t s_lo = (uint32_t)sample, s_hi = (uint32_t)(sample >> 32);
     const uint32_t plane_pairs = (uint32_t)((uint64_t)(L.ny - 1) * (uint64_t)(L.nx / 2));
     const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
 
-    auto slot = [](int p) { return (p + 9) % 3; };
+    auto slot = [](int p) { return (p + 4) & 3; };
     auto interior_plane = [&](int k) { return k >= 1 && k <= L.nz - 1; };
     auto make_item = [&](int r, int c2) {
         ZItem t;
@@ -138,7 +151,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         // unconditional and reads exactly the zeros the guarded form produced (columns past either
         // end of a row land in the zero padding of the layout)
         const int jc = j < 0 ? 0 : (j > L.ny ? L.ny : j);
-        t.goff = (long long)jc * L.sx + i + L.off;
+        t.goff = (int)((long long)jc * L.sx + i + L.off);
         t.pbase = (uint32_t)((uint64_t)(j - 1) * (uint64_t)(L.nx / 2) + (uint64_t)((i - 1) >> 1));
         t.lds = r * RS + c2;  // odd element; the even element is at +WP
         t.flags = (rin ? 1 : 0) | ((i >= 1 && i <= L.nx - 1) ? 2 : 0) | ((i + 1 >= 1 && i + 1 <= L.nx - 1) ? 4 : 0) |
@@ -146,34 +159,42 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         return t;
     };
 
-    ZItem ci[NC];
-#pragma unroll
-    for (int u = 0; u < NC; ++u) {
-        const int it = tid + u * NT;
-        ci[u] = make_item(2 + it / XP, 2 + it % XP);
-    }
-    ZItem hi[NH];
-#pragma unroll
-    for (int u = 0; u < NH; ++u) {
-        int it = tid + u * NT;
-        if (it >= NHALO) {
-            hi[u] = make_item(0, 0);
-            hi[u].flags = 0;
-            continue;
+    // ---- this thread's pair item ----
+    const bool core_wave = wave < NCW, active_wave = wave < NCW + 2;  // wave-uniform
+    int ir = 2, ic = 2;
+    if (core_wave) {
+        ir = 2 + 4 * (wave >> 1) + (wave & 1) + (lane >= 32 ? 2 : 0);  // rows r, r + 2: one parity
+        ic = 2 + (lane & 31);
+    } else if (active_wave) {
+        const int h = wave - NCW;
+        // lanes past the halo items mirror lane 0's item: the same arithmetic writes the same bits
+        // to the same LDS word, so the duplicate is harmless
+        const int l = (lane < 32 + TY) ? lane : 0;
+        if (l < 32) {
+            ir = h == 0 ? 1 : R - 2;
+            ic = 2 + l;
+        } else {  // left / right column of the core rows of the row's parity
+            const int m = l - 32;
+            ir = (h == 0 ? 3 : 2) + 2 * (m >> 1);
+            ic = (m & 1) ? WP - 2 : 1;
         }
-        int r, c2;
-        if (it < XP + 2) {
-            r = 1; c2 = 1 + it;
-        } else if (it < 2 * (XP + 2)) {
-            r = R - 2; c2 = 1 + it - (XP + 2);
-        } else {
-            it -= 2 * (XP + 2);
-            r = 2 + (it >> 1);
-            c2 = (it & 1) ? WP - 2 : 1;
-        }
-        hi[u] = make_item(r, c2);
     }
-    long long xoff[NLX];
+    const ZItem t = make_item(ir, ic);
+    // (i + j) & 1 of the wave's items (all i odd, rows of one parity): wave-uniform
+    const int wpar = __builtin_amdgcn_readfirstlane((t.flags >> 3) & 1);
+    // element (0 odd position, 1 even) taking the first colour on plane k: wave-uniform.  Chunks
+    // start on odd planes, so it is E0 on the steps p = k0-1, k0+1, ... (even p) and 1 - E0 on the
+    // others.  The plain sweep compiles the z march below once per value of E0 and runs the steps in
+    // pairs, so every element choice in it is a compile-time constant: no selects, and pair loads
+    // and stores stay 16-byte accesses (the two copies execute the same sequence of barriers).  The
+    // fused-prolongation sweep keeps one copy with wave-uniform selects (its registers are the
+    // binding limit: 2 workgroups of 12 waves per CU need <= 80 VGPRs).
+    const int E0 = __builtin_amdgcn_readfirstlane(((wpar ^ (k0 - 1)) & 1) == fc ? 0 : 1);
+    // the odd / even element is an interior vertex (per lane; boundary vertices are never written)
+    const bool rowin = (t.flags & 1) != 0;
+    const bool in0 = rowin && (t.flags & 2), in1 = rowin && (t.flags & 4);
+
+    int xoff[NLX];
     int xlds[NLX];
 #pragma unroll
     for (int u = 0; u < NLX; ++u) {
@@ -185,14 +206,14 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
             // prolongation's odd-row terms (PROLONG) are skipped by whole wavefronts
             constexpr int NE = (R + 1) / 2;  // rows r = 0, 2, 4, ...
             const int r = it < NE * WP ? 2 * (it / WP) : 2 * ((it - NE * WP) / WP) + 1;
-            const ZItem t = make_item(r, it % WP);
-            xlds[u] = t.lds;
-            xoff[u] = t.goff;
+            const ZItem q = make_item(r, it % WP);
+            xlds[u] = q.lds;
+            xoff[u] = q.goff;
         }
     }
     // PROLONG: per staged pair, the row parity and the coarse-ring offset of its first parent
     // (coarse column q = (i-1)/2 = q0-2+c2, coarse row j>>1)
-    int pjodd[NLX], pcro[NLX];
+    int pcro[NLX];  // 2 x (coarse-ring offset) + row parity
     // planes outside [0, nz] are clamped onto the zero boundary planes 0 / nz
     auto plane_base = [&](const double* v, int k) { return v + (long long)(k < 0 ? 0 : (k > L.nz ? L.nz : k)) * L.sp; };
 
@@ -236,12 +257,13 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     // alpha w = alpha 2^-(#odd of j, k) / 2 (odd position) or alpha 2^-(...) (even position): exact
     // scalings, equal to the reference's products alpha * w.
     const double al0 = a.alpha, al1 = a.alpha * 0.5;
-    auto prolong_pair = [&](double2 v, int jodd, int k, int cro) {
+    // KO: k & 1 when known at compile time (the z march: chunks start on odd planes), else -1
+    auto prolong_pair = [&](double2 v, int jodd, int k, int cro, auto KO) {
 #if MGMC_ZS_EXP == 8  // timing experiment: coarse ring loads only, no prolongation arithmetic
         return v;
 #endif
         const int K0 = k >> 1;
-        const int kodd = k & 1;
+        const int kodd = decltype(KO)::value >= 0 ? decltype(KO)::value : (k & 1);
         const double awx = ldexp(al1, -(jodd + kodd)), awy = ldexp(al0, -(jodd + kodd));
         const double* cp0 = cring + cro;
 #pragma unroll
@@ -269,8 +291,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
 #pragma unroll
     for (int u = 0; u < NLX; ++u) {
         const int c2 = xlds[u] < 0 ? 0 : xlds[u] % RS, j = xlds[u] < 0 ? j0 : j0 - 2 + xlds[u] / RS;
-        pjodd[u] = j & 1;
-        pcro[u] = c2 + 1 + ((j >> 1) - Jst) * CW;  // ring column of coarse q0-2+c2
+        pcro[u] = 2 * (c2 + 1 + ((j >> 1) - Jst) * CW) + (j & 1);  // ring column of coarse q0-2+c2
     }
 
     // ---- global <-> LDS / registers ----
@@ -280,22 +301,20 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
 #pragma unroll
         for (int u = 0; u < NLX; ++u) px[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
     };
-    auto deposit_x = [&](int k) {
+    auto deposit_x = [&](int k, auto KO) {
         double* dst = xs + slot(k) * PS;
 #pragma unroll
         for (int u = 0; u < NLX; ++u) {
             if (xlds[u] < 0) continue;
             double2 v = px[u];
-            if (PROLONG && interior_plane(k)) v = prolong_pair(v, pjodd[u], k, pcro[u]);
+            if (PROLONG && interior_plane(k)) v = prolong_pair(v, pcro[u] & 1, k, pcro[u] >> 1, KO);
             dst[xlds[u]] = v.x;
             dst[xlds[u] + WP] = v.y;
         }
     };
-    auto load_f = [&](int k, const ZItem& t) {
-        const double* q = plane_base(a.f, k) + t.goff;
-        if (MGMC_ZS_NT_F) return make_double2(__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1));
-        return *reinterpret_cast<const double2*>(q);
-    };
+    // f of the item on plane k: (first-colour element, other element) -- two 8-byte loads at
+    // wave-uniform element offsets instead of a pair load and per-lane selects
+    auto load_f = [&](int k) { return *reinterpret_cast<const double2*>(plane_base(a.f, k) + t.goff); };
 
     // fma-chain stencil sum (ascending column order) at LDS offset o of plane k.  The fine FD
     // stencil is symmetric (launch_zsweep checks a[4]=a[22], a[10]=a[16], a[12]=a[14]), so four
@@ -318,11 +337,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         res = fma(cz, sp[o], res);
         return res;
     };
-    // first-colour update of pair item t on plane k; returns the second colour's right hand side
-    // c = fma(sd, z_other, f_other) (the same fma the second-colour update would evaluate)
-    auto first_pair = [&](int k, const ZItem& t, double2 fv) -> double {
-        if (!(t.flags & 1) || !(t.flags & 6)) return 0.0;
-        const int e = (((t.flags >> 3) ^ k) & 1) == fc ? 0 : 1;  // element of the first colour
+    // the Box-Muller pair of this item on plane k (z.x: odd position i, z.y: even i+1)
+    auto noise = [&](int k) -> double2 {
         const uint32_t pair = (uint32_t)(k - 1) * plane_pairs + t.pbase;
         uint32_t key0 = a.G.key.k0, key1 = a.G.key.k1;
         asm volatile("" : "+s"(key0), "+s"(key1));  // keep the round-key schedule out of the SGPR budget
@@ -336,95 +352,90 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
 #if MGMC_ZS_EXP == 1 || MGMC_ZS_EXP == 5  // timing experiment: no noise generation
         z0 = (double)(rnd.v[0] & 1); z1 = (double)(rnd.v[2] & 1);
 #else
-        normal_pair_t(rnd, &z0, &z1, tab, tab + 64, tab + 128, tab + 192);  // z0: odd position i, z1: even i+1
+        normal_pair_t(rnd, &z0, &z1, tab, tab + 64, tab + 128, tab + 192);
 #endif
-        if (t.flags & (2 << e)) {
-            const int o = t.lds + (e ? WP : 0);
-            const double res = row_sum(k, o, e, xs[slot(k - 1) * PS + o]);
-            const double crhs = fma(sd, e == 0 ? z0 : z1, e == 0 ? fv.x : fv.y);
-            double* s0 = xs + slot(k) * PS;
-            s0[o] = fma(wd, crhs - res, s0[o]);
-        }
-        return e == 0 ? fma(sd, z1, fv.y) : fma(sd, z0, fv.x);
+        return make_double2(z0, z1);
     };
-    // second-colour update of core item t on plane k; returns the new value (the old one where the
-    // vertex is not interior).  No update ever reads a second-colour value after its update (the first
-    // colour reads the old ones, the second colour only first-colour neighbours), so the result goes
-    // to the store and not back to LDS; below = the new first-colour value at (i, j, k-1), kept in a
-    // register since plane k-1 has already left the LDS ring.
-    auto second_pair = [&](int k, const ZItem& t, double crhs, double below) -> double {
-        const int e = (((t.flags >> 3) ^ k) & 1) == fc ? 1 : 0;  // element of the second colour
-        const int o = t.lds + (e ? WP : 0);
-        const double old = xs[slot(k) * PS + o];
-        if (!(t.flags & 1) || !(t.flags & (2 << e))) return old;
-        const double res = row_sum(k, o, e, below);
-        return fma(wd, crhs - res, old);
-    };
-
-    // One z step p (LDS ring = planes p-1, p, p+1):
-    //   deposit x(p+1) (into the slot plane p-2 left), issue x(p+2) and f(p+1)      | barrier
-    //   first colour on plane p (core + halo ring)                                 | barrier
-    //   second colour on plane p-1 (core); plane p-1 is final: store it from the new
-    //   second-colour values (registers) and the first-colour values (LDS), and keep
-    //   the latter as the next step's z-below values                               | barrier
+    // One z step p (LDS ring = planes p-2 .. p+1):
+    //   deposit x(p+1) (into the slot plane p-3 left), issue x(p+2) and f(p+1)   | barrier
+    //   first colour on plane p (core + halo ring)                              | barrier
+    //   second colour on plane p-1 (core); plane p-1 is final: store it from the new second-colour
+    //   values (registers) and the first-colour values (LDS), and keep the latter as the next
+    //   step's z-below values; draw the noise of plane p+1
+    // (the next step's deposit writes the slot of plane p-2, which nothing reads any more).
     // f(p) arrives in fcur (loaded one step earlier), f(p+1) goes to fnxt; the second colour's right
-    // hand sides of plane p go to pk_out, those of plane p-1 come from pk_in; fb_in / fb_out hold the
-    // first-colour values of planes p-2 / p-1 at the second-colour positions of planes p-1 / p.  The
-    // loop runs the steps in pairs with the register sets swapped, so nothing is copied.
+    // hand side of plane p goes to pk_out, that of plane p-1 comes from pk_in.  The loop runs the
+    // steps in pairs with the register sets swapped, so nothing is copied.
     // PROLONG, coarse ring: the deposit of fine plane p+1 reads coarse planes (p+1)>>1 .. (p+2)>>1;
     // even steps (p even: chunks start on odd planes) issue coarse plane (p+4)/2, odd steps deposit it
     // (its slot held plane (p-1)/2, last read at step p-1).
-    auto step = [&](int p, bool odd_step, double2 (&fcur)[NC], double2 (&fnxt)[NC], double2 (&fhcur)[NH],
-                    double2 (&fhnxt)[NH], const double (&pk_in)[NC], double (&pk_out)[NC], const double (&fb_in)[NC],
-                    double (&fb_out)[NC]) __attribute__((always_inline)) {
-        deposit_x(p + 1);
-        if (PROLONG) {
-            if (odd_step) deposit_c((p + 3) / 2);
-            else issue_c((p + 4) / 2);
-        }
-        issue_x(p + 2);
-#pragma unroll
-        for (int u = 0; u < NC; ++u) fnxt[u] = load_f(p + 1, ci[u]);
-#pragma unroll
-        for (int u = 0; u < NH; ++u) fhnxt[u] = load_f(p + 1, hi[u]);
-        ZS_STEP_SYNC();
-        if (interior_plane(p)) {
-#pragma unroll
-            for (int u = 0; u < NC; ++u) pk_out[u] = first_pair(p, ci[u], fcur[u]);
-#pragma unroll
-            for (int u = 0; u < NH; ++u)
-                if (MGMC_ZS_EXP != 2 && MGMC_ZS_EXP != 5) (void)first_pair(p, hi[u], fhcur[u]);
-        }
-        ZS_STEP_SYNC();
-        const int k = p - 1;
-        const bool own = k >= k0 && k < k1;  // a core plane of this tile (interior)
-        double sv[NC];
-#pragma unroll
-        for (int u = 0; u < NC; ++u) sv[u] = own ? second_pair(k, ci[u], pk_in[u], fb_in[u]) : 0.0;
-        double* base = a.xout + (long long)k * L.sp;
-#pragma unroll
-        for (int u = 0; u < NC; ++u) {
-            const int ef = (((ci[u].flags >> 3) ^ k) & 1) == fc ? 0 : 1;  // first-colour element on plane k
-            const double fv = xs[slot(k) * PS + ci[u].lds + (ef ? WP : 0)];
-            fb_out[u] = fv;
-            if (own && (ci[u].flags & 1)) {
-                const double2 out = ef == 0 ? make_double2(fv, sv[u]) : make_double2(sv[u], fv);
-                if (MGMC_ZS_NT_STORE) {  // streaming store: keep the write stream out of L2
-                    __builtin_nontemporal_store(out.x, base + ci[u].goff);
-                    __builtin_nontemporal_store(out.y, base + ci[u].goff + 1);
-                } else {
-                    *reinterpret_cast<double2*>(base + ci[u].goff) = out;
-                }
+    double2 z = make_double2(0.0, 0.0);
+    double fb = 0.0;  // first-colour value below (plane p-2) at the second-colour position of p-1
+    // E0c: std::integral_constant (E0 known at compile time in this copy of the march) or RunE0 (a
+    // wave-uniform run-time value: the fused-prolongation sweep, one copy, fewer registers)
+    auto run = [&](auto E0c) __attribute__((always_inline)) {
+        const int E0c_v = E0c.value;
+        auto step = [&](int p, auto ODDc, double2& fcur, double2& fnxt, double pk_in, double& pk_out)
+                        __attribute__((always_inline)) {
+            constexpr bool odd_step = decltype(ODDc)::value;
+            const int e = odd_step ? 1 - E0c_v : E0c_v;  // first-colour element on plane p
+            const int o1 = t.lds + e * WP, o2 = t.lds + (1 - e) * WP;
+            const bool inf = e ? in1 : in0;  // (compile-time choice)
+            deposit_x(p + 1, std::integral_constant<int, odd_step ? 0 : 1>{});  // p even on even steps
+            if (PROLONG) {
+                if (odd_step) deposit_c((p + 3) / 2);
+                else issue_c((p + 4) / 2);
             }
+            issue_x(p + 2);
+            if (active_wave) fnxt = load_f(p + 1);
+            ZS_STEP_SYNC();
+            // first colour on plane p: c = fma(sd, z, f), x = fma(omega/diag, c - S, x); the second
+            // colour's right-hand side of the pair, c' = fma(sd, z', f')
+            if (interior_plane(p) && (MGMC_ZS_EXP != 2 && MGMC_ZS_EXP != 5 ? active_wave : core_wave)) {
+                if (inf) {
+                    const double res = row_sum(p, o1, e, xs[slot(p - 1) * PS + o1]);
+                    const double crhs = fma(sd, e ? z.y : z.x, e ? fcur.y : fcur.x);
+                    double* s0 = xs + slot(p) * PS;
+                    s0[o1] = fma(wd, crhs - res, s0[o1]);
+                }
+                pk_out = fma(sd, e ? z.x : z.y, e ? fcur.x : fcur.y);
+            }
+            ZS_STEP_SYNC();
+            // second colour on plane k = p-1 (its element is e: the parity flips with the plane)
+            const int k = p - 1;
+            if (core_wave) {
+                const bool own = k >= k0 && k < k1;  // a core plane of this tile (interior)
+                const double* s0 = xs + slot(k) * PS;
+                const double fv = s0[o2];             // final first-colour value
+                if (own && rowin) {
+                    double sv = s0[o1];
+                    if (inf) sv = fma(wd, pk_in - row_sum(k, o1, e, fb), sv);
+                    double* dst = a.xout + (long long)k * L.sp + t.goff;
+                    // (x, y) = (odd, even) element; the second colour is element e here
+                    const double2 out = e ? make_double2(fv, sv) : make_double2(sv, fv);
+                    if (MGMC_ZS_NT_STORE) {  // streaming store: keep the write stream out of L2
+                        __builtin_nontemporal_store(out.x, dst);
+                        __builtin_nontemporal_store(out.y, dst + 1);
+                    } else {
+                        *reinterpret_cast<double2*>(dst) = out;
+                    }
+                }
+                fb = fv;
+            }
+            if (active_wave && interior_plane(p + 1)) z = noise(p + 1);
+        };
+        double2 fA = make_double2(0.0, 0.0), fB = make_double2(0.0, 0.0);
+        double pkA = 0.0, pkB = 0.0;
+        if (active_wave) fA = load_f(k0 - 1);
+        if (active_wave && interior_plane(k0 - 1)) z = noise(k0 - 1);
+        for (int p = k0 - 1; p <= k1; p += 2) {
+            step(p, std::integral_constant<bool, false>{}, fA, fB, pkB, pkA);
+            if (p + 1 <= k1) step(p + 1, std::integral_constant<bool, true>{}, fB, fA, pkA, pkB);
         }
-        ZS_STEP_SYNC();
     };
 
-    double2 fA[NC], fB[NC], fhA[NH], fhB[NH];
-    double pkA[NC], pkB[NC], fbA[NC], fbB[NC];
-#pragma unroll
-    for (int u = 0; u < NC; ++u) pkA[u] = pkB[u] = fbA[u] = fbB[u] = 0.0;
-    // prologue: planes k0-2, k0-1 in LDS, x(k0) and f(k0-1) in flight (k0 is odd: tz even)
+    // prologue: planes k0-2, k0-1 in LDS, x(k0) and f(k0-1) in flight, noise of plane k0-1 (k0 is
+    // odd: tz even)
     if (PROLONG) {  // coarse planes (k0-3)/2, (k0-1)/2 for the first two deposits, then (k0+1)/2
         issue_c((k0 - 3) / 2);
         deposit_c((k0 - 3) / 2);
@@ -433,9 +444,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         __syncthreads();
     }
     issue_x(k0 - 2);
-    deposit_x(k0 - 2);
+    deposit_x(k0 - 2, std::integral_constant<int, -1>{});
     issue_x(k0 - 1);
-    deposit_x(k0 - 1);
+    deposit_x(k0 - 1, std::integral_constant<int, -1>{});
     if (PROLONG) {
         __syncthreads();
         issue_c((k0 + 1) / 2);
@@ -443,14 +454,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         __syncthreads();
     }
     issue_x(k0);
-#pragma unroll
-    for (int u = 0; u < NC; ++u) fA[u] = load_f(k0 - 1, ci[u]);
-#pragma unroll
-    for (int u = 0; u < NH; ++u) fhA[u] = load_f(k0 - 1, hi[u]);
-    for (int p = k0 - 1; p <= k1; p += 2) {
-        step(p, false, fA, fB, fhA, fhB, pkB, pkA, fbB, fbA);
-        if (p + 1 <= k1) step(p + 1, true, fB, fA, fhB, fhA, pkA, pkB, fbA, fbB);
-    }
+    if (PROLONG) run(RunE0{E0});
+    else if (E0) run(std::integral_constant<int, 1>{});  // wave-uniform branch
+    else run(std::integral_constant<int, 0>{});
 }
 
 #ifndef MGMC_ZS_LDS_EXTRA
@@ -459,7 +465,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
 inline size_t zsweep_lds_bytes(int XP, int TY, bool prolong) {
     const int RS = 2 * (XP + 4) + 2, R = TY + 4;
     const int coarse = prolong ? 2 * (TY / 2 + 3) * (XP + 8) : 0;
-    return (size_t)(3 * R * RS + 3 * 64 + 130 + coarse) * sizeof(double) + (prolong ? 0 : MGMC_ZS_LDS_EXTRA);
+    return (size_t)(4 * R * RS + 3 * 64 + 130 + coarse) * sizeof(double) + (prolong ? 0 : MGMC_ZS_LDS_EXTRA);
 }
 
 }  // namespace mgmc

@@ -6,15 +6,17 @@ SRCS="mgmc_capi.hip mgmc_hierarchy.cpp mgmc_operators.cpp -L/opt/rocm/lib -lrccl
 for n in ${EXPS:-1 2 3 4}; do
   $HIPX -DMGMC_ZS_EXP=$n -o ../../build/libmgmc_exp$n.so $SRCS &
 done
-# cache-policy variants: 7 non-temporal stores, 8 non-temporal f loads, 9 both
+# cache-policy variant 7: plain (temporal) sweep stores
 for n in ${NTEXPS:-}; do
-  d="-DMGMC_ZS_NT_STORE=$(( n == 7 || n == 9 )) -DMGMC_ZS_NT_F=$(( n == 8 || n == 9 ))"
-  $HIPX $d -o ../../build/libmgmc_exp$n.so $SRCS &
+  $HIPX -DMGMC_ZS_NT_STORE=0 -o ../../build/libmgmc_exp$n.so $SRCS &
 done
-# fine-sweep tile shapes XPxTYxNT[xTZ] (x-pairs, rows, threads, z-chunk): build/libmgmc_exps<shape>.so
+# fine-sweep tile shapes TYxMINW[xTZ[xTYPxMINWP]] (rows per tile, waves/SIMD floor, z-chunk, then
+# the same for the fused-prolongation sweep; 32 x-pairs):
+# build/libmgmc_exps<shape>.so
 for s in ${SHAPES:-}; do
-  IFS=x read -r xp ty nt tz <<< "$s"
-  d="-DMGMC_ZS_SHAPE_XP=$xp -DMGMC_ZS_SHAPE_TY=$ty -DMGMC_ZS_SHAPE_NT=$nt ${tz:+-DMGMC_ZS_SHAPE_TZ=$tz}"
+  IFS=x read -r ty mw tz typ mwp <<< "$s"
+  d="-DMGMC_ZS_SHAPE_TY=$ty -DMGMC_ZS_SHAPE_MINW=$mw ${tz:+-DMGMC_ZS_SHAPE_TZ=$tz}"
+  d="$d ${typ:+-DMGMC_ZS_SHAPE_TYP=$typ -DMGMC_ZS_SHAPE_MINWP=$mwp}"
   $HIPX $d -o ../../build/libmgmc_exps$s.so $SRCS &
 done
 wait
