@@ -90,9 +90,13 @@ constexpr int zs_threads(int TY) { return 256 * ((TY / 2 + 2 + 3) / 4); }
 template <int XP, int TY, int NT, int PROLONG, int MINW>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW))) k_zsweep_rb7(ZSweepArgs a) {
     static_assert(XP == 32 && TY % 4 == 0 && TY <= 32 && NT == zs_threads(TY), "tile shape");
-    constexpr int WP = XP + 4;     // pairs per LDS row: positions [2*q0-3, 2*q0+2*XP+4]
+    // pairs per LDS row: positions [2*q0-1, 2*q0+2*XP+2] -- the core pairs and one halo pair per side.
+    // The halo ring's column items need only their element next to the tile (the even one on the left,
+    // the odd one on the right), whose x neighbours are staged; their other element's update reads a
+    // wrapped-around slot and lands in a slot no update of this tile ever reads.
+    constexpr int WP = XP + 2;
     // LDS row = [odd positions of the WP pairs | even positions | 2 pad]: lanes owning consecutive
-    // pairs read consecutive doubles (conflict-free); the row stride (2XP+10 doubles = 20 mod 64 banks)
+    // pairs read consecutive doubles (conflict-free); the row stride (2XP+6 doubles = 12 mod 64 banks)
     // spreads the column accesses of the x-halo items over the banks
     constexpr int RS = 2 * WP + 2;
     constexpr int R = TY + 4;      // rows j0-2 .. j0+TY+1
@@ -132,7 +136,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     const int j0 = 1 + tyi * TY;          // first core row
     const int k0 = 1 + tzi * a.tz;        // first core plane
     const int k1 = min(k0 + a.tz, L.nz);  // one past the last core plane
-    const int ibase = 2 * q0 - 3;         // position of LDS column 0
+    const int ibase = 2 * q0 - 1;         // position of LDS column 0
     const int fc = a.G.colour;            // first colour
     const double sd = a.G.sd, wd = a.G.wd;
     const uint64_t sample = *a.G.sample;
@@ -161,10 +165,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
 
     // ---- this thread's pair item ----
     const bool core_wave = wave < NCW, active_wave = wave < NCW + 2;  // wave-uniform
-    int ir = 2, ic = 2;
+    int ir = 2, ic = 1;
     if (core_wave) {
         ir = 2 + 4 * (wave >> 1) + (wave & 1) + (lane >= 32 ? 2 : 0);  // rows r, r + 2: one parity
-        ic = 2 + (lane & 31);
+        ic = 1 + (lane & 31);
     } else if (active_wave) {
         const int h = wave - NCW;
         // lanes past the halo items mirror lane 0's item: the same arithmetic writes the same bits
@@ -172,11 +176,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         const int l = (lane < 32 + TY) ? lane : 0;
         if (l < 32) {
             ir = h == 0 ? 1 : R - 2;
-            ic = 2 + l;
+            ic = 1 + l;
         } else {  // left / right column of the core rows of the row's parity
             const int m = l - 32;
             ir = (h == 0 ? 3 : 2) + 2 * (m >> 1);
-            ic = (m & 1) ? WP - 2 : 1;
+            ic = (m & 1) ? WP - 1 : 0;
         }
     }
     const ZItem t = make_item(ir, ic);
@@ -212,7 +216,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         }
     }
     // PROLONG: per staged pair, the row parity and the coarse-ring offset of its first parent
-    // (coarse column q = (i-1)/2 = q0-2+c2, coarse row j>>1)
+    // (coarse column q = (i-1)/2 = q0-1+c2, coarse row j>>1)
     int pcro[NLX];  // 2 x (coarse-ring offset) + row parity
     // planes outside [0, nz] are clamped onto the zero boundary planes 0 / nz
     auto plane_base = [&](const double* v, int k) { return v + (long long)(k < 0 ? 0 : (k > L.nz ? L.nz : k)) * L.sp; };
@@ -291,7 +295,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
 #pragma unroll
     for (int u = 0; u < NLX; ++u) {
         const int c2 = xlds[u] < 0 ? 0 : xlds[u] % RS, j = xlds[u] < 0 ? j0 : j0 - 2 + xlds[u] / RS;
-        pcro[u] = 2 * (c2 + 1 + ((j >> 1) - Jst) * CW) + (j & 1);  // ring column of coarse q0-2+c2
+        pcro[u] = 2 * (c2 + 2 + ((j >> 1) - Jst) * CW) + (j & 1);  // ring column of coarse q0-1+c2
     }
 
     // ---- global <-> LDS / registers ----
@@ -463,7 +467,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
 #define MGMC_ZS_LDS_EXTRA 0  // timing experiments only: extra LDS bytes of the plain variant (occupancy)
 #endif
 inline size_t zsweep_lds_bytes(int XP, int TY, bool prolong) {
-    const int RS = 2 * (XP + 4) + 2, R = TY + 4;
+    const int RS = 2 * (XP + 2) + 2, R = TY + 4;
     const int coarse = prolong ? 2 * (TY / 2 + 3) * (XP + 8) : 0;
     return (size_t)(4 * R * RS + 3 * 64 + 130 + coarse) * sizeof(double) + (prolong ? 0 : MGMC_ZS_LDS_EXTRA);
 }
