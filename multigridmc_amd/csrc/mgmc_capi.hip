@@ -147,13 +147,16 @@ bool read_path_flags(uint32_t* flags, std::string* bad) {
 #ifndef MGMC_ZS_SHAPE_TZ
 #define MGMC_ZS_SHAPE_TZ 32
 #endif
+#ifndef MGMC_ZS_SHAPE_TZP
+#define MGMC_ZS_SHAPE_TZP 128
+#endif
 #ifndef MGMC_ZS_SHAPE_TYP  // the fused-prolongation (post-)sweep
 #define MGMC_ZS_SHAPE_TYP 16
 #define MGMC_ZS_SHAPE_MINWP 6
 #endif
 constexpr int ZS_XP = 32, ZS_TY = MGMC_ZS_SHAPE_TY, ZS_NT = zs_threads(ZS_TY), ZS_MINW = MGMC_ZS_SHAPE_MINW,
               ZS_TZ = MGMC_ZS_SHAPE_TZ, ZS_TYP = MGMC_ZS_SHAPE_TYP, ZS_NTP = zs_threads(ZS_TYP),
-              ZS_MINWP = MGMC_ZS_SHAPE_MINWP, ZS_TZP = 64;
+              ZS_MINWP = MGMC_ZS_SHAPE_MINWP, ZS_TZP = MGMC_ZS_SHAPE_TZP;
 
 // device copy of a level's low-rank part (mgmc_lowrank.hpp); one allocation list, freed together
 struct LowRankDev {

@@ -63,7 +63,8 @@ struct ZItem {
 
 // MGMC_ZS_EXP (timing experiments only, scripts/build_exp.sh; 0 in the product): 1 no Box-Muller,
 // 2 no halo ring, 3 no Philox, 4 no stencil, 5 memory skeleton (1 + 2 + 4), 6 no step barriers
-// (wrong results: sync cost only)
+// (wrong results: sync cost only), 8 no prolongation arithmetic, 9 wave-uniform Box-Muller table
+// indices
 #ifndef MGMC_ZS_EXP
 #define MGMC_ZS_EXP 0
 #endif
@@ -353,7 +354,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         const Philox4 rnd = philox4x32_10(pair, a.G.tag, s_lo, s_hi, key0, key1);
 #endif
         double z0, z1;
-#if MGMC_ZS_EXP == 1 || MGMC_ZS_EXP == 5  // timing experiment: no noise generation
+#if MGMC_ZS_EXP == 9  // timing experiment: wave-uniform table indices (no LDS bank conflicts in Box-Muller)
+        Philox4 rnd9 = rnd;
+        rnd9.v[0] &= 0x3FFFFu; rnd9.v[2] &= 0x3FFFFu;
+        normal_pair_t(rnd9, &z0, &z1, tab, tab + 64, tab + 128, tab + 192);
+#elif MGMC_ZS_EXP == 1 || MGMC_ZS_EXP == 5  // timing experiment: no noise generation
         z0 = (double)(rnd.v[0] & 1); z1 = (double)(rnd.v[2] & 1);
 #else
         normal_pair_t(rnd, &z0, &z1, tab, tab + 64, tab + 128, tab + 192);

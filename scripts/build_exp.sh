@@ -3,7 +3,7 @@
 cd "$(dirname "$0")/../multigridmc_amd/csrc" && mkdir -p ../../build
 HIPX="/opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off -fPIC -w --offload-arch=gfx950 -shared"
 SRCS="mgmc_capi.hip mgmc_hierarchy.cpp mgmc_operators.cpp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib"
-for n in ${EXPS:-1 2 3 4}; do
+for n in ${EXPS:-1 2 3 4}; do  # MGMC_ZS_EXP variants
   $HIPX -DMGMC_ZS_EXP=$n -o ../../build/libmgmc_exp$n.so $SRCS &
 done
 # cache-policy variant 7: plain (temporal) sweep stores
@@ -18,5 +18,9 @@ for s in ${SHAPES:-}; do
   d="-DMGMC_ZS_SHAPE_TY=$ty -DMGMC_ZS_SHAPE_MINW=$mw ${tz:+-DMGMC_ZS_SHAPE_TZ=$tz}"
   d="$d ${typ:+-DMGMC_ZS_SHAPE_TYP=$typ -DMGMC_ZS_SHAPE_MINWP=$mwp}"
   $HIPX $d -o ../../build/libmgmc_exps$s.so $SRCS &
+done
+# fused-prolongation sweep z-chunk depths: build/libmgmc_expz<TZP>.so
+for z in ${TZPS:-}; do
+  $HIPX -DMGMC_ZS_SHAPE_TZP=$z -o ../../build/libmgmc_expz$z.so $SRCS &
 done
 wait
