@@ -15,10 +15,11 @@ a sparse Cholesky factorisation.  As in the reference, the "exact" observed stat
 refer to the measured (posterior) operator built on top of the chosen operator.
 
 Out of scope (not the device hot path): the Cholesky and SSOR samplers of the whole lattice
-(do_cholesky / do_ssor are reported and skipped), the periodic-kappa correlation length model and
-the squared_shiftedlaplace_fd prior (neither is a constant 3^d-point stencil), and the VTK output of
-posterior_statistics.  pdemodel = "shiftedlaplace_fd" and "shiftedlaplace_fem" are both on the
-device path.
+(do_cholesky / do_ssor are reported and skipped) and the VTK output of posterior_statistics.
+Every prior of the reference is on the device path (driver_mgmc.cc:398-429): pdemodel =
+"shiftedlaplace_fd", "shiftedlaplace_fem" and "squared_shiftedlaplace_fd" (2D), with the
+"constant" or the "periodic" correlation length model; operators with per-vertex coefficients go to
+the device as matrices (mgmc_create_csr).
 """
 from __future__ import annotations
 
@@ -30,10 +31,11 @@ import time
 import numpy as np
 
 from .measured import MeasuredOperator, measurement_vector
-from .parameters import (ConstantCorrelationLengthModelParameters, GeneralParameters, LatticeParameters,
-                         MeasurementFileError, MeasurementParameters, MultigridParameters, PriorParameters,
-                         SamplingParameters, read_config)
-from .sampler import Lattice, MultigridMCSampler, ShiftedLaplaceFDOperator, ShiftedLaplaceFEMOperator
+from .parameters import (ConfigError, ConstantCorrelationLengthModelParameters, GeneralParameters,
+                         LatticeParameters, MeasurementFileError, MeasurementParameters, MultigridParameters,
+                         PeriodicCorrelationLengthModelParameters, PriorParameters, SamplingParameters, read_config)
+from .sampler import (ConstantCorrelationLengthModel, Lattice, MultigridMCSampler, PeriodicCorrelationLengthModel,
+                      ShiftedLaplaceFDOperator, ShiftedLaplaceFEMOperator, SquaredShiftedLaplaceFDOperator)
 
 SEED = 5418513  # driver_mgmc.cc:448
 
@@ -232,16 +234,29 @@ def main(argv=None) -> int:
     else:
         print(f"ERROR: Invalid dimension : {general.dim}")
         return -1
-    if prior_params.correlationlength_model != "constant":
-        print(f"Error: correlationlengthmodel '{prior_params.correlationlength_model}' is not on the device path")
+    # driver_mgmc.cc:398-429
+    try:
+        if prior_params.correlationlength_model == "constant":
+            model = ConstantCorrelationLengthModel(ConstantCorrelationLengthModelParameters.from_config(cfg).Lambda)
+        elif prior_params.correlationlength_model == "periodic":
+            pp = PeriodicCorrelationLengthModelParameters.from_config(cfg)
+            model = PeriodicCorrelationLengthModel(pp.Lambda_min, pp.Lambda_max)
+        else:
+            print(f"Error: invalid correlationlengthmodel '{prior_params.correlationlength_model}'")
+            return -1
+    except ConfigError as e:
+        print(str(e))
         return -1
-    # driver_mgmc.cc:414-429
-    prior_classes = {"shiftedlaplace_fd": ShiftedLaplaceFDOperator, "shiftedlaplace_fem": ShiftedLaplaceFEMOperator}
+    prior_classes = {"shiftedlaplace_fd": ShiftedLaplaceFDOperator, "shiftedlaplace_fem": ShiftedLaplaceFEMOperator,
+                     "squared_shiftedlaplace_fd": SquaredShiftedLaplaceFDOperator}
     if prior_params.pde_model not in prior_classes:
-        print(f"Error: prior '{prior_params.pde_model}' is not on the device path")
+        print(f"Error: invalid prior '{prior_params.pde_model}'")
         return -1
-    kappa_sq = ConstantCorrelationLengthModelParameters.from_config(cfg).kappa_sq
-    prior = prior_classes[prior_params.pde_model](lattice, kappa_sq)
+    try:
+        prior = prior_classes[prior_params.pde_model](lattice, model)
+    except ValueError as e:  # squared_shiftedlaplace_fd in 3D (squared_shiftedlaplace_fd_operator.cc:15-19)
+        print(f"ERROR: {e}")
+        return -1
     posterior = MeasuredOperator(prior, measurement_params)
     if general.operator_name == "prior":
         linear_operator = prior

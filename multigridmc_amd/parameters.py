@@ -218,6 +218,23 @@ class ConstantCorrelationLengthModelParameters:
 
 
 @dataclass
+class PeriodicCorrelationLengthModelParameters:
+    """parameters.cc:224-243 (Lambda_max >= Lambda_min > 0, else the reference exits with -1)."""
+    Lambda_min: float = 0.2
+    Lambda_max: float = 0.4
+
+    @classmethod
+    def from_config(cls, cfg: dict) -> "PeriodicCorrelationLengthModelParameters":
+        g = _get(cfg, "periodiccorrelationlengthmodel")
+        out = cls(float(g["Lambda_min"]), float(g["Lambda_max"]))
+        if not out.Lambda_max >= out.Lambda_min:
+            raise ConfigError("ERROR: upper bound on correlation length has to exceed lower bound.")
+        if not out.Lambda_min > 0:
+            raise ConfigError("ERROR: lower bound on correlation length has to be positive.")
+        return out
+
+
+@dataclass
 class MeasurementParameters:
     radius: float = 0.0
     sample_location: list = field(default_factory=lambda: [0.5, 0.5])

@@ -67,3 +67,21 @@ def test_driver_usage_and_loud_failure_without_gpu(tmp_path, capsys):
         pytest.skip("a HIP device is present (the driver run is covered by test_gpu_exact.py)")
     with pytest.raises(mg.MgmcError):  # no HIP device here: the product path fails loudly
         main([str(tmp_path / "parameters_template.cfg")])
+
+
+@pytest.mark.parametrize("lmin,lmax,msg", [(0.4, 0.2, "upper bound on correlation length"),
+                                           (0.0, 0.4, "lower bound on correlation length")])
+def test_driver_rejects_invalid_periodic_model(tmp_path, capsys, lmin, lmax, msg):
+    """parameters.cc:233-242: Lambda_max >= Lambda_min > 0, else the message and exit(-1) -- before any
+    device work (no GPU needed)."""
+    import os
+    import re
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    text = open(os.path.join(gold, "parameters_template.cfg")).read()
+    text = re.sub(r'correlationlengthmodel = "constant";', 'correlationlengthmodel = "periodic";', text)
+    text = re.sub(r"Lambda_min = 0.2;", f"Lambda_min = {lmin};", text)
+    text = re.sub(r"Lambda_max = 0.4;", f"Lambda_max = {lmax};", text)
+    (tmp_path / "parameters.cfg").write_text(text)
+    (tmp_path / "measurements_template.cfg").write_text(open(os.path.join(gold, "measurements_template.cfg")).read())
+    assert main([str(tmp_path / "parameters.cfg")]) == -1
+    assert msg in capsys.readouterr().out

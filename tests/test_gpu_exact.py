@@ -128,12 +128,16 @@ def test_posterior_qoi_mean_and_variance_at_128_cubed(hip_device):
     s.close()
 
 
-@pytest.mark.parametrize("pde", ["shiftedlaplace_fd", "shiftedlaplace_fem"])
-def test_driver_posterior_template_run(hip_device, tmp_path, monkeypatch, pde):
+@pytest.mark.parametrize("pde,model", [("shiftedlaplace_fd", "constant"), ("shiftedlaplace_fem", "constant"),
+                                       ("shiftedlaplace_fd", "periodic"), ("shiftedlaplace_fem", "periodic"),
+                                       ("squared_shiftedlaplace_fd", "constant"),
+                                       ("squared_shiftedlaplace_fd", "periodic")])
+def test_driver_posterior_template_run(hip_device, tmp_path, monkeypatch, pde, model):
     """multigridmc_amd.driver on the reference's parameters_template.cfg / measurements_template.cfg
-    (config 1: 2D posterior, 8 measurements, W-cycle), lattice 64^2 and shortened sampling: the
-    timeseries and convergence files are written in the reference's formats, and the sample mean
-    and variance of z agree with the exact observed statistics within 5 sigma (IACT)."""
+    (config 1: 2D posterior, 8 measurements, W-cycle), lattice 64^2 and shortened sampling, for every
+    prior and correlation length model of driver_mgmc.cc:398-429: the timeseries and convergence files
+    are written in the reference's formats, and the sample mean and variance of z agree with the exact
+    observed statistics within 5 sigma (IACT)."""
     import os
     import re
     from multigridmc_amd.driver import main
@@ -144,7 +148,8 @@ def test_driver_posterior_template_run(hip_device, tmp_path, monkeypatch, pde):
     text = re.sub(r"nsamples = 10000;", "nsamples = 20000;", text)
     text = re.sub(r"nsamples = 1000;", "nsamples = 200;", text)
     text = re.sub(r'pdemodel = "shiftedlaplace_fd";', f'pdemodel = "{pde}";', text)
-    assert f'pdemodel = "{pde}";' in text
+    text = re.sub(r'correlationlengthmodel = "constant";', f'correlationlengthmodel = "{model}";', text)
+    assert f'pdemodel = "{pde}";' in text and f'correlationlengthmodel = "{model}";' in text
     (tmp_path / "parameters.cfg").write_text(text)
     (tmp_path / "measurements_template.cfg").write_text(open(os.path.join(gold, "measurements_template.cfg")).read())
     monkeypatch.chdir(tmp_path)
@@ -160,8 +165,10 @@ def test_driver_posterior_template_run(hip_device, tmp_path, monkeypatch, pde):
     cfg = read_config(str(tmp_path / "parameters.cfg"))
     mp = MeasurementParameters.from_config(cfg, str(tmp_path))
     lat = mg.Lattice(64, 64)
-    prior_cls = mg.ShiftedLaplaceFEMOperator if pde == "shiftedlaplace_fem" else mg.ShiftedLaplaceFDOperator
-    op = mg.MeasuredOperator(prior_cls(lat, 25.0), mp)
+    prior_cls = {"shiftedlaplace_fd": mg.ShiftedLaplaceFDOperator, "shiftedlaplace_fem": mg.ShiftedLaplaceFEMOperator,
+                 "squared_shiftedlaplace_fd": mg.SquaredShiftedLaplaceFDOperator}[pde]
+    cl = mg.ConstantCorrelationLengthModel(0.2) if model == "constant" else mg.PeriodicCorrelationLengthModel(0.2, 0.4)
+    op = mg.MeasuredOperator(prior_cls(lat, cl), mp)
     s = mg.MultigridMCSampler(op, SEED, MultigridParameters.from_config(cfg))
     rows, vals = mg.measurement_vector(lat, mp.sample_location, mp.radius)
     mean_exact, var_exact = ExactTargets(s).observed_mean_and_variance(_measured_values(mp), rows, vals)
