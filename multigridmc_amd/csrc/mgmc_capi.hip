@@ -398,21 +398,20 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
     a.G.colour = (direction == MGMC_FORWARD) ? 0 : 1;
     const long long txy = (long long)((lv.L.nx / 2) / ZS_XP) * ((lv.L.ny - 1 + ZS_TY - 1) / ZS_TY);
     const long long txyp = (long long)((lv.L.nx / 2) / ZS_XP) * ((lv.L.ny - 1 + ZS_TYP - 1) / ZS_TYP);
-    if (coarse) {
-        // fused-prolongation sweep: 512-thread workgroups (one core pair per thread: 127 VGPRs,
-        // 2 workgroups = 16 waves per CU against 3 x 4 waves with 256 threads, which the 6.7 KB
-        // coarse ring and 161 VGPRs allowed) and chunks up to 64 planes deep as long as the grid
-        // keeps two rounds of workgroups (512^3: tz 64, 2,048 tiles, 906-911 -> 841-851 us;
-        // 256^3: tz 16, 142 -> 118 us; interleaved A/B).  tz stays even: chunks start on odd planes
-        // (coarse ring schedule)
-        a.tz = ZS_TZP;
-        while (a.tz > 8 && txyp * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 2LL * 2 * lv.num_cu) a.tz /= 2;
+    // z-chunk depth: the deepest chunk (fewest prologue steps, 2 per chunk) that still keeps 3/4 of
+    // the 2 x num_cu workgroup slots busy -- 512^3: 32 (plain) / 128 (post) planes, 256^3: 32 / 32.
+    // Even: chunks start on odd planes (the first-colour element schedule, the coarse ring)
+    auto depth = [&](long long tiles_xy, int tzmax) {
+        int tz = tzmax;
+        while (tz > 8 && 4 * tiles_xy * ((lv.L.nz - 1 + tz - 1) / tz) < 3LL * 2 * lv.num_cu) tz /= 2;
+        return tz;
+    };
+    if (coarse) {  // fused-prolongation sweep
+        a.tz = depth(txyp, ZS_TZP);
         launch_zsweep_t<ZS_XP, ZS_TYP, ZS_NTP, ZS_MINWP>(lv, a, true, s);
         return;
     }
-    // shallower z chunks until the grid has >= 1024 tiles (4 per CU): 256^3 -> 16 planes
-    a.tz = ZS_TZ;
-    while (a.tz > 8 && txy * ((lv.L.nz - 1 + a.tz - 1) / a.tz) < 1024) a.tz /= 2;
+    a.tz = depth(txy, ZS_TZ);
     launch_zsweep_t<ZS_XP, ZS_TY, ZS_NT, ZS_MINW>(lv, a, false, s);
 }
 

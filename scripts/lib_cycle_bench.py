@@ -1,5 +1,5 @@
 """In-cycle timing of library builds: for each library (product or build/libmgmc_exp<N>.so), K timed
-512^3 V-cycles (mgmc_sample_timed: fine pre / post sweep segments) in a fresh child process, and the
+N^3 (default 512^3, NLEVEL 7; env N / NLEVEL) V-cycles (mgmc_sample_timed: fine pre / post sweep segments) in a fresh child process, and the
 plain single-graph replay of the same K cycles.  python scripts/lib_cycle_bench.py [exps, 0 = product]"""
 import json
 import os
@@ -11,8 +11,10 @@ CHILD = r'''
 import sys, json, time
 sys.path.insert(0, %r)
 import multigridmc_amd as mg
-lat = mg.Lattice3d(512, 512, 512)
-s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 1, mg.MultigridParameters(nlevel=7))
+import os
+n, nl = int(os.environ.get("N", "512")), int(os.environ.get("NLEVEL", "7"))
+lat = mg.Lattice3d(n, n, n)
+s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 1, mg.MultigridParameters(nlevel=nl))
 s.sample(5)
 import hashlib
 digest = hashlib.sha1(s.get_state().tobytes()).hexdigest()[:12]  # same bits in every correct build
