@@ -72,6 +72,9 @@ def parse():
                     help="ShiftedLaplaceFEMOperator prior (27/9-point fine level); no CPU baseline")
     ap.add_argument("--radius", type=float, default=0.0, help="measurement radius (--posterior)")
     ap.add_argument("--measure-global", action="store_true", help="add the global average measurement (--posterior)")
+    ap.add_argument("--chains", type=int, default=1, metavar="K",
+                    help="independent chains per GPU, batched in one handle (mgmc_create_batch): every kernel "
+                         "of the cycle covers all K, chain ids rank * K .. rank * K + K - 1")
     return ap.parse_args()
 
 
@@ -187,8 +190,8 @@ class Collectives:
         if self.kind == "gloo":
             import numpy as np
             out = [None] * self.world
-            self.dist.all_gather_object(out, list(self.s.qoi_moments()))
-            return np.array(out)
+            self.dist.all_gather_object(out, [list(self.s.qoi_moments(c)) for c in range(self.s.nchains)])
+            return np.array(out).reshape(-1, 3)
         return self.s.comm_allgather_moments(self.world)
 
 
@@ -234,7 +237,8 @@ def main():
     t_setup = time.perf_counter()
     # MGMC_BENCH_DEVICE pins every rank to one device (rehearsing the N>1 host path on a 1-GPU box)
     device = int(os.environ.get("MGMC_BENCH_DEVICE", local_rank))
-    sampler = mg.MultigridMCSampler(op, SEED, params, device=device, chain_id=rank)
+    K = args.chains
+    sampler = mg.MultigridMCSampler(op, SEED, params, device=device, chain_id=rank * K, nchains=K)
     t_setup = time.perf_counter() - t_setup
     qoi = mg.measurement_vector_index(lat, [0.5] * args.dim)
     n0 = lat.Nvertex
@@ -267,18 +271,19 @@ def main():
     nq, mean, m2 = merge_moments([tuple(r) for r in parts])
 
     if rank == 0:
-        value = world * args.steps / elapsed
+        value = world * K * args.steps / elapsed
         roof, per_kernel = None, {}
         if timed and timed["npre"] > 0:
             plain3d = args.dim == 3 and not args.fem and not args.posterior
             tr_pre, prov = stored_traffic(args.traffic_file, n, "pre_sweep") if plain3d else (None, None)
             tr_post, prov2 = stored_traffic(args.traffic_file, n, "post_sweep") if plain3d else (None, None)
-            pre = sweep_roofline(timed["pre_ms"], timed["npre"], 24.0 * n0, tr_pre, prov,
+            pre = sweep_roofline(timed["pre_ms"], timed["npre"], 24.0 * n0 * K, tr_pre if K == 1 else None, prov,
                                  "fine pre-sweep k_zsweep_rb7 (one red-black Gibbs sweep of level 0)")
             per_kernel["pre_sweep"] = pre
             if timed["npost"] > 0:
                 n1 = mg.Lattice(*((n // 2,) * args.dim)).Nvertex
-                post = sweep_roofline(timed["post_ms"], timed["npost"], 24.0 * n0 + 8.0 * n1, tr_post, prov2,
+                post = sweep_roofline(timed["post_ms"], timed["npost"], (24.0 * n0 + 8.0 * n1) * K,
+                                      tr_post if K == 1 else None, prov2,
                                       "fine post-sweep k_zsweep_rb7<PROLONG> (prolongate-add of level 1 fused, "
                                       "24 B per fine + 8 B per coarse unknown; segment includes the ~4 us QoI record)")
                 per_kernel["post_sweep"] = post
@@ -312,9 +317,10 @@ def main():
             "config": {"workload": f"{args.dim}D {n}^{args.dim} shifted-Laplace {'FEM' if args.fem else 'FD'} "
                                    f"prior (kappa^2 = 25), "
                                    f"{nlevel}-level V-cycle, SOR Gibbs 1/1, SSOR coarse 1, omega 1, "
-                                   f"one independent chain per GPU",
-                       "lattice": [n] * args.dim, "unknowns": n0, "nlevel": nlevel, "chains": world,
-                       "parallelism": f"chains{world} (independent MCMC chains, 1 per GPU, no data-path "
+                                   + ("one independent chain per GPU" if K == 1 else
+                                      f"{K} independent chains per GPU batched in one handle"),
+                       "lattice": [n] * args.dim, "unknowns": n0, "nlevel": nlevel, "chains": world * K,
+                       "parallelism": f"chains{world * K} (independent MCMC chains, {K} per GPU, no data-path "
                                       f"collective; final QoI-moment all-gather over {coll.kind})",
                        "collectives": coll.kind, "rccl_ranks": coll.rccl_ranks},
             "roofline": roof,
@@ -335,7 +341,8 @@ def main():
                             f"{args.posterior} measurements of radius {args.radius}"
                             + (" + global average" if args.measure_global else ""))
             line["config"]["workload"] = (f"BASELINE config 5: 3D {n}^3 posterior Q = A + B Sigma^-1 B^T (m = {m}), "
-                                          f"{nlevel}-level V-cycle, SOR Gibbs 1/1 with the B_bar fix, SSOR coarse 1")
+                                          f"{nlevel}-level V-cycle, SOR Gibbs 1/1 with the B_bar fix, SSOR coarse 1"
+                                          + (f", {K} chains per GPU batched" if K > 1 else ""))
             line["config"]["m_lowrank"] = m
             line["config"]["bbar_rows_forward_per_level"] = rows
             line["config"]["setup_s"] = round(t_setup, 2)

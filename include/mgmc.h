@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MGMC_ABI_VERSION 3
+#define MGMC_ABI_VERSION 4
 
 /* error codes */
 #define MGMC_OK 0
@@ -150,6 +150,21 @@ int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chai
  * levels such as the squared FD operator's).  cfg.kappa_sq and cfg.fine_operator are ignored. */
 int mgmc_create_csr(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr, const int32_t* col,
                     const double* val, int device, uint64_t seed, uint64_t chain_id, mgmc_handle** out);
+/* Batched chains (ABI 4): nchains (1..16) independent chains chain0, chain0+1, ... in one handle.
+ * They share the hierarchy, the stencils and the low-rank data (B, B_bar); each keeps its own state
+ * and right-hand side in HBM and its own Philox key make_key(seed, chain0 + c), so chain c draws
+ * exactly what a single-chain handle with chain_id = chain0 + c draws (bitwise).  Every kernel of
+ * the cycle covers all chains in one launch; the low-rank fix reads B_bar once per row for all
+ * chains (x -= B_bar W, W = B^T X: the (N x m)(m x C) product of the batch, sor_smoother.cc:47-51).
+ * The entry points below without _chain act on every chain (set_rhs, set_state: the same vector)
+ * or on chain 0 (get_state, get_series, qoi_moments).  Replaces running several
+ * MultigridMCSampler objects (driver_mgmc.cc:188-314 measure_convergence's chains). */
+int mgmc_create_batch(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chain0, int nchains,
+                      mgmc_handle** out);
+int mgmc_create_csr_batch(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr, const int32_t* col,
+                          const double* val, int device, uint64_t seed, uint64_t chain0, int nchains,
+                          mgmc_handle** out);
+int mgmc_nchains(const mgmc_handle* h);
 int mgmc_destroy(mgmc_handle* h);
 int mgmc_level_desc_get(const mgmc_handle* h, int level, mgmc_level_desc* out);
 
@@ -173,6 +188,8 @@ int mgmc_lowrank_info(const mgmc_handle* h, int level, int direction, int* m, in
 int mgmc_set_rhs(mgmc_handle* h, const double* f, size_t n);       /* fix_rhs: f stays in HBM */
 int mgmc_set_state(mgmc_handle* h, const double* x, size_t n);
 int mgmc_get_state(mgmc_handle* h, double* x, size_t n);
+int mgmc_set_state_chain(mgmc_handle* h, int chain, const double* x, size_t n);
+int mgmc_get_state_chain(mgmc_handle* h, int chain, double* x, size_t n);
 /* Sampler::apply(f, x): upload f and x, run one MGMC cycle, download x (PCIe inclusive). */
 int mgmc_apply(mgmc_handle* h, const double* f, double* x, size_t n);
 
@@ -187,6 +204,7 @@ int mgmc_sample_async(mgmc_handle* h, int nsteps, int64_t qoi_index);
 int mgmc_synchronize(mgmc_handle* h);
 /* out[0] = n, out[1] = mean, out[2] = M2 (sum of squared deviations) of the recorded QoI */
 int mgmc_qoi_moments(mgmc_handle* h, double out[3]);
+int mgmc_qoi_moments_chain(mgmc_handle* h, int chain, double out[3]);
 int mgmc_reset_moments(mgmc_handle* h);
 int mgmc_set_sample_index(mgmc_handle* h, uint64_t index);
 int mgmc_get_sample_index(mgmc_handle* h, uint64_t* index);
@@ -194,6 +212,7 @@ int mgmc_get_sample_index(mgmc_handle* h, uint64_t* index);
  * for the handle's stream).  With mgmc_sample_async on several handles this collects the series of
  * chains that ran concurrently (measure_convergence's batched chains, driver_mgmc.cc:188-314). */
 int mgmc_get_series(mgmc_handle* h, double* out, size_t n);
+int mgmc_get_series_chain(mgmc_handle* h, int chain, double* out, size_t n);
 /* HIP stream (hipStream_t) the handle enqueues on */
 int mgmc_get_stream(mgmc_handle* h, void** stream);
 
@@ -249,7 +268,8 @@ int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* tot
 /* rank 0 creates the id and ships it to the other ranks (any host channel) */
 int mgmc_comm_unique_id(unsigned char out[MGMC_UNIQUE_ID_BYTES]);
 int mgmc_comm_init(mgmc_handle* h, int nranks, int rank, const unsigned char id[MGMC_UNIQUE_ID_BYTES]);
-/* all ranks: out[3*r .. 3*r+2] = (n, mean, M2) of rank r's device-side QoI moments */
+/* all ranks: out[3*(r*nchains + c) .. +2] = (n, mean, M2) of chain c of rank r's handle (device-side
+ * QoI moments; 3 * nranks * mgmc_nchains(h) doubles) */
 int mgmc_comm_allgather_moments(mgmc_handle* h, double* out);
 /* all ranks: *value <- max over ranks (used for the max-over-ranks benchmark time) */
 int mgmc_comm_allreduce_max(mgmc_handle* h, double* value);

@@ -29,7 +29,7 @@ OPERATOR_SQUARED_FD = 2
 KAPPA_CONSTANT = 0
 KAPPA_PERIODIC = 1
 KAPPA_GIVEN = 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 SOLVER_LOOP = 0
 SOLVER_CG = 1
 FORWARD = 1
@@ -82,6 +82,10 @@ SIGNATURES = [
                                 c_uint64, c_uint64, POINTER(c_void_p)]),
     ("mgmc_operator_csr_size", c_int, [POINTER(MgmcOperatorDesc), POINTER(c_int64), POINTER(c_int64)]),
     ("mgmc_operator_csr", c_int, [POINTER(MgmcOperatorDesc), POINTER(c_int64), POINTER(ctypes.c_int32), _DP]),
+    ("mgmc_create_batch", c_int, [POINTER(MgmcConfig), c_int, c_uint64, c_uint64, c_int, POINTER(c_void_p)]),
+    ("mgmc_create_csr_batch", c_int, [POINTER(MgmcConfig), c_int64, POINTER(c_int64), POINTER(ctypes.c_int32), _DP,
+                                      c_int, c_uint64, c_uint64, c_int, POINTER(c_void_p)]),
+    ("mgmc_nchains", c_int, [_H]),
     ("mgmc_destroy", c_int, [_H]),
     ("mgmc_level_desc_get", c_int, [_H, c_int, POINTER(MgmcLevelDesc)]),
     ("mgmc_set_lowrank", c_int, [_H, c_int, POINTER(c_int64), POINTER(c_int64), _DP, _DP]),
@@ -89,15 +93,19 @@ SIGNATURES = [
     ("mgmc_set_rhs", c_int, [_H, _DP, c_size_t]),
     ("mgmc_set_state", c_int, [_H, _DP, c_size_t]),
     ("mgmc_get_state", c_int, [_H, _DP, c_size_t]),
+    ("mgmc_set_state_chain", c_int, [_H, c_int, _DP, c_size_t]),
+    ("mgmc_get_state_chain", c_int, [_H, c_int, _DP, c_size_t]),
     ("mgmc_apply", c_int, [_H, _DP, _DP, c_size_t]),
     ("mgmc_sample", c_int, [_H, c_int, c_int64, _DP]),
     ("mgmc_sample_async", c_int, [_H, c_int, c_int64]),
     ("mgmc_synchronize", c_int, [_H]),
     ("mgmc_qoi_moments", c_int, [_H, _DP]),
+    ("mgmc_qoi_moments_chain", c_int, [_H, c_int, _DP]),
     ("mgmc_reset_moments", c_int, [_H]),
     ("mgmc_set_sample_index", c_int, [_H, c_uint64]),
     ("mgmc_get_sample_index", c_int, [_H, POINTER(c_uint64)]),
     ("mgmc_get_series", c_int, [_H, POINTER(c_double), c_size_t]),
+    ("mgmc_get_series_chain", c_int, [_H, c_int, POINTER(c_double), c_size_t]),
     ("mgmc_get_stream", c_int, [_H, POINTER(c_void_p)]),
     ("mgmc_operator_apply", c_int, [_H, c_int, _DP, _DP]),
     ("mgmc_smoother_apply", c_int, [_H, c_int, c_int, c_int, _DP, _DP]),

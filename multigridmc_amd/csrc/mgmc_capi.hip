@@ -91,6 +91,7 @@ enum PathFlag : uint32_t {
     PATH_NO_LR_MERGE = 1u << 8,           // low-rank: separate restore / patch launches around restriction
     PATH_NO_LR_PREFETCH = 1u << 9,        // low-rank small fix without the up-front loads
     PATH_NO_COARSE_PRECOMPUTE = 1u << 10, // coarse SSOR: right-hand sides inside the colour passes
+    PATH_NO_LR_DENSE = 1u << 11,          // dense low-rank column: the row lists over every vertex
 };
 
 struct PathToken {
@@ -103,7 +104,7 @@ constexpr PathToken kPathTokens[] = {
     {"zsweep", PATH_NO_ZSWEEP},       {"pairs", PATH_NO_PAIRS},
     {"zrestrict", PATH_NO_ZRESTRICT}, {"lr_small", PATH_NO_LR_SMALL},
     {"lr_merge", PATH_NO_LR_MERGE},   {"lr_prefetch", PATH_NO_LR_PREFETCH},
-    {"coarse_precompute", PATH_NO_COARSE_PRECOMPUTE},
+    {"coarse_precompute", PATH_NO_COARSE_PRECOMPUTE}, {"lr_dense", PATH_NO_LR_DENSE},
 };
 
 // parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
@@ -185,6 +186,17 @@ struct LowRankDev {
     int* t_ent_off = nullptr;      // the same offsets in k_tail's LDS layout (small levels)
     int* t_rows_off = nullptr;
     int* t_bar_off[2] = {nullptr, nullptr};
+    // dense-column path (one dense column g, mgmc_lowrank.hpp k_lr_dense_*): the row lists above
+    // hold only the local rows; the dense-only rows stream B_g / Y_g, and the patched right-hand
+    // side goes to fe (nchains x L.nstore) instead of f
+    bool dense_path = false;
+    int dense_g = -1;
+    uint32_t* skip_b = nullptr;                 // bit p: not a dense-only row of the patch
+    uint32_t* skip_y[2] = {nullptr, nullptr};   // bit p: not a dense-only row of B_bar (per direction)
+    double* yg[2] = {nullptr, nullptr};         // column g of Y (padded, per direction)
+    double* minv_g[2] = {nullptr, nullptr};     // row g of Minv (per direction)
+    double* fe = nullptr;
+    long long nbar_all[2] = {0, 0};             // B_bar rows in total (local + dense-only with Y_g != 0)
     std::vector<void*> allocs;
 };
 
@@ -221,12 +233,14 @@ void free_lowrank(LowRankDev& lr) {
 struct mgmc_handle {
     mgmc_config cfg;
     int device = 0;
-    uint64_t seed = 0, chain = 0;
+    uint64_t seed = 0, chain = 0;   // chain = the first chain of a batch (mgmc_create_batch)
+    int nchains = 1;                // chains of the batch: level vectors, QoI series and moments
+                                    // are nchains copies, L.nstore / capacity / 4 doubles apart
     RngKey key;
     std::vector<Level> levels;
     hipStream_t stream = nullptr;
     uint64_t* ctrl = nullptr;       // [0] sample index [1] series length [2] qoi index [3] scratch sample
-    double* mom = nullptr;          // running (n, mean, M2)
+    double* mom = nullptr;          // running (n, mean, M2, pad) per chain
     double* series = nullptr;
     uint64_t series_cap = 0;
     double* lex_tmp = nullptr;      // staging buffer in reference layout (device)
@@ -300,7 +314,20 @@ GibbsArg make_gibbs(const mgmc_handle* h, const Level& lv, uint32_t tag, int col
     g.tag = tag;
     g.colour = colour;
     g.sample = sample;
+    g.chain0 = (uint32_t)h->chain;
+    g.seed_hi = (uint32_t)(h->seed >> 32);
     return g;
+}
+
+// chain c of a batch: its Philox key (make_key(seed, chain0 + c)) and its copy of a level vector
+RngKey chain_key_host(const GibbsArg& g, int c) {
+    RngKey k = g.key;
+    if (c) k.k1 = (g.chain0 + (uint32_t)c) ^ g.seed_hi;
+    return k;
+}
+template <class T>
+T* chain_ptr(T* v, const Level& lv, int c) {
+    return v ? v + (long long)c * lv.L.nstore : v;
 }
 
 template <int DIM, int NPTS, bool NOISE>
@@ -345,8 +372,17 @@ void launch_fsweep(const Level& lv, double* x, const double* f, const GibbsArg& 
     }
 }
 
-void launch_sweep(const Level& lv, double* x, const double* f, const GibbsArg& g, int direction, bool noise,
-                  hipStream_t s) {
+void launch_sweep(const Level& lv, double* x, const double* f, const GibbsArg& g0, int direction, bool noise,
+                  hipStream_t s, int nch = 1) {
+    if (nch > 1) {  // batched chains on the generic colour-pass kernels: one launch sequence per chain
+        for (int c = 0; c < nch; ++c) {
+            GibbsArg g = g0;
+            g.key = chain_key_host(g0, c);
+            launch_sweep(lv, chain_ptr(x, lv, c), chain_ptr(f, lv, c), g, direction, noise, s, 1);
+        }
+        return;
+    }
+    const GibbsArg& g = g0;
     if (lv.field) {
         launch_fsweep(lv, x, f, g, direction, noise, s);
         return;
@@ -365,7 +401,7 @@ void launch_sweep(const Level& lv, double* x, const double* f, const GibbsArg& g
 }
 
 template <int XP, int TY, int NT, int MINW = 1>
-void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s) {
+void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s, int nch) {
     a.ntx = (lv.L.nx / 2) / XP;
     a.nty = (lv.L.ny - 1 + TY - 1) / TY;
     a.ntz = (lv.L.nz - 1 + a.tz - 1) / a.tz;
@@ -375,17 +411,20 @@ void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s)
     // alpha a power of two (coarse_scaling 1): fma prolongation terms, same bits (mgmc_zsweep.hpp)
     int ex;
     const bool pow2 = std::isnormal(a.alpha) && std::frexp(std::fabs(a.alpha), &ex) == 0.5 && ex > -900 && ex < 900;
+    const dim3 grid(nb, 1, nch);  // batched chains: blockIdx.z
     if (prolong && pow2)
-        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 2, MINW>), dim3(nb), dim3(NT), lds, s, a);
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 2, MINW>), grid, dim3(NT), lds, s, a);
     else if (prolong)
-        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 1, MINW>), dim3(nb), dim3(NT), lds, s, a);
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 1, MINW>), grid, dim3(NT), lds, s, a);
     else
-        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 0, MINW>), dim3(nb), dim3(NT), lds, s, a);
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 0, MINW>), grid, dim3(NT), lds, s, a);
 }
 
 void launch_zsweep(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g0,
-                   int direction, const Level* coarse, const double* xc, double alpha, hipStream_t s) {
+                   int direction, const Level* coarse, const double* xc, double alpha, hipStream_t s, int nch = 1) {
     ZSweepArgs a;
+    a.cs = lv.L.nstore;
+    a.csc = coarse ? coarse->L.nstore : 0;
     a.L = lv.L;
     a.xin = xin;
     a.xout = xout;
@@ -408,11 +447,11 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
     };
     if (coarse) {  // fused-prolongation sweep
         a.tz = depth(txyp, ZS_TZP);
-        launch_zsweep_t<ZS_XP, ZS_TYP, ZS_NTP, ZS_MINWP>(lv, a, true, s);
+        launch_zsweep_t<ZS_XP, ZS_TYP, ZS_NTP, ZS_MINWP>(lv, a, true, s, nch);
         return;
     }
     a.tz = depth(txy, ZS_TZ);
-    launch_zsweep_t<ZS_XP, ZS_TY, ZS_NT, ZS_MINW>(lv, a, false, s);
+    launch_zsweep_t<ZS_XP, ZS_TY, ZS_NT, ZS_MINW>(lv, a, false, s, nch);
 }
 
 // colour-pair passes of a Galerkin 9/27-point level (in place): forward colours (0,1), (2,3), ...,
@@ -434,19 +473,21 @@ bool quads_eligible(const LevelSpec& sp, const Layout& L, uint32_t paths) {
 
 // one red-black sweep of a 2D 5-point level, xin -> xout (mgmc_rb2d.hpp)
 void launch_rb2d(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
-                 bool noise, hipStream_t s) {
+                 bool noise, hipStream_t s, int nch = 1) {
     const int ntx = (lv.L.nx - 1 + RB2_TW - 1) / RB2_TW, nty = (lv.L.ny - 1 + RB2_TH - 1) / RB2_TH;
     const int c1 = direction == MGMC_FORWARD ? 0 : 1;
-    const dim3 grid(ntx * nty), block(RB2_NT);
+    const dim3 grid(ntx * nty, 1, nch), block(RB2_NT);
+    const long long cs = lv.L.nstore;
     if (noise)
-        hipLaunchKernelGGL((k_rb2d<true>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx);
+        hipLaunchKernelGGL((k_rb2d<true>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx, cs);
     else
-        hipLaunchKernelGGL((k_rb2d<false>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx);
+        hipLaunchKernelGGL((k_rb2d<false>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx, cs);
 }
 
 void launch_quads(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
-                  hipStream_t s) {
+                  hipStream_t s, int nch = 1) {
     QuadPassArgs a;
+    a.cs = lv.L.nstore;
     a.L = lv.L;
     a.x0 = xin;
     a.xout = xout;
@@ -469,19 +510,21 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
         const int first = 2 - a.kp;
         const int nk = dim == 3 ? (first > lv.L.nz - 1 ? 0 : (lv.L.nz - 1 - first) / 2 + 1) : 1;
         if (nk == 0) continue;
-        const int nb = a.nblk_y * nk;
+        const dim3 grid(a.nblk_y * nk, 1, nch);
         if (dim == 3) {
-            if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false>), dim3(nb), dim3(nt), lds, s, a);
-            else hipLaunchKernelGGL((k_sweep_quads<3, true>), dim3(nb), dim3(nt), lds, s, a);
+            if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false>), grid, dim3(nt), lds, s, a);
+            else hipLaunchKernelGGL((k_sweep_quads<3, true>), grid, dim3(nt), lds, s, a);
         } else {
-            if (fwd) hipLaunchKernelGGL((k_sweep_quads<2, false>), dim3(nb), dim3(nt), lds, s, a);
-            else hipLaunchKernelGGL((k_sweep_quads<2, true>), dim3(nb), dim3(nt), lds, s, a);
+            if (fwd) hipLaunchKernelGGL((k_sweep_quads<2, false>), grid, dim3(nt), lds, s, a);
+            else hipLaunchKernelGGL((k_sweep_quads<2, true>), grid, dim3(nt), lds, s, a);
         }
     }
 }
 
-void launch_pairs(const Level& lv, double* x, const double* f, const GibbsArg& g, int direction, hipStream_t s) {
+void launch_pairs(const Level& lv, double* x, const double* f, const GibbsArg& g, int direction, hipStream_t s,
+                  int nch = 1) {
     PairPassArgs a;
+    a.cs = lv.L.nstore;
     a.L = lv.L;
     a.x = x;
     a.f = f;
@@ -502,22 +545,23 @@ void launch_pairs(const Level& lv, double* x, const double* f, const GibbsArg& g
         a.nrows_j = count(lv.L.ny, a.jp);
         a.nrows = a.nrows_j * (dim == 3 ? count(lv.L.nz, a.kp) : 1);
         if (a.nrows == 0) continue;
-        const int nb = (a.nrows + a.rows_per_block - 1) / a.rows_per_block;
+        const dim3 grid((a.nrows + a.rows_per_block - 1) / a.rows_per_block, 1, nch);
         const int nt = a.rows_per_block * npair;
         const bool odd = c & 1;
         if (dim == 3) {
-            if (odd) hipLaunchKernelGGL((k_sweep_pairs<3, true>), dim3(nb), dim3(nt), 0, s, a);
-            else hipLaunchKernelGGL((k_sweep_pairs<3, false>), dim3(nb), dim3(nt), 0, s, a);
+            if (odd) hipLaunchKernelGGL((k_sweep_pairs<3, true>), grid, dim3(nt), 0, s, a);
+            else hipLaunchKernelGGL((k_sweep_pairs<3, false>), grid, dim3(nt), 0, s, a);
         } else {
-            if (odd) hipLaunchKernelGGL((k_sweep_pairs<2, true>), dim3(nb), dim3(nt), 0, s, a);
-            else hipLaunchKernelGGL((k_sweep_pairs<2, false>), dim3(nb), dim3(nt), 0, s, a);
+            if (odd) hipLaunchKernelGGL((k_sweep_pairs<2, true>), grid, dim3(nt), 0, s, a);
+            else hipLaunchKernelGGL((k_sweep_pairs<2, false>), grid, dim3(nt), 0, s, a);
         }
     }
 }
 
-void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStream_t s) {
+void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStream_t s, int nch = 1) {
     const int dim = lv.spec.dim, np = lv.spec.npoints, nc = lv.spec.ncolours;
-    dim3 block(1024), grid(1);
+    dim3 block(1024), grid(1, 1, nch);
+    const long long chs = lv.L.nstore;
     // precomputed right hand sides (k_coarse_ssor_lds) when they fit next to x and f
     const long long ndof = (long long)(lv.L.nx - 1) * (lv.L.ny - 1) * (dim == 3 ? lv.L.nz - 1 : 1);
     const size_t lds_pre = lv.lds_bytes + (size_t)nsweeps * ndof * sizeof(double);
@@ -527,10 +571,10 @@ void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStrea
     do {                                                                                                           \
         if (pre)                                                                                                   \
             hipLaunchKernelGGL((k_coarse_ssor_lds<D, P, true>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g,   \
-                               nsweeps, nc);                                                                       \
+                               nsweeps, nc, chs);                                                                  \
         else                                                                                                       \
             hipLaunchKernelGGL((k_coarse_ssor_lds<D, P, false>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g,  \
-                               nsweeps, nc);                                                                       \
+                               nsweeps, nc, chs);                                                                  \
     } while (0)
     if (dim == 3 && np == 27) MGMC_COARSE_LAUNCH(3, 27);
     else if (dim == 3 && np == 7) MGMC_COARSE_LAUNCH(3, 7);
@@ -541,8 +585,10 @@ void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStrea
 
 template <int NPTS, int CX, int CY, int NT>
 void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, const double* f, double* fc, double* xc,
-                           hipStream_t s) {
+                           hipStream_t s, int nch) {
     ZRestrictArgs a;
+    a.csf = lf.L.nstore;
+    a.csc = lc.L.nstore;
     a.Lf = lf.L;
     a.Lc = lc.L;
     a.x = x;
@@ -568,11 +614,19 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
     a.ntz = (lc.L.nz - 1 + a.kz - 1) / a.kz;
     const int nt = a.ntx * a.nty * a.ntz;
     const int nb = (nt + 7) / 8 * 8;
-    hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT>), dim3(nb), dim3(NT), zrestrict_lds_bytes(CX, CY), s, a);
+    hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT>), dim3(nb, 1, nch), dim3(NT), zrestrict_lds_bytes(CX, CY), s,
+                       a);
 }
 
 void launch_residual_restrict(const Level& lf, const Level& lc, const double* x, const double* f, double* fc,
-                              double* xc, int zero_xc, hipStream_t s) {
+                              double* xc, int zero_xc, hipStream_t s, int nch = 1) {
+    const bool zr = lf.spec.dim == 3 && zero_xc && !lf.field && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8;
+    if (nch > 1 && !zr) {  // batched chains on the generic kernels: one launch per chain
+        for (int c = 0; c < nch; ++c)
+            launch_residual_restrict(lf, lc, chain_ptr(x, lf, c), chain_ptr(f, lf, c), chain_ptr(fc, lc, c),
+                                     chain_ptr(xc, lc, c), zero_xc, s, 1);
+        return;
+    }
     if (lf.field) {  // r = f - A x into the level's scratch, then fc = R r (and x_c = 0)
         dim3 block(64, 4, 1);
         dim3 grid = grid3(lf.L.nx - 1, lf.L.ny - 1, lf.spec.dim == 3 ? lf.L.nz - 1 : 1, block);
@@ -593,16 +647,16 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
     if (lf.spec.dim == 3 && zero_xc && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8) {
         const bool small = lc.L.nx < 32;
         if (lf.spec.npoints == 7) {
-            if (small) launch_zresrestrict_t<7, 16, 4, 64>(lf, lc, x, f, fc, xc, s);
+            if (small) launch_zresrestrict_t<7, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch);
             // 64 x 8 coarse points, 512 threads, 80 KB of LDS (2 workgroups per CU): half the y halo
             // of 64 x 4 (19 x planes rows per 16 fine rows instead of 11 per 8); 512^3 with kz 32:
             // 505-525 -> 488-502 us (interleaved A/B); at 256^3 too few tiles (73 against 66 us)
             else if ((long long)((lc.L.nx + 62) / 64) * ((lc.L.ny + 6) / 8) * (lc.L.nz - 1) >= 16 * 1024)
-                launch_zresrestrict_t<7, 64, 8, 512>(lf, lc, x, f, fc, xc, s);
-            else launch_zresrestrict_t<7, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
+                launch_zresrestrict_t<7, 64, 8, 512>(lf, lc, x, f, fc, xc, s, nch);
+            else launch_zresrestrict_t<7, 64, 4, 256>(lf, lc, x, f, fc, xc, s, nch);
         } else {
-            if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s);
-            else launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s);
+            if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch);
+            else launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s, nch);
         }
         return;
     }
@@ -619,13 +673,16 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
         hipLaunchKernelGGL((k_residual_restrict<2, 9>), grid, block, 0, s, lf.L, lc.L, x, f, fc, xc, lf.S, zero_xc);
 }
 
-void launch_prolongate(const Level& lf, const Level& lc, double* x, const double* xc, double alpha, hipStream_t s) {
+void launch_prolongate(const Level& lf, const Level& lc, double* x, const double* xc, double alpha, hipStream_t s,
+                       int nch = 1) {
     dim3 block(64, 4, 1);
-    dim3 grid = grid3(lf.L.nx / 2, lf.L.ny - 1, lf.spec.dim == 3 ? lf.L.nz - 1 : 1, block);
+    const int zper = lf.spec.dim == 3 ? lf.L.nz - 1 : 1;  // batched chains: blockIdx.z = chain * zper + plane
+    dim3 grid = grid3(lf.L.nx / 2, lf.L.ny - 1, zper * nch, block);
+    const long long csf = lf.L.nstore, csc = lc.L.nstore;
     if (lf.spec.dim == 3)
-        hipLaunchKernelGGL((k_prolongate_pairs<3>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha);
+        hipLaunchKernelGGL((k_prolongate_pairs<3>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha, zper, csf, csc);
     else
-        hipLaunchKernelGGL((k_prolongate_pairs<2>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha);
+        hipLaunchKernelGGL((k_prolongate_pairs<2>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha, zper, csf, csc);
 }
 
 void launch_pack(const Level& lv, const double* lex, double* pad, bool pack, hipStream_t s) {
@@ -646,18 +703,20 @@ void launch_pack(const Level& lv, const double* lex, double* pad, bool pack, hip
 
 // ---- low-rank part (mgmc_lowrank.hpp) ----
 // w = (sc_k B_k)^T v for all columns
-void lr_dots(const Level& lv, const double* v, const double* sc, hipStream_t s) {
+// (batched chains: v cs apart; the partials nblk and w m apart per chain)
+void lr_dots(const Level& lv, const double* v, const double* sc, hipStream_t s, int nch = 1) {
     const LowRankDev& r = lv.lr;
     if (r.nblk > 0)
-        hipLaunchKernelGGL(k_lr_partials, dim3(r.nblk), dim3(64), 0, s, lv.L, (const LRColMeta*)r.meta,
+        hipLaunchKernelGGL(k_lr_partials, dim3(r.nblk, nch), dim3(64), 0, s, lv.L, (const LRColMeta*)r.meta,
                            (const int*)r.blk_col, (const long long*)r.ent_off, (const double*)r.ent_val,
-                           (const double*)r.dense_val, sc, v, r.part);
-    hipLaunchKernelGGL(k_lr_totals, dim3(r.m), dim3(64), 0, s, (const LRColMeta*)r.meta, (const double*)r.part, r.w);
+                           (const double*)r.dense_val, sc, v, r.part, (long long)lv.L.nstore, r.nblk);
+    hipLaunchKernelGGL(k_lr_totals, dim3(r.m, 1, nch), dim3(64), 0, s, (const LRColMeta*)r.meta, (const double*)r.part,
+                       r.w, r.nblk, r.m);
 }
 
 // patch y on the rows of B (LR_PATCH_NOISE: y += B Sigma^{-1/2} xi'; RESIDUAL: y -= B w; APPLY: y += B w)
 void lr_patch(const mgmc_handle* h, const Level& lv, int mode, double* y, uint32_t tag, const uint64_t* sample,
-              hipStream_t s) {
+              hipStream_t s, int nch = 1) {
     const LowRankDev& r = lv.lr;
     if (r.nrows == 0) return;
     LRPatchArgs a;
@@ -674,26 +733,89 @@ void lr_patch(const mgmc_handle* h, const Level& lv, int mode, double* y, uint32
     a.y = y;
     a.save = r.save;
     a.mode = mode;
-    hipLaunchKernelGGL(k_lr_patch, dim3((r.nrows + 255) / 256), dim3(256), 0, s, a);
+    a.cs = lv.L.nstore;
+    a.chain0 = (uint32_t)h->chain;
+    a.seed_hi = (uint32_t)(h->seed >> 32);
+    hipLaunchKernelGGL(k_lr_patch, dim3((r.nrows + 255) / 256, 1, nch), dim3(256), 0, s, a);
+}
+
+// the right-hand side a low-rank level's sweep (LR_PATCH_NOISE: f + B Sigma^{-1/2} xi') or
+// residual (LR_PATCH_RESIDUAL: f - B t, t = r.w) reads; returns the vector to read.  Dense-column
+// path: written to r.fe, f untouched; otherwise f is patched in place (saved for lr_restore).
+// LR_PATCH_APPLY: f += B t in place on either path.
+double* lr_rhs(const mgmc_handle* h, const Level& lv, int mode, double* f, uint32_t tag, const uint64_t* sample,
+               hipStream_t s, int nch = 1) {
+    const LowRankDev& r = lv.lr;
+    if (!r.dense_path) {
+        lr_patch(h, lv, mode, f, tag, sample, s, nch);
+        return f;
+    }
+    LRDenseArgs a;
+    a.m = r.m;
+    a.g = r.dense_g;
+    a.mode = mode;
+    a.nch = nch;
+    a.cs = lv.L.nstore;
+    a.chain0 = (uint32_t)h->chain;
+    a.seed_hi = (uint32_t)(h->seed >> 32);
+    a.key = h->key;
+    a.tag = tag;
+    a.sample = sample;
+    a.sq = r.sq;
+    a.t = r.w;
+    a.f = f;
+    a.out = mode == LR_PATCH_APPLY ? f : r.fe;
+    a.nrows = r.nrows;
+    a.nbs = (r.nrows + LRD_NT - 1) / LRD_NT;
+    a.off = r.rows_off;
+    a.coef = r.rows_coef;
+    a.mask = r.rows_mask;
+    a.n = lv.L.nstore;
+    a.skip = r.skip_b;
+    a.bg = r.dense_val;  // the only dense column
+    const long long nbd = (a.n + LRD_ELEMS - 1) / LRD_ELEMS;
+    hipLaunchKernelGGL(k_lr_dense_rhs, dim3((unsigned)(a.nbs + nbd)), dim3(LRD_NT), 0, s, a);
+    return a.out;
 }
 
 // after a sweep in `direction`: x -= B_bar (B^T x) (sor_smoother.cc:47-51); restores f_restore
-// on the rows of B when the sweep ran on a noise-patched f
-void lr_fix(const Level& lv, double* x, int direction, double* f_restore, hipStream_t s) {
+// on the rows of B when the sweep ran on a noise-patched f (not on the dense-column path, whose
+// sweeps read r.fe)
+void lr_fix(const Level& lv, double* x, int direction, double* f_restore, hipStream_t s, int nch = 1) {
     const LowRankDev& r = lv.lr;
-    lr_dots(lv, x, r.sc_one, s);
+    lr_dots(lv, x, r.sc_one, s, nch);
     const int d = direction == MGMC_FORWARD ? 0 : 1;
+    if (r.dense_path) {
+        LRDenseUpdateArgs a;
+        a.m = r.m;
+        a.g = r.dense_g;
+        a.nch = nch;
+        a.cs = lv.L.nstore;
+        a.w = r.w;
+        a.x = x;
+        a.nbar = r.nbar[d];
+        a.nbs = (r.nbar[d] + LRD_NT - 1) / LRD_NT;
+        a.bar_off = r.bar_off[d];
+        a.bar_val = r.bar_val[d];
+        a.n = lv.L.nstore;
+        a.skip = r.skip_y[d];
+        a.yg = r.yg[d];
+        a.minv_g = r.minv_g[d];
+        const long long nbd = (a.n + LRD_ELEMS - 1) / LRD_ELEMS;
+        hipLaunchKernelGGL(k_lr_dense_update, dim3((unsigned)(a.nbs + nbd)), dim3(LRD_NT), 0, s, a);
+        return;
+    }
     const int nrest = f_restore ? r.nrows : 0;
     const int n = std::max(r.nbar[d], nrest);
     if (n == 0) return;
     hipLaunchKernelGGL(k_lr_update, dim3((n + 255) / 256), dim3(256), 0, s, r.m, r.nbar[d],
                        (const long long*)r.bar_off[d], (const double*)r.bar_val[d], (const double*)r.w, x, nrest,
-                       (const long long*)r.rows_off, (const double*)r.save, f_restore);
+                       (const long long*)r.rows_off, (const double*)r.save, f_restore, nch, (long long)lv.L.nstore);
 }
 
 // the fused between-sweeps kernel (k_lr_small): fix x, restore f, patch f for the next op
 void lr_small(const mgmc_handle* h, const Level& lv, double* x, int direction, int next, uint32_t next_tag,
-              const uint64_t* sample, hipStream_t s) {
+              const uint64_t* sample, hipStream_t s, int nch = 1) {
     const LowRankDev& r = lv.lr;
     const int d = direction == MGMC_FORWARD ? 0 : 1;
     LRSmallArgs a;
@@ -719,11 +841,14 @@ void lr_small(const mgmc_handle* h, const Level& lv, double* x, int direction, i
     a.key = h->key;
     a.tag = next_tag;
     a.sample = sample;
+    a.cs = lv.L.nstore;  // batched chains: one workgroup per chain
+    a.chain0 = (uint32_t)h->chain;
+    a.seed_hi = (uint32_t)(h->seed >> 32);
     // k_lr_small_pf: one entry per lane, <= 8 columns, <= 2 rows of B_bar and of B per thread
     if (r.m <= 8 && r.max_col_n <= 64 && a.nbar <= 2048 && a.nrows <= 2048 && !(lv.paths & PATH_NO_LR_PREFETCH))
-        hipLaunchKernelGGL((k_lr_small_pf<8, 2>), dim3(1), dim3(1024), 0, s, a);
+        hipLaunchKernelGGL((k_lr_small_pf<8, 2>), dim3(nch), dim3(1024), 0, s, a);
     else
-        hipLaunchKernelGGL(k_lr_small, dim3(1), dim3(1024), 0, s, a);
+        hipLaunchKernelGGL(k_lr_small, dim3(nch), dim3(1024), 0, s, a);
 }
 
 LRJob lr_job(const Level& lv, int restore, int noise, uint32_t tag) {
@@ -746,7 +871,7 @@ LRJob lr_job(const Level& lv, int restore, int noise, uint32_t tag) {
 // after a residual + restriction of a low-rank level: restore f (+ the patch of the first
 // post-sweep) and the coarse level's first pre-sweep patch in one launch (k_lr_restore_patch)
 void lr_restore_patch(const mgmc_handle* h, const Op& op, const Level& lv, const Level& lc, const uint64_t* sample,
-                      hipStream_t s) {
+                      hipStream_t s, int nch = 1) {
     LRRestorePatchArgs a;
     a.job[0] = lr_job(lv, 1, op.lr_post_patch, op.lr_post_tag);
     a.job[1] = op.lr_coarse_patch ? lr_job(lc, 0, 1, op.lr_coarse_tag) : lr_job(lc, 0, 0, 0);
@@ -755,14 +880,18 @@ void lr_restore_patch(const mgmc_handle* h, const Op& op, const Level& lv, const
     const int nb = a.nb0 + (a.job[1].nrows + 255) / 256;
     a.key = h->key;
     a.sample = sample;
-    if (nb > 0) hipLaunchKernelGGL(k_lr_restore_patch, dim3(nb), dim3(256), 0, s, a);
+    a.cs[0] = lv.L.nstore;
+    a.cs[1] = lc.L.nstore;
+    a.chain0 = (uint32_t)h->chain;
+    a.seed_hi = (uint32_t)(h->seed >> 32);
+    if (nb > 0) hipLaunchKernelGGL(k_lr_restore_patch, dim3(nb, 1, nch), dim3(256), 0, s, a);
 }
 
-void lr_restore(const Level& lv, double* f, hipStream_t s) {
+void lr_restore(const Level& lv, double* f, hipStream_t s, int nch = 1) {
     const LowRankDev& r = lv.lr;
-    if (r.nrows == 0) return;
-    hipLaunchKernelGGL(k_lr_restore, dim3((r.nrows + 255) / 256), dim3(256), 0, s, r.nrows,
-                       (const long long*)r.rows_off, (const double*)r.save, f);
+    if (r.nrows == 0 || r.dense_path) return;  // dense-column path: f was never patched
+    hipLaunchKernelGGL(k_lr_restore, dim3((r.nrows + 255) / 256, 1, nch), dim3(256), 0, s, r.nrows,
+                       (const long long*)r.rows_off, (const double*)r.save, f, (long long)lv.L.nstore);
 }
 
 // y = Q x on a level (LinearOperator::apply, linear_operator.hh:66-76)
@@ -784,13 +913,13 @@ void launch_operator_apply(const mgmc_handle* h, const Level& lv, const double* 
         hipLaunchKernelGGL((k_operator_apply<2, 9>), grid, block, 0, s, lv.L, xs, ys, lv.S);
     if (lv.lr.m > 0) {  // y += B (Sigma^{-1} B^T x)  (linear_operator.hh:71-75)
         lr_dots(lv, xs, lv.lr.sc_inv, s);
-        lr_patch(h, lv, LR_PATCH_APPLY, ys, 0, h->ctrl + 3, s);
+        lr_rhs(h, lv, LR_PATCH_APPLY, ys, 0, h->ctrl + 3, s);
     }
 }
 
 // coarsest level: x = G f (+ U xi) with the dense Cholesky factors (mgmc_cholesky.hpp)
 void launch_coarse_chol(const mgmc_handle* h, const Level& lv, const double* f, double* x, bool noise, uint32_t tag,
-                        const uint64_t* sample, hipStream_t s) {
+                        const uint64_t* sample, hipStream_t s, int nch = 1) {
     CholArgs a;
     a.L = lv.L;
     a.n = h->chol_n;
@@ -802,7 +931,10 @@ void launch_coarse_chol(const mgmc_handle* h, const Level& lv, const double* f, 
     a.key = h->key;
     a.tag = tag;
     a.sample = sample;
-    const dim3 grid((unsigned)((a.n + 255) / 256)), block(256);
+    a.cs = lv.L.nstore;
+    a.chain0 = (uint32_t)h->chain;
+    a.seed_hi = (uint32_t)(h->seed >> 32);
+    const dim3 grid((unsigned)((a.n + 255) / 256), 1, nch), block(256);
     const size_t lds = 2 * (size_t)a.n * sizeof(double);
     if (lv.spec.dim == 3)
         hipLaunchKernelGGL(k_coarse_chol<3>, grid, block, lds, s, a);
@@ -937,10 +1069,12 @@ void build_ops(mgmc_handle* h) {
         for (size_t q = 0; q < h->ops.size(); ++q) {
             Op& op = h->ops[q];
             const int l = op.level;
-            if (op.kind != OP_RESIDUAL_RESTRICT || h->levels[l].lr.m == 0) continue;
+            // (not on dense-column levels: their patches write lr.fe, f is never patched or restored)
+            if (op.kind != OP_RESIDUAL_RESTRICT || h->levels[l].lr.m == 0 || h->levels[l].lr.dense_path) continue;
             if (q + 1 < h->ops.size()) {
                 Op& nx = h->ops[q + 1];
-                if (nx.kind == OP_SWEEP && nx.level == l + 1 && h->levels[l + 1].lr.m > 0 && !nx.lr_skip_patch) {
+                if (nx.kind == OP_SWEEP && nx.level == l + 1 && h->levels[l + 1].lr.m > 0 &&
+                    !h->levels[l + 1].lr.dense_path && !nx.lr_skip_patch) {
                     op.lr_coarse_patch = 1;
                     op.lr_coarse_tag = nx.tag;
                     nx.lr_skip_patch = 1;
@@ -1112,6 +1246,9 @@ int build_tails(mgmc_handle* h) {
         A.xg = h->levels[lt].x;
         A.fg = h->levels[lt].f;
         A.Lg = h->levels[lt].L;
+        A.cs = h->levels[lt].L.nstore;  // batched chains: one workgroup per chain
+        A.chain0 = (uint32_t)h->chain;
+        A.seed_hi = (uint32_t)(h->seed >> 32);
         TailArgs* d = nullptr;
         HIPCHK(h, hipMalloc(&d, sizeof(TailArgs)));
         HIPCHK(h, hipMemcpy(d, &A, sizeof(TailArgs), hipMemcpyHostToDevice));
@@ -1133,6 +1270,7 @@ int build_tails(mgmc_handle* h) {
 
 void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
     const uint64_t* sample = h->ctrl;  // ctrl[0]
+    const int nch = h->nchains;        // batched chains: every launch covers all of them
     for (size_t q = begin; q < end; ++q) {
         const Op& op = h->ops[q];
         Level& lv = h->levels[op.level];
@@ -1140,73 +1278,77 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
             case OP_SWEEP: {
                 GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
                 const bool lr = lv.lr.m > 0;
-                if (lr && !op.lr_skip_patch) lr_patch(h, lv, LR_PATCH_NOISE, lv.f, op.tag, sample, s);
+                double* fs = lv.f;  // the right-hand side the sweep reads
+                if (lr && !op.lr_skip_patch) fs = lr_rhs(h, lv, LR_PATCH_NOISE, lv.f, op.tag, sample, s, nch);
                 double* xo = lv.x;
                 if (lv.zsweep) {
                     const Level* lc = op.prolong ? &h->levels[op.level + 1] : nullptr;
                     xo = lv.buf(1 - op.src);
-                    launch_zsweep(lv, lv.buf(op.src), xo, lv.f, g, op.direction, lc, lc ? lc->x : nullptr,
-                                  h->cfg.coarse_scaling, s);
+                    launch_zsweep(lv, lv.buf(op.src), xo, fs, g, op.direction, lc, lc ? lc->x : nullptr,
+                                  h->cfg.coarse_scaling, s, nch);
                 } else if (lv.quads) {
                     xo = lv.buf(1 - op.src);
-                    launch_quads(lv, lv.buf(op.src), xo, lv.f, g, op.direction, s);
+                    launch_quads(lv, lv.buf(op.src), xo, fs, g, op.direction, s, nch);
                 } else if (lv.rb2d) {
                     xo = lv.buf(1 - op.src);
-                    launch_rb2d(lv, lv.buf(op.src), xo, lv.f, g, op.direction, true, s);
+                    launch_rb2d(lv, lv.buf(op.src), xo, fs, g, op.direction, true, s, nch);
                 } else if (lv.pairs) {
-                    launch_pairs(lv, lv.x, lv.f, g, op.direction, s);
+                    launch_pairs(lv, lv.x, fs, g, op.direction, s, nch);
                 } else {
-                    launch_sweep(lv, lv.x, lv.f, g, op.direction, true, s);
+                    launch_sweep(lv, lv.x, fs, g, op.direction, true, s, nch);
                 }
                 if (lr && lv.lr.small)
-                    lr_small(h, lv, xo, op.direction, op.lr_next, op.lr_next_tag, sample, s);
+                    lr_small(h, lv, xo, op.direction, op.lr_next, op.lr_next_tag, sample, s, nch);
                 else if (lr)
-                    lr_fix(lv, xo, op.direction, lv.f, s);
+                    lr_fix(lv, xo, op.direction, lv.lr.dense_path ? nullptr : lv.f, s, nch);
                 break;
             }
             case OP_COARSE_CHOL: {
-                launch_coarse_chol(h, lv, lv.f, lv.x, true, op.tag, sample, s);
+                launch_coarse_chol(h, lv, lv.f, lv.x, true, op.tag, sample, s, nch);
                 break;
             }
             case OP_COARSE_LDS: {
                 GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
-                launch_coarse_lds(lv, g, op.nsweeps, s);
+                launch_coarse_lds(lv, g, op.nsweeps, s, nch);
                 break;
             }
             case OP_RESIDUAL_RESTRICT: {
                 Level& lc = h->levels[op.level + 1];
                 const bool lr = lv.lr.m > 0;
+                double* fr = lv.f;
                 if (lr && !op.lr_skip_patch) {  // r = (f - B Sigma^{-1} B^T x) - A x
-                    lr_dots(lv, lv.buf(op.src), lv.lr.sc_inv, s);
-                    lr_patch(h, lv, LR_PATCH_RESIDUAL, lv.f, 0, sample, s);
+                    lr_dots(lv, lv.buf(op.src), lv.lr.sc_inv, s, nch);
+                    fr = lr_rhs(h, lv, LR_PATCH_RESIDUAL, lv.f, 0, sample, s, nch);
                 }
-                launch_residual_restrict(lv, lc, lv.buf(op.src), lv.f, lc.f, lc.x, 1, s);
+                launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch);
                 if (lr && (op.lr_post_patch || op.lr_coarse_patch))
-                    lr_restore_patch(h, op, lv, lc, sample, s);
+                    lr_restore_patch(h, op, lv, lc, sample, s, nch);
                 else if (lr)
-                    lr_restore(lv, lv.f, s);
+                    lr_restore(lv, lv.f, s, nch);
                 break;
             }
             case OP_PROLONGATE: {
                 Level& lc = h->levels[op.level + 1];
-                launch_prolongate(lv, lc, lv.buf(op.src), lc.x, h->cfg.coarse_scaling, s);
+                launch_prolongate(lv, lc, lv.buf(op.src), lc.x, h->cfg.coarse_scaling, s, nch);
                 break;
             }
-            case OP_COPY: {
-                hipMemcpyAsync(lv.x, lv.buf(op.src), lv.L.nstore * sizeof(double), hipMemcpyDeviceToDevice, s);
+            case OP_COPY: {  // the chains' copies are contiguous
+                hipMemcpyAsync(lv.x, lv.buf(op.src), (size_t)nch * lv.L.nstore * sizeof(double),
+                               hipMemcpyDeviceToDevice, s);
                 break;
             }
-            case OP_TAIL: {
+            case OP_TAIL: {  // one workgroup per chain
                 const size_t lds = h->tail_lds[op.tail];
                 if (lv.spec.dim == 3)
-                    hipLaunchKernelGGL(k_tail<3>, dim3(1), dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
+                    hipLaunchKernelGGL(k_tail<3>, dim3(nch), dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
                 else
-                    hipLaunchKernelGGL(k_tail<2>, dim3(1), dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
+                    hipLaunchKernelGGL(k_tail<2>, dim3(nch), dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
                 break;
             }
             case OP_QOI: {
-                hipLaunchKernelGGL(k_qoi_record, dim3(1), dim3(64), 0, s, (const double*)h->levels[0].x, h->ctrl,
-                                   h->series, h->series_cap, h->mom);
+                hipLaunchKernelGGL(k_qoi_record, dim3(1), dim3(64 * ((nch + 63) / 64)), 0, s,
+                                   (const double*)h->levels[0].x, h->ctrl, h->series, h->series_cap, h->mom, nch,
+                                   (long long)h->levels[0].L.nstore);
                 break;
             }
         }
@@ -1296,7 +1438,7 @@ int ensure_series(mgmc_handle* h, uint64_t needed) {
     uint64_t cap = std::max<uint64_t>(needed, 2 * h->series_cap);
     double* p = nullptr;
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    HIPCHK(h, hipMalloc(&p, cap * sizeof(double)));
+    HIPCHK(h, hipMalloc(&p, cap * h->nchains * sizeof(double)));  // chain c's series c * cap on
     if (h->series) HIPCHK(h, hipFree(h->series));
     h->series = p;
     h->series_cap = cap;
@@ -1520,9 +1662,11 @@ int mgmc_describe(const mgmc_config* cfg, mgmc_level_desc* out, int max_levels) 
 // mgmc_create / mgmc_create_csr: csr = the fine operator's matrix (null: the constant-coefficient
 // hierarchy of cfg), every level then built from matrices
 static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, uint64_t seed, uint64_t chain_id,
-                       mgmc_handle** out) {
+                       int nchains, mgmc_handle** out) {
     if (!cfg || !out) return fail(nullptr, MGMC_E_INVALID, "null argument");
     *out = nullptr;
+    if (nchains < 1 || nchains > LR_MAX_CH)
+        return fail(nullptr, MGMC_E_INVALID, "nchains must be in [1, " + std::to_string(LR_MAX_CH) + "]");
     const std::string err = validate_config(*cfg);
     if (!err.empty()) return fail(nullptr, MGMC_E_INVALID, err);
     std::vector<CsrHost> mats;  // per level (matrix path)
@@ -1550,6 +1694,7 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
     h->device = device;
     h->seed = seed;
     h->chain = chain_id;
+    h->nchains = nchains;
     h->key = make_key(seed, chain_id);
     int ncu = 0;  // per handle: concurrent mgmc_create calls share no mutable state
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
@@ -1589,13 +1734,14 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
                            h->field_mode && (fields[l].scheme == 9 || fields[l].scheme == 27));
         memcpy(lv.S.a, specs[l].st, sizeof(lv.S.a));
         const size_t bytes = lv.L.nstore * sizeof(double);
-        if (hipMalloc(&lv.x, bytes) != hipSuccess || hipMalloc(&lv.f, bytes) != hipSuccess) {
+        const size_t cbytes = bytes * nchains;  // x, x2, f of every chain, L.nstore apart
+        if (hipMalloc(&lv.x, cbytes) != hipSuccess || hipMalloc(&lv.f, cbytes) != hipSuccess) {
             h->levels.push_back(lv);
             h->last_error = "device allocation failed";
             return bail(MGMC_E_NOMEM);
         }
-        hipMemsetAsync(lv.x, 0, bytes, h->stream);
-        hipMemsetAsync(lv.f, 0, bytes, h->stream);
+        hipMemsetAsync(lv.x, 0, cbytes, h->stream);
+        hipMemsetAsync(lv.f, 0, cbytes, h->stream);
         if (h->field_mode) {  // per-vertex coefficients and a residual scratch
             const FieldHost& fh = fields[l];
             lv.field = true;
@@ -1630,17 +1776,18 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
                   !(h->paths & PATH_NO_RB2D);
         lv.quads = lv.pairs && quads_eligible(lv.spec, lv.L, h->paths) && (tail0 < 0 || (int)l < tail0);
         if (lv.pingpong()) {
-            if (hipMalloc(&lv.x2, bytes) != hipSuccess) {
+            if (hipMalloc(&lv.x2, cbytes) != hipSuccess) {
                 h->levels.push_back(lv);
                 h->last_error = "device allocation failed";
                 return bail(MGMC_E_NOMEM);
             }
-            hipMemsetAsync(lv.x2, 0, bytes, h->stream);
+            hipMemsetAsync(lv.x2, 0, cbytes, h->stream);
         }
         if (!lv.field && l + 1 == specs.size() && 2 * bytes <= lds_limit) lv.lds_bytes = 2 * bytes;
         h->levels.push_back(lv);
     }
-    if (hipMalloc(&h->ctrl, 8 * sizeof(uint64_t)) != hipSuccess || hipMalloc(&h->mom, 4 * sizeof(double)) != hipSuccess) {
+    if (hipMalloc(&h->ctrl, 8 * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&h->mom, 4 * sizeof(double) * nchains) != hipSuccess) {
         h->last_error = "device allocation failed";
         return bail(MGMC_E_NOMEM);
     }
@@ -1649,7 +1796,7 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
     const long long probe = l0.L.at(l0.L.nx / 2, l0.L.ny / 2, cfg->dim == 3 ? l0.L.nz / 2 : 0);
     uint64_t ctrl0[8] = {0, 0, (uint64_t)(int64_t)-1, 0, 0, 0, (uint64_t)probe, 0};
     hipMemcpyAsync(h->ctrl, ctrl0, sizeof(ctrl0), hipMemcpyHostToDevice, h->stream);
-    hipMemsetAsync(h->mom, 0, 4 * sizeof(double), h->stream);
+    hipMemsetAsync(h->mom, 0, 4 * sizeof(double) * nchains, h->stream);
     if (cfg->coarse_solver == MGMC_COARSE_CHOLESKY && (rc = build_coarse_chol(h, nullptr, nullptr, 0)) != MGMC_OK)
         return bail(rc);
     // op sequence of one sample
@@ -1672,11 +1819,24 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
 }
 
 int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chain_id, mgmc_handle** out) {
-    return create_impl(cfg, nullptr, device, seed, chain_id, out);
+    return create_impl(cfg, nullptr, device, seed, chain_id, 1, out);
 }
+
+int mgmc_create_batch(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chain0, int nchains,
+                      mgmc_handle** out) {
+    return create_impl(cfg, nullptr, device, seed, chain0, nchains, out);
+}
+
+int mgmc_nchains(const mgmc_handle* h) { return h ? h->nchains : fail(nullptr, MGMC_E_INVALID, "null handle"); }
 
 int mgmc_create_csr(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr, const int32_t* col,
                     const double* val, int device, uint64_t seed, uint64_t chain_id, mgmc_handle** out) {
+    return mgmc_create_csr_batch(cfg, nrow, rowptr, col, val, device, seed, chain_id, 1, out);
+}
+
+int mgmc_create_csr_batch(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr, const int32_t* col,
+                          const double* val, int device, uint64_t seed, uint64_t chain0, int nchains,
+                          mgmc_handle** out) {
     if (!cfg || !rowptr || !col || !val || !out || nrow < 1) return fail(nullptr, MGMC_E_INVALID, "null argument");
     if (rowptr[0] != 0 || rowptr[nrow] < nrow) return fail(nullptr, MGMC_E_INVALID, "mgmc_create_csr: invalid row pointer");
     mgmc_config c = *cfg;  // the matrix replaces kappa^2 and the fine-operator choice
@@ -1687,7 +1847,7 @@ int mgmc_create_csr(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr,
     A.rowptr.assign(rowptr, rowptr + nrow + 1);
     A.col.assign(col, col + rowptr[nrow]);
     A.val.assign(val, val + rowptr[nrow]);
-    return create_impl(&c, &A, device, seed, chain_id, out);
+    return create_impl(&c, &A, device, seed, chain0, nchains, out);
 }
 
 int mgmc_operator_csr_size(const mgmc_operator_desc* d, int64_t* nrow, int64_t* nnz) {
@@ -1753,33 +1913,52 @@ int mgmc_level_desc_get(const mgmc_handle* h, int level, mgmc_level_desc* out) {
     return MGMC_OK;
 }
 
-int mgmc_set_rhs(mgmc_handle* h, const double* f, size_t n) {
-    if (!h || !f) return fail(h, MGMC_E_INVALID, "null argument");
-    if (n != h->levels[0].spec.ndof) return fail(h, MGMC_E_INVALID, "rhs size mismatch");
+// fine-level vector v of chain c (c < 0: every chain gets the upload of chain 0)
+static int put_fine(mgmc_handle* h, double* v, int c, const double* host, size_t n, const char* what) {
+    if (!h || !host) return fail(h, MGMC_E_INVALID, "null argument");
+    if (n != h->levels[0].spec.ndof) return fail(h, MGMC_E_INVALID, std::string(what) + " size mismatch");
+    if (c >= h->nchains) return fail(h, MGMC_E_INVALID, "chain index out of range");
     HIPCHK(h, hipSetDevice(h->device));
-    int rc = upload(h, 0, f, h->levels[0].f);
+    const size_t ns = h->levels[0].L.nstore;
+    int rc = upload(h, 0, host, v + (size_t)std::max(c, 0) * ns);
+    if (rc) return rc;
+    if (c < 0)
+        for (int q = 1; q < h->nchains; ++q)
+            HIPCHK(h, hipMemcpyAsync(v + q * ns, v, ns * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    return MGMC_OK;
+}
+
+int mgmc_set_rhs(mgmc_handle* h, const double* f, size_t n) {
+    int rc = put_fine(h, h ? h->levels[0].f : nullptr, -1, f, n, "rhs");
     if (rc) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return MGMC_OK;
 }
 
-int mgmc_set_state(mgmc_handle* h, const double* x, size_t n) {
-    if (!h || !x) return fail(h, MGMC_E_INVALID, "null argument");
-    if (n != h->levels[0].spec.ndof) return fail(h, MGMC_E_INVALID, "state size mismatch");
-    HIPCHK(h, hipSetDevice(h->device));
-    int rc = upload(h, 0, x, h->levels[0].x);
+static int set_state_impl(mgmc_handle* h, int c, const double* x, size_t n) {
+    int rc = put_fine(h, h ? h->levels[0].x : nullptr, c, x, n, "state");
     if (rc) return rc;
     HIPCHK(h, hipMemsetAsync(h->ctrl + 5, 0, sizeof(uint64_t), h->stream));  // a new state: guard cleared
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return MGMC_OK;
 }
 
-int mgmc_get_state(mgmc_handle* h, double* x, size_t n) {
+int mgmc_set_state(mgmc_handle* h, const double* x, size_t n) { return set_state_impl(h, -1, x, n); }
+
+int mgmc_set_state_chain(mgmc_handle* h, int chain, const double* x, size_t n) {
+    if (chain < 0) return fail(h, MGMC_E_INVALID, "chain index out of range");
+    return set_state_impl(h, chain, x, n);
+}
+
+int mgmc_get_state_chain(mgmc_handle* h, int chain, double* x, size_t n) {
     if (!h || !x) return fail(h, MGMC_E_INVALID, "null argument");
     if (n != h->levels[0].spec.ndof) return fail(h, MGMC_E_INVALID, "state size mismatch");
+    if (chain < 0 || chain >= h->nchains) return fail(h, MGMC_E_INVALID, "chain index out of range");
     HIPCHK(h, hipSetDevice(h->device));
-    return download(h, 0, h->levels[0].x, x);
+    return download(h, 0, h->levels[0].x + (size_t)chain * h->levels[0].L.nstore, x);
 }
+
+int mgmc_get_state(mgmc_handle* h, double* x, size_t n) { return mgmc_get_state_chain(h, 0, x, n); }
 
 // the device-side non-finite guard (ctrl[5], set by k_qoi_record): MGMC_E_NONFINITE with the sample
 // index and the watched vertex, instead of a chain that silently carries NaN / Inf
@@ -1855,11 +2034,14 @@ int mgmc_sample(mgmc_handle* h, int nsteps, int64_t qoi_index, double* qoi_out) 
     return check_finite(h);
 }
 
-int mgmc_qoi_moments(mgmc_handle* h, double out[3]) {
+int mgmc_qoi_moments(mgmc_handle* h, double out[3]) { return mgmc_qoi_moments_chain(h, 0, out); }
+
+int mgmc_qoi_moments_chain(mgmc_handle* h, int chain, double out[3]) {
     if (!h || !out) return fail(h, MGMC_E_INVALID, "null argument");
+    if (chain < 0 || chain >= h->nchains) return fail(h, MGMC_E_INVALID, "chain index out of range");
     HIPCHK(h, hipSetDevice(h->device));
     double m[4];
-    HIPCHK(h, hipMemcpyAsync(m, h->mom, sizeof(m), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(m, h->mom + 4 * chain, sizeof(m), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     out[0] = m[0];
     out[1] = m[1];
@@ -1870,7 +2052,7 @@ int mgmc_qoi_moments(mgmc_handle* h, double out[3]) {
 int mgmc_reset_moments(mgmc_handle* h) {
     if (!h) return fail(nullptr, MGMC_E_INVALID, "null handle");
     HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipMemsetAsync(h->mom, 0, 4 * sizeof(double), h->stream));
+    HIPCHK(h, hipMemsetAsync(h->mom, 0, 4 * sizeof(double) * h->nchains, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return MGMC_OK;
 }
@@ -1883,11 +2065,16 @@ int mgmc_set_sample_index(mgmc_handle* h, uint64_t index) {
     return MGMC_OK;
 }
 
-int mgmc_get_series(mgmc_handle* h, double* out, size_t n) {
+int mgmc_get_series(mgmc_handle* h, double* out, size_t n) { return mgmc_get_series_chain(h, 0, out, n); }
+
+int mgmc_get_series_chain(mgmc_handle* h, int chain, double* out, size_t n) {
     if (!h || (!out && n > 0)) return fail(h, MGMC_E_INVALID, "null argument");
     if (n > h->series_cap) return fail(h, MGMC_E_INVALID, "more values than the series holds");
+    if (chain < 0 || chain >= h->nchains) return fail(h, MGMC_E_INVALID, "chain index out of range");
     HIPCHK(h, hipSetDevice(h->device));
-    if (n > 0) HIPCHK(h, hipMemcpyAsync(out, h->series, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    if (n > 0)
+        HIPCHK(h, hipMemcpyAsync(out, h->series + (size_t)chain * h->series_cap, n * sizeof(double),
+                                 hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return MGMC_OK;
 }
@@ -1937,23 +2124,23 @@ static int sweep_component(mgmc_handle* h, int level, int direction, int nsweeps
     int cur = 1;
     for (int s = 0; s < nsweeps; ++s) {
         GibbsArg g = make_gibbs(h, lv, tag + (uint32_t)s, 0, h->ctrl + 3);
-        if (lr && noise) lr_patch(h, lv, LR_PATCH_NOISE, lv.scratch[0], tag + (uint32_t)s, h->ctrl + 3, h->stream);
+        double* fb = lv.scratch[0];
+        if (lr && noise) fb = lr_rhs(h, lv, LR_PATCH_NOISE, lv.scratch[0], tag + (uint32_t)s, h->ctrl + 3, h->stream);
         if (noise && lv.zsweep) {  // the fused z-marching kernel of the V-cycle (out of place)
-            launch_zsweep(lv, lv.scratch[cur], lv.scratch[3 - cur], lv.scratch[0], g, direction, nullptr, nullptr, 0.0,
-                          h->stream);
+            launch_zsweep(lv, lv.scratch[cur], lv.scratch[3 - cur], fb, g, direction, nullptr, nullptr, 0.0, h->stream);
             cur = 3 - cur;
         } else if (noise && lv.quads) {  // two colour pairs per launch (out of place)
-            launch_quads(lv, lv.scratch[cur], lv.scratch[3 - cur], lv.scratch[0], g, direction, h->stream);
+            launch_quads(lv, lv.scratch[cur], lv.scratch[3 - cur], fb, g, direction, h->stream);
             cur = 3 - cur;
         } else if (noise && lv.rb2d) {  // one-launch 2D red-black sweep (out of place)
-            launch_rb2d(lv, lv.scratch[cur], lv.scratch[3 - cur], lv.scratch[0], g, direction, true, h->stream);
+            launch_rb2d(lv, lv.scratch[cur], lv.scratch[3 - cur], fb, g, direction, true, h->stream);
             cur = 3 - cur;
         } else if (noise && lv.pairs) {  // the colour-pair passes of the V-cycle (in place)
-            launch_pairs(lv, lv.scratch[cur], lv.scratch[0], g, direction, h->stream);
+            launch_pairs(lv, lv.scratch[cur], fb, g, direction, h->stream);
         } else {
-            launch_sweep(lv, lv.scratch[cur], lv.scratch[0], g, direction, noise, h->stream);
+            launch_sweep(lv, lv.scratch[cur], fb, g, direction, noise, h->stream);
         }
-        if (lr) lr_fix(lv, lv.scratch[cur], direction, noise ? lv.scratch[0] : nullptr, h->stream);
+        if (lr) lr_fix(lv, lv.scratch[cur], direction, noise && fb == lv.scratch[0] ? lv.scratch[0] : nullptr, h->stream);
     }
     HIPCHK(h, hipGetLastError());
     return download(h, level, lv.scratch[cur], x);
@@ -2014,11 +2201,12 @@ int mgmc_residual_restrict(mgmc_handle* h, int level, const double* f, const dou
     Level& lc = h->levels[level + 1];
     if ((rc = upload(h, level, f, lf.scratch[0]))) return rc;
     if ((rc = upload(h, level, x, lf.scratch[1]))) return rc;
+    double* fr = lf.scratch[0];
     if (lf.lr.m > 0) {  // f - B Sigma^{-1} B^T x, then the residual kernel
         lr_dots(lf, lf.scratch[1], lf.lr.sc_inv, h->stream);
-        lr_patch(h, lf, LR_PATCH_RESIDUAL, lf.scratch[0], 0, h->ctrl + 3, h->stream);
+        fr = lr_rhs(h, lf, LR_PATCH_RESIDUAL, lf.scratch[0], 0, h->ctrl + 3, h->stream);
     }
-    launch_residual_restrict(lf, lc, lf.scratch[1], lf.scratch[0], lc.scratch[0], lc.scratch[1], 1, h->stream);
+    launch_residual_restrict(lf, lc, lf.scratch[1], fr, lc.scratch[0], lc.scratch[1], 1, h->stream);
     HIPCHK(h, hipGetLastError());
     return download(h, level + 1, lc.scratch[0], fc);
 }
@@ -2156,11 +2344,12 @@ void mg_precond(mgmc_handle* h, int level, double* x, double* f, hipStream_t s) 
             sweep(MGMC_FORWARD);
             if (c.smoother == MGMC_SMOOTHER_SSOR) sweep(MGMC_BACKWARD);
         }
+        double* fr = f;
         if (lv.lr.m > 0) {
             lr_dots(lv, x, lv.lr.sc_inv, s);
-            lr_patch(h, lv, LR_PATCH_RESIDUAL, f, 0, h->ctrl + 3, s);
+            fr = lr_rhs(h, lv, LR_PATCH_RESIDUAL, f, 0, h->ctrl + 3, s);
         }
-        launch_residual_restrict(lv, lc, x, f, lc.scratch[1], lc.scratch[0], 1, s);  // zeroes x_{l+1}
+        launch_residual_restrict(lv, lc, x, fr, lc.scratch[1], lc.scratch[0], 1, s);  // zeroes x_{l+1}
         if (lv.lr.m > 0) lr_restore(lv, f, s);
         mg_precond(h, level + 1, lc.scratch[0], lc.scratch[1], s);
         launch_prolongate(lv, lc, x, lc.scratch[0], c.coarse_scaling, s);
@@ -2389,10 +2578,37 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
             HIPCHK(h, hipStreamSynchronize(h->stream));
         }
     }
-    // rows of B (ascending), with the row's coefficients of every column
+    // dense-column path: exactly one dense column (mgmc_lowrank.hpp k_lr_dense_*)
+    r.dense_path = ndense == 1 && !(h->paths & PATH_NO_LR_DENSE);
+    r.dense_g = -1;
+    for (int k = 0; k < m; ++k)
+        if (cols[k].dense) r.dense_g = k;
+    const int g = r.dense_path ? r.dense_g : -1;
+    // bit p of a skip mask over the padded store: set unless p is an interior vertex of `dense_only`
+    auto skip_mask = [&](const std::vector<char>& local, uint32_t** dst) {
+        std::vector<uint32_t> words((size_t)(lv.L.nstore + 31) / 32, 0xFFFFFFFFu);
+        for (long long i = 0; i < N; ++i)
+            if (!local[i]) {
+                const long long p = ref_to_padded(lv, i);
+                words[p >> 5] &= ~(1u << (p & 31));
+            }
+        return lr_to_device(h, r, dst, words);
+    };
+    // rows of B (ascending), with the row's coefficients of every column (dense-column path: the
+    // rows with an entry in a column other than g)
     std::vector<int> slot(N, -1);
-    for (const auto& c : cols)
-        for (const auto& e : c.ent) slot[e.first] = 0;
+    for (int k = 0; k < m; ++k)
+        if (k != g)
+            for (const auto& e : cols[k].ent) slot[e.first] = 0;
+    if (g >= 0) {
+        std::vector<char> local(N);
+        for (long long i = 0; i < N; ++i) local[i] = slot[i] == 0;
+        if ((rc = skip_mask(local, &r.skip_b))) return rc;
+        const size_t fb = (size_t)lv.L.nstore * h->nchains * sizeof(double);
+        if (hipMalloc(&r.fe, fb) != hipSuccess) return fail(h, MGMC_E_NOMEM, "device allocation failed");
+        r.allocs.push_back(r.fe);
+        HIPCHK(h, hipMemsetAsync(r.fe, 0, fb, h->stream));
+    }
     int nrows = 0;
     std::vector<long long> rows_off;
     std::vector<int> t_rows_off;
@@ -2407,11 +2623,13 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
     for (int k = 0; k < m; ++k)
         for (const auto& e : cols[k].ent) {
             const int u = slot[e.first];
+            if (u < 0) continue;  // a dense-only row (dense-column path)
             coef[(size_t)u * m + k] = e.second;
             mask[u] |= 1ull << k;
         }
     r.nrows = nrows;
-    std::vector<double> sc_one(m, 1.0), sc_inv(m), sq(m), zeros(std::max(nrows, 1), 0.0);
+    // per-chain scratch of a batch: saved f (nrows), dot partials (nblk) and dots (m) per chain
+    std::vector<double> sc_one(m, 1.0), sc_inv(m), sq(m), zeros((size_t)std::max(nrows, 1) * h->nchains, 0.0);
     for (int k = 0; k < m; ++k) {
         sc_inv[k] = 1.0 / sigma[k];
         sq[k] = sqrt(1.0 / sigma[k]);  // Sigma^{-1/2} (sor_sampler.cc:30-33)
@@ -2421,7 +2639,7 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
         (rc = lr_to_device(h, r, &r.sc_one, sc_one)) || (rc = lr_to_device(h, r, &r.sc_inv, sc_inv)) ||
         (rc = lr_to_device(h, r, &r.sq, sq)) || (rc = lr_to_device(h, r, &r.t_rows_off, t_rows_off)))
         return rc;
-    std::vector<double> partz(std::max(r.nblk, 1), 0.0), wz(m, 0.0);
+    std::vector<double> partz((size_t)std::max(r.nblk, 1) * h->nchains, 0.0), wz((size_t)m * h->nchains, 0.0);
     if ((rc = lr_to_device(h, r, &r.part, partz)) || (rc = lr_to_device(h, r, &r.w, wz))) return rc;
 
     // B_bar for the forward and backward splittings
@@ -2451,11 +2669,32 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
         std::vector<long long> boff;
         std::vector<int> t_boff;
         std::vector<double> bval;
+        r.nbar_all[d] = 0;
+        if (g >= 0) {  // dense-only rows: Y_il = 0 for every l != g; Y_g and row g of Minv on the device
+            std::vector<char> local(N);
+            for (long long i = 0; i < N; ++i) {
+                const double* yi = &Y[(size_t)i * m];
+                bool loc = false;
+                for (int l = 0; l < m; ++l) loc = loc || (l != g && yi[l] != 0.0);
+                local[i] = loc;
+                col[i] = yi[g];
+                if (!loc && yi[g] != 0.0) ++r.nbar_all[d];
+            }
+            if ((rc = skip_mask(local, &r.skip_y[d]))) return rc;
+            const size_t yb = (size_t)lv.L.nstore * sizeof(double);
+            if (hipMalloc(&r.yg[d], yb) != hipSuccess) return fail(h, MGMC_E_NOMEM, "device allocation failed");
+            r.allocs.push_back(r.yg[d]);
+            HIPCHK(h, hipMemsetAsync(r.yg[d], 0, yb, h->stream));
+            if ((rc = upload(h, level, col.data(), r.yg[d]))) return rc;
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            std::vector<double> mg(Minv.begin() + (size_t)g * m, Minv.begin() + (size_t)(g + 1) * m);
+            if ((rc = lr_to_device(h, r, &r.minv_g[d], mg))) return rc;
+        }
         for (long long i = 0; i < N; ++i) {
             const double* yi = &Y[(size_t)i * m];
             bool nz = false;
-            for (int l = 0; l < m; ++l) nz = nz || yi[l] != 0.0;
-            if (!nz) continue;  // B_bar row is exactly zero: x - 0 = x
+            for (int l = 0; l < m; ++l) nz = nz || ((g < 0 || l != g) && yi[l] != 0.0);
+            if (!nz) continue;  // B_bar row is exactly zero: x - 0 = x (dense-column path: a dense-only row)
             boff.push_back(ref_to_padded(lv, i));
             t_boff.push_back(ref_to_tail(lv, i));
             for (int k = 0; k < m; ++k) {
@@ -2465,6 +2704,7 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
             }
         }
         r.nbar[d] = (int)boff.size();
+        r.nbar_all[d] += r.nbar[d];
         if ((rc = lr_to_device(h, r, &r.bar_off[d], boff)) || (rc = lr_to_device(h, r, &r.bar_val[d], bval)) ||
             (rc = lr_to_device(h, r, &r.t_bar_off[d], t_boff)))
             return rc;
@@ -2535,7 +2775,7 @@ int mgmc_lowrank_info(const mgmc_handle* h, int level, int direction, int* m, in
     if (direction != MGMC_FORWARD && direction != MGMC_BACKWARD) return fail(nullptr, MGMC_E_INVALID, "invalid direction");
     const LowRankDev& r = h->levels[level].lr;
     *m = r.m;
-    *nrows_bbar = r.nbar[direction == MGMC_FORWARD ? 0 : 1];
+    *nrows_bbar = r.nbar_all[direction == MGMC_FORWARD ? 0 : 1];  // local + dense-only rows
     return MGMC_OK;
 }
 
@@ -2567,18 +2807,29 @@ int mgmc_comm_init(mgmc_handle* h, int nranks, int rank, const unsigned char id_
     h->nranks = nranks;
     h->rank = rank;
     if (h->comm_buf) HIPCHK(h, hipFree(h->comm_buf));
-    HIPCHK(h, hipMalloc(&h->comm_buf, (size_t)(4 * nranks + 4) * sizeof(double)));
+    HIPCHK(h, hipMalloc(&h->comm_buf, (size_t)(4 * nranks + 4) * h->nchains * sizeof(double)));
     return MGMC_OK;
 }
 
 int mgmc_comm_allgather_moments(mgmc_handle* h, double* out) {
     if (!h || !out) return fail(h, MGMC_E_INVALID, "null argument");
     HIPCHK(h, hipSetDevice(h->device));
-    if (!h->comm) return mgmc_qoi_moments(h, out);  // single chain
-    double* send = h->comm_buf + 4 * h->nranks;
-    HIPCHK(h, hipMemcpyAsync(send, h->mom, 3 * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
-    NCCLCHK(h, ncclAllGather(send, h->comm_buf, 3, ncclDouble, h->comm, h->stream));
-    HIPCHK(h, hipMemcpyAsync(out, h->comm_buf, 3 * h->nranks * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    const int nch = h->nchains;
+    if (!h->comm) {  // one rank: this handle's chains
+        for (int c = 0; c < nch; ++c) {
+            int rc = mgmc_qoi_moments_chain(h, c, out + 3 * c);
+            if (rc) return rc;
+        }
+        return MGMC_OK;
+    }
+    // (count, mean, M2) of every chain packed to 3 doubles (the device moments are 4 apart), one
+    // all-gather of 3 * nchains doubles per rank
+    double* send = h->comm_buf + (size_t)4 * h->nranks * nch;
+    HIPCHK(h, hipMemcpy2DAsync(send, 3 * sizeof(double), h->mom, 4 * sizeof(double), 3 * sizeof(double), nch,
+                               hipMemcpyDeviceToDevice, h->stream));
+    NCCLCHK(h, ncclAllGather(send, h->comm_buf, 3 * nch, ncclDouble, h->comm, h->stream));
+    HIPCHK(h, hipMemcpyAsync(out, h->comm_buf, (size_t)3 * h->nranks * nch * sizeof(double), hipMemcpyDeviceToHost,
+                             h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return MGMC_OK;
 }

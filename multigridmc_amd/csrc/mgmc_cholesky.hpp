@@ -34,6 +34,8 @@ struct CholArgs {
     RngKey key;
     uint32_t tag;
     const uint64_t* sample;
+    long long cs;               // batched chains (blockIdx.z): doubles between chains of f and x
+    uint32_t chain0, seed_hi;   // chain c's Philox key: (key.k0, lo32(chain0 + c) ^ seed_hi)
 };
 
 template <int DIM>
@@ -47,6 +49,12 @@ __device__ __forceinline__ long long chol_vertex(const Layout& L, int e, int* i,
 
 template <int DIM>
 __global__ void __launch_bounds__(256) k_coarse_chol(CholArgs a) {
+    {
+        const int ch = (int)blockIdx.z;
+        a.f += ch * a.cs;
+        a.x += ch * a.cs;
+        if (ch) a.key.k1 = (a.chain0 + (uint32_t)ch) ^ a.seed_hi;
+    }
     extern __shared__ double sh[];
     double* fl = sh;
     double* xi = sh + a.n;

@@ -31,6 +31,7 @@ struct PairPassArgs {
     GibbsArg G;
     int jp, kp;        // row parities of the pass (kp unused in 2D)
     int rows_per_block, nrows_j, nrows;  // pass rows: j = 2 - jp + 2 t (t < nrows_j), k likewise
+    long long cs;      // batched chains: doubles between chains (blockIdx.z = chain)
 };
 
 // FIRST_ODD: the odd position (i parity 1) is updated first (backward sweeps).  A template parameter,
@@ -39,6 +40,12 @@ template <int DIM, bool FIRST_ODD>
 __global__ void __launch_bounds__(256) k_sweep_pairs(PairPassArgs a) {
     constexpr int NPTS = DIM == 3 ? 27 : 9;
     __shared__ double xnew[256 + 2];  // new first-colour values, [1 + tid]; zero guards at both ends
+    {
+        const int ch = batch_chain();
+        a.x += ch * a.cs;
+        a.f += ch * a.cs;
+        a.G.key = chain_key(a.G, ch);
+    }
     const Layout& L = a.L;
     const int npair = L.nx / 2;
     const int tid = threadIdx.x;
@@ -149,10 +156,19 @@ struct QuadPassArgs {
     int jp1, kp;        // row parity of the first pair (first colour's bit 1), plane parity (bit 2)
     int T;              // rows of parity jp2 per workgroup (2T+1 rows in all)
     int nblk_y;         // workgroups along j
+    long long cs;       // batched chains: doubles between chains (blockIdx.z = chain)
 };
 
 template <int DIM, bool FIRST_ODD>
 __global__ void __launch_bounds__(1024) k_sweep_quads(QuadPassArgs a) {
+    {
+        const int ch = batch_chain();
+        a.x0 += ch * a.cs;
+        a.xz += ch * a.cs;
+        a.xout += ch * a.cs;
+        a.f += ch * a.cs;
+        a.G.key = chain_key(a.G, ch);
+    }
     // T+1 thread rows of npair threads: thread row t runs the first pair on local row 2t (phase 1),
     // then the second pair on local row 2t+1 (phase 2, t < T)
     constexpr int NPTS = DIM == 3 ? 27 : 9;

@@ -67,11 +67,22 @@ struct GibbsArg {
     double omega;
     double sd;  // sqrt(diag*(2-omega)/omega)
     double wd;  // omega/diag
-    RngKey key;
+    RngKey key;  // chain 0 of a batched launch
     uint32_t tag;
     int colour;
     const uint64_t* sample;  // device word holding the sample index
+    uint32_t chain0, seed_hi;  // Philox key of chain c: (lo32(seed), lo32(chain0 + c) ^ hi32(seed))
 };
+
+// Batched chains (mgmc_create_batch): a handle's C chains share the hierarchy and run every kernel
+// of the cycle in one launch, chain c = blockIdx.z / zper of the launch (zper = blocks of the
+// kernel's own z dimension); chain c's vectors start c * stride doubles after chain 0's.
+__device__ __forceinline__ int batch_chain(int zper = 1) { return (int)blockIdx.z / zper; }
+__device__ __forceinline__ RngKey chain_key(const GibbsArg& G, int c) {
+    RngKey k = G.key;
+    if (c) k.k1 = (G.chain0 + (uint32_t)c) ^ G.seed_hi;
+    return k;
+}
 
 // ascending-column-order row sum  sum_k a_k x_k  starting from 0.0
 template <int DIM, int NPTS>
@@ -216,8 +227,14 @@ __device__ __forceinline__ int colour_of(int i, int j, int k) {
 template <int DIM, int NPTS, bool PRE>
 __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __restrict__ xg,
                                                           const double* __restrict__ fg, StencilArg S, GibbsArg G,
-                                                          int nsweeps, int ncolours) {
+                                                          int nsweeps, int ncolours, long long chs) {
     constexpr bool precompute = PRE;  // a template parameter: the colour passes carry no Philox code
+    {  // batched chains (blockIdx.z)
+        const int ch = batch_chain();
+        xg += ch * chs;
+        fg += ch * chs;
+        G.key = chain_key(G, ch);
+    }
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* xs = smem;
     double* fs = smem + L.nstore;
@@ -429,10 +446,14 @@ __global__ void __launch_bounds__(256) k_prolongate_add(Layout Lf, Layout Lc, do
 // as k_prolongate_add / the reference's scatter order. ----
 template <int DIM>
 __global__ void __launch_bounds__(256) k_prolongate_pairs(Layout Lf, Layout Lc, double* __restrict__ x,
-                                                          const double* __restrict__ xc, double alpha) {
+                                                          const double* __restrict__ xc, double alpha, int zper,
+                                                          long long csf, long long csc) {
+    const int ch = batch_chain(zper);  // batched chains: blockIdx.z = ch * zper + plane block
+    x += ch * csf;
+    xc += ch * csc;
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     const int j = blockIdx.y * blockDim.y + threadIdx.y + 1;
-    const int k = (DIM == 3) ? (int)blockIdx.z + 1 : 0;
+    const int k = (DIM == 3) ? (int)blockIdx.z - ch * zper + 1 : 0;
     const int i = 2 * q + 1;
     if (i > Lf.nx - 1 || j > Lf.ny - 1) return;
     const long long p = Lf.at(i, j, k);
@@ -515,23 +536,35 @@ __global__ void __launch_bounds__(256) k_unpack(Layout L, const double* __restri
 // ctrl[5] = non-finite guard (0, or 1 + the sample index at which the watched value first was NaN /
 // Inf), ctrl[6] = storage index watched when no QoI is recorded (the lattice centre)
 __global__ void k_qoi_record(const double* __restrict__ x, uint64_t* ctrl, double* series, uint64_t capacity,
-                             double* mom) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+                             double* mom, int nchains, long long cs) {
+    // thread c records chain c (series and moments chain c * capacity / c * 4 on); the control words
+    // are advanced once, after every chain has read them
+    __shared__ int bad;
+    const int c = threadIdx.x;
+    if (c == 0) bad = 0;
+    __syncthreads();
     const long long q = (long long)ctrl[2];
-    const double z = x[q >= 0 ? q : (long long)ctrl[6]];
-    if (!isfinite(z) && ctrl[5] == 0) ctrl[5] = ctrl[0] + 1;
-    if (q >= 0) {
-        const uint64_t n = ctrl[1];
-        if (n < capacity) series[n] = z;
-        ctrl[1] = n + 1;
-        const double cnt = mom[0] + 1.0;
-        const double delta = z - mom[1];
-        const double mean = mom[1] + delta / cnt;
-        mom[2] = mom[2] + delta * (z - mean);
-        mom[1] = mean;
-        mom[0] = cnt;
+    const uint64_t n = ctrl[1], s0 = ctrl[0];
+    if (c < nchains) {
+        const double z = x[(long long)c * cs + (q >= 0 ? q : (long long)ctrl[6])];
+        if (!isfinite(z)) bad = 1;
+        if (q >= 0) {
+            double* m = mom + 4 * c;
+            if (n < capacity) series[(long long)c * capacity + n] = z;
+            const double cnt = m[0] + 1.0;
+            const double delta = z - m[1];
+            const double mean = m[1] + delta / cnt;
+            m[2] = m[2] + delta * (z - mean);
+            m[1] = mean;
+            m[0] = cnt;
+        }
     }
-    ctrl[0] = ctrl[0] + 1;
+    __syncthreads();
+    if (c == 0) {
+        if (bad && ctrl[5] == 0) ctrl[5] = s0 + 1;
+        if (q >= 0) ctrl[1] = n + 1;
+        ctrl[0] = s0 + 1;
+    }
 }
 
 // ---- normals for the RNG parity test ----

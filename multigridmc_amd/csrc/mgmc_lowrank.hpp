@@ -55,49 +55,92 @@ struct LRColMeta {
 };
 
 // ---- dot products, stage 1: one wavefront per block of LR_BLK entries ----
+// Batched chains: blockIdx.y = chain (v cs apart, the partials nblk apart).  A dense column lists
+// every vertex in reference order: lane l's entries e, e + 64, ... are walked with incremental
+// (i, j, k) (no 64-bit division per entry).  The lane's sum runs in entry order; the entries are
+// taken LRP_U at a time with their loads issued together (the coarse levels' dots are a handful of
+// wavefronts, each a chain of up to 64 dependent global round trips otherwise).
+constexpr int LRP_U = 8;
 __global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRColMeta* __restrict__ meta,
                                                      const int* __restrict__ blk_col,
                                                      const long long* __restrict__ ent_off,
                                                      const double* __restrict__ ent_val,
                                                      const double* __restrict__ dense_val,
                                                      const double* __restrict__ sc, const double* __restrict__ v,
-                                                     double* __restrict__ part) {
+                                                     double* __restrict__ part, long long cs, int nblk) {
     const int b = blockIdx.x;
+    const int ch = blockIdx.y;
     const int lane = threadIdx.x;
     const int k = blk_col[b];
     const LRColMeta c = meta[k];
     const long long e0 = (long long)(b - c.blk0) * LR_BLK;
     const long long end = min(c.n, e0 + LR_BLK);
     const double s = sc[k];
+    const double* vc = v + ch * cs;
+    const long long e1 = e0 + lane;
+    const int cnt = e1 < end ? (int)((end - e1 + 63) / 64) : 0;  // entries of this lane
     double acc = 0.0;
     if (c.dense >= 0) {
         const double* dv = dense_val + (long long)c.dense * L.nstore;
-        const long long nxi = L.nx - 1, nyi = L.ny - 1;
-        for (long long e = e0 + lane; e < end; e += 64) {
-            const int i = (int)(e % nxi) + 1;
-            const long long r = e / nxi;
-            const int j = (int)(r % nyi) + 1;
-            const int kk = L.dim == 3 ? (int)(r / nyi) + 1 : 0;
-            const long long p = L.at(i, j, kk);
-            acc = acc + (s * dv[p]) * v[p];
+        const int nxi = L.nx - 1, nyi = L.ny - 1;
+        int i = (int)(e1 % nxi) + 1;
+        const long long r = e1 / nxi;
+        int j = (int)(r % nyi) + 1;
+        int kk = L.dim == 3 ? (int)(r / nyi) + 1 : 0;
+        for (int base = 0; base < cnt; base += LRP_U) {
+            long long p[LRP_U];
+            double a[LRP_U], x[LRP_U];
+#pragma unroll
+            for (int u = 0; u < LRP_U; ++u) {
+                p[u] = L.at(i, j, kk);
+                i += 64;  // advance by 64 entries (nxi may be < 64: carry repeatedly)
+                while (i > nxi) {
+                    i -= nxi;
+                    if (++j > nyi) {
+                        j = 1;
+                        ++kk;
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < LRP_U; ++u)
+                if (base + u < cnt) {
+                    a[u] = dv[p[u]];
+                    x[u] = vc[p[u]];
+                }
+#pragma unroll
+            for (int u = 0; u < LRP_U; ++u)
+                if (base + u < cnt) acc = acc + (s * a[u]) * x[u];
         }
     } else {
-        for (long long e = e0 + lane; e < end; e += 64) {
-            const long long q = c.ent0 + e;
-            acc = acc + (s * ent_val[q]) * v[ent_off[q]];
+        const long long q0 = c.ent0 + e1;
+        for (int base = 0; base < cnt; base += LRP_U) {
+            double a[LRP_U], x[LRP_U];
+#pragma unroll
+            for (int u = 0; u < LRP_U; ++u)
+                if (base + u < cnt) {
+                    const long long q = q0 + 64ll * (base + u);
+                    a[u] = ent_val[q];
+                    x[u] = vc[ent_off[q]];
+                }
+#pragma unroll
+            for (int u = 0; u < LRP_U; ++u)
+                if (base + u < cnt) acc = acc + (s * a[u]) * x[u];
         }
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
-    if (lane == 0) part[b] = acc;
+    if (lane == 0) part[(long long)ch * nblk + b] = acc;
 }
 
 // ---- dot products, stage 2: one wavefront per column ----
 __global__ void __launch_bounds__(64) k_lr_totals(const LRColMeta* __restrict__ meta, const double* __restrict__ part,
-                                                   double* __restrict__ out) {
+                                                   double* __restrict__ out, int nblk, int m) {
     const int k = blockIdx.x;
     const int lane = threadIdx.x;
     const LRColMeta c = meta[k];
+    part += (long long)blockIdx.z * nblk;  // batched chains (blockIdx.z): part nblk, out m apart
+    out += (long long)blockIdx.z * m;
     double acc = 0.0;
     for (int b = lane; b < c.nblk; b += 64) acc = acc + part[c.blk0 + b];
 #pragma unroll
@@ -124,9 +167,23 @@ struct LRPatchArgs {
     double* y;
     double* save;
     int mode;
+    long long cs;               // batched chains (blockIdx.z): y cs, save nrows, t m apart
+    uint32_t chain0, seed_hi;   // chain c's Philox key: (key.k0, lo32(chain0 + c) ^ seed_hi)
 };
 
+__device__ __forceinline__ RngKey lr_chain_key(RngKey key, uint32_t chain0, uint32_t seed_hi, int ch) {
+    if (ch) key.k1 = (chain0 + (uint32_t)ch) ^ seed_hi;
+    return key;
+}
+
 __global__ void __launch_bounds__(256) k_lr_patch(LRPatchArgs a) {
+    {
+        const int ch = batch_chain();
+        a.y += ch * a.cs;
+        a.save += (long long)ch * a.nrows;
+        if (a.t) a.t += ch * a.m;
+        a.key = lr_chain_key(a.key, a.chain0, a.seed_hi, ch);
+    }
     __shared__ double s[LR_MAX_M];
     if (a.mode == LR_PATCH_NOISE) {
         const int t = threadIdx.x;
@@ -157,28 +214,40 @@ __global__ void __launch_bounds__(256) k_lr_patch(LRPatchArgs a) {
 }
 
 // ---- smoother fix x -= B_bar w on B_bar's rows; optionally restore f on the rows of B ----
+// Batched chains: every row of B_bar is read once and applied to all nch chains (x, f cs apart, w m
+// apart, the saved f nrest apart) -- the (N x m) (m x C) product of the chain batch, each chain's
+// entry the single-chain fma chain over k ascending.
+constexpr int LR_MAX_CH = 16;  // chains of one batched handle (w of every chain in LDS)
 __global__ void __launch_bounds__(256) k_lr_update(int m, int nbar, const long long* __restrict__ bar_off,
                                                     const double* __restrict__ bar_val, const double* __restrict__ w,
                                                     double* __restrict__ x, int nrest,
                                                     const long long* __restrict__ rest_off,
-                                                    const double* __restrict__ rest_val, double* __restrict__ f) {
-    __shared__ double ws[LR_MAX_M];
-    if ((int)threadIdx.x < m) ws[threadIdx.x] = w[threadIdx.x];
+                                                    const double* __restrict__ rest_val, double* __restrict__ f,
+                                                    int nch, long long cs) {
+    __shared__ double ws[LR_MAX_CH * LR_MAX_M];
+    for (int q = threadIdx.x; q < nch * m; q += blockDim.x) ws[q] = w[q];
     __syncthreads();
     const int u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u < nbar) {
-        const double* bv = bar_val + (long long)u * m;
-        double acc = 0.0;
-        for (int k = 0; k < m; ++k) acc = fma(bv[k], ws[k], acc);
+        const double* bv = bar_val + (long long)u * m;  // from HBM once, then from L1 for chains 1..
         const long long p = bar_off[u];
-        x[p] = x[p] - acc;
+        for (int ch = 0; ch < nch; ++ch) {
+            double acc = 0.0;
+            for (int k = 0; k < m; ++k) acc = fma(bv[k], ws[ch * m + k], acc);
+            double* xc = x + ch * cs;
+            xc[p] = xc[p] - acc;
+        }
     }
-    if (u < nrest) f[rest_off[u]] = rest_val[u];
+    if (u < nrest)
+        for (int ch = 0; ch < nch; ++ch) f[ch * cs + rest_off[u]] = rest_val[(long long)ch * nrest + u];
 }
 
 // ---- restore f on the rows of B ----
 __global__ void __launch_bounds__(256) k_lr_restore(int n, const long long* __restrict__ off,
-                                                     const double* __restrict__ save, double* __restrict__ f) {
+                                                     const double* __restrict__ save, double* __restrict__ f,
+                                                     long long cs) {
+    save += (long long)blockIdx.z * n;  // batched chains (blockIdx.z)
+    f += blockIdx.z * cs;
     const int u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u < n) f[off[u]] = save[u];
 }
@@ -207,12 +276,18 @@ struct LRRestorePatchArgs {
     int nb0;
     RngKey key;
     const uint64_t* sample;
+    long long cs[2];            // batched chains (blockIdx.z): f of job 0 / 1 cs apart, save nrows apart
+    uint32_t chain0, seed_hi;
 };
 
 __global__ void __launch_bounds__(256) k_lr_restore_patch(LRRestorePatchArgs a) {
     __shared__ double s[LR_MAX_M];
     const bool second = (int)blockIdx.x >= a.nb0;
-    const LRJob& j = a.job[second ? 1 : 0];
+    const int ch = batch_chain();
+    a.key = lr_chain_key(a.key, a.chain0, a.seed_hi, ch);
+    LRJob j = a.job[second ? 1 : 0];
+    j.f += ch * a.cs[second ? 1 : 0];
+    j.save += (long long)ch * j.nrows;
     const int u = (second ? (int)blockIdx.x - a.nb0 : (int)blockIdx.x) * blockDim.x + threadIdx.x;
     if (j.noise) {
         const int t = threadIdx.x;
@@ -249,6 +324,189 @@ __global__ void __launch_bounds__(256) k_lr_restore_patch(LRRestorePatchArgs a) 
     j.f[p] = y + e;
 }
 
+// ---- dense-column path: one dense column g of B (the global average measurement) ----
+// A dense column makes every row a row of B and of B_bar, and the row lists above then cost
+// 8 (m + 2) bytes per vertex and launch.  But on every row where only column g of B (and of
+// Y = (L + D/omega)^{-1} B) is nonzero -- all rows except a few dozen around each point
+// measurement -- both are one number per vertex:
+//   * patch  e_i = 0.0 + B_ig s_g                (the row's mask holds only bit g)
+//   * B_bar  B_bar_ik = fma(Y_ig, Minv_gk, 0.0)   (the setup's fma chain over l, Y_il = 0 for l != g)
+// so those "dense-only" rows stream B_g / Y_g over the padded store (coalesced; bit p of `skip`
+// set = not a dense-only interior vertex) and only the remaining "local" rows keep the row lists
+// -- the same arithmetic, bit for bit.  The patched right-hand side goes to a separate vector
+// (out = f +/- e) which the level's sweep / residual reads: no saved copy, no restore.
+// Batched chains: every thread loops over the chains (f, out, x cs apart), B_g / Y_g and the row
+// lists are read once for all of them.
+// threads per block, 16-byte pairs of the padded store per thread (L.nstore and every chain / column
+// offset are multiples of 16 doubles), store entries per block
+constexpr int LRD_NT = 256, LRD_PER = 2, LRD_ELEMS = 2 * LRD_PER * LRD_NT;
+
+// the pairs of one thread: p[r] (even) clamped into [0, n), ok[r][h] = a dense-only vertex p + h
+__device__ __forceinline__ void lrd_pairs(const uint32_t* __restrict__ skip, long long n, int nbs, long long p[LRD_PER],
+                                          bool ok[LRD_PER][2]) {
+    const long long q0 = 2 * ((long long)((int)blockIdx.x - nbs) * (LRD_PER * LRD_NT) + threadIdx.x);
+#pragma unroll
+    for (int r = 0; r < LRD_PER; ++r) {
+        const long long q = q0 + 2ll * r * LRD_NT;
+        p[r] = q < n ? q : n - 2;
+        const uint32_t w = skip[p[r] >> 5] >> (p[r] & 31);  // p even: both bits in one word
+        ok[r][0] = q < n && !(w & 1);
+        ok[r][1] = q < n && !(w & 2);
+    }
+}
+
+struct LRDenseArgs {
+    int m, g, mode, nch;      // mode: LR_PATCH_NOISE / RESIDUAL (out = f -/+ e) / APPLY (out == f, +=)
+    long long cs;             // chain stride of f, out, x
+    uint32_t chain0, seed_hi;
+    RngKey key;
+    uint32_t tag;
+    const uint64_t* sample;
+    const double* sq;         // noise: sqrt(1 / Sigma_k)
+    const double* t;          // residual / apply: the m dots of every chain, m apart
+    const double* f;
+    double* out;
+    // local rows (blocks [0, nbs)): padded offsets, m coefficients, column masks
+    int nrows, nbs;
+    const long long* off;
+    const double* coef;
+    const uint64_t* mask;
+    // dense-only rows (blocks [nbs, ...)): padded range [0, n)
+    long long n;
+    const uint32_t* skip;
+    const double* bg;
+};
+
+__global__ void __launch_bounds__(LRD_NT) k_lr_dense_rhs(LRDenseArgs a) {
+    __shared__ double s[LR_MAX_CH * LR_MAX_M];
+    const bool local = (int)blockIdx.x < a.nbs;
+    const int m = a.m;
+    if (a.mode == LR_PATCH_NOISE) {
+        const int np = (m + 1) / 2;
+        const uint64_t sample = *a.sample;
+        for (int q = threadIdx.x; q < a.nch * np; q += LRD_NT) {
+            const int ch = q / np, pr = q - ch * np;
+            if (!local && pr != a.g / 2) continue;  // dense-only rows need s_g alone
+            const RngKey k = lr_chain_key(a.key, a.chain0, a.seed_hi, ch);
+            const Philox4 r = philox4x32_10(LR_PAIR0 + (uint32_t)pr, a.tag, (uint32_t)sample, (uint32_t)(sample >> 32),
+                                            k.k0, k.k1);
+            double z0, z1;
+            normal_pair(r, &z0, &z1);
+            s[ch * m + 2 * pr] = a.sq[2 * pr] * z0;
+            if (2 * pr + 1 < m) s[ch * m + 2 * pr + 1] = a.sq[2 * pr + 1] * z1;
+        }
+    } else {
+        for (int q = threadIdx.x; q < a.nch * m; q += LRD_NT) s[q] = a.t[q];
+    }
+    __syncthreads();
+    const bool minus = a.mode == LR_PATCH_RESIDUAL;
+    if (local) {
+        const int u = blockIdx.x * LRD_NT + threadIdx.x;
+        if (u >= a.nrows) return;
+        const long long p = a.off[u];
+        const uint64_t msk = a.mask[u];
+        const double* cf = a.coef + (long long)u * m;
+        for (int ch = 0; ch < a.nch; ++ch) {
+            double e = 0.0;
+            for (int k = 0; k < m; ++k)
+                if ((msk >> k) & 1) e = e + cf[k] * s[ch * m + k];
+            const double y = a.f[ch * a.cs + p];
+            a.out[ch * a.cs + p] = minus ? y - e : y + e;
+        }
+        return;
+    }
+    // 16-byte pairs, every load unconditional (p clamped into the store), the stores masked
+    long long p[LRD_PER];
+    bool ok[LRD_PER][2];
+    lrd_pairs(a.skip, a.n, a.nbs, p, ok);
+    double2 bv[LRD_PER];
+#pragma unroll
+    for (int r = 0; r < LRD_PER; ++r) bv[r] = *(const double2*)(a.bg + p[r]);
+    for (int ch = 0; ch < a.nch; ++ch) {
+        const double sg = s[ch * m + a.g];
+        const double* fc = a.f + ch * a.cs;
+        double* oc = a.out + ch * a.cs;
+        double2 y[LRD_PER];
+#pragma unroll
+        for (int r = 0; r < LRD_PER; ++r) y[r] = *(const double2*)(fc + p[r]);
+#pragma unroll
+        for (int r = 0; r < LRD_PER; ++r) {
+            const double e0 = 0.0 + bv[r].x * sg, e1 = 0.0 + bv[r].y * sg;
+            double2 o;
+            o.x = minus ? y[r].x - e0 : y[r].x + e0;
+            o.y = minus ? y[r].y - e1 : y[r].y + e1;
+            if (ok[r][0] && ok[r][1]) *(double2*)(oc + p[r]) = o;
+            else if (ok[r][0]) oc[p[r]] = o.x;
+            else if (ok[r][1]) oc[p[r] + 1] = o.y;
+        }
+    }
+}
+
+// smoother fix x -= B_bar w: local rows from the row list (blocks [0, nbs)), dense-only rows
+// with B_bar_ik = fma(Y_ig, Minv_gk, 0.0) recomputed on the fly
+struct LRDenseUpdateArgs {
+    int m, g, nch;
+    long long cs;
+    const double* w;          // the m dots of every chain, m apart
+    double* x;
+    int nbar, nbs;
+    const long long* bar_off;
+    const double* bar_val;
+    long long n;
+    const uint32_t* skip;
+    const double* yg;
+    const double* minv_g;     // row g of Minv
+};
+
+__global__ void __launch_bounds__(LRD_NT) k_lr_dense_update(LRDenseUpdateArgs a) {
+    __shared__ double ws[LR_MAX_CH * LR_MAX_M];
+    __shared__ double mg[LR_MAX_M];
+    const int m = a.m;
+    for (int q = threadIdx.x; q < a.nch * m; q += LRD_NT) ws[q] = a.w[q];
+    for (int q = threadIdx.x; q < m; q += LRD_NT) mg[q] = a.minv_g[q];
+    __syncthreads();
+    if ((int)blockIdx.x < a.nbs) {
+        const int u = blockIdx.x * LRD_NT + threadIdx.x;
+        if (u >= a.nbar) return;
+        const double* bv = a.bar_val + (long long)u * m;
+        const long long p = a.bar_off[u];
+        for (int ch = 0; ch < a.nch; ++ch) {
+            double acc = 0.0;
+            for (int k = 0; k < m; ++k) acc = fma(bv[k], ws[ch * m + k], acc);
+            double* xc = a.x + ch * a.cs;
+            xc[p] = xc[p] - acc;
+        }
+        return;
+    }
+    long long p[LRD_PER];
+    bool ok[LRD_PER][2];
+    lrd_pairs(a.skip, a.n, a.nbs, p, ok);
+    double2 yv[LRD_PER];
+#pragma unroll
+    for (int r = 0; r < LRD_PER; ++r) yv[r] = *(const double2*)(a.yg + p[r]);
+    for (int ch = 0; ch < a.nch; ++ch) {
+        double* xc = a.x + ch * a.cs;
+        double2 xv[LRD_PER];
+#pragma unroll
+        for (int r = 0; r < LRD_PER; ++r) xv[r] = *(const double2*)(xc + p[r]);
+#pragma unroll
+        for (int r = 0; r < LRD_PER; ++r) {
+            double acc0 = 0.0, acc1 = 0.0;
+            for (int k = 0; k < m; ++k) {
+                const double wk = ws[ch * m + k], mk = mg[k];
+                acc0 = fma(fma(yv[r].x, mk, 0.0), wk, acc0);
+                acc1 = fma(fma(yv[r].y, mk, 0.0), wk, acc1);
+            }
+            double2 o;
+            o.x = xv[r].x - acc0;
+            o.y = xv[r].y - acc1;
+            if (ok[r][0] && ok[r][1]) *(double2*)(xc + p[r]) = o;
+            else if (ok[r][0]) xc[p[r]] = o.x;
+            else if (ok[r][1]) xc[p[r] + 1] = o.y;
+        }
+    }
+}
+
 // ---- one workgroup for everything between two sweeps of a level with a small low-rank part ----
 // (every column sparse with <= LR_BLK entries, few B_bar rows): the fix after a sweep, the restore
 // of f, and the patch the next op of the level needs (noise of the next sweep, or the posterior
@@ -280,7 +538,17 @@ struct LRSmallArgs {
     RngKey key;
     uint32_t tag;  // sweep tag of the next sweep (LR_NEXT_NOISE)
     const uint64_t* sample;
+    long long cs;               // batched chains: one workgroup per chain, x / f cs apart, save nrows apart
+    uint32_t chain0, seed_hi;
 };
+
+__device__ __forceinline__ void lr_small_chain(LRSmallArgs& a) {
+    const int ch = blockIdx.x;
+    a.x += ch * a.cs;
+    a.f += ch * a.cs;
+    a.save += (long long)ch * a.nrows;
+    a.key = lr_chain_key(a.key, a.chain0, a.seed_hi, ch);
+}
 
 __device__ __forceinline__ double lr_wave_dot(const LRColMeta& c, const long long* __restrict__ ent_off,
                                               const double* __restrict__ ent_val, double sc,
@@ -299,6 +567,7 @@ __device__ __forceinline__ double lr_wave_dot(const LRColMeta& c, const long lon
 }
 
 __global__ void __launch_bounds__(1024) k_lr_small(LRSmallArgs a) {
+    lr_small_chain(a);
     __shared__ double ws[LR_MAX_M], ts[LR_MAX_M];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nwave = blockDim.x >> 6;
@@ -361,6 +630,7 @@ __global__ void __launch_bounds__(1024) k_lr_small(LRSmallArgs a) {
 // k ascending, the patch the masked mul+add chain.
 template <int M, int PR>
 __global__ void __launch_bounds__(1024) k_lr_small_pf(LRSmallArgs a) {
+    lr_small_chain(a);
     __shared__ double ws[LR_MAX_M], ts[LR_MAX_M];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int nt = blockDim.x;

@@ -27,7 +27,14 @@ __device__ __forceinline__ int rb2_lidx(int r, int c) { return r * RB2_W + (c & 
 template <bool NOISE>
 __global__ void __launch_bounds__(RB2_NT) k_rb2d(Layout L, const double* __restrict__ xin, double* __restrict__ xout,
                                               const double* __restrict__ f, StencilArg S, GibbsArg G, int c1,
-                                              int ntx) {
+                                              int ntx, long long chs) {
+    {  // batched chains (blockIdx.z)
+        const int ch = batch_chain();
+        xin += ch * chs;
+        xout += ch * chs;
+        f += ch * chs;
+        G.key = chain_key(G, ch);
+    }
     __shared__ double xs[RB2_H * RB2_W];
     __shared__ double cs[RB2_H * RB2_W];  // right hand sides c = fma(sd, xi, f) of the updated vertices
     const int tid = threadIdx.x;

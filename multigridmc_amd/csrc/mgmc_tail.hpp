@@ -74,6 +74,8 @@ struct TailArgs {
     double* xg;            // level lt in HBM (its padded layout Lg)
     const double* fg;
     Layout Lg;
+    long long cs;          // batched chains: doubles between chains of level lt (one workgroup per chain)
+    uint32_t chain0, seed_hi;  // chain c's Philox key: (key.k0, lo32(chain0 + c) ^ seed_hi)
     TailLevel lv[TAIL_MAX_LEVELS];
     TailOp ops[TAIL_MAX_OPS];
 };
@@ -87,6 +89,11 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
     for (int q = tid; q < ntot; q += nt) lds[q] = 0.0;
     __syncthreads();
     const uint64_t sample = *A->sample;
+    const int ch = blockIdx.x;  // batched chains: one workgroup per chain
+    double* const xg = A->xg + ch * A->cs;
+    const double* const fg = A->fg + ch * A->cs;
+    RngKey key = A->key;
+    if (ch) key.k1 = (A->chain0 + (uint32_t)ch) ^ A->seed_hi;
     const uint32_t s_lo = (uint32_t)sample, s_hi = (uint32_t)(sample >> 32);
     double* scr = lds + A->oscr;
 
@@ -146,8 +153,8 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
         for (int q = tid; q < nd; q += nt) {
             int i, j, k;
             coords(t0.G, q, i, j, k);
-            lds[t0.ox + (int)t0.G.at(i, j, k)] = A->xg[A->Lg.at(i, j, k)];
-            lds[t0.of + (int)t0.G.at(i, j, k)] = A->fg[A->Lg.at(i, j, k)];
+            lds[t0.ox + (int)t0.G.at(i, j, k)] = xg[A->Lg.at(i, j, k)];
+            lds[t0.of + (int)t0.G.at(i, j, k)] = fg[A->Lg.at(i, j, k)];
         }
     }
     __syncthreads();
@@ -159,7 +166,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
         double* f = lds + t.of;
         if (t.m > 0) {  // f += B Sigma^{-1/2} xi' (the sweep's m extra normals)
             if (2 * tid < t.m) {
-                const Philox4 r = philox4x32_10(LR_PAIR0 + (uint32_t)tid, tag, s_lo, s_hi, A->key.k0, A->key.k1);
+                const Philox4 r = philox4x32_10(LR_PAIR0 + (uint32_t)tid, tag, s_lo, s_hi, key.k0, key.k1);
                 double z0, z1;
                 normal_pair(r, &z0, &z1);
                 lr_s[2 * tid] = t.sq[2 * tid] * z0;
@@ -176,7 +183,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             const int j = row % (G.ny - 1) + 1, k = DIM == 3 ? row / (G.ny - 1) + 1 : 0;
             const int i0 = 2 * m + 1;
             if (i0 > G.nx - 1) continue;
-            const Philox4 rnd = philox4x32_10(pair_id<DIM>(G, i0, j, k), tag, s_lo, s_hi, A->key.k0, A->key.k1);
+            const Philox4 rnd = philox4x32_10(pair_id<DIM>(G, i0, j, k), tag, s_lo, s_hi, key.k0, key.k1);
             double z0, z1;
             normal_pair(rnd, &z0, &z1);
             const int p = (int)G.at(i0, j, k);
@@ -327,7 +334,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
         for (int q = tid; q < nd; q += nt) {
             int i, j, k;
             coords(t0.G, q, i, j, k);
-            A->xg[A->Lg.at(i, j, k)] = lds[t0.ox + (int)t0.G.at(i, j, k)];
+            xg[A->Lg.at(i, j, k)] = lds[t0.ox + (int)t0.G.at(i, j, k)];
         }
     }
 }

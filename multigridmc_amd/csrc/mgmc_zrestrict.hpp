@@ -32,6 +32,7 @@ struct ZRestrictArgs {
     StencilArg S;
     int kz;            // coarse planes per chunk
     int ntx, nty, ntz;
+    long long csf, csc;  // batched chains: doubles between chains on the fine / coarse level
 };
 
 template <int NPTS, int CX, int CY, int NT>
@@ -52,6 +53,13 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
     double* xs = smem;                 // [3][XR][XS] x planes k-1, k, k+1
     double* rs = xs + 3 * XPS;         // [RR][RSr] residual of plane k
 
+    {  // batched chains (blockIdx.z)
+        const int ch = batch_chain();
+        a.x += ch * a.csf;
+        a.f += ch * a.csf;
+        a.fc += ch * a.csc;
+        a.xc += ch * a.csc;
+    }
     const Layout& Lf = a.Lf;
     const Layout& Lc = a.Lc;
     const int nb = gridDim.x, b = blockIdx.x, per = nb >> 3;

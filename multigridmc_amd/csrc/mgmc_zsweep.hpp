@@ -50,6 +50,7 @@ struct ZSweepArgs {
     GibbsArg G;                // colour field = first colour (0 forward, 1 backward)
     int tz;                    // planes per z-chunk
     int ntx, nty, ntz;         // tile counts
+    long long cs, csc;         // batched chains: doubles between chains of the level / coarse level
 };
 
 // One pair item of a tile: LDS offset, plane-independent global offset, Philox pair base,
@@ -121,6 +122,14 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     constexpr int NLC = PROLONG ? (CR * CWP + NT - 1) / NT : 1;
     double* cring = tab + 322;
 
+    {  // batched chains: this launch's chain (blockIdx.z), its vectors and its Philox key
+        const int ch = batch_chain();
+        a.xin += ch * a.cs;
+        a.xout += ch * a.cs;
+        a.f += ch * a.cs;
+        if (PROLONG) a.xc += ch * a.csc;
+        a.G.key = chain_key(a.G, ch);
+    }
     const Layout& L = a.L;
     // XCD-aware tile order: blocks b and b+8 share an XCD, give them neighbouring tiles
     const int nb = gridDim.x;

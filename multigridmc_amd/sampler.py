@@ -293,10 +293,16 @@ class MultigridMCSampler:
     PCIe (like the reference's by-reference vectors), sample() runs the device-resident loop."""
 
     def __init__(self, linear_operator, seed: int, params: MultigridParameters,
-                 device: int = 0, chain_id: int = 0):
+                 device: int = 0, chain_id: int = 0, nchains: int = 1):
+        """nchains > 1: a batch of independent chains chain_id, chain_id + 1, ... in one handle
+        (mgmc_create_batch): every kernel of a cycle covers all of them, chain c draws exactly what a
+        one-chain sampler with chain_id + c draws.  set_state / fix_rhs set every chain, get_state,
+        sample and qoi_moments take a `chain` argument (default 0; chain=None in sample and get_state
+        returns all chains)."""
         self.linear_operator = linear_operator
         self.params = params
         self.seed, self.device, self.chain_id = int(seed), int(device), int(chain_id)
+        self.nchains = int(nchains)
         self.config = make_config(linear_operator, params)
         self.lib = load_library()
         h = ctypes.c_void_p()
@@ -304,13 +310,17 @@ class MultigridMCSampler:
         if getattr(base, "variable_coefficients", False):
             # per-vertex coefficients: the assembled matrix (A_sparse) and a Galerkin hierarchy of matrices
             rowptr, col, val = base.get_csr()
-            check(self.lib.mgmc_create_csr(ctypes.byref(self.config), len(rowptr) - 1,
-                                           rowptr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
-                                           col.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _dp(val), int(device),
-                                           int(seed) & (2**64 - 1), int(chain_id) & (2**64 - 1), ctypes.byref(h)))
-        else:
+            check(self.lib.mgmc_create_csr_batch(ctypes.byref(self.config), len(rowptr) - 1,
+                                                 rowptr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                                 col.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _dp(val),
+                                                 int(device), int(seed) & (2**64 - 1), int(chain_id) & (2**64 - 1),
+                                                 self.nchains, ctypes.byref(h)))
+        elif self.nchains == 1:
             check(self.lib.mgmc_create(ctypes.byref(self.config), int(device), int(seed) & (2**64 - 1),
                                        int(chain_id) & (2**64 - 1), ctypes.byref(h)))
+        else:
+            check(self.lib.mgmc_create_batch(ctypes.byref(self.config), int(device), int(seed) & (2**64 - 1),
+                                             int(chain_id) & (2**64 - 1), self.nchains, ctypes.byref(h)))
         self.handle = h
         self.ndof = linear_operator.get_ndof()
         self.nlevel = params.nlevel
@@ -403,19 +413,33 @@ class MultigridMCSampler:
         self._device_rhs = f
 
     # -- device-resident chain (driver_mgmc.cc:66-94) --
-    def set_state(self, x):
+    def set_state(self, x, chain=None):
+        """every chain (chain=None) or one chain of a batch"""
         x = _as_f64(x, self.ndof, "x")
-        self._chk(self.lib.mgmc_set_state(self.handle, _dp(x), self.ndof))
+        if chain is None:
+            self._chk(self.lib.mgmc_set_state(self.handle, _dp(x), self.ndof))
+        else:
+            self._chk(self.lib.mgmc_set_state_chain(self.handle, int(chain), _dp(x), self.ndof))
 
-    def get_state(self) -> np.ndarray:
+    def get_state(self, chain=0) -> np.ndarray:
+        """one chain's state; chain=None: an (nchains, ndof) array"""
+        if chain is None:
+            return np.stack([self.get_state(c) for c in range(self.nchains)])
         x = np.empty(self.ndof)
-        self._chk(self.lib.mgmc_get_state(self.handle, _dp(x), self.ndof))
+        self._chk(self.lib.mgmc_get_state_chain(self.handle, int(chain), _dp(x), self.ndof))
         return x
 
-    def sample(self, nsteps: int, qoi_index: int = -1) -> np.ndarray:
-        out = np.empty(max(nsteps, 0))
-        self._chk(self.lib.mgmc_sample(self.handle, int(nsteps), int(qoi_index), _dp(out) if qoi_index >= 0 else None))
-        return out
+    def sample(self, nsteps: int, qoi_index: int = -1, chain=0) -> np.ndarray:
+        """nsteps cycles of every chain; the QoI series of one chain (chain=None: (nchains, nsteps))"""
+        if chain == 0 or qoi_index < 0:
+            out = np.empty(max(nsteps, 0))
+            self._chk(self.lib.mgmc_sample(self.handle, int(nsteps), int(qoi_index),
+                                           _dp(out) if qoi_index >= 0 else None))
+            return out
+        self._chk(self.lib.mgmc_sample(self.handle, int(nsteps), int(qoi_index), None))
+        if chain is None:
+            return np.stack([self.get_series(nsteps, c) for c in range(self.nchains)])
+        return self.get_series(nsteps, chain)
 
     def sample_async(self, nsteps: int, qoi_index: int = -1):
         self._chk(self.lib.mgmc_sample_async(self.handle, int(nsteps), int(qoi_index)))
@@ -434,25 +458,26 @@ class MultigridMCSampler:
         return {"total_ms": tot.value, "pre_ms": pre.value, "npre": npre.value, "post_ms": post.value,
                 "npost": npost.value}
 
-    def qoi_moments(self):
+    def qoi_moments(self, chain: int = 0):
         out = np.zeros(3)
-        self._chk(self.lib.mgmc_qoi_moments(self.handle, _dp(out)))
+        self._chk(self.lib.mgmc_qoi_moments_chain(self.handle, int(chain), _dp(out)))
         return out
 
     def reset_moments(self):
         self._chk(self.lib.mgmc_reset_moments(self.handle))
 
-    def get_series(self, n: int) -> np.ndarray:
+    def get_series(self, n: int, chain: int = 0) -> np.ndarray:
         """The QoI series of the last sample / sample_async call (waits for this handle's stream)."""
         out = np.empty(max(int(n), 0))
-        self._chk(self.lib.mgmc_get_series(self.handle, _dp(out), out.size))
+        self._chk(self.lib.mgmc_get_series_chain(self.handle, int(chain), _dp(out), out.size))
         return out
 
     def clone(self) -> "MultigridMCSampler":
         """A second handle of the same chain: same operator, parameters, device and Philox key
         (seed, chain_id), its own state, right hand side and HIP stream.  With disjoint sample
         indices it reproduces the draws this handle would make there (batched chains)."""
-        c = MultigridMCSampler(self.linear_operator, self.seed, self.params, self.device, self.chain_id)
+        c = MultigridMCSampler(self.linear_operator, self.seed, self.params, self.device, self.chain_id,
+                               self.nchains)
         if self._device_rhs is not None:  # the same right hand side as this handle's device copy
             c.fix_rhs(self._device_rhs)
             if self._fixed_rhs is None:
@@ -532,7 +557,8 @@ class MultigridMCSampler:
         self._chk(self.lib.mgmc_comm_init(self.handle, int(nranks), int(rank), unique_id))
 
     def comm_allgather_moments(self, nranks: int) -> np.ndarray:
-        out = np.zeros(3 * max(nranks, 1))
+        """(count, mean, M2) of every chain of every rank: rows rank-major, nranks * nchains of them"""
+        out = np.zeros(3 * max(nranks, 1) * self.nchains)
         self._chk(self.lib.mgmc_comm_allgather_moments(self.handle, _dp(out)))
         return out.reshape(-1, 3)
 

@@ -176,13 +176,16 @@ def test_posterior_statistics_vs_exact_covariance(hip_device, shape, kw, glob, n
 
 @pytest.mark.parametrize("name,paths", [(n, "tail") for n in TAIL_CONFIGS] +
                          [(n, q) for n in ("3d32_points_tail_W", "2d32_point_global", "3d_aniso_zres_points")
-                          for q in ("lr_small", "lr_merge", "lr_prefetch", "lr_small,lr_merge,tail")])
+                          for q in ("lr_small", "lr_merge", "lr_prefetch", "lr_small,lr_merge,tail")] +
+                         [(n, "lr_dense") for n in ("2d32_point_global", "3d32_ball_global", "2d32_point_global_chol")])
 def test_lowrank_paths_match(hip_device, name, paths, monkeypatch):
     """Low-rank kernel paths switched off (MGMC_DISABLE): tail = the coarse levels' sub-cycle as
     separate launches instead of k_tail (low-rank patches, fix and residual in LDS); lr_small = the
     generic fix / patch / restore launches instead of the single-workgroup k_lr_small; lr_merge =
     separate restore and patch launches around the residual + restriction; lr_prefetch = k_lr_small
-    without its up-front loads.  QoI series and state bitwise against the oracle, on and off."""
+    without its up-front loads; lr_dense = the row lists over every vertex for a dense column (the
+    global average measurement) instead of streaming B_g / Y_g with the patched right-hand side in
+    a separate vector.  QoI series and state bitwise against the oracle, on and off."""
     out = []
     for env in (paths, None):
         if env:

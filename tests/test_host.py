@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in include/mgmc.h but not exported"
         assert s in bound, f"{s} not bound in multigridmc_amd/_native.py"
-    assert lib.mgmc_abi_version() == 3
+    assert lib.mgmc_abi_version() == 4
 
 
 def test_library_is_gfx950_code_object():
@@ -102,7 +102,7 @@ def test_product_reads_only_documented_switches():
             src += open(os.path.join(csrc, fn)).read()
     assert sorted(set(re.findall(r'getenv\("([A-Z_0-9]+)"\)', src))) == ["MGMC_DISABLE", "MGMC_GRAPH_UNROLL"]
     tokens = re.findall(r'\{"([a-z_0-9]+)", PATH_NO_', src)
-    assert len(tokens) == 11
+    assert len(tokens) == 12
     tested = open(os.path.join(ROOT, "tests", "test_gpu_parity.py")).read() + \
         open(os.path.join(ROOT, "tests", "test_gpu_lowrank.py")).read()
     for t in tokens:
@@ -260,7 +260,7 @@ def test_cpp_host_side_describe_and_loud_failure(tmp_path, asan):
     exe = build_client(tmp_path, asan=asan)
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
     out = subprocess.run([exe, "describe"], capture_output=True, text=True, check=True, env=env).stdout.split("\n")
-    assert out[0] == "abi 3"
+    assert out[0] == "abi 4"
     cfg_levels = mg.describe(mg.make_config(mg.ShiftedLaplaceFDOperator(mg.Lattice3d(64, 64, 64), 25.0),
                                             mg.MultigridParameters(nlevel=4)))
     for level, line in enumerate(out[1:5]):
@@ -299,8 +299,10 @@ class _FakeChain:
     def synchronize(self):
         pass
 
-    def qoi_moments(self):
-        return np.array([10.0 + self.rank, 0.5 * self.rank, 2.0])
+    nchains = 2
+
+    def qoi_moments(self, chain=0):
+        return np.array([10.0 + self.rank + chain, 0.5 * self.rank, 2.0])
 
     def comm_barrier(self):
         import torch.distributed as dist
@@ -315,8 +317,8 @@ class _FakeChain:
     def comm_allgather_moments(self, world):
         import torch.distributed as dist
         out = [None] * world
-        dist.all_gather_object(out, list(self.qoi_moments()))
-        return np.array(out)
+        dist.all_gather_object(out, [list(self.qoi_moments(c)) for c in range(self.nchains)])
+        return np.array(out).reshape(-1, 3)
 
 
 def _bench_coll_worker(rank, world, port, mode, q):
@@ -369,7 +371,8 @@ def test_bench_collectives_world2(mode):
             assert kind == ("gloo" if mode == "rehearsal" else "rccl")
             assert nranks == (0 if mode == "rehearsal" else 2)
             assert tmax == 2.0
-            assert parts == [[10.0, 0.0, 2.0], [11.0, 0.5, 2.0]]
+            # every chain of every rank, rank-major (2 chains per rank)
+            assert parts == [[10.0, 0.0, 2.0], [11.0, 0.0, 2.0], [11.0, 0.5, 2.0], [12.0, 0.5, 2.0]]
         else:
             err, msg = res[r][0], res[r][1]
             assert err == ("MgmcError" if mode == "init_fails" else "CommError"), (err, msg)
