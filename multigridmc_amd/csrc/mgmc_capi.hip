@@ -196,6 +196,7 @@ struct LowRankDev {
     double* yg[2] = {nullptr, nullptr};         // column g of Y (padded, per direction)
     double* minv_g[2] = {nullptr, nullptr};     // row g of Minv (per direction)
     double* fe = nullptr;
+    double* fe2 = nullptr;                      // ... of the first post-sweep, written with the residual's
     long long nbar_all[2] = {0, 0};             // B_bar rows in total (local + dense-only with Y_g != 0)
     std::vector<void*> allocs;
 };
@@ -707,9 +708,10 @@ void launch_pack(const Level& lv, const double* lex, double* pad, bool pack, hip
 void lr_dots(const Level& lv, const double* v, const double* sc, hipStream_t s, int nch = 1) {
     const LowRankDev& r = lv.lr;
     if (r.nblk > 0)
-        hipLaunchKernelGGL(k_lr_partials, dim3(r.nblk, nch), dim3(64), 0, s, lv.L, (const LRColMeta*)r.meta,
-                           (const int*)r.blk_col, (const long long*)r.ent_off, (const double*)r.ent_val,
-                           (const double*)r.dense_val, sc, v, r.part, (long long)lv.L.nstore, r.nblk);
+        hipLaunchKernelGGL(k_lr_partials, dim3(r.nblk, (nch + LRP_CH - 1) / LRP_CH), dim3(64), 0, s, lv.L,
+                           (const LRColMeta*)r.meta, (const int*)r.blk_col, (const long long*)r.ent_off,
+                           (const double*)r.ent_val, (const double*)r.dense_val, sc, v, r.part,
+                           (long long)lv.L.nstore, r.nblk, nch);
     hipLaunchKernelGGL(k_lr_totals, dim3(r.m, 1, nch), dim3(64), 0, s, (const LRColMeta*)r.meta, (const double*)r.part,
                        r.w, r.nblk, r.m);
 }
@@ -743,8 +745,10 @@ void lr_patch(const mgmc_handle* h, const Level& lv, int mode, double* y, uint32
 // residual (LR_PATCH_RESIDUAL: f - B t, t = r.w) reads; returns the vector to read.  Dense-column
 // path: written to r.fe, f untouched; otherwise f is patched in place (saved for lr_restore).
 // LR_PATCH_APPLY: f += B t in place on either path.
+// post_tag >= 0 (dense-column path, LR_PATCH_RESIDUAL): the same launch also writes r.fe2 =
+// f + B Sigma^{-1/2} xi' of the level's first post-sweep (tag post_tag), which then reads r.fe2
 double* lr_rhs(const mgmc_handle* h, const Level& lv, int mode, double* f, uint32_t tag, const uint64_t* sample,
-               hipStream_t s, int nch = 1) {
+               hipStream_t s, int nch = 1, int64_t post_tag = -1) {
     const LowRankDev& r = lv.lr;
     if (!r.dense_path) {
         lr_patch(h, lv, mode, f, tag, sample, s, nch);
@@ -765,6 +769,8 @@ double* lr_rhs(const mgmc_handle* h, const Level& lv, int mode, double* f, uint3
     a.t = r.w;
     a.f = f;
     a.out = mode == LR_PATCH_APPLY ? f : r.fe;
+    a.out2 = post_tag >= 0 ? r.fe2 : nullptr;
+    a.tag2 = post_tag >= 0 ? (uint32_t)post_tag : 0u;
     a.nrows = r.nrows;
     a.nbs = (r.nrows + LRD_NT - 1) / LRD_NT;
     a.off = r.rows_off;
@@ -1069,9 +1075,10 @@ void build_ops(mgmc_handle* h) {
         for (size_t q = 0; q < h->ops.size(); ++q) {
             Op& op = h->ops[q];
             const int l = op.level;
-            // (not on dense-column levels: their patches write lr.fe, f is never patched or restored)
-            if (op.kind != OP_RESIDUAL_RESTRICT || h->levels[l].lr.m == 0 || h->levels[l].lr.dense_path) continue;
-            if (q + 1 < h->ops.size()) {
+            // (dense-column levels: f is never patched or restored; the residual's launch writes the
+            // first post-sweep's right-hand side to lr.fe2, and the coarse patch stays separate)
+            if (op.kind != OP_RESIDUAL_RESTRICT || h->levels[l].lr.m == 0) continue;
+            if (q + 1 < h->ops.size() && !h->levels[l].lr.dense_path) {
                 Op& nx = h->ops[q + 1];
                 if (nx.kind == OP_SWEEP && nx.level == l + 1 && h->levels[l + 1].lr.m > 0 &&
                     !h->levels[l + 1].lr.dense_path && !nx.lr_skip_patch) {
@@ -1280,6 +1287,7 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 const bool lr = lv.lr.m > 0;
                 double* fs = lv.f;  // the right-hand side the sweep reads
                 if (lr && !op.lr_skip_patch) fs = lr_rhs(h, lv, LR_PATCH_NOISE, lv.f, op.tag, sample, s, nch);
+                else if (lr && lv.lr.dense_path) fs = lv.lr.fe2;  // written with the level's residual
                 double* xo = lv.x;
                 if (lv.zsweep) {
                     const Level* lc = op.prolong ? &h->levels[op.level + 1] : nullptr;
@@ -1318,10 +1326,13 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 double* fr = lv.f;
                 if (lr && !op.lr_skip_patch) {  // r = (f - B Sigma^{-1} B^T x) - A x
                     lr_dots(lv, lv.buf(op.src), lv.lr.sc_inv, s, nch);
-                    fr = lr_rhs(h, lv, LR_PATCH_RESIDUAL, lv.f, 0, sample, s, nch);
+                    fr = lr_rhs(h, lv, LR_PATCH_RESIDUAL, lv.f, 0, sample, s, nch,
+                                lv.lr.dense_path && op.lr_post_patch ? (int64_t)op.lr_post_tag : -1);
                 }
                 launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch);
-                if (lr && (op.lr_post_patch || op.lr_coarse_patch))
+                if (lr && lv.lr.dense_path)
+                    ;  // f was never patched; the post-sweep's rhs went to lr.fe2 above
+                else if (lr && (op.lr_post_patch || op.lr_coarse_patch))
                     lr_restore_patch(h, op, lv, lc, sample, s, nch);
                 else if (lr)
                     lr_restore(lv, lv.f, s, nch);
@@ -2605,9 +2616,11 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
         for (long long i = 0; i < N; ++i) local[i] = slot[i] == 0;
         if ((rc = skip_mask(local, &r.skip_b))) return rc;
         const size_t fb = (size_t)lv.L.nstore * h->nchains * sizeof(double);
-        if (hipMalloc(&r.fe, fb) != hipSuccess) return fail(h, MGMC_E_NOMEM, "device allocation failed");
-        r.allocs.push_back(r.fe);
-        HIPCHK(h, hipMemsetAsync(r.fe, 0, fb, h->stream));
+        for (double** q : {&r.fe, &r.fe2}) {
+            if (hipMalloc(q, fb) != hipSuccess) return fail(h, MGMC_E_NOMEM, "device allocation failed");
+            r.allocs.push_back(*q);
+            HIPCHK(h, hipMemsetAsync(*q, 0, fb, h->stream));
+        }
     }
     int nrows = 0;
     std::vector<long long> rows_off;

@@ -55,31 +55,35 @@ struct LRColMeta {
 };
 
 // ---- dot products, stage 1: one wavefront per block of LR_BLK entries ----
-// Batched chains: blockIdx.y = chain (v cs apart, the partials nblk apart).  A dense column lists
-// every vertex in reference order: lane l's entries e, e + 64, ... are walked with incremental
-// (i, j, k) (no 64-bit division per entry).  The lane's sum runs in entry order; the entries are
-// taken LRP_U at a time with their loads issued together (the coarse levels' dots are a handful of
-// wavefronts, each a chain of up to 64 dependent global round trips otherwise).
-constexpr int LRP_U = 8;
+// A dense column lists every vertex in reference order: lane l's entries e, e + 64, ... are walked
+// with incremental (i, j, k) (no 64-bit division per entry).  The lane's sum runs in entry order;
+// the entries are taken LRP_U at a time with their loads issued together (the coarse levels' dots
+// are a handful of wavefronts, each a chain of up to 64 dependent global round trips otherwise).
+// Batched chains: blockIdx.y = a group of LRP_CH chains; the column value of an entry is loaded
+// once for the group (v cs apart, the partials nblk apart per chain).
+constexpr int LRP_U = 8, LRP_CH = 4;
 __global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRColMeta* __restrict__ meta,
                                                      const int* __restrict__ blk_col,
                                                      const long long* __restrict__ ent_off,
                                                      const double* __restrict__ ent_val,
                                                      const double* __restrict__ dense_val,
                                                      const double* __restrict__ sc, const double* __restrict__ v,
-                                                     double* __restrict__ part, long long cs, int nblk) {
+                                                     double* __restrict__ part, long long cs, int nblk, int nch) {
     const int b = blockIdx.x;
-    const int ch = blockIdx.y;
+    const int ch0 = blockIdx.y * LRP_CH;
+    const int nc = min(LRP_CH, nch - ch0);
     const int lane = threadIdx.x;
     const int k = blk_col[b];
     const LRColMeta c = meta[k];
     const long long e0 = (long long)(b - c.blk0) * LR_BLK;
     const long long end = min(c.n, e0 + LR_BLK);
     const double s = sc[k];
-    const double* vc = v + ch * cs;
+    const double* vc = v + ch0 * cs;
     const long long e1 = e0 + lane;
     const int cnt = e1 < end ? (int)((end - e1 + 63) / 64) : 0;  // entries of this lane
-    double acc = 0.0;
+    double acc[LRP_CH];
+#pragma unroll
+    for (int q = 0; q < LRP_CH; ++q) acc[q] = 0.0;
     if (c.dense >= 0) {
         const double* dv = dense_val + (long long)c.dense * L.nstore;
         const int nxi = L.nx - 1, nyi = L.ny - 1;
@@ -89,7 +93,7 @@ __global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRColMeta* _
         int kk = L.dim == 3 ? (int)(r / nyi) + 1 : 0;
         for (int base = 0; base < cnt; base += LRP_U) {
             long long p[LRP_U];
-            double a[LRP_U], x[LRP_U];
+            double a[LRP_U], x[LRP_CH][LRP_U];
 #pragma unroll
             for (int u = 0; u < LRP_U; ++u) {
                 p[u] = L.at(i, j, kk);
@@ -106,31 +110,44 @@ __global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRColMeta* _
             for (int u = 0; u < LRP_U; ++u)
                 if (base + u < cnt) {
                     a[u] = dv[p[u]];
-                    x[u] = vc[p[u]];
+#pragma unroll
+                    for (int q = 0; q < LRP_CH; ++q)
+                        if (q < nc) x[q][u] = vc[q * cs + p[u]];
                 }
 #pragma unroll
-            for (int u = 0; u < LRP_U; ++u)
-                if (base + u < cnt) acc = acc + (s * a[u]) * x[u];
+            for (int q = 0; q < LRP_CH; ++q)
+#pragma unroll
+                for (int u = 0; u < LRP_U; ++u)
+                    if (q < nc && base + u < cnt) acc[q] = acc[q] + (s * a[u]) * x[q][u];
         }
     } else {
         const long long q0 = c.ent0 + e1;
         for (int base = 0; base < cnt; base += LRP_U) {
-            double a[LRP_U], x[LRP_U];
+            double a[LRP_U], x[LRP_CH][LRP_U];
 #pragma unroll
             for (int u = 0; u < LRP_U; ++u)
                 if (base + u < cnt) {
                     const long long q = q0 + 64ll * (base + u);
                     a[u] = ent_val[q];
-                    x[u] = vc[ent_off[q]];
+                    const long long o = ent_off[q];
+#pragma unroll
+                    for (int w = 0; w < LRP_CH; ++w)
+                        if (w < nc) x[w][u] = vc[w * cs + o];
                 }
 #pragma unroll
-            for (int u = 0; u < LRP_U; ++u)
-                if (base + u < cnt) acc = acc + (s * a[u]) * x[u];
+            for (int w = 0; w < LRP_CH; ++w)
+#pragma unroll
+                for (int u = 0; u < LRP_U; ++u)
+                    if (w < nc && base + u < cnt) acc[w] = acc[w] + (s * a[u]) * x[w][u];
         }
     }
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
-    if (lane == 0) part[(long long)ch * nblk + b] = acc;
+    for (int q = 0; q < LRP_CH; ++q) {
+        double t = acc[q];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) t = t + __shfl_xor(t, off, 64);
+        if (lane == 0 && q < nc) part[(long long)(ch0 + q) * nblk + b] = t;
+    }
 }
 
 // ---- dot products, stage 2: one wavefront per column ----
@@ -366,6 +383,8 @@ struct LRDenseArgs {
     const double* t;          // residual / apply: the m dots of every chain, m apart
     const double* f;
     double* out;
+    double* out2;             // RESIDUAL with out2: also out2 = f + B Sigma^{-1/2} xi' of sweep tag2
+    uint32_t tag2;            //   (the level's first post-sweep: f is not written in between)
     // local rows (blocks [0, nbs)): padded offsets, m coefficients, column masks
     int nrows, nbs;
     const long long* off;
@@ -377,26 +396,34 @@ struct LRDenseArgs {
     const double* bg;
 };
 
+// s[ch * m + k] = sq_k xi'_k of sweep `tag` for every chain (only k = g, g's pair, if !all)
+__device__ __forceinline__ void lrd_noise(const LRDenseArgs& a, uint32_t tag, bool all, double* s) {
+    const int m = a.m, np = (m + 1) / 2;
+    const uint64_t sample = *a.sample;
+    for (int q = threadIdx.x; q < a.nch * np; q += LRD_NT) {
+        const int ch = q / np, pr = q - ch * np;
+        if (!all && pr != a.g / 2) continue;  // dense-only rows need s_g alone
+        const RngKey k = lr_chain_key(a.key, a.chain0, a.seed_hi, ch);
+        const Philox4 r =
+            philox4x32_10(LR_PAIR0 + (uint32_t)pr, tag, (uint32_t)sample, (uint32_t)(sample >> 32), k.k0, k.k1);
+        double z0, z1;
+        normal_pair(r, &z0, &z1);
+        s[ch * m + 2 * pr] = a.sq[2 * pr] * z0;
+        if (2 * pr + 1 < m) s[ch * m + 2 * pr + 1] = a.sq[2 * pr + 1] * z1;
+    }
+}
+
 __global__ void __launch_bounds__(LRD_NT) k_lr_dense_rhs(LRDenseArgs a) {
     __shared__ double s[LR_MAX_CH * LR_MAX_M];
+    __shared__ double s2[LR_MAX_CH * LR_MAX_M];
     const bool local = (int)blockIdx.x < a.nbs;
     const int m = a.m;
+    const bool two = a.out2 != nullptr;
     if (a.mode == LR_PATCH_NOISE) {
-        const int np = (m + 1) / 2;
-        const uint64_t sample = *a.sample;
-        for (int q = threadIdx.x; q < a.nch * np; q += LRD_NT) {
-            const int ch = q / np, pr = q - ch * np;
-            if (!local && pr != a.g / 2) continue;  // dense-only rows need s_g alone
-            const RngKey k = lr_chain_key(a.key, a.chain0, a.seed_hi, ch);
-            const Philox4 r = philox4x32_10(LR_PAIR0 + (uint32_t)pr, a.tag, (uint32_t)sample, (uint32_t)(sample >> 32),
-                                            k.k0, k.k1);
-            double z0, z1;
-            normal_pair(r, &z0, &z1);
-            s[ch * m + 2 * pr] = a.sq[2 * pr] * z0;
-            if (2 * pr + 1 < m) s[ch * m + 2 * pr + 1] = a.sq[2 * pr + 1] * z1;
-        }
+        lrd_noise(a, a.tag, local, s);
     } else {
         for (int q = threadIdx.x; q < a.nch * m; q += LRD_NT) s[q] = a.t[q];
+        if (two) lrd_noise(a, a.tag2, local, s2);
     }
     __syncthreads();
     const bool minus = a.mode == LR_PATCH_RESIDUAL;
@@ -407,11 +434,15 @@ __global__ void __launch_bounds__(LRD_NT) k_lr_dense_rhs(LRDenseArgs a) {
         const uint64_t msk = a.mask[u];
         const double* cf = a.coef + (long long)u * m;
         for (int ch = 0; ch < a.nch; ++ch) {
-            double e = 0.0;
+            double e = 0.0, e2 = 0.0;
             for (int k = 0; k < m; ++k)
-                if ((msk >> k) & 1) e = e + cf[k] * s[ch * m + k];
+                if ((msk >> k) & 1) {
+                    e = e + cf[k] * s[ch * m + k];
+                    if (two) e2 = e2 + cf[k] * s2[ch * m + k];
+                }
             const double y = a.f[ch * a.cs + p];
             a.out[ch * a.cs + p] = minus ? y - e : y + e;
+            if (two) a.out2[ch * a.cs + p] = y + e2;
         }
         return;
     }
@@ -438,6 +469,19 @@ __global__ void __launch_bounds__(LRD_NT) k_lr_dense_rhs(LRDenseArgs a) {
             if (ok[r][0] && ok[r][1]) *(double2*)(oc + p[r]) = o;
             else if (ok[r][0]) oc[p[r]] = o.x;
             else if (ok[r][1]) oc[p[r] + 1] = o.y;
+        }
+        if (two) {
+            const double sg2 = s2[ch * m + a.g];
+            double* o2c = a.out2 + ch * a.cs;
+#pragma unroll
+            for (int r = 0; r < LRD_PER; ++r) {
+                double2 o;
+                o.x = y[r].x + (0.0 + bv[r].x * sg2);
+                o.y = y[r].y + (0.0 + bv[r].y * sg2);
+                if (ok[r][0] && ok[r][1]) *(double2*)(o2c + p[r]) = o;
+                else if (ok[r][0]) o2c[p[r]] = o.x;
+                else if (ok[r][1]) o2c[p[r] + 1] = o.y;
+            }
         }
     }
 }
