@@ -73,9 +73,11 @@ inline mgmc_config make_config(int dim, int nx, int ny, int nz, double kappa_sq,
 // MultigridMCSampler::apply (sampler/multigridmc_sampler.cc:132-138).
 class HipMultigridMCSampler {
    public:
-    HipMultigridMCSampler(const mgmc_config& cfg, int device, uint64_t seed, uint64_t chain_id = 0) {
+    // nchains > 1: a batch of chains chain_id .. chain_id + nchains - 1 in one handle
+    // (mgmc_create_batch); apply / set_state act on every chain, the *_chain accessors on one
+    HipMultigridMCSampler(const mgmc_config& cfg, int device, uint64_t seed, uint64_t chain_id = 0, int nchains = 1) {
         mgmc_handle* h = nullptr;
-        check(mgmc_create(&cfg, device, seed, chain_id, &h), nullptr, "mgmc_create");
+        check(mgmc_create_batch(&cfg, device, seed, chain_id, nchains, &h), nullptr, "mgmc_create");
         h_.reset(h);
         mgmc_level_desc d{};
         check(mgmc_level_desc_get(h_.get(), 0, &d), h_.get(), "mgmc_level_desc_get");
@@ -119,6 +121,14 @@ class HipMultigridMCSampler {
     void get_state(double* x) const { check(mgmc_get_state(h_.get(), x, ndof_), h_.get(), "mgmc_get_state"); }
     // (n, mean, M2) of the recorded QoI
     void qoi_moments(double out[3]) const { check(mgmc_qoi_moments(h_.get(), out), h_.get(), "mgmc_qoi_moments"); }
+    // one chain of a batch
+    int nchains() const { return mgmc_nchains(h_.get()); }
+    void get_state(int chain, double* x) const {
+        check(mgmc_get_state_chain(h_.get(), chain, x, ndof_), h_.get(), "mgmc_get_state_chain");
+    }
+    void qoi_moments(int chain, double out[3]) const {
+        check(mgmc_qoi_moments_chain(h_.get(), chain, out), h_.get(), "mgmc_qoi_moments_chain");
+    }
 
    private:
     struct Deleter {
