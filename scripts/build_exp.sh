@@ -23,4 +23,10 @@ done
 for z in ${TZPS:-}; do
   $HIPX -DMGMC_ZS_SHAPE_TZP=$z -o ../../build/libmgmc_expz$z.so $SRCS &
 done
+# 27-point z-march variants: slab rows SR x minimum nx (build/libmgmc_expq<SR>x<MIN>.so; MIN above
+# every level's nx = the pair / quad passes)
+for q in ${Z27S:-}; do
+  IFS=x read -r sr mn <<< "$q"
+  $HIPX -DMGMC_Z27_EXPERIMENT -DMGMC_Z27_SR=$sr -DMGMC_Z27_MIN_NX=$mn -o ../../build/libmgmc_expq$q.so $SRCS &
+done
 wait
