@@ -471,9 +471,12 @@ bool pairs_eligible(const LevelSpec& sp, const Layout& L) {
 // level (2D 1024^2 FD cycle 0.135 -> 0.129 ms, FEM 0.147 -> 0.139 ms; A/B in one box call).  On the
 // large 3D levels it loses (512^3 level 1: 2 x 105 us against 4 x 41 us per sweep): the
 // second pair's loads wait for the first pair's rows.  Levels that k_tail runs are left to it (caller).
+#ifndef MGMC_QUADS_MAXPAIR  // (timing-experiment builds override it: scripts/build_exp.sh QMAX)
+#define MGMC_QUADS_MAXPAIR 32
+#endif
 bool quads_eligible(const LevelSpec& sp, const Layout& L, uint32_t paths) {
     if (!pairs_eligible(sp, L) || (paths & PATH_NO_QUADS)) return false;
-    return sp.dim == 2 || L.nx / 2 <= 32;
+    return sp.dim == 2 || L.nx / 2 <= MGMC_QUADS_MAXPAIR;
 }
 
 // one red-black sweep of a 2D 5-point level, xin -> xout (mgmc_rb2d.hpp)
@@ -502,7 +505,10 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
     const int dim = lv.spec.dim;
     const int npair = lv.L.nx / 2;
     // T+1 thread rows of npair threads (<= 512 threads: 2 workgroups per CU)
-    a.T = std::max(1, 512 / npair - 1);
+#ifndef MGMC_QUADS_NT  // (timing-experiment builds override it: scripts/build_exp.sh QMAX=<pairs>x<threads>)
+#define MGMC_QUADS_NT 512
+#endif
+    a.T = std::max(1, MGMC_QUADS_NT / npair - 1);
     a.nblk_y = (lv.L.ny - 1 + 2 * a.T - 1) / (2 * a.T);
     const int nt = npair * (a.T + 1);
     const size_t lds = (size_t)(2 * a.T + 1) * (lv.L.nx + 2) * sizeof(double);

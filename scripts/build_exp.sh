@@ -29,4 +29,9 @@ for q in ${Z27S:-}; do
   IFS=x read -r sr mn <<< "$q"
   $HIPX -DMGMC_Z27_EXPERIMENT -DMGMC_Z27_SR=$sr -DMGMC_Z27_MIN_NX=$mn -o ../../build/libmgmc_expq$q.so $SRCS &
 done
+# quad passes on 3D levels with rows of up to QMAX pairs (build/libmgmc_expm<QMAX>.so)
+for q in ${QMAX:-}; do
+  IFS=x read -r mp nt <<< "$q"
+  $HIPX -DMGMC_QUADS_MAXPAIR=$mp ${nt:+-DMGMC_QUADS_NT=$nt} -o ../../build/libmgmc_expm$q.so $SRCS &
+done
 wait
