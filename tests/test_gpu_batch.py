@@ -119,3 +119,19 @@ def test_batched_chain_argument_validation(hip_device):
     with pytest.raises(mg.MgmcError):
         b.qoi_moments(-1)
     b.close()
+
+
+def test_batched_config5_global_at_256_cubed(hip_device):
+    """BASELINE config 5 with the global average (the dense-column path) at full size, 2 chains in
+    one handle: each chain's QoI series and state bitwise equal to its one-chain handle."""
+    from tests.test_gpu_configs import _config5
+    lat, op, p = _config5(True)
+    qoi = mg.measurement_vector_index(lat, [0.5] * lat.dim)
+    b = mg.MultigridMCSampler(op, SEED, p, chain_id=CHAIN0, nchains=2)
+    zb = b.sample(3, qoi, chain=None)
+    for c in range(2):
+        s = mg.MultigridMCSampler(op, SEED, p, chain_id=CHAIN0 + c)
+        assert np.array_equal(s.sample(3, qoi), zb[c])
+        assert np.array_equal(s.get_state(), b.get_state(c))
+        s.close()
+    b.close()
