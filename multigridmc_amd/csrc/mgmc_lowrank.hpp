@@ -150,6 +150,76 @@ __global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRColMeta* _
     }
 }
 
+// ---- dot products, stage 1 on small levels: the same partials, the loads spread over a workgroup ----
+// A level with few blocks runs only a handful of wavefronts whose lanes each chase 64 dependent
+// round trips.  Here 256 threads form the block's 4096 products (s B_e) v_e at once into LDS, then
+// lane l of the first wavefront adds its entries l, l+64, ... in entry order and the butterfly
+// follows: the single-wavefront kernel's sums, bit for bit.  One chain per blockIdx.y.
+constexpr int LRS_NT = 256;
+__global__ void __launch_bounds__(LRS_NT) k_lr_partials_staged(Layout L, const LRColMeta* __restrict__ meta,
+                                                               const int* __restrict__ blk_col,
+                                                               const long long* __restrict__ ent_off,
+                                                               const double* __restrict__ ent_val,
+                                                               const double* __restrict__ dense_val,
+                                                               const double* __restrict__ sc,
+                                                               const double* __restrict__ v, double* __restrict__ part,
+                                                               long long cs, int nblk) {
+    __shared__ double prod[LR_BLK];
+    const int b = blockIdx.x;
+    const int ch = blockIdx.y;
+    const int tid = threadIdx.x;
+    const int k = blk_col[b];
+    const LRColMeta c = meta[k];
+    const long long e0 = (long long)(b - c.blk0) * LR_BLK;
+    const int cnt = (int)min((long long)LR_BLK, c.n - e0);  // entries of this block
+    const double s = sc[k];
+    const double* vc = v + ch * cs;
+    constexpr int PER = LR_BLK / LRS_NT;
+    if (c.dense >= 0) {
+        const double* dv = dense_val + (long long)c.dense * L.nstore;
+        const int nxi = L.nx - 1, nyi = L.ny - 1;
+        const long long e1 = e0 + tid;
+        int i = (int)(e1 % nxi) + 1;
+        const long long r = e1 / nxi;
+        int j = (int)(r % nyi) + 1;
+        int kk = L.dim == 3 ? (int)(r / nyi) + 1 : 0;
+        long long p[PER];
+#pragma unroll
+        for (int t = 0; t < PER; ++t) {
+            p[t] = L.at(i, j, kk);
+            i += LRS_NT;  // advance by 256 entries (carry repeatedly)
+            while (i > nxi) {
+                i -= nxi;
+                if (++j > nyi) {
+                    j = 1;
+                    ++kk;
+                }
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < PER; ++t) {
+            const int e = tid + t * LRS_NT;
+            if (e < cnt) prod[e] = (s * dv[p[t]]) * vc[p[t]];
+        }
+    } else {
+#pragma unroll
+        for (int t = 0; t < PER; ++t) {
+            const int e = tid + t * LRS_NT;
+            if (e < cnt) {
+                const long long q = c.ent0 + e0 + e;
+                prod[e] = (s * ent_val[q]) * vc[ent_off[q]];
+            }
+        }
+    }
+    __syncthreads();
+    if (tid >= 64) return;
+    double acc = 0.0;
+    for (int e = tid; e < cnt; e += 64) acc = acc + prod[e];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+    if (tid == 0) part[(long long)ch * nblk + b] = acc;
+}
+
 // ---- dot products, stage 2: one wavefront per column ----
 __global__ void __launch_bounds__(64) k_lr_totals(const LRColMeta* __restrict__ meta, const double* __restrict__ part,
                                                    double* __restrict__ out, int nblk, int m) {

@@ -34,4 +34,8 @@ for q in ${QMAX:-}; do
   IFS=x read -r mp nt <<< "$q"
   $HIPX -DMGMC_QUADS_MAXPAIR=$mp ${nt:+-DMGMC_QUADS_NT=$nt} -o ../../build/libmgmc_expm$q.so $SRCS &
 done
+# low-rank dots: the staged kernel below LRSW wavefronts of the per-block kernel (build/libmgmc_expw<N>.so)
+for w in ${LRSW:-}; do
+  $HIPX -DLRS_MAX_WAVES=$w -o ../../build/libmgmc_expw$w.so $SRCS &
+done
 wait
