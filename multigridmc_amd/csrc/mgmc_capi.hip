@@ -2624,6 +2624,11 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
     std::vector<int> t_ent_off;
     std::vector<double> ent_val;
     int ndense = 0;
+    // a dense column of a level with at most LR_BLK vertices is one block either way: it is kept as
+    // an entry list (every row, ascending: the dense order), so the level can take the small-level
+    // kernels (k_lr_small, k_tail)
+    std::vector<char> dense_here(m);
+    for (int k = 0; k < m; ++k) dense_here[k] = cols[k].dense && N > LR_BLK;
     for (int k = 0; k < m; ++k) {
         const LRColumn& c = cols[k];
         LRColMeta& mt = meta[k];
@@ -2633,7 +2638,7 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
         mt.nblk = (int)((mt.n + LR_BLK - 1) / LR_BLK);
         mt.pad_ = 0;
         for (int b = 0; b < mt.nblk; ++b) blk_col.push_back(k);
-        if (c.dense) {
+        if (dense_here[k]) {
             mt.dense = ndense++;
             mt.ent0 = 0;
         } else {
@@ -2658,7 +2663,7 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
         HIPCHK(h, hipMemsetAsync(r.dense_val, 0, bytes, h->stream));
         std::vector<double> v(N);
         for (int k = 0; k < m; ++k) {
-            if (!cols[k].dense) continue;
+            if (!dense_here[k]) continue;
             for (long long i = 0; i < N; ++i) v[i] = cols[k].ent[i].second;
             if ((rc = upload(h, level, v.data(), r.dense_val + (size_t)meta[k].dense * lv.L.nstore))) return rc;
             HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -2668,7 +2673,7 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
     r.dense_path = ndense == 1 && !(h->paths & PATH_NO_LR_DENSE);
     r.dense_g = -1;
     for (int k = 0; k < m; ++k)
-        if (cols[k].dense) r.dense_g = k;
+        if (dense_here[k]) r.dense_g = k;
     const int g = r.dense_path ? r.dense_g : -1;
     // bit p of a skip mask over the padded store: set unless p is an interior vertex of `dense_only`
     auto skip_mask = [&](const std::vector<char>& local, uint32_t** dst) {

@@ -31,6 +31,8 @@ CONFIGS = {
     "3d32_points_tail_W": ((32, 32, 32), dict(nlevel=4, cycle=2, ncoarsesmooth=2), (0.0, 6, False)),
     "3d48_ball_tail_ssor": ((48, 48, 48), dict(nlevel=4, smoother="SSOR"), (0.1, 3, False)),
     "2d128_points_tail": ((128, 128), dict(nlevel=5), (0.0, 4, False)),
+    # dense-column path on the fine level (> 4096 vertices), the global column as an entry list below
+    "2d128_point_global_W": ((128, 128), dict(nlevel=4, cycle=2), (0.0, 4, True)),
 }
 TAIL_CONFIGS = ["2d64_ball_ssor_W", "3d32_points_tail_W", "3d48_ball_tail_ssor", "2d128_points_tail"]
 
@@ -177,7 +179,7 @@ def test_posterior_statistics_vs_exact_covariance(hip_device, shape, kw, glob, n
 @pytest.mark.parametrize("name,paths", [(n, "tail") for n in TAIL_CONFIGS] +
                          [(n, q) for n in ("3d32_points_tail_W", "2d32_point_global", "3d_aniso_zres_points")
                           for q in ("lr_small", "lr_merge", "lr_prefetch", "lr_small,lr_merge,tail")] +
-                         [(n, "lr_dense") for n in ("2d32_point_global", "3d32_ball_global", "2d32_point_global_chol")])
+                         [(n, "lr_dense") for n in ("2d128_point_global_W", "3d32_ball_global")])
 def test_lowrank_paths_match(hip_device, name, paths, monkeypatch):
     """Low-rank kernel paths switched off (MGMC_DISABLE): tail = the coarse levels' sub-cycle as
     separate launches instead of k_tail (low-rank patches, fix and residual in LDS); lr_small = the
