@@ -27,6 +27,10 @@
 #pragma once
 #include "mgmc_kernels.hpp"
 
+#ifndef MGMC_Z27_EXP  // timing decomposition (wrong results): 1 no Philox, 2 one stencil column, 4 no mid-phase barrier
+#define MGMC_Z27_EXP 0
+#endif
+
 namespace mgmc {
 
 constexpr int Z27_SW = 64;                 // slab columns: LDS column c is lattice i = ib + c (ib even)
@@ -117,7 +121,25 @@ __global__ void __launch_bounds__(Z27_NT) k_zsweep27(Z27Args a) {
 
     // the colours of the rows of parity P of plane k (the first vertex of each pair, exchange, the
     // second); stores the core to x_out when `out`
-    auto phase = [&](int k, int P, double2 fv, bool out) {
+    // the Box-Muller pair of the thread's pair in the rows of parity P of plane k (0 where the
+    // pair's odd vertex is not updated)
+    auto noise = [&](int k, int P) {
+        const int r = row_of(P);
+        const int j = jb + r;
+        const bool odd_in = k >= 1 && k <= L.nz - 1 && m < 31 && r >= 1 && r <= Z27_SR - 2 && j >= 1 &&
+                            j <= L.ny - 1 && odd_col;
+        double2 z = make_double2(0.0, 0.0);
+        if (odd_in && !(MGMC_Z27_EXP & 1)) {
+            const Philox4 rnd = philox4x32_10(pair_id<3>(L, i0, j, k), a.G.tag, s_lo, s_hi, a.G.key.k0, a.G.key.k1);
+            normal_pair(rnd, &z.x, &z.y);
+        }
+        return z;
+    };
+    // one phase with the noise zc of its own pairs (computed during the phase before); the noise
+    // of the next phase (plane nk, rows of parity nP) is computed here, between the exchange read
+    // and the second vertex's chain, where it overlaps the LDS latency instead of stalling the
+    // phase after the barrier
+    auto phase = [&](int k, int P, double2 fv, bool out, double2 zc, int nk, int nP, double2& zn) {
         const int r = row_of(P);
         const int j = jb + r;
         const bool act = k >= 1 && k <= L.nz - 1 && m < 31 && r >= 1 && r <= Z27_SR - 2 && j >= 1 && j <= L.ny - 1;
@@ -149,6 +171,7 @@ __global__ void __launch_bounds__(Z27_NT) k_zsweep27(Z27Args a) {
 #pragma unroll
                 for (int dx = -1; dx <= 1; ++dx) {
                     const int q = rr * 3 + dx + 1;
+                    if ((MGMC_Z27_EXP & 2) && dx != 0) continue;
                     if (q == 0) {
                         res1 = a.S.a[0] * v[s1 - 1];
                         res2 = a.S.a[0] * v[s2 - 1];
@@ -166,11 +189,7 @@ __global__ void __launch_bounds__(Z27_NT) k_zsweep27(Z27Args a) {
 #pragma unroll
             for (int rr = 0; rr < 5; ++rr) keep[rr][0] = keep[rr][1] = keep[rr][2] = keep[rr][3] = 0.0;
         }
-        double z0 = 0.0, z1 = 0.0;  // cos -> odd position, sin -> even position
-        if (odd_in) {
-            const Philox4 rnd = philox4x32_10(pair_id<3>(L, i0, j, k), a.G.tag, s_lo, s_hi, a.G.key.k0, a.G.key.k1);
-            normal_pair(rnd, &z0, &z1);
-        }
+        const double z0 = zc.x, z1 = zc.y;  // cos -> odd position, sin -> even position
         const bool in1 = s1 == 1 ? odd_in : even_in, in2 = s1 == 1 ? even_in : odd_in;
         double v1 = keep[0][s1];
         if (in1) {
@@ -178,18 +197,20 @@ __global__ void __launch_bounds__(Z27_NT) k_zsweep27(Z27Args a) {
             v1 = fma(wd, c - res1, v1);
             own[2 * m + s1] = v1;
         }
-        __syncthreads();
+        if (!(MGMC_Z27_EXP & 4)) __syncthreads();
         keep[0][s1] = v1;
         if (act) {
             if (s1 == 1) keep[0][3] = own[2 * m + 3];  // second = even 2m+2: the next pair's new odd vertex
             else keep[0][0] = own[2 * m];              // second = odd 2m+1: the previous pair's new even vertex
         }
+        zn = noise(nk, nP);
         double v2 = keep[0][s2];
         if (in2) {
 #pragma unroll
             for (int rr = C; rr < 9; ++rr)
 #pragma unroll
-                for (int dx = -1; dx <= 1; ++dx) res2 = fma(a.S.a[rr * 3 + dx + 1], keep[rr - C][s2 + dx], res2);
+                for (int dx = -1; dx <= 1; ++dx)
+                    if (!(MGMC_Z27_EXP & 2) || dx == 0) res2 = fma(a.S.a[rr * 3 + dx + 1], keep[rr - C][s2 + dx], res2);
             const double c = fma(sd, s1 == 1 ? z1 : z0, s1 == 1 ? fv.y : fv.x);
             v2 = fma(wd, c - res2, v2);
             own[2 * m + s2] = v2;
@@ -217,18 +238,20 @@ __global__ void __launch_bounds__(Z27_NT) k_zsweep27(Z27Args a) {
     __syncthreads();
     // f of each phase is loaded one phase ahead (its latency hides behind the phase before)
     double2 fa = load_f(qa, J1);
+    double2 z = noise(qa, J1);
     for (int q = qa; q <= qb; q += 2) {
         const bool two = q - 1 >= k0;  // the K2 plane q-1 (neighbours q-2, q new)
         double2 fb = load_f(q, 1 - J1);
-        phase(q, J1, fa, q >= k0 && q < k1);
+        phase(q, J1, fa, q >= k0 && q < k1, z, q, 1 - J1, z);
         double2 fc = two ? load_f(q - 1, J1) : make_double2(0.0, 0.0);
-        phase(q, 1 - J1, fb, q >= k0 && q < k1);
         if (two) {
+            phase(q, 1 - J1, fb, q >= k0 && q < k1, z, q - 1, J1, z);
             double2 fd = load_f(q - 1, 1 - J1);
-            phase(q - 1, J1, fc, true);
+            phase(q - 1, J1, fc, true, z, q - 1, 1 - J1, z);
             fa = load_f(q + 2, J1);
-            phase(q - 1, 1 - J1, fd, true);
+            phase(q - 1, 1 - J1, fd, true, z, q + 2, J1, z);
         } else {
+            phase(q, 1 - J1, fb, q >= k0 && q < k1, z, q + 2, J1, z);
             fa = load_f(q + 2, J1);
         }
         if (q + 2 <= qb) {  // planes q+2, q+3 into the slots of q-2, q-1

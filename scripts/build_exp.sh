@@ -26,8 +26,9 @@ done
 # 27-point z-march variants: slab rows SR x minimum nx (build/libmgmc_expq<SR>x<MIN>.so; MIN above
 # every level's nx = the pair / quad passes)
 for q in ${Z27S:-}; do
-  IFS=x read -r sr mn <<< "$q"
-  $HIPX -DMGMC_Z27_EXPERIMENT -DMGMC_Z27_SR=$sr -DMGMC_Z27_MIN_NX=$mn -o ../../build/libmgmc_expq$q.so $SRCS &
+  IFS=x read -r sr mn ex <<< "$q"
+  $HIPX -DMGMC_Z27_EXPERIMENT -DMGMC_Z27_SR=$sr -DMGMC_Z27_MIN_NX=$mn ${ex:+-DMGMC_Z27_EXP=$ex} \
+    -o ../../build/libmgmc_expq$q.so $SRCS &
 done
 # quad passes on 3D levels with rows of up to QMAX pairs (build/libmgmc_expm<QMAX>.so)
 for q in ${QMAX:-}; do
