@@ -42,37 +42,63 @@ __global__ void __launch_bounds__(RB2_NT) k_rb2d(Layout L, const double* __restr
     const int i0 = 1 + tx * RB2_TW, j0 = 1 + ty * RB2_TH;
     const int ib = i0 - 2, jb = j0 - 2;  // lattice coordinates of LDS (0, 0)
     const uint64_t sample = NOISE ? *G.sample : 0;
-    for (int q = tid; q < RB2_H * RB2_W; q += RB2_NT) {
+    // all global loads of the workgroup first (the old state with its 2-vertex halo, f of the
+    // updated vertices), then the Box-Muller draws while they are in flight, then the LDS deposits
+    // -- the draws no longer wait behind the loads (same values, same arithmetic)
+    constexpr int NSX = (RB2_H * RB2_W + RB2_NT - 1) / RB2_NT;
+    double xv[NSX];
+#pragma unroll
+    for (int u = 0; u < NSX; ++u) {
+        const int q = tid + u * RB2_NT;
         const int r = q / RB2_W, c = q - r * RB2_W;
         const int i = ib + c, j = jb + r;
-        const double v = (i >= 0 && i <= L.nx && j >= 0 && j <= L.ny) ? xin[L.at(i, j, 0)] : 0.0;
-        xs[rb2_lidx(r, c)] = v;
+        xv[u] = (q < RB2_H * RB2_W && i >= 0 && i <= L.nx && j >= 0 && j <= L.ny) ? xin[L.at(i, j, 0)] : 0.0;
     }
     // right hand sides of every vertex the two passes update (rows [j0-1, j0+TH], columns [i0-1,
     // i0+TW]): f does not change during the sweep, so they are evaluated up front, one Box-Muller per
     // pair (odd i, i+1) -- the values point_normal gives each vertex
-    {
-        constexpr int NP = RB2_TW / 2 + 2;  // pairs with odd i from i0-2 to i0+TW
-        for (int q = tid; q < NP * (RB2_TH + 2); q += RB2_NT) {
-            const int r = q / NP, m = q - r * NP;
-            const int j = j0 - 1 + r, io = i0 - 2 + 2 * m;
-            if (j < 1 || j > L.ny - 1) continue;
-            double z0 = 0.0, z1 = 0.0;
-            if (NOISE && io >= 1 && io <= L.nx - 1) {
-                const Philox4 rnd =
-                    philox4x32_10(pair_id<2>(L, io, j, 0), G.tag, (uint32_t)sample, (uint32_t)(sample >> 32), G.key.k0,
-                                  G.key.k1);
-                normal_pair(rnd, &z0, &z1);
-            }
-            if (io >= 1 && io <= L.nx - 1 && io >= i0 - 1) {
-                const double fv = f[L.at(io, j, 0)];
-                cs[rb2_lidx(j - jb, io - ib)] = NOISE ? fma(G.sd, z0, fv) : fv;
-            }
-            if (io + 1 >= 1 && io + 1 <= L.nx - 1 && io + 1 <= i0 + RB2_TW) {
-                const double fv = f[L.at(io + 1, j, 0)];
-                cs[rb2_lidx(j - jb, io + 1 - ib)] = NOISE ? fma(G.sd, z1, fv) : fv;
-            }
+    constexpr int NP = RB2_TW / 2 + 2;  // pairs with odd i from i0-2 to i0+TW
+    constexpr int NPI = (NP * (RB2_TH + 2) + RB2_NT - 1) / RB2_NT;
+    double fa[NPI], fb[NPI];
+    bool wa[NPI], wb[NPI];
+    int ja[NPI], ia[NPI];
+#pragma unroll
+    for (int u = 0; u < NPI; ++u) {
+        const int q = tid + u * RB2_NT;
+        const int r = q / NP, m = q - r * NP;
+        const int j = j0 - 1 + r, io = i0 - 2 + 2 * m;
+        const bool row = q < NP * (RB2_TH + 2) && j >= 1 && j <= L.ny - 1;
+        ja[u] = j;
+        ia[u] = io;
+        wa[u] = row && io >= 1 && io <= L.nx - 1 && io >= i0 - 1;
+        wb[u] = row && io + 1 >= 1 && io + 1 <= L.nx - 1 && io + 1 <= i0 + RB2_TW;
+        fa[u] = wa[u] ? f[L.at(io, j, 0)] : 0.0;
+        fb[u] = wb[u] ? f[L.at(io + 1, j, 0)] : 0.0;
+    }
+    double za[NPI], zb[NPI];
+#pragma unroll
+    for (int u = 0; u < NPI; ++u) {
+        const int q = tid + u * RB2_NT;
+        const int j = ja[u], io = ia[u];
+        za[u] = zb[u] = 0.0;
+        if (NOISE && q < NP * (RB2_TH + 2) && j >= 1 && j <= L.ny - 1 && io >= 1 && io <= L.nx - 1) {
+            const Philox4 rnd = philox4x32_10(pair_id<2>(L, io, j, 0), G.tag, (uint32_t)sample,
+                                              (uint32_t)(sample >> 32), G.key.k0, G.key.k1);
+            normal_pair(rnd, &za[u], &zb[u]);
         }
+    }
+#pragma unroll
+    for (int u = 0; u < NSX; ++u) {
+        const int q = tid + u * RB2_NT;
+        if (q < RB2_H * RB2_W) {
+            const int r = q / RB2_W, c = q - r * RB2_W;
+            xs[rb2_lidx(r, c)] = xv[u];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NPI; ++u) {
+        if (wa[u]) cs[rb2_lidx(ja[u] - jb, ia[u] - ib)] = NOISE ? fma(G.sd, za[u], fa[u]) : fa[u];
+        if (wb[u]) cs[rb2_lidx(ja[u] - jb, ia[u] + 1 - ib)] = NOISE ? fma(G.sd, zb[u], fb[u]) : fb[u];
     }
     __syncthreads();
     // one colour on columns [ia, ia + w) x rows [ja, ja + h) (interior vertices only)
