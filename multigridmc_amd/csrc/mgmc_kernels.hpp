@@ -239,21 +239,77 @@ __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __re
     double* xs = smem;
     double* fs = smem + L.nstore;
     double* cs = fs + L.nstore;  // [nsweeps][ndof] right hand sides (precompute)
-    for (long long q = threadIdx.x; q < L.nstore; q += blockDim.x) {
+    // the level's x and f: the first MAXS loads of every thread are issued before the Box-Muller
+    // draws below and deposited after them, so the draws overlap the loads' latency
+    constexpr int MAXS = 6;
+    double sx[MAXS], sf[MAXS];
+#pragma unroll
+    for (int u = 0; u < MAXS; ++u) {
+        const long long q = threadIdx.x + (long long)u * blockDim.x;
+        sx[u] = q < L.nstore ? xg[q] : 0.0;
+        sf[u] = q < L.nstore ? fg[q] : 0.0;
+    }
+    const uint64_t sample = *G.sample;
+    const int nxi = L.nx - 1, nyi = L.ny - 1;
+    const long long ndof = (long long)nxi * nyi * (DIM == 3 ? (L.nz - 1) : 1);
+    const int npair = L.nx / 2;
+    const int nrow = nyi * (DIM == 3 ? (L.nz - 1) : 1);
+    // one Philox block and Box-Muller per pair (odd i, i+1) and sweep: cos -> odd, sin -> even,
+    // the values point_normal gives each vertex (the first MAXP items of every thread here)
+    // 32-bit index arithmetic: an LDS-resident level has far fewer than 2^31 items
+    constexpr int MAXP = precompute ? 4 : 1;
+    double pz0[MAXP], pz1[MAXP];
+    if constexpr (precompute) {
+#pragma unroll
+        for (int u = 0; u < MAXP; ++u) {
+            const int t = (int)threadIdx.x + u * (int)blockDim.x;
+            pz0[u] = pz1[u] = 0.0;
+            if (t >= nsweeps * nrow * npair) continue;
+            const int m = t % npair;
+            const int rt = t / npair;
+            const int row = rt % nrow;
+            const int sw = rt / nrow;
+            const int i0 = 2 * m + 1;
+            if (i0 > nxi) continue;
+            const int j = row % nyi + 1;
+            const int k = (DIM == 3) ? row / nyi + 1 : 0;
+            const Philox4 rnd = philox4x32_10(pair_id<DIM>(L, i0, j, k), G.tag + (uint32_t)sw, (uint32_t)sample,
+                                              (uint32_t)(sample >> 32), G.key.k0, G.key.k1);
+            normal_pair(rnd, &pz0[u], &pz1[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < MAXS; ++u) {
+        const long long q = threadIdx.x + (long long)u * blockDim.x;
+        if (q < L.nstore) {
+            xs[q] = sx[u];
+            fs[q] = sf[u];
+        }
+    }
+    for (long long q = threadIdx.x + (long long)MAXS * blockDim.x; q < L.nstore; q += blockDim.x) {
         xs[q] = xg[q];
         fs[q] = fg[q];
     }
     __syncthreads();
-    const uint64_t sample = *G.sample;
-    const int nxi = L.nx - 1, nyi = L.ny - 1;
-    const long long ndof = (long long)nxi * nyi * (DIM == 3 ? (L.nz - 1) : 1);
     if constexpr (precompute) {
-        // one Philox block and Box-Muller per pair (odd i, i+1) and sweep: cos -> odd, sin -> even,
-        // the values point_normal gives each vertex
-        // 32-bit index arithmetic: an LDS-resident level has far fewer than 2^31 items
-        const int npair = L.nx / 2;
-        const int nrow = nyi * (DIM == 3 ? (L.nz - 1) : 1);
-        for (int t = threadIdx.x; t < nsweeps * nrow * npair; t += blockDim.x) {
+#pragma unroll
+        for (int u = 0; u < MAXP; ++u) {
+            const int t = (int)threadIdx.x + u * (int)blockDim.x;
+            if (t >= nsweeps * nrow * npair) continue;
+            const int m = t % npair;
+            const int rt = t / npair;
+            const int row = rt % nrow;
+            const int sw = rt / nrow;
+            const int i0 = 2 * m + 1;
+            if (i0 > nxi) continue;
+            const int j = row % nyi + 1;
+            const int k = (DIM == 3) ? row / nyi + 1 : 0;
+            const long long q = (long long)sw * ndof + (long long)row * nxi + (i0 - 1);
+            const long long p = L.at(i0, j, k);
+            cs[q] = fma(G.sd, pz0[u], fs[p]);
+            if (i0 + 1 <= nxi) cs[q + 1] = fma(G.sd, pz1[u], fs[p + 1]);
+        }
+        for (int t = threadIdx.x + MAXP * blockDim.x; t < nsweeps * nrow * npair; t += blockDim.x) {
             const int m = t % npair;
             const int rt = t / npair;
             const int row = rt % nrow;
