@@ -285,7 +285,7 @@ def main():
                 post = sweep_roofline(timed["post_ms"], timed["npost"], (24.0 * n0 + 8.0 * n1) * K,
                                       tr_post if K == 1 else None, prov2,
                                       "fine post-sweep k_zsweep_rb7<PROLONG> (prolongate-add of level 1 fused, "
-                                      "24 B per fine + 8 B per coarse unknown; segment includes the ~4 us QoI record)")
+                                      "24 B per fine + 8 B per coarse unknown; its own segment of the cycle graph)")
                 per_kernel["post_sweep"] = post
             # the dominant kernel (the longer of the two) is the headline roofline
             roof = dict(max(per_kernel.values(), key=lambda r: r["avg_launch_ms"]))

@@ -258,8 +258,8 @@ struct mgmc_handle {
     // post-sampler, after the QoI record): mgmc_sample_timed points them at per-step events
     hipGraph_t graph_timed_src = nullptr;
     hipGraphExec_t graph_timed = nullptr;
-    hipGraphNode_t timed_node[4] = {nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t timed_ev0[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipGraphNode_t timed_node[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t timed_ev0[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     int unroll = 1;
     int64_t qoi_store_index = -1;
     std::string last_error;
@@ -1455,16 +1455,17 @@ void destroy_graphs(mgmc_handle* h) {
     h->graph_timed_src = nullptr;
 }
 
-// the timed cycle: the same ops in one graph with an external event-record node at each of the four
-// segment boundaries (no extra graph launches; mgmc_sample_timed re-targets the nodes per step)
+// the timed cycle: the same ops in one graph with an external event-record node at each of the five
+// segment boundaries (no extra graph launches; mgmc_sample_timed re-targets the nodes per step):
+// fine pre-sampler | coarse-grid correction | fine post-sampler | QoI record
 int capture_timed(mgmc_handle* h) {
     for (auto& e : h->timed_ev0)
         if (!e) HIPCHK(h, hipEventCreate(&e));
-    const size_t b[4] = {0, h->seg_end_pre, h->seg_begin_post, h->ops.size()};
+    const size_t b[5] = {0, h->seg_end_pre, h->seg_begin_post, h->seg_end_post, h->ops.size()};
     HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < 5; ++q) {
         HIPCHK(h, hipEventRecordWithFlags(h->timed_ev0[q], h->stream, hipEventRecordExternal));
-        if (q < 3) enqueue_ops(h, b[q], b[q + 1], h->stream);
+        if (q < 4) enqueue_ops(h, b[q], b[q + 1], h->stream);
     }
     HIPCHK(h, hipStreamEndCapture(h->stream, &h->graph_timed_src));
     size_t nn = 0;
@@ -1477,10 +1478,10 @@ int capture_timed(mgmc_handle* h) {
         if (ty != hipGraphNodeTypeEventRecord) continue;
         hipEvent_t e = nullptr;
         HIPCHK(h, hipGraphEventRecordNodeGetEvent(nd, &e));
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < 5; ++q)
             if (e == h->timed_ev0[q]) h->timed_node[q] = nd;
     }
-    for (int q = 0; q < 4; ++q)
+    for (int q = 0; q < 5; ++q)
         if (!h->timed_node[q]) return fail(h, MGMC_E_HIP, "timed graph: event-record node not captured");
     HIPCHK(h, hipGraphInstantiate(&h->graph_timed, h->graph_timed_src, nullptr, nullptr, 0));
     return MGMC_OK;
@@ -2359,10 +2360,10 @@ int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* tot
     if (rc) return rc;
     HIPCHK(h, hipMemsetAsync(h->ctrl + 1, 0, sizeof(uint64_t), h->stream));
     if ((rc = ensure_series(h, (uint64_t)nsteps))) return rc;
-    // one graph launch per cycle; its four event-record nodes are re-targeted at this step's events
-    // before the launch (boundaries: fine pre-sampler | coarse-grid correction | fine post-sampler +
+    // one graph launch per cycle; its five event-record nodes are re-targeted at this step's events
+    // before the launch (boundaries: fine pre-sampler | coarse-grid correction | fine post-sampler |
     // QoI record)
-    constexpr int NSEG = 4;
+    constexpr int NSEG = 5;
     std::vector<hipEvent_t> ev(NSEG * (size_t)nsteps);
     for (auto& e : ev) HIPCHK(h, hipEventCreate(&e));
     for (int s = 0; s < nsteps; ++s) {
@@ -2387,7 +2388,7 @@ int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* tot
     for (size_t q = 0; q < h->ops.size(); ++q)
         if (h->ops[q].kind == OP_SWEEP && h->ops[q].level == 0) {
             if (q < h->seg_end_pre) ++cpre;
-            else if (q >= h->seg_begin_post) ++cpost;
+            else if (q >= h->seg_begin_post && q < h->seg_end_post) ++cpost;
         }
     *npre = cpre * nsteps;
     *npost = cpost * nsteps;

@@ -448,7 +448,7 @@ class MultigridMCSampler:
         self._chk(self.lib.mgmc_synchronize(self.handle))
 
     def sample_timed(self, nsteps: int, qoi_index: int = -1) -> dict:
-        """nsteps cycles replayed as [fine pre-sampler | coarse correction | fine post-sampler + QoI]
+        """nsteps cycles replayed as [fine pre-sampler | coarse correction | fine post-sampler | QoI]
         graph segments with HIP events on the handle's stream (mgmc_sample_timed)."""
         tot, pre, post = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         npre, npost = ctypes.c_int(), ctypes.c_int()
