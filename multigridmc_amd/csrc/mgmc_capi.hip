@@ -1170,11 +1170,20 @@ constexpr size_t TAIL_LDS_LIMIT = 150 * 1024;
 // one 1024-thread workgroup (1024 / 512 / 256 threads: 256^3 cycle 0.529 / 0.538 / 0.570 ms, round 1)
 constexpr int TAIL_NT = 1024;
 
+// 3D plane stride padded to sp = 8 (mod 16) doubles: k_tail's colour passes give the two halves of a
+// half-wave the planes k and k+2, whose ds_read_b64 bank pairs (d mod 32) then sit 16 apart, so the
+// stride-2 class access is 2-way (the least a stride-2 access allows) instead of 4-way with sx odd
+// and unpadded planes (MI355X_MICROARCH.md LDS banking)
+long long tail_plane_stride(int nx, int ny) {
+    const long long sp = (long long)(nx + 1) * (ny + 1);
+    return sp + ((8 - sp % 16) + 16) % 16;
+}
+
 Layout tail_layout(const Layout& L) {
     Layout G = L;
     G.off = 0;
     G.sx = L.nx + 1;
-    G.sp = G.sx * (L.ny + 1);
+    G.sp = L.dim == 3 ? tail_plane_stride(L.nx, L.ny) : G.sx * (L.ny + 1);
     G.nstore = L.dim == 3 ? G.sp * (L.nz + 1) : G.sp;
     return G;
 }
@@ -1189,7 +1198,8 @@ int tail_start_by_size(const std::vector<LevelSpec>& specs, const mgmc_config& c
         for (int l = lt; l < L && ok; ++l) {
             const LevelSpec& sp = specs[l];
             ok = sp.npoints == (sp.dim == 3 ? 27 : 9);
-            const size_t v = (size_t)(sp.n[0] + 1) * (sp.n[1] + 1) * (sp.dim == 3 ? sp.n[2] + 1 : 1);
+            const size_t v = sp.dim == 3 ? (size_t)tail_plane_stride(sp.n[0], sp.n[1]) * (sp.n[2] + 1)
+                                         : (size_t)(sp.n[0] + 1) * (sp.n[1] + 1);
             tot += 2 * v;
             vmax = std::max(vmax, v);
         }

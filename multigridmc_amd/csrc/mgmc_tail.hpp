@@ -23,12 +23,16 @@
 //    after it w = B^T x by one wavefront per column (lr_wave_dot's order) and x -= B_bar w, f restored;
 //    before a residual f -= B (Sigma^{-1} B^T x), restored after the restriction
 //    (sor_sampler.cc:48-56, sor_smoother.cc:41-53, linear_operator.hh:66-76).
-// LDS layout per level: the (nx+1)(ny+1)(nz+1) vertices including the zero boundary, x fastest, no
-// padding; one scratch array (right hand sides / residuals) of the largest tail level; the saved f
+// LDS layout per level: the (nx+1)(ny+1)(nz+1) vertices including the zero boundary, x fastest, rows
+// unpadded, 3D planes padded to 8 (mod 16) doubles (tail_layout, mgmc_capi.hip); one scratch array (right hand sides / residuals) of the largest tail level; the saved f
 // on the rows of B of every low-rank level.
 #pragma once
 #include "mgmc_kernels.hpp"
 #include "mgmc_lowrank.hpp"
+
+#ifndef MGMC_TAIL_EXP
+#define MGMC_TAIL_EXP 0
+#endif
 
 namespace mgmc {
 
@@ -45,7 +49,7 @@ struct TailOp {
 };
 
 struct TailLevel {
-    Layout G;      // LDS layout (off 0, sx = nx+1, sp = sx (ny+1))
+    Layout G;      // LDS layout (off 0, sx = nx+1, sp = sx (ny+1), 3D padded to 8 mod 16)
     int ox, of;    // LDS offsets (doubles) of x and f
     int ncolours;
     double sd, wd; // sqrt(diag (2-omega)/omega), omega/diag
@@ -183,9 +187,14 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             const int j = row % (G.ny - 1) + 1, k = DIM == 3 ? row / (G.ny - 1) + 1 : 0;
             const int i0 = 2 * m + 1;
             if (i0 > G.nx - 1) continue;
-            const Philox4 rnd = philox4x32_10(pair_id<DIM>(G, i0, j, k), tag, s_lo, s_hi, key.k0, key.k1);
             double z0, z1;
+#if MGMC_TAIL_EXP == 1  // timing experiment only (wrong samples): no Philox / Box-Muller in the tail
+            z0 = 1e-3 * (double)(q & 7);
+            z1 = 1e-3 * (double)(tag & 7);
+#else
+            const Philox4 rnd = philox4x32_10(pair_id<DIM>(G, i0, j, k), tag, s_lo, s_hi, key.k0, key.k1);
             normal_pair(rnd, &z0, &z1);
+#endif
             const int p = (int)G.at(i0, j, k);
             scr[p] = fma(t.sd, z0, f[p]);
             if (i0 + 1 <= G.nx - 1) scr[p + 1] = fma(t.sd, z1, f[p + 1]);
@@ -200,18 +209,24 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             const int cj = fj > G.ny - 1 ? 0 : (G.ny - 1 - fj) / 2 + 1;
             const int ck = DIM == 3 ? (fk > G.nz - 1 ? 0 : (G.nz - 1 - fk) / 2 + 1) : 1;
             // small classes (<= 8 x 8 x 16, 2D 32 x 32 vertices): thread bits are the class
-            // coordinates, no index division on the pass's critical path
+            // coordinates, no index division on the pass's critical path.  3D: tid = ti | tk0 << 3 |
+            // tj << 4 | (tk >> 1) << 7, so a half-wave holds class planes tk and tk+1 (vertex planes
+            // 2 apart, 16 bank pairs apart with the padded plane stride of tail_layout): 2-way banks
             const bool fast = DIM == 3 ? (ci <= 8 && cj <= 8 && ck * 64 <= nt) : (ci <= 32 && cj * 32 <= nt);
+#if MGMC_TAIL_EXP == 2  // timing experiment only: colour passes reduced to their barriers
+            if (false) {
+#else
             if (fast) {
+#endif
                 const int ti = DIM == 3 ? (tid & 7) : (tid & 31);
-                const int tj = DIM == 3 ? ((tid >> 3) & 7) : (tid >> 5);
-                const int tk = DIM == 3 ? (tid >> 6) : 0;
+                const int tj = DIM == 3 ? ((tid >> 4) & 7) : (tid >> 5);
+                const int tk = DIM == 3 ? (((tid >> 3) & 1) | ((tid >> 7) << 1)) : 0;
                 if (ti < ci && tj < cj && tk < ck) {
                     const int p = (int)G.at(fi + 2 * ti, fj + 2 * tj, DIM == 3 ? fk + 2 * tk : 0);
                     const double res = stencil_fma<DIM, NPTS>(x, p, G, t.S);
                     x[p] = fma(t.wd, scr[p] - res, x[p]);
                 }
-            } else {
+            } else if (MGMC_TAIL_EXP != 2) {
                 for (int q = tid; q < ci * cj * ck; q += nt) {
                     const int i = fi + 2 * (q % ci), r = q / ci;
                     const int j = fj + 2 * (r % cj), k = DIM == 3 ? fk + 2 * (r / cj) : 0;

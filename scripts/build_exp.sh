@@ -39,4 +39,9 @@ done
 for w in ${LRSW:-}; do
   $HIPX -DLRS_MAX_WAVES=$w -o ../../build/libmgmc_expw$w.so $SRCS &
 done
+# k_tail timing builds (MGMC_TAIL_EXP, mgmc_tail.hpp): 1 no noise draws, 2 no colour-pass updates
+# (build/libmgmc_expt<N>.so; wrong samples, timing only)
+for n in ${TAILEXPS:-}; do
+  $HIPX -DMGMC_TAIL_EXP=$n -o ../../build/libmgmc_expt$n.so $SRCS &
+done
 wait
