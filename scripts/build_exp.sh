@@ -44,4 +44,8 @@ done
 for n in ${TAILEXPS:-}; do
   $HIPX -DMGMC_TAIL_EXP=$n -o ../../build/libmgmc_expt$n.so $SRCS &
 done
+# coarse SSOR kernel timing build (MGMC_COARSE_EXP=1: no noise draws; build/libmgmc_expc1.so)
+for n in ${COARSEEXPS:-}; do
+  $HIPX -DMGMC_COARSE_EXP=$n -o ../../build/libmgmc_expc$n.so $SRCS &
+done
 wait
