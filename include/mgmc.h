@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MGMC_ABI_VERSION 4
+#define MGMC_ABI_VERSION 5
 
 /* error codes */
 #define MGMC_OK 0
@@ -139,6 +139,13 @@ typedef struct mgmc_operator_desc {
 int mgmc_operator_csr_size(const mgmc_operator_desc* d, int64_t* nrow, int64_t* nnz);
 /* fill rowptr[nrow + 1], col[nnz], val[nnz] */
 int mgmc_operator_csr(const mgmc_operator_desc* d, int64_t* rowptr, int32_t* col, double* val);
+
+/* The colouring mgmc_create_csr gives a level with this matrix (ABI 5; host only): 2 (red-black, a
+ * fine level whose couplings are all axis neighbours), 4 / 8 (coordinate parities, other reach-1
+ * levels) or 9 / 27 (coordinates mod 3, reach-2 levels).  cfg gives the level's lattice; level 0 is
+ * the fine level.  Same validation as mgmc_create_csr. */
+int mgmc_csr_colour_scheme(const mgmc_config* cfg, int level, int64_t nrow, const int64_t* rowptr, const int32_t* col,
+                           int* scheme);
 
 /* ---- lifetime ---- */
 int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chain_id, mgmc_handle** out);

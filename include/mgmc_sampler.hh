@@ -17,6 +17,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <memory>
 #include <string>
 #include <vector>
@@ -87,10 +88,12 @@ class HipMultigridMCSampler {
     mgmc_handle* handle() const { return h_.get(); }
 
     // Sampler::apply(f, x): x in/out on the host (PCIe inclusive).  Without a fixed rhs, f is uploaded
-    // and used.  After fix_rhs (the promise of Sampler::fix_rhs, sampler/sampler.hh:49-56, kept as
-    // CholeskySampler::apply keeps g_rhs) the fixed rhs is used and f is not read (nullptr is fine).
+    // and used.  After fix_rhs, f = nullptr or a vector equal to the fixed one skips the upload; any
+    // other f is used, as the reference uses the f it is given (MultigridMCSampler keeps
+    // Sampler::fix_rhs a no-op, sampler/sampler.hh:56), and becomes the resident fixed rhs.
     // multigridmc_amd/sampler.py MultigridMCSampler.apply behaves the same.
-    void apply(const double* f, double* x) const {
+    void apply(const double* f, double* x) const {  // const like Sampler::apply (sampler.hh:41)
+        if (rhs_fixed_ && f && std::memcmp(f, fixed_.data(), ndof_ * sizeof(double)) != 0) set_fixed(f);
         if (rhs_fixed_) {
             check(mgmc_set_state(h_.get(), x, ndof_), h_.get(), "mgmc_set_state");
             check(mgmc_sample(h_.get(), 1, -1, nullptr), h_.get(), "mgmc_sample");
@@ -99,11 +102,11 @@ class HipMultigridMCSampler {
             check(mgmc_apply(h_.get(), f, x, ndof_), h_.get(), "mgmc_apply");
         }
     }
-    void fix_rhs(const double* f) {
-        check(mgmc_set_rhs(h_.get(), f, ndof_), h_.get(), "mgmc_set_rhs");
-        rhs_fixed_ = true;
+    void fix_rhs(const double* f) { set_fixed(f); }
+    void unfix_rhs() {
+        rhs_fixed_ = false;
+        fixed_.clear();
     }
-    void unfix_rhs() { rhs_fixed_ = false; }
     // Posterior operator (MeasuredOperator, measured_operator.cc:9-49): B as CSC (m columns, rows
     // ascending), Sigma diagonal; m = 0 drops it.  Sets up every level's B_bar (sor_smoother.cc:17-37).
     void set_lowrank(int m, const int64_t* colptr, const int64_t* rows, const double* vals, const double* sigma) {
@@ -136,7 +139,15 @@ class HipMultigridMCSampler {
     };
     std::unique_ptr<mgmc_handle, Deleter> h_;
     size_t ndof_ = 0;
-    bool rhs_fixed_ = false;
+    // the fixed rhs: resident in HBM plus a host copy that apply compares its f with (mutable like the
+    // reference sampler's scratch, sampler/multigridmc_sampler.hh:66-72)
+    mutable bool rhs_fixed_ = false;
+    mutable std::vector<double> fixed_;
+    void set_fixed(const double* f) const {
+        check(mgmc_set_rhs(h_.get(), f, ndof_), h_.get(), "mgmc_set_rhs");
+        fixed_.assign(f, f + ndof_);
+        rhs_fixed_ = true;
+    }
 };
 
 // Deterministic multicolour SOR smoother on level `level` of a sampler's hierarchy

@@ -19,9 +19,11 @@ from .sampler import (  # noqa: F401
     ShiftedLaplaceFDOperator,
     ShiftedLaplaceFEMOperator,
     SquaredShiftedLaplaceFDOperator,
+    SparseMatrixOperator,
     ConstantCorrelationLengthModel,
     PeriodicCorrelationLengthModel,
     comm_unique_id,
+    csr_colour_scheme,
     describe,
     make_config,
     measurement_vector_index,

@@ -29,7 +29,7 @@ OPERATOR_SQUARED_FD = 2
 KAPPA_CONSTANT = 0
 KAPPA_PERIODIC = 1
 KAPPA_GIVEN = 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 SOLVER_LOOP = 0
 SOLVER_CG = 1
 FORWARD = 1
@@ -82,6 +82,8 @@ SIGNATURES = [
                                 c_uint64, c_uint64, POINTER(c_void_p)]),
     ("mgmc_operator_csr_size", c_int, [POINTER(MgmcOperatorDesc), POINTER(c_int64), POINTER(c_int64)]),
     ("mgmc_operator_csr", c_int, [POINTER(MgmcOperatorDesc), POINTER(c_int64), POINTER(ctypes.c_int32), _DP]),
+    ("mgmc_csr_colour_scheme", c_int, [POINTER(MgmcConfig), c_int, c_int64, POINTER(c_int64), POINTER(ctypes.c_int32),
+                                       POINTER(c_int)]),
     ("mgmc_create_batch", c_int, [POINTER(MgmcConfig), c_int, c_uint64, c_uint64, c_int, POINTER(c_void_p)]),
     ("mgmc_create_csr_batch", c_int, [POINTER(MgmcConfig), c_int64, POINTER(c_int64), POINTER(ctypes.c_int32), _DP,
                                       c_int, c_uint64, c_uint64, c_int, POINTER(c_void_p)]),

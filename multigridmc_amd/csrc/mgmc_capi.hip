@@ -1665,6 +1665,14 @@ struct FieldHost {
     double centre[27];
 };
 
+// the colouring of a matrix level (the oracle's init_colouring): 3^d classes (coordinates mod 3) for
+// reach-2 couplings, red-black for a fine level whose couplings are all axis neighbours, 2^d
+// coordinate parities otherwise
+static int colour_scheme(int dim, int level, int reach, bool axis_only) {
+    if (reach >= 2) return dim == 3 ? 27 : 9;
+    return (level == 0 && axis_only) ? 2 : (1 << dim);
+}
+
 FieldHost make_field(const CsrHost& A, int dim, const int* n, int level) {
     FieldHost F;
     const int64_t nxi = n[0] - 1, nyi = n[1] - 1;
@@ -1699,7 +1707,14 @@ FieldHost make_field(const CsrHost& A, int dim, const int* n, int level) {
         if (k == key(0, 0, 0)) F.diag = F.np;
         ++F.np;
     }
-    F.scheme = reach >= 2 ? (dim == 3 ? 27 : 9) : ((level == 0 && maxnnz <= 2 * dim + 1) ? 2 : (1 << dim));
+    // red-black only when every coupling is an axis neighbour (the 5/7-point pattern): a row of at
+    // most 2d+1 entries that couples diagonal neighbours ((+-1, +-1), edge neighbours in 3D) would
+    // put coupled vertices into one colour
+    bool axis_only = true;
+    for (int k = 0; k < 125; ++k)
+        if (present[k] && std::abs(k % 5 - 2) + std::abs((k / 5) % 5 - 2) + std::abs(k / 25 - 2) > 1) axis_only = false;
+    (void)maxnnz;
+    F.scheme = colour_scheme(dim, level, reach, axis_only);
     F.coef.assign((size_t)A.nrow * F.np, 0.0);
     for (int64_t r = 0; r < A.nrow; ++r) {
         int a[3], b[3];
@@ -1928,11 +1943,49 @@ int mgmc_create_csr(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr,
     return mgmc_create_csr_batch(cfg, nrow, rowptr, col, val, device, seed, chain_id, 1, out);
 }
 
+// the matrix's shape against cfg's lattice, before anything reads rowptr[nrow] or copies entries:
+// nrow = the interior vertex count, rowptr non-decreasing from 0, at most 125 entries per row (the
+// 5^d box of reach-2 couplings)
+static std::string check_csr_shape(const mgmc_config& cfg, int64_t nrow, const int64_t* rowptr) {
+    const std::string err = validate_config(cfg);
+    if (!err.empty()) return err;
+    int64_t expect = (int64_t)(cfg.nx - 1) * (cfg.ny - 1);
+    if (cfg.dim == 3) expect *= (cfg.nz - 1);
+    if (nrow != expect)
+        return "nrow " + std::to_string(nrow) + " != the lattice's " + std::to_string(expect) + " interior vertices";
+    if (rowptr[0] != 0) return "rowptr[0] != 0";
+    for (int64_t r = 0; r < nrow; ++r) {
+        const int64_t len = rowptr[r + 1] - rowptr[r];
+        if (len < 1 || len > 125) return "row " + std::to_string(r) + " has " + std::to_string(len) + " entries";
+    }
+    return "";
+}
+
+int mgmc_csr_colour_scheme(const mgmc_config* cfg, int level, int64_t nrow, const int64_t* rowptr, const int32_t* col,
+                           int* scheme) {
+    if (!cfg || !rowptr || !col || !scheme || nrow < 1 || level < 0) return fail(nullptr, MGMC_E_INVALID, "null argument");
+    mgmc_config c = *cfg;
+    c.nlevel = 1;
+    const std::string e0 = check_csr_shape(c, nrow, rowptr);
+    if (!e0.empty()) return fail(nullptr, MGMC_E_INVALID, "mgmc_csr_colour_scheme: " + e0);
+    CsrHost A;
+    A.nrow = nrow;
+    A.rowptr.assign(rowptr, rowptr + nrow + 1);
+    A.col.assign(col, col + rowptr[nrow]);
+    A.val.assign((size_t)rowptr[nrow], 1.0);
+    const int n[3] = {cfg->nx, cfg->ny, cfg->dim == 3 ? cfg->nz : 1};
+    const std::string e = check_lattice_csr(cfg->dim, n, A);
+    if (!e.empty()) return fail(nullptr, MGMC_E_INVALID, "mgmc_csr_colour_scheme: " + e);
+    *scheme = make_field(A, cfg->dim, n, level).scheme;
+    return MGMC_OK;
+}
+
 int mgmc_create_csr_batch(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr, const int32_t* col,
                           const double* val, int device, uint64_t seed, uint64_t chain0, int nchains,
                           mgmc_handle** out) {
     if (!cfg || !rowptr || !col || !val || !out || nrow < 1) return fail(nullptr, MGMC_E_INVALID, "null argument");
-    if (rowptr[0] != 0 || rowptr[nrow] < nrow) return fail(nullptr, MGMC_E_INVALID, "mgmc_create_csr: invalid row pointer");
+    const std::string e0 = check_csr_shape(*cfg, nrow, rowptr);
+    if (!e0.empty()) return fail(nullptr, MGMC_E_INVALID, "mgmc_create_csr: " + e0);
     mgmc_config c = *cfg;  // the matrix replaces kappa^2 and the fine-operator choice
     c.kappa_sq = 0.0;
     c.fine_operator = MGMC_OPERATOR_FD;

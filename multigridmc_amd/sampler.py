@@ -227,6 +227,54 @@ class SquaredShiftedLaplaceFDOperator(ShiftedLaplaceFDOperator):
         return True
 
 
+class SparseMatrixOperator(ShiftedLaplaceFDOperator):
+    """Any LinearOperator given by its matrix A_sparse (linear_operator.hh:187) on a lattice: CSR with
+    interior vertices as rows (x fastest), columns strictly ascending, a positive diagonal and
+    couplings at most two vertices apart.  The device takes the matrix path (mgmc_create_csr): the
+    Galerkin levels R A R^T are formed on the host, the colouring follows the couplings
+    (csr_colour_scheme).  This is what the reference-side adapter feeds from get_sparse()
+    (INTEGRATION.md)."""
+
+    def __init__(self, lattice: Lattice, A):
+        import scipy.sparse as sp
+        A = sp.csr_matrix(A)
+        A.sort_indices()
+        n = lattice.Nvertex
+        if A.shape != (n, n):
+            raise ValueError(f"matrix is {A.shape}, the lattice has {n} interior vertices")
+        self.lattice = lattice
+        self.correlation_model = None
+        self.kappa_sq = 0.0
+        self._csr = (A.indptr.astype(np.int64), A.indices.astype(np.int32), A.data.astype(np.float64))
+
+    @property
+    def variable_coefficients(self) -> bool:
+        return True
+
+    def get_csr(self):
+        return self._csr
+
+
+def csr_colour_scheme(lattice: Lattice, rowptr, col, level: int = 0) -> int:
+    """Colour classes the device sweeps a matrix level with (mgmc_csr_colour_scheme, host only):
+    2 (red-black: all couplings axis neighbours, fine level only), 2^d (coordinate parities) or
+    3^d (coordinates mod 3: couplings two vertices apart)."""
+    lib = load_library()
+    c = MgmcConfig()
+    c.dim = lattice.dim
+    c.nx, c.ny = lattice.shape[0], lattice.shape[1]
+    c.nz = lattice.shape[2] if lattice.dim == 3 else 0
+    c.nlevel, c.cycle, c.npresmooth, c.npostsmooth, c.ncoarsesmooth = 1, 1, 1, 1, 1
+    c.omega, c.coarse_scaling = 1.0, 1.0
+    rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+    col = np.ascontiguousarray(col, dtype=np.int32)
+    out = ctypes.c_int()
+    check(lib.mgmc_csr_colour_scheme(ctypes.byref(c), int(level), len(rowptr) - 1,
+                                     rowptr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                     col.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ctypes.byref(out)))
+    return out.value
+
+
 def measurement_vector_index(lattice: Lattice, x0, radius: float = 0.0) -> int:
     """Index of the radius-0 measurement vector (measured_operator.cc:74-91): the interior vertex
     nearest to x0.  The distance is separable, so the nearest vertex is found per direction;
@@ -399,10 +447,15 @@ class MultigridMCSampler:
 
     def apply(self, f, x: np.ndarray):
         """Draw a new sample x (in/out), one MGMC cycle (MultigridMCSampler::apply,
-        multigridmc_sampler.cc:132-138).  Without a fixed rhs f is uploaded and used; after fix_rhs
-        the fixed rhs is used and f is not read (pass None or the fixed vector)."""
+        multigridmc_sampler.cc:132-138).  Without a fixed rhs f is uploaded and used.  After fix_rhs,
+        f = None or a vector equal to the fixed one skips the upload; any other f is used, as the
+        reference uses the f it is given (MultigridMCSampler keeps Sampler::fix_rhs a no-op), and
+        becomes the resident fixed rhs."""
         if not (isinstance(x, np.ndarray) and x.dtype == np.float64 and x.flags.c_contiguous and x.shape == (self.ndof,)):
             raise ValueError("x must be a contiguous float64 array of length ndof")
+        if self._fixed_rhs is not None and f is not None and not np.array_equal(_as_f64(f, self.ndof, "f"),
+                                                                                 self._fixed_rhs):
+            self.fix_rhs(f)
         if self._fixed_rhs is not None:
             self._chk(self.lib.mgmc_set_state(self.handle, _dp(x), self.ndof))
             self._chk(self.lib.mgmc_sample(self.handle, 1, -1, None))

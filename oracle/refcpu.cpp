@@ -32,7 +32,7 @@
 //                 arithmetic).  This replays the device chain bit for bit; it is written
 //                 independently of multigridmc_amd/csrc.  Tier T2.
 //
-// Build: oracle/Makefile (g++ -O2 -ffp-contract=off, shared library + cpu baseline binary).
+// Build: oracle/Makefile (g++ -O3 -ffp-contract=off -fopenmp, shared library; threads default to 1).
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -50,6 +50,34 @@
 #include "log_table_oracle.h"
 
 namespace orc {
+
+// Worker threads of the oracle's row-parallel loops (orc_set_threads; default 1 = serial, and the
+// CPU baseline never changes it).  Only loops whose iterations are independent are split -- rows of
+// an SpMV, vertices of one colour class, coarse points of a restriction, fine planes of a
+// prolongation -- and every element is produced by the same operation sequence whatever the thread
+// count, so a threaded oracle gives bitwise the serial oracle's results.  This is what makes the
+// headline 512^3 hierarchy checkable in a GPU test (tests/test_gpu_headline.py).
+static int g_threads = 1;
+template <class F>
+static void par_for(int64_t n, F&& f) {
+    if (g_threads <= 1 || n < 8192) {
+        for (int64_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+#pragma omp parallel for num_threads(g_threads) schedule(static)
+    for (int64_t i = 0; i < n; ++i) f(i);
+}
+template <class F>
+static int64_t par_max(int64_t n, F&& f) {
+    int64_t m = 0;
+    if (g_threads <= 1 || n < 8192) {
+        for (int64_t i = 0; i < n; ++i) m = std::max(m, (int64_t)f(i));
+        return m;
+    }
+#pragma omp parallel for num_threads(g_threads) schedule(static) reduction(max : m)
+    for (int64_t i = 0; i < n; ++i) m = std::max(m, (int64_t)f(i));
+    return m;
+}
 
 // =============================================================================================
 // Lattice (lattice/lattice1d.hh, lattice2d.hh, lattice3d.hh): n cells -> (n-1)^d interior
@@ -133,11 +161,30 @@ struct CSR {
 // y = A x with Eigen's ColMajor accumulation order: y_i = ((0 + a_i,j1 x_j1) + a_i,j2 x_j2) ...
 // with j ascending (A symmetric, so the row-wise ascending sum is the same sequence)
 static void spmv(const CSR& A, const double* x, double* y) {
-    for (int64_t r = 0; r < A.nrow; ++r) {
+    par_for(A.nrow, [&](int64_t r) {
         double s = 0.0;
         for (int64_t q = A.rowptr[r]; q < A.rowptr[r + 1]; ++q) s += A.val[q] * x[A.col[q]];
         y[r] = s;
-    }
+    });
+}
+
+// CSR from a per-row builder row(ell, cols, vals) -> count (entries sorted by column, at most 27):
+// counts first, then every row written at its offset (row-parallel, same entries as a serial build)
+template <class RowFn>
+static CSR csr_from_rows(int64_t nrow, RowFn&& row) {
+    CSR A;
+    A.nrow = A.ncol = nrow;
+    A.rowptr.assign(nrow + 1, 0);
+    par_for(nrow, [&](int64_t ell) {
+        int32_t c[27];
+        double v[27];
+        A.rowptr[ell + 1] = row(ell, c, v);
+    });
+    for (int64_t r = 0; r < nrow; ++r) A.rowptr[r + 1] += A.rowptr[r];
+    A.col.resize((size_t)A.rowptr[nrow]);
+    A.val.resize((size_t)A.rowptr[nrow]);
+    par_for(nrow, [&](int64_t ell) { row(ell, A.col.data() + A.rowptr[ell], A.val.data() + A.rowptr[ell]); });
+    return A;
 }
 
 // C = A * B (Gustavson, dense accumulator, sorted output)
@@ -235,15 +282,11 @@ static CSR fd_operator(const Lattice& lat, const KappaModel& kappa) {
         hinv2[d] = 1. / (h * h);
         cell_volume *= h;
     }
-    CSR A;
-    const int64_t nrow = lat.nvertex();
-    A.nrow = A.ncol = nrow;
-    A.rowptr.assign(nrow + 1, 0);
-    A.col.reserve((size_t)nrow * (2 * dim + 1));
-    A.val.reserve((size_t)nrow * (2 * dim + 1));
-    std::vector<std::pair<int64_t, double>> row;
-    for (int64_t ell = 0; ell < nrow; ++ell) {
-        row.clear();
+    // triplets of one row (shifts in (d, -/+) order, then the diagonal), sorted by column as
+    // setFromTriplets leaves them (columns are distinct)
+    auto row = [&](int64_t ell, int32_t* cols, double* vals) -> int64_t {
+        std::pair<int64_t, double> r[7];
+        int cnt = 0;
         double xv[3] = {0, 0, 0};
         vertex_coords(lat, ell, xv);
         double diagonal = cell_volume * kappa(xv, dim);
@@ -252,21 +295,21 @@ static CSR fd_operator(const Lattice& lat, const KappaModel& kappa) {
                 int s[3] = {0, 0, 0};
                 s[d] = 2 * j - 1;
                 int64_t e;
-                if (lat.shifted(ell, s, e)) row.push_back({e, -cell_volume * hinv2[d]});
+                if (lat.shifted(ell, s, e)) r[cnt++] = {e, -cell_volume * hinv2[d]};
             }
             diagonal += 2. * cell_volume * hinv2[d];
         }
-        row.push_back({ell, diagonal});
-        std::sort(row.begin(), row.end(), [](const std::pair<int64_t, double>& a, const std::pair<int64_t, double>& b) {
+        r[cnt++] = {ell, diagonal};
+        std::sort(r, r + cnt, [](const std::pair<int64_t, double>& a, const std::pair<int64_t, double>& b) {
             return a.first < b.first;
         });
-        for (auto& e : row) {
-            A.col.push_back((int32_t)e.first);
-            A.val.push_back(e.second);
+        for (int q = 0; q < cnt; ++q) {
+            cols[q] = (int32_t)r[q].first;
+            vals[q] = r[q].second;
         }
-        A.rowptr[ell + 1] = (int64_t)A.col.size();
-    }
-    return A;
+        return cnt;
+    };
+    return csr_from_rows(lat.nvertex(), row);
 }
 
 // ShiftedLaplaceFEMOperator with constant kappa^2 (shiftedlaplace_fem_operator.cc:9-145): sparsity
@@ -456,6 +499,7 @@ struct Intergrid {
     int stencil_size = 0;
     std::vector<double> matrix;
     std::vector<int64_t> colidx;
+    std::vector<int> shift_last;  // shift of stencil entry k in the last dimension
     explicit Intergrid(const Lattice& lat) : fine(lat), coarse(lat.coarse()) {
         const int dim = lat.dim;
         stencil_size = (int)lround(pow(3, dim));
@@ -473,10 +517,11 @@ struct Intergrid {
             }
             matrix.push_back(m);
             shift.push_back(s);
+            shift_last.push_back(s[dim - 1]);
         }
         const int64_t nc = coarse.nvertex();
         colidx.resize((size_t)nc * stencil_size);
-        for (int64_t ec = 0; ec < nc; ++ec) {
+        par_for(nc, [&](int64_t ec) {
             int idx[3];
             coarse.lin2euc(ec, idx);
             for (int d = 0; d < dim; ++d) idx[d] *= 2;
@@ -489,22 +534,51 @@ struct Intergrid {
                 }
                 colidx[(size_t)ec * stencil_size + j] = e;
             }
-        }
+        });
     }
     void restrict_(const double* x, double* xc) const {
-        const int64_t nc = coarse.nvertex();
-        for (int64_t ec = 0; ec < nc; ++ec) {
+        par_for(coarse.nvertex(), [&](int64_t ec) {
             double result = 0;
             for (int k = 0; k < stencil_size; ++k) result += matrix[k] * x[colidx[(size_t)ec * stencil_size + k]];
             xc[ec] = result;
-        }
+        });
     }
+    // The reference's scatter (coarse index ascending, then k).  Split by the fine vertices' last
+    // coordinate p: the targets on fine plane (2D: row) p come from the coarse planes kc with
+    // 2 kc + s = p, visited in ascending kc, each in ascending ec, taking the k whose last shift is
+    // s.  Each fine vertex therefore receives its terms in the serial order (one per (ec, k)).
     void prolongate_add(double alpha, const double* xc, double* x) const {
+        const int dim = fine.dim;
         const int64_t nc = coarse.nvertex();
-        for (int64_t ec = 0; ec < nc; ++ec) {
-            const double v = xc[ec];
-            for (int k = 0; k < stencil_size; ++k) x[colidx[(size_t)ec * stencil_size + k]] += alpha * matrix[k] * v;
+        const int ncl = coarse.n[dim - 1];       // coarse planes 1 .. ncl-1
+        const int64_t cplane = nc / (ncl - 1);  // coarse points per plane
+        auto plane = [&](int64_t pi) {
+            const int p = (int)pi + 1;  // fine plane 1 .. nfl-1
+            for (int kc = (p - 1) / 2; kc <= (p + 1) / 2; ++kc) {
+                if (kc < 1 || kc > ncl - 1) continue;
+                const int s = p - 2 * kc;
+                if (s < -1 || s > 1) continue;
+                for (int64_t ec = (int64_t)(kc - 1) * cplane; ec < (int64_t)kc * cplane; ++ec) {
+                    const double v = xc[ec];
+                    for (int k = 0; k < stencil_size; ++k)
+                        if (shift_last[k] == s) x[colidx[(size_t)ec * stencil_size + k]] += alpha * matrix[k] * v;
+                }
+            }
+        };
+        if (g_threads <= 1) {  // the reference's loop as written
+            for (int64_t ec = 0; ec < nc; ++ec) {
+                const double v = xc[ec];
+                for (int k = 0; k < stencil_size; ++k) x[colidx[(size_t)ec * stencil_size + k]] += alpha * matrix[k] * v;
+            }
+            return;
         }
+        const int nfl = fine.n[dim - 1];
+        if (nfl - 1 < 64) {
+            for (int64_t pi = 0; pi < nfl - 1; ++pi) plane(pi);
+            return;
+        }
+#pragma omp parallel for num_threads(g_threads) schedule(static, 1)
+        for (int64_t pi = 0; pi < nfl - 1; ++pi) plane(pi);
     }
     CSR to_sparse() const {
         CSR R;
@@ -557,13 +631,10 @@ static inline int sidx(int dim, int dx, int dy, int dz) {
 }
 
 static CSR stencil_csr(const Lattice& lat, const double st[27]) {
-    CSR A;
-    const int64_t nrow = lat.nvertex();
     const int dim = lat.dim;
-    A.nrow = A.ncol = nrow;
-    A.rowptr.assign(nrow + 1, 0);
     const int zr = dim == 3 ? 1 : 0, yr = dim >= 2 ? 1 : 0;
-    for (int64_t ell = 0; ell < nrow; ++ell) {
+    return csr_from_rows(lat.nvertex(), [&](int64_t ell, int32_t* cols, double* vals) -> int64_t {
+        int64_t cnt = 0;
         for (int dz = -zr; dz <= zr; ++dz)
             for (int dy = -yr; dy <= yr; ++dy)
                 for (int dx = -1; dx <= 1; ++dx) {
@@ -572,13 +643,12 @@ static CSR stencil_csr(const Lattice& lat, const double st[27]) {
                     int s[3] = {dx, dy, dz};
                     int64_t e;
                     if (lat.shifted(ell, s, e)) {
-                        A.col.push_back((int32_t)e);
-                        A.val.push_back(v);
+                        cols[cnt] = (int32_t)e;
+                        vals[cnt++] = v;
                     }
                 }
-        A.rowptr[ell + 1] = (int64_t)A.col.size();
-    }
-    return A;
+        return cnt;
+    });
 }
 
 static void stencil_of_interior_row(const CSR& A, const Lattice& lat, double st[27]) {
@@ -716,39 +786,49 @@ struct Ctx {
     uint32_t tag = 0;     // multicolour: running sweep tag within the current cycle
 };
 
-static int64_t max_row_nnz(const CSR& A) {
-    int64_t m = 0;
-    for (int64_t r = 0; r < A.nrow; ++r) m = std::max(m, A.rowptr[r + 1] - A.rowptr[r]);
-    return m;
-}
-
 // largest coordinate distance between coupled vertices (1 for 3^d-point operators, 2 for the
 // squared FD operator and its Galerkin levels)
 static int coupling_reach(const Level& L) {
-    int reach = 0, a[3], b[3];
-    for (int64_t r = 0; r < L.A.nrow; ++r) {
+    return (int)par_max(L.A.nrow, [&](int64_t r) {
+        int reach = 0, a[3], b[3];
         L.lat.lin2euc(r, a);
         for (int64_t q = L.A.rowptr[r]; q < L.A.rowptr[r + 1]; ++q) {
             L.lat.lin2euc(L.A.col[q], b);
             for (int d = 0; d < L.lat.dim; ++d) reach = std::max(reach, std::abs(a[d] - b[d]));
         }
-    }
-    return reach;
+        return reach;
+    });
 }
 
-// colour classes of the multicolour sweeps: red-black for a 5/7-point fine level, coordinate parities
-// (2^d colours) for reach-1 levels, coordinates mod 3 (3^d colours) for reach-2 levels
-static void init_colouring(Level& L, bool fd_level) {
+// 1 if some row couples two vertices that are not axis neighbours (|dx| + |dy| + |dz| > 1)
+static bool off_axis_coupling(const Level& L) {
+    return par_max(L.A.nrow, [&](int64_t r) {
+               int a[3], b[3];
+               L.lat.lin2euc(r, a);
+               for (int64_t q = L.A.rowptr[r]; q < L.A.rowptr[r + 1]; ++q) {
+                   L.lat.lin2euc(L.A.col[q], b);
+                   int taxi = 0;
+                   for (int d = 0; d < L.lat.dim; ++d) taxi += std::abs(a[d] - b[d]);
+                   if (taxi > 1) return 1;
+               }
+               return 0;
+           }) != 0;
+}
+
+// colour classes of the multicolour sweeps: red-black for a fine level whose couplings are all axis
+// neighbours (the 5/7-point FD pattern), coordinate parities (2^d colours) for other reach-1
+// levels, coordinates mod 3 (3^d colours) for reach-2 levels
+static void init_colouring(Level& L, bool fine_level) {
     const int64_t n = L.lat.nvertex();
     L.colour.resize(n);
     L.pair.resize(n);
     L.cos_branch.resize(n);
     const int dim = L.lat.dim;
     const bool mod3 = coupling_reach(L) >= 2;
-    if (mod3) fd_level = false;
+    bool fd_level = fine_level && !mod3 && !off_axis_coupling(L);
     L.ncolours = fd_level ? 2 : (mod3 ? (dim == 3 ? 27 : 9) : (1 << dim));
-    int idx[3];
-    for (int64_t e = 0; e < n; ++e) {
+    par_for(n, [&](int64_t e) {
+        int idx[3];
         L.lat.lin2euc(e, idx);
         if (fd_level)
             L.colour[e] = (idx[0] + idx[1] + idx[2]) & 1;
@@ -761,7 +841,7 @@ static void init_colouring(Level& L, bool fd_level) {
         if (dim == 3) row = (uint64_t)(idx[2] - 1) * (uint64_t)(L.lat.n[1] - 1) + (uint64_t)(idx[1] - 1);
         L.pair[e] = (uint32_t)(row * (uint64_t)(L.lat.n[0] / 2) + (uint64_t)((idx[0] - 1) >> 1));
         L.cos_branch[e] = (idx[0] & 1) ? 1 : 0;
-    }
+    });
 }
 
 // one SOR update of row ell (sor_smoother.cc:70-75), reference arithmetic
@@ -844,7 +924,7 @@ static void posterior_residual(const Level& L, const double* f, const double* x,
     const int64_t n = L.A.nrow;
     if (mode == FAITHFUL || L.lr.m == 0) {
         posterior_apply(L, x, r, mode);
-        for (int64_t q = 0; q < n; ++q) r[q] = f[q] - r[q];
+        par_for(n, [&](int64_t q) { r[q] = f[q] - r[q]; });
         return;
     }
     std::vector<double> t(L.lr.m), g(n);
@@ -894,10 +974,10 @@ struct SORSmoother {
     SORSmoother(const Level* L_, double omega_, Direction d) : L(L_), omega(omega_), direction(d) {
         diag.resize(L->A.nrow);
         wd.resize(L->A.nrow);
-        for (int64_t r = 0; r < L->A.nrow; ++r) {
+        par_for(L->A.nrow, [&](int64_t r) {
             diag[r] = L->A.diag(r);
             wd[r] = omega / diag[r];
-        }
+        });
     }
     // bar(B) = (L + D/omega)^{-1} B (Sigma + B^T (L + D/omega)^{-1} B)^{-1} (forward; L^T backward),
     // sor_smoother.cc:17-37.  The triangular solves: FAITHFUL = lexicographic substitution (the
@@ -969,8 +1049,10 @@ struct SORSmoother {
             const int nc = L->ncolours;
             for (int cc = 0; cc < nc; ++cc) {
                 const int colour = (direction == FORWARD) ? cc : nc - 1 - cc;
-                for (int64_t ell = 0; ell < nrow; ++ell)
+                // a colour class reads only other colours: its rows are independent
+                par_for(nrow, [&](int64_t ell) {
                     if (L->colour[ell] == colour) sor_row_fused(L->A, wd.data(), b, x, ell);
+                });
             }
         }
     }
@@ -997,8 +1079,7 @@ struct SORSampler : Sampler {
         const int64_t nrow = L->A.nrow;
         c_rhs.resize(nrow);
         sqrt_precision_diag.resize(nrow);
-        for (int64_t ell = 0; ell < nrow; ++ell)
-            sqrt_precision_diag[ell] = sqrt(smoother.diag[ell] * (2. - omega) / omega);
+        par_for(nrow, [&](int64_t ell) { sqrt_precision_diag[ell] = sqrt(smoother.diag[ell] * (2. - omega) / omega); });
     }
     void apply(const double* f, double* x) override {
         const int64_t n = (int64_t)c_rhs.size();
@@ -1021,8 +1102,10 @@ struct SORSampler : Sampler {
                 const uint32_t tag = ctx->tag++;
                 // low-rank noise first: f_eff = f + B Sigma^{-1/2} xi', xi'_k from Philox pair
                 // LR_PAIR0 + k/2 (cos for even k) of this sweep's tag; c = fma(sd, xi, f_eff)
-                std::vector<double> feff(f, f + n);
+                std::vector<double> feff;
+                const double* fe = f;
                 if (L->lr.m > 0) {
+                    feff.assign(f, f + n);
                     std::vector<double> sv(L->lr.m), e(n);
                     for (int k = 0; k < L->lr.m; ++k) {
                         double z0, z1;
@@ -1031,13 +1114,15 @@ struct SORSampler : Sampler {
                     }
                     lr_expand(*L, sv.data(), e.data());
                     for (int64_t ell = 0; ell < n; ++ell) feff[ell] = f[ell] + e[ell];
+                    fe = feff.data();
                 }
-                for (int64_t ell = 0; ell < n; ++ell) {
+                const uint64_t sample = ctx->sample;
+                par_for(n, [&](int64_t ell) {
                     double z0, z1;
-                    philox_normals(ctx->seed, ctx->chain, L->pair[ell], tag, ctx->sample, z0, z1);
+                    philox_normals(ctx->seed, ctx->chain, L->pair[ell], tag, sample, z0, z1);
                     const double xi = L->cos_branch[ell] ? z0 : z1;
-                    c_rhs[ell] = fma(sqrt_precision_diag[ell], xi, feff[ell]);
-                }
+                    c_rhs[ell] = fma(sqrt_precision_diag[ell], xi, fe[ell]);
+                });
             }
             smoother.apply(ctx->mode, c_rhs.data(), x);
         }
@@ -1193,9 +1278,9 @@ struct MGMC : Sampler {
         for (int level = 0; level < p.nlevel; ++level) {
             std::unique_ptr<Level> L(new Level());
             L->lat = lattice;
-            L->A = A;
+            L->A = std::move(A);  // every branch below assigns A before the next level
             // 2 colours for a 5/7-point fine level (FD), 2^d for 3^d-point levels (FEM, Galerkin)
-            if (lattice.dim >= 2) init_colouring(*L, level == 0 && max_row_nnz(L->A) <= 2 * lattice.dim + 1);
+            if (lattice.dim >= 2) init_colouring(*L, level == 0);
             x_ell.emplace_back(L->A.nrow, 0.0);
             f_ell.emplace_back(L->A.nrow, 0.0);
             r_ell.emplace_back(L->A.nrow, 0.0);
@@ -1361,6 +1446,10 @@ orc_handle* orc_create_csr(const orc_params* q, int mode, uint64_t seed, int64_t
 
 void orc_destroy(orc_handle* h) { delete h; }
 
+// worker threads of the row-parallel loops (see g_threads); results do not depend on it
+void orc_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
+int orc_get_threads(void) { return g_threads; }
+
 // the reference's fine operators (any correlation-length model) as CSR: pde 0 FD, 1 FEM, 2 squared
 // FD (2D); kmodel 0 constant (kappa^2 = 1 / pow(Lambda, 2)), 1 periodic (Lambda_min, Lambda_max)
 static CSR model_operator(int dim, const int* n, int pde, int kmodel, double Lambda, double Lmin, double Lmax) {
@@ -1403,6 +1492,17 @@ void orc_get_csr(orc_handle* h, int level, int64_t* rowptr, int32_t* col, double
     memcpy(rowptr, A.rowptr.data(), (A.nrow + 1) * sizeof(int64_t));
     memcpy(col, A.col.data(), A.col.size() * sizeof(int32_t));
     memcpy(val, A.val.data(), A.val.size() * sizeof(double));
+}
+
+// one row of a level's CSR (columns ascending): returns the entry count (<= 27 copied)
+int64_t orc_get_row(orc_handle* h, int level, int64_t row, int32_t* col, double* val) {
+    const CSR& A = h->mg->levels[level]->A;
+    const int64_t b = A.rowptr[row], e = A.rowptr[row + 1];
+    for (int64_t q = b; q < e && q - b < 27; ++q) {
+        col[q - b] = A.col[q];
+        val[q - b] = A.val[q];
+    }
+    return e - b;
 }
 
 void orc_set_rhs(orc_handle* h, const double* f) { std::copy(f, f + h->f.size(), h->f.begin()); }

@@ -43,10 +43,13 @@ def lib():
             "orc_create_csr": (c_void_p, [POINTER(OrcParams), c_int, c_uint64, c_int64, POINTER(c_int64),
                                           POINTER(c_int32), _DP]),
             "orc_destroy": (None, [c_void_p]),
+            "orc_set_threads": (None, [c_int]),
+            "orc_get_threads": (c_int, []),
             "orc_ndof": (c_int64, [c_void_p, c_int]),
             "orc_nlevel": (c_int, [c_void_p]),
             "orc_nnz": (c_int64, [c_void_p, c_int]),
             "orc_get_csr": (None, [c_void_p, c_int, POINTER(c_int64), POINTER(c_int32), _DP]),
+            "orc_get_row": (c_int64, [c_void_p, c_int, c_int64, POINTER(c_int32), _DP]),
             "orc_set_rhs": (None, [c_void_p, _DP]),
             "orc_set_state": (None, [c_void_p, _DP]),
             "orc_get_state": (None, [c_void_p, _DP]),
@@ -183,6 +186,13 @@ class Oracle:
                            col.ctypes.data_as(POINTER(c_int32)), dp(val))
         return sp.csr_matrix((val, col, rowptr), shape=(n, n))
 
+    def csr_row(self, level, row):
+        """(columns, values) of one row of a level's CSR, without copying the matrix."""
+        col = np.empty(27, dtype=np.int32)
+        val = np.empty(27)
+        k = int(self.L.orc_get_row(self.h, level, row, col.ctypes.data_as(POINTER(c_int32)), dp(val)))
+        return col[:k].copy(), val[:k].copy()
+
     def apply(self, f, x):
         f = np.ascontiguousarray(f, dtype=np.float64)
         self.L.orc_apply(self.h, dp(f), dp(x))
@@ -285,6 +295,20 @@ def operator_csr(shape, pde, periodic=False, Lambda=0.2, Lambda_min=0.2, Lambda_
     lib().orc_operator_csr(*args, rowptr.ctypes.data_as(POINTER(c_int64)), col.ctypes.data_as(POINTER(c_int32)),
                            dp(val))
     return rowptr, col, val
+
+
+def set_threads(n: int) -> None:
+    """Worker threads of the oracle's row-parallel loops (bitwise the same results; default 1)."""
+    lib().orc_set_threads(int(n))
+
+
+def cpu_share() -> int:
+    """Cores this process may use (affinity mask, capped by OMP_NUM_THREADS on the GPU box)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def philox_normals(seed, chain, pair0, n, tag, sample):

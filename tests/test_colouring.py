@@ -115,8 +115,10 @@ def test_matrix_levels_have_no_same_colour_coupling(op, shape, nlevel):
         off = C.row != C.col
         d = np.abs(xyz[:, C.col] - xyz[:, C.row]).max(axis=0)
         reach = int(d.max())
-        maxnnz = int(np.diff(A.indptr).max())
-        scheme = (27 if dim == 3 else 9) if reach >= 2 else (2 if level == 0 and maxnnz <= 2 * dim + 1 else 2 ** dim)
+        A.sort_indices()
+        scheme = mg.csr_colour_scheme(mg.Lattice(*n), A.indptr, A.indices, level)  # make_field's rule
+        assert scheme == ((27 if dim == 3 else 9) if reach >= 2 else (2 if level == 0 and dim * 2 + 1 >= int(
+            np.diff(A.indptr).max()) else 2 ** dim))
         schemes.append(scheme)
         col = _field_colour(scheme, xyz)
         clash = off & (col[C.row] == col[C.col])
@@ -137,3 +139,70 @@ def test_checker_catches_a_conflict():
     """The checker itself: red-black colouring of a 9-point (diagonal) stencil must be flagged."""
     offs = _offsets(2, np.ones(9))
     assert any(_stencil_colour(5, o) == _stencil_colour(5, (0, 0)) for o in offs)
+
+
+def _offset_csr(dim, shape, offsets, diag=10.0, off=-1.0):
+    """CSR on an interior-vertex lattice coupling every vertex to the given offsets (plus itself)."""
+    xyz = _coords(list(shape), dim)
+    n = xyz.shape[1]
+    fi = [v - 1 for v in shape]
+    rows, cols, vals = [], [], []
+    for o in [(0,) * dim] + list(offsets):
+        nb = xyz + np.array(o)[:, None]
+        ok = np.all((nb >= 1) & (nb <= np.array(fi)[:, None]), axis=0)
+        lin = sum((nb[d] - 1) * int(np.prod(fi[:d])) for d in range(dim))
+        rows.append(np.arange(n)[ok])
+        cols.append(lin[ok])
+        vals.append(np.full(int(ok.sum()), diag if not any(o) else off))
+    A = sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(n, n))
+    A.sort_indices()
+    return A
+
+
+@pytest.mark.parametrize("dim,shape,offsets,expect", [
+    (2, (16, 16), [(1, 1), (-1, -1), (1, -1), (-1, 1)], 4),                          # 5 entries, all diagonal
+    (3, (8, 8, 8), [(1, 1, 0), (-1, -1, 0), (0, 0, 1), (0, 0, -1), (1, 0, 0), (-1, 0, 0)], 8),  # 7 entries, 2 edge
+    (2, (16, 16), [(1, 0), (-1, 0), (0, 1), (0, -1)], 2),                            # the 5-point FD pattern
+    (3, (8, 8, 8), [(1, 0, 0), (-1, 0, 0), (0, 0, 2), (0, 0, -2)], 27),              # reach 2
+])
+def test_user_csr_colouring_has_no_same_colour_coupling(dim, shape, offsets, expect):
+    """A user matrix of at most 2d+1 entries per row is swept red-black only when every coupling is
+    an axis neighbour (diagonal couplings put coupled vertices in one red-black
+    colour).  The library's choice (mgmc_csr_colour_scheme = make_field's rule) has no clash."""
+    lat = mg.Lattice(*shape)
+    A = _offset_csr(dim, shape, offsets)
+    scheme = mg.csr_colour_scheme(lat, A.indptr, A.indices)
+    assert scheme == expect
+    xyz = _coords(list(shape), dim)
+    C = A.tocoo()
+    col = _field_colour(scheme, xyz)
+    assert not ((C.row != C.col) & (col[C.row] == col[C.col])).any()
+    # the same matrix on a coarse level never gets red-black
+    if expect == 2:
+        assert mg.csr_colour_scheme(lat, A.indptr, A.indices, level=1) == 2 ** dim
+
+
+def test_csr_shape_checked_before_reading_entries():
+    """mgmc_create_csr / mgmc_csr_colour_scheme validate nrow against the lattice and the row
+    pointer's monotonicity before reading rowptr[nrow] or copying entries."""
+    lat = mg.Lattice(8, 8)
+    A = _offset_csr(2, (8, 8), [(1, 0), (-1, 0), (0, 1), (0, -1)])
+    with pytest.raises(mg.MgmcError, match="interior vertices"):
+        mg.csr_colour_scheme(mg.Lattice(16, 8), A.indptr, A.indices)
+    bad = A.indptr.copy()
+    bad[5] = bad[4] - 1  # decreasing
+    with pytest.raises(mg.MgmcError, match="entries"):
+        mg.csr_colour_scheme(lat, bad, A.indices)
+    # mgmc_create_csr with a lattice of 105 interior vertices and a 49-row matrix: refused on the host
+    import ctypes
+    from multigridmc_amd import _native
+    lib = mg.load_library()
+    cfg = mg.make_config(mg.ShiftedLaplaceFDOperator(mg.Lattice(16, 8), 25.0), mg.MultigridParameters(nlevel=1))
+    h = ctypes.c_void_p()
+    rp = A.indptr.astype(np.int64)
+    ci = A.indices.astype(np.int32)
+    va = A.data.astype(np.float64)
+    rc = lib.mgmc_create_csr(ctypes.byref(cfg), len(rp) - 1, rp.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                             ci.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                             va.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 0, 1, 0, ctypes.byref(h))
+    assert rc == _native.MGMC_E_INVALID and b"mgmc_create_csr: nrow 49" in lib.mgmc_last_error(None)

@@ -1,0 +1,130 @@
+"""Parity at the headline configuration itself (-m gpu): BASELINE config 4, 3D 512^3, 7-level
+V-cycle, one chain -- the hierarchy bench.py times.
+
+The kernel instances this configuration selects exist only at this size (mgmc_capi.hip): the fine
+residual + restriction `k_zresrestrict<7,64,8,512>` (chosen when the coarse level has >= 16 K tile
+planes), the fused-prolongation post-sweep's 128-plane z chunks, the level-1 colour-pair passes at
+their full 128-pair row width and the 512^3 `k_tail`.  Every one of them is compared here bit for
+bit (np.array_equal) with the CPU oracle's MULTICOLOUR replay of the same hierarchy (the device's
+level stencils, Philox key (5418513, 0)).  The residual + restriction components are also the
+FAITHFUL arithmetic: with no low-rank part the oracle's residual is the reference's
+`A_sparse * x` then `f - r` (linear_operator.hh:66-76, multigridmc_sampler.cc:118-120), in CSR order.
+
+The oracle runs its row-parallel loops on the CPU share (tests/oracle_lib.set_threads; bitwise the
+serial oracle's results): setup about 30 s and 4-8 s per cycle on 16 cores.  Progress lines go to
+the real stderr so a long step is visibly alive.
+"""
+import sys
+import time
+
+import numpy as np
+import pytest
+
+import multigridmc_amd as mg
+from tests import oracle_lib as O
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
+
+SEED = 5418513
+SHAPE = (512, 512, 512)
+NLEVEL = 7
+
+
+def _log(msg):
+    sys.__stderr__.write(f"[headline 512^3] {msg}\n")
+    sys.__stderr__.flush()
+
+
+@pytest.fixture(scope="module")
+def headline(hip_device):
+    t0 = time.time()
+    lat = mg.Lattice(*SHAPE)
+    p = mg.MultigridParameters(nlevel=NLEVEL, smoother="SOR", coarse_solver="SSOR", npresmooth=1, npostsmooth=1,
+                               ncoarsesmooth=1, omega=1.0, cycle=1, coarse_scaling=1.0)
+    s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), SEED, p, device=0, chain_id=0)
+    st = np.concatenate([s.level_desc(level)["stencil"] for level in range(NLEVEL)])
+    _log(f"device handle {time.time() - t0:.1f} s")
+    O.set_threads(O.cpu_share())
+    orc = O.Oracle.fd(SHAPE, p, 25.0, mode=O.MULTICOLOUR, seed=SEED, chain=0, override_stencils=st)
+    _log(f"oracle hierarchy ({O.cpu_share()} threads) {time.time() - t0:.1f} s")
+    yield s, orc, lat, p
+    s.close()
+    del orc
+    O.set_threads(1)
+
+
+def test_headline_fine_stencil_is_the_reference_operator(headline):
+    """The device's level-0 stencil is the reference FD row (shiftedlaplace_fd_operator.cc:9-57):
+    the oracle's own assembly of the 512^3 operator (not the override) has it on an interior row."""
+    s, orc, lat, p = headline
+    st = s.level_desc(0)["stencil"]
+    row = lat.Nvertex // 2 + 511 * 5 + 7  # an interior vertex
+    cols, vals = orc.csr_row(0, row)
+    n = 511
+    expect = {row - n * n: st[4], row - n: st[10], row - 1: st[12], row: st[13], row + 1: st[14], row + n: st[16],
+              row + n * n: st[22]}
+    assert dict(zip(cols.tolist(), vals.tolist())) == expect
+
+
+@pytest.mark.parametrize("level", [0, 1])
+def test_headline_residual_restrict_bitwise(headline, level):
+    """R (f - A x) at 512^3 (level 0: k_zresrestrict<7,64,8,512>) and 255^3 (level 1: the 27-point
+    instance) against the oracle's CSR SpMV + restriction, bit for bit."""
+    s, orc, lat, p = headline
+    rng = np.random.default_rng(100 + level)
+    n = s.level_desc(level)["ndof"]
+    f = rng.standard_normal(n)
+    x = rng.standard_normal(n)
+    t0 = time.time()
+    d = s.residual_restrict(level, f, x)
+    o = orc.residual_restrict(level, f, x)
+    _log(f"residual_restrict level {level}: {time.time() - t0:.1f} s")
+    assert np.array_equal(d, o)
+
+
+@pytest.mark.parametrize("level,direction", [(0, mg.FORWARD), (1, mg.BACKWARD)])
+def test_headline_noisy_sweep_bitwise(headline, level, direction):
+    """One Gibbs sweep (SORSampler::apply, sor_sampler.cc:37-59) at full width: the fine z-marching
+    red-black sweep (512^3) and the level-1 colour-pair passes (255^3, 128-pair rows)."""
+    s, orc, lat, p = headline
+    rng = np.random.default_rng(200 + level)
+    n = s.level_desc(level)["ndof"]
+    f = rng.standard_normal(n)
+    x = rng.standard_normal(n)
+    t0 = time.time()
+    d = s.sor_sampler_apply(level, direction, 3 + level, 41, f, x)
+    o = orc.sor_sampler_apply(level, direction, 3 + level, 41, f, x)
+    _log(f"sor_sampler_apply level {level}: {time.time() - t0:.1f} s")
+    assert np.array_equal(d, o)
+
+
+def test_headline_cycle_and_qoi_series_bitwise(headline):
+    """Sampler::apply (one 7-level V-cycle from x = 0, multigridmc_sampler.cc:132-138), then the
+    device-resident measure_sampling_time loop (driver_mgmc.cc:66-78) for 3 samples with the QoI at
+    the lattice centre: cycle state, QoI series and final state equal the oracle's exactly.  This
+    runs the benchmark's graph: fused-prolongation post-sweep (128-plane chunks), k_zresrestrict
+    <7,64,8,512>, the level-1 pair passes, the 512^3 k_tail and the QoI record."""
+    s, orc, lat, p = headline
+    f = np.random.default_rng(11).standard_normal(lat.Nvertex)
+    x_dev = np.zeros(lat.Nvertex)
+    x_orc = np.zeros(lat.Nvertex)
+    t0 = time.time()
+    s.apply(f, x_dev)
+    orc.apply(f, x_orc)
+    _log(f"apply: {time.time() - t0:.1f} s")
+    assert np.all(np.isfinite(x_dev)) and np.std(x_dev) > 0
+    assert np.array_equal(x_dev, x_orc)
+    qoi = mg.measurement_vector_index(lat, [0.5, 0.5, 0.5])
+    assert qoi == lat.Nvertex // 2  # vertex (256, 256, 256)
+    s.fix_rhs(f)
+    s.set_state(x_dev)
+    orc.set_rhs(f)
+    orc.set_state(x_orc)
+    del x_dev, x_orc
+    t0 = time.time()
+    z_dev = s.sample(3, qoi)
+    z_orc = orc.sample(3, qoi)
+    _log(f"3-sample series: {time.time() - t0:.1f} s")
+    assert np.array_equal(z_dev, z_orc)
+    assert np.array_equal(s.get_state(), orc.get_state())
+    assert s.get_sample_index() == 4

@@ -181,3 +181,34 @@ def test_reference_2d_mgmc_sampler_case(hip_device):
     assert err_mean < 2e-2, err_mean
     assert err_cov < 2e-2, err_cov
     s.close()
+
+
+@pytest.mark.parametrize("shape,offsets,kw", [
+    ((32, 32), [(1, 1), (-1, -1), (1, -1), (-1, 1)], dict(nlevel=3)),
+    ((16, 16, 16), [(1, 1, 0), (-1, -1, 0), (0, 0, 1), (0, 0, -1), (1, 0, 0), (-1, 0, 0)], dict(nlevel=2)),
+])
+def test_user_matrix_with_diagonal_couplings_cycles_bitwise(hip_device, shape, offsets, kw):
+    """A user's A_sparse (SparseMatrixOperator -> mgmc_create_csr) with at most 2d+1 entries per row
+    that couples diagonal / edge neighbours is swept in 2^d parity colours, not red-black (ADVICE
+    round 2), on the device and in the oracle alike: two cycles and a QoI series bit for bit."""
+    from tests.test_colouring import _offset_csr
+    dim = len(shape)
+    A = _offset_csr(dim, shape, offsets, diag=2.0 * len(offsets) + 1.0, off=-1.0)
+    lat = mg.Lattice(*shape)
+    p = mg.MultigridParameters(**{"smoother": "SOR", "coarse_solver": "SSOR", **kw})
+    s = mg.MultigridMCSampler(mg.SparseMatrixOperator(lat, A), SEED, p, device=0)
+    assert s.level_desc(0)["ncolours"] == 2 ** dim
+    mc = O.Oracle.csr(shape, p, A.indptr, A.indices, A.data, mode=O.MULTICOLOUR, seed=SEED)
+    f = np.random.default_rng(9).standard_normal(lat.Nvertex)
+    xd, xo = np.zeros(lat.Nvertex), np.zeros(lat.Nvertex)
+    for _ in range(2):
+        s.apply(f, xd)
+        mc.apply(f, xo)
+    assert np.array_equal(xd, xo)
+    q = mg.measurement_vector_index(lat, [0.5] * dim)
+    s.fix_rhs(f)
+    s.set_state(xd)
+    mc.set_rhs(f)
+    mc.set_state(xd)
+    assert np.array_equal(s.sample(4, q), mc.sample(4, q))
+    s.close()
