@@ -147,6 +147,15 @@ int mgmc_operator_csr(const mgmc_operator_desc* d, int64_t* rowptr, int32_t* col
 int mgmc_csr_colour_scheme(const mgmc_config* cfg, int level, int64_t nrow, const int64_t* rowptr, const int32_t* col,
                            int* scheme);
 
+/* The constant stencil of a matrix (ABI 5; host only): MGMC_OK and stencil[27] (offset order of
+ * mgmc_level_desc) if every row of the CSR is that 3^d stencil truncated at the lattice boundary, in
+ * ascending column order with bitwise equal values -- the matrix of a constant-coefficient operator
+ * such as ShiftedLaplaceFDOperator / ShiftedLaplaceFEMOperator with a constant correlation length;
+ * MGMC_E_UNSUPPORTED otherwise (use mgmc_create_csr).  A reference-side adapter calls this on
+ * LinearOperator::get_sparse() (linear_operator.hh:93) to pick the stencil fast path. */
+int mgmc_stencil_of_csr(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr, const int32_t* col,
+                        const double* val, double* stencil);
+
 /* ---- lifetime ---- */
 int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chain_id, mgmc_handle** out);
 /* A sampler on a fine operator given as a matrix (LinearOperator::A_sparse, linear_operator.hh:187):
@@ -171,6 +180,12 @@ int mgmc_create_batch(const mgmc_config* cfg, int device, uint64_t seed, uint64_
 int mgmc_create_csr_batch(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr, const int32_t* col,
                           const double* val, int device, uint64_t seed, uint64_t chain0, int nchains,
                           mgmc_handle** out);
+/* A sampler whose fine level is the constant stencil fine_stencil[27] (ABI 5; e.g. from
+ * mgmc_stencil_of_csr): the stencil hierarchy of mgmc_create (Galerkin levels by stencil RAP, the
+ * fused z-marching / pair-pass kernels) without a kappa^2.  Couplings only to axis neighbours:
+ * red-black fine sweeps; otherwise 2^d colours.  cfg.kappa_sq and cfg.fine_operator are ignored. */
+int mgmc_create_stencil_batch(const mgmc_config* cfg, const double* fine_stencil, int device, uint64_t seed,
+                              uint64_t chain0, int nchains, mgmc_handle** out);
 int mgmc_nchains(const mgmc_handle* h);
 int mgmc_destroy(mgmc_handle* h);
 int mgmc_level_desc_get(const mgmc_handle* h, int level, mgmc_level_desc* out);

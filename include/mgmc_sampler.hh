@@ -79,10 +79,23 @@ class HipMultigridMCSampler {
     HipMultigridMCSampler(const mgmc_config& cfg, int device, uint64_t seed, uint64_t chain_id = 0, int nchains = 1) {
         mgmc_handle* h = nullptr;
         check(mgmc_create_batch(&cfg, device, seed, chain_id, nchains, &h), nullptr, "mgmc_create");
-        h_.reset(h);
-        mgmc_level_desc d{};
-        check(mgmc_level_desc_get(h_.get(), 0, &d), h_.get(), "mgmc_level_desc_get");
-        ndof_ = (size_t)d.ndof;
+        adopt(h);
+    }
+    // fine level given as a constant 3^d stencil (mgmc_create_stencil_batch, e.g. from mgmc_stencil_of_csr)
+    HipMultigridMCSampler(const mgmc_config& cfg, const double* fine_stencil, int device, uint64_t seed,
+                          uint64_t chain_id = 0, int nchains = 1) {
+        mgmc_handle* h = nullptr;
+        check(mgmc_create_stencil_batch(&cfg, fine_stencil, device, seed, chain_id, nchains, &h), nullptr,
+              "mgmc_create_stencil");
+        adopt(h);
+    }
+    // fine level given as a matrix, LinearOperator::A_sparse (mgmc_create_csr_batch)
+    HipMultigridMCSampler(const mgmc_config& cfg, int64_t nrow, const int64_t* rowptr, const int32_t* col,
+                          const double* val, int device, uint64_t seed, uint64_t chain_id = 0, int nchains = 1) {
+        mgmc_handle* h = nullptr;
+        check(mgmc_create_csr_batch(&cfg, nrow, rowptr, col, val, device, seed, chain_id, nchains, &h), nullptr,
+              "mgmc_create_csr");
+        adopt(h);
     }
     size_t get_ndof() const { return ndof_; }
     mgmc_handle* handle() const { return h_.get(); }
@@ -134,6 +147,12 @@ class HipMultigridMCSampler {
     }
 
    private:
+    void adopt(mgmc_handle* h) {
+        h_.reset(h);
+        mgmc_level_desc d{};
+        check(mgmc_level_desc_get(h_.get(), 0, &d), h_.get(), "mgmc_level_desc_get");
+        ndof_ = (size_t)d.ndof;
+    }
     struct Deleter {
         void operator()(mgmc_handle* h) const { mgmc_destroy(h); }
     };

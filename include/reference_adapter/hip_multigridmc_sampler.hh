@@ -1,0 +1,174 @@
+// hip_multigridmc_sampler.hh -- reference-side adapter: the MI355X MGMC sampler as a `Sampler` of
+// nilsfriess/MultigridMC.  A maintainer drops this file into the reference as
+// src/sampler/hip_multigridmc_sampler.hh and links -lmgmc_hip.
+//
+// It is written against the reference's own interfaces (citations relative to its src/):
+//   Sampler                    sampler/sampler.hh:23-72 (ctor :31-34, apply :41, fix_rhs :56, unfix_rhs :63)
+//   LinearOperator             linear_operator/linear_operator.hh:28-198 (get_lattice :54, get_ndof :79,
+//                              get_m_lowrank :82, get_sparse :93, get_B :96, get_Sigma :99)
+//   Lattice                    lattice/lattice.hh:18-129 (shape :113, dim :116)
+//   MultigridParameters        auxilliary/parameters.hh:145-174
+//   MultigridMCSampler         sampler/multigridmc_sampler.cc:8-138 (what this replaces)
+//
+// Every operator goes through its matrix: get_sparse() is the precision matrix A_sparse, an Eigen
+// ColMajor SparseMatrix<double> with int indices.  Its compressed-column arrays are handed over as
+// the rows of the matrix (column j of A is row j of A^T): that is exactly what the reference's SOR
+// sweeps read (SORSmoother::apply_sparse, smoother/sor_smoother.cc:56-78, walks the ColMajor storage
+// as rows), and it is A itself for the symmetric operators of the reference.
+//   * mgmc_stencil_of_csr: if every row is one constant 3^d stencil truncated at the boundary
+//     (ShiftedLaplaceFDOperator / ShiftedLaplaceFEMOperator with a constant correlation length), the
+//     sampler takes the stencil fast path (mgmc_create_stencil_batch: stencil Galerkin hierarchy,
+//     fused z-marching fine sweeps, no matrix in HBM).
+//   * otherwise (periodic correlation length, SquaredShiftedLaplaceFDOperator, any user matrix) the
+//     matrix path (mgmc_create_csr_batch: Galerkin products of the matrix, per-vertex coefficients).
+// A MeasuredOperator's low-rank part (get_m_lowrank() > 0) is installed from get_B() (ColMajor =
+// the CSC form mgmc_set_lowrank takes) and get_Sigma().diagonal().
+//
+// Noise: the reference's sampler draws from the shared std::mt19937_64; the device stream is
+// counter-based (Philox keyed by seed and chain id), so the constructor takes
+// the seed as one draw of the shared engine -- a run is still a deterministic function of the
+// driver's seed.  Errors print and exit(-1) like the reference (multigridmc_sampler.cc:47-49).
+#pragma once
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "auxilliary/parameters.hh"
+#include "sampler/sampler.hh"
+#include "mgmc_sampler.hh"  // this repo: include/mgmc_sampler.hh (over include/mgmc.h)
+
+class HipMultigridMCSampler : public Sampler {
+   public:
+    enum class Path { stencil, matrix };
+
+    // The reference's MultigridMCSampler(linear_operator, rng, params, cholesky_params) plus where to
+    // run: the HIP device and the chain id of the Philox key (one chain per rank, nchains per handle).
+    HipMultigridMCSampler(const std::shared_ptr<LinearOperator> linear_operator_, std::mt19937_64& rng_,
+                          const MultigridParameters params_, int device = 0, uint64_t chain_id = 0, int nchains = 1)
+        : Sampler(linear_operator_, rng_), seed(rng_()) {
+        const Plan plan = classify(*linear_operator_, params_);
+        if (plan.path == Path::stencil)
+            impl.reset(new mgmc::HipMultigridMCSampler(plan.cfg, plan.stencil, device, seed, chain_id, nchains));
+        else
+            impl.reset(new mgmc::HipMultigridMCSampler(plan.cfg, (int64_t)plan.outer.size() - 1, plan.outer.data(),
+                                                       plan.inner, plan.values, device, seed, chain_id, nchains));
+        path_ = plan.path;
+        if (linear_operator_->get_m_lowrank() > 0) install_lowrank(*linear_operator_);
+    }
+
+    // sampler.hh:41 -- one call = one MGMC cycle (multigridmc_sampler.cc:132-138), x in/out on the host
+    void apply(const Eigen::VectorXd& f, Eigen::VectorXd& x) const override {
+        if ((size_t)x.size() != impl->get_ndof() || (size_t)f.size() != impl->get_ndof()) {
+            std::fprintf(stderr, "ERROR: HipMultigridMCSampler::apply: vector size %td / %td, operator %zu\n", f.size(),
+                         x.size(), impl->get_ndof());
+            std::exit(-1);
+        }
+        impl->apply(f.data(), x.data());
+    }
+    void fix_rhs(const Eigen::VectorXd& f) override { impl->fix_rhs(f.data()); }  // sampler.hh:56
+    void unfix_rhs() override { impl->unfix_rhs(); }                              // sampler.hh:63
+
+    // The device-resident loop for measure_sampling_time (driver_mgmc.cc:66-80): nsamples cycles on
+    // the fixed rhs, x stays in HBM, the QoI x[qoi_index] is recorded on the device.
+    std::vector<double> sample(int nsamples, int64_t qoi_index) const { return impl->sample(nsamples, qoi_index); }
+    // (n, mean, M2) of the recorded QoI (driver_mgmc.cc:86-94 statistics, Welford on the device)
+    void qoi_moments(double out[3]) const { impl->qoi_moments(out); }
+    void set_state(const Eigen::VectorXd& x) { impl->set_state(x.data()); }
+    void get_state(Eigen::VectorXd& x) const { impl->get_state(x.data()); }
+
+    Path path() const { return path_; }
+    uint64_t get_seed() const { return seed; }
+    mgmc_handle* handle() const { return impl->handle(); }
+
+    // Host-only decision (no device touched): the config and the stencil or matrix a sampler for
+    // this operator would be built from.
+    struct Plan {
+        Path path = Path::matrix;
+        mgmc_config cfg{};
+        double stencil[27] = {0};
+        std::vector<int64_t> outer;  // row pointer (the ColMajor outer index, widened)
+        const int32_t* inner = nullptr;
+        const double* values = nullptr;
+    };
+    static Plan classify(const LinearOperator& op, const MultigridParameters& p) {
+        Plan plan;
+        const std::shared_ptr<Lattice> lat = op.get_lattice();
+        const Eigen::VectorXi shape = lat->shape();
+        const int dim = lat->dim();
+        if (dim != 2 && dim != 3) {
+            std::fprintf(stderr, "ERROR: HipMultigridMCSampler needs a 2D or 3D lattice, got %dD\n", dim);
+            std::exit(-1);
+        }
+        plan.cfg = mgmc::make_config(dim, shape[0], shape[1], dim == 3 ? shape[2] : 0, 0.0, to_mgmc(p));
+        const LinearOperator::SparseMatrixType& A = op.get_sparse();
+        if (!A.isCompressed() || A.rows() != A.cols() || (int64_t)A.rows() != (int64_t)op.get_ndof()) {
+            std::fprintf(stderr, "ERROR: HipMultigridMCSampler: A_sparse must be square and compressed\n");
+            std::exit(-1);
+        }
+        const int64_t n = A.rows();
+        static_assert(sizeof(LinearOperator::SparseMatrixType::StorageIndex) == sizeof(int32_t),
+                      "Eigen's default int StorageIndex");
+        plan.outer.assign(A.outerIndexPtr(), A.outerIndexPtr() + n + 1);
+        plan.inner = reinterpret_cast<const int32_t*>(A.innerIndexPtr());
+        plan.values = A.valuePtr();
+        const int rc = mgmc_stencil_of_csr(&plan.cfg, n, plan.outer.data(), plan.inner, plan.values, plan.stencil);
+        if (rc == MGMC_OK)
+            plan.path = Path::stencil;
+        else if (rc == MGMC_E_UNSUPPORTED)
+            plan.path = Path::matrix;
+        else
+            mgmc::check(rc, nullptr, "mgmc_stencil_of_csr");
+        return plan;
+    }
+
+   private:
+    static mgmc::MultigridParameters to_mgmc(const MultigridParameters& p) {
+        mgmc::MultigridParameters q;
+        q.nlevel = (int)p.nlevel;
+        q.npresmooth = (int)p.npresmooth;
+        q.npostsmooth = (int)p.npostsmooth;
+        q.ncoarsesmooth = (int)p.ncoarsesmooth;
+        q.omega = p.omega;
+        q.cycle = (int)p.cycle;
+        q.coarse_scaling = p.coarse_scaling;
+        q.verbose = p.verbose;
+        // the reference accepts exactly these names (multigridmc_sampler.cc:34-49, :52-73)
+        if (p.smoother == "SOR")
+            q.smoother = MGMC_SMOOTHER_SOR;
+        else if (p.smoother == "SSOR")
+            q.smoother = MGMC_SMOOTHER_SSOR;
+        else {
+            std::fprintf(stderr, "ERROR: invalid sampler \'%s\'\n", p.smoother.c_str());
+            std::exit(-1);
+        }
+        if (p.coarse_solver == "SSOR")
+            q.coarse_solver = MGMC_COARSE_SSOR;
+        else if (p.coarse_solver == "Cholesky")
+            q.coarse_solver = MGMC_COARSE_CHOLESKY;
+        else {
+            std::fprintf(stderr, "ERROR: multigrid coarse sampler \'%s\'\n", p.coarse_solver.c_str());
+            std::exit(-1);
+        }
+        return q;
+    }
+
+    // MeasuredOperator (measured_operator.cc:9-49): B (ColMajor: colptr / row index / values, the CSC
+    // form of mgmc_set_lowrank) and Sigma's diagonal
+    void install_lowrank(const LinearOperator& op) {
+        const LinearOperator::SparseMatrixType& B = op.get_B();
+        const int m = (int)B.cols();
+        std::vector<int64_t> colptr(B.outerIndexPtr(), B.outerIndexPtr() + m + 1);
+        std::vector<int64_t> rows(B.innerIndexPtr(), B.innerIndexPtr() + B.nonZeros());
+        const Eigen::VectorXd sigma = op.get_Sigma().diagonal();
+        impl->set_lowrank(m, colptr.data(), rows.data(), B.valuePtr(), sigma.data());
+    }
+
+    const uint64_t seed;
+    Path path_ = Path::matrix;
+    std::unique_ptr<mgmc::HipMultigridMCSampler> impl;
+};

@@ -27,6 +27,7 @@ from .sampler import (  # noqa: F401
     describe,
     make_config,
     measurement_vector_index,
+    sampler_csr_matrix,
 )
 
 __version__ = "0.1.0"

@@ -1767,7 +1767,7 @@ int mgmc_describe(const mgmc_config* cfg, mgmc_level_desc* out, int max_levels) 
 // mgmc_create / mgmc_create_csr: csr = the fine operator's matrix (null: the constant-coefficient
 // hierarchy of cfg), every level then built from matrices
 static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, uint64_t seed, uint64_t chain_id,
-                       int nchains, mgmc_handle** out) {
+                       int nchains, mgmc_handle** out, const double* fine_st = nullptr) {
     if (!cfg || !out) return fail(nullptr, MGMC_E_INVALID, "null argument");
     *out = nullptr;
     if (nchains < 1 || nchains > LR_MAX_CH)
@@ -1817,7 +1817,7 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
         h->last_error = "hipStreamCreate failed";
         return bail(MGMC_E_HIP);
     }
-    std::vector<LevelSpec> specs = build_hierarchy(*cfg);
+    std::vector<LevelSpec> specs = build_hierarchy(*cfg, fine_st);
     h->field_mode = csr != nullptr;
     std::vector<FieldHost> fields;
     for (size_t l = 0; l < mats.size(); ++l) {
@@ -1995,6 +1995,74 @@ int mgmc_create_csr_batch(const mgmc_config* cfg, int64_t nrow, const int64_t* r
     A.col.assign(col, col + rowptr[nrow]);
     A.val.assign(val, val + rowptr[nrow]);
     return create_impl(&c, &A, device, seed, chain0, nchains, out);
+}
+
+int mgmc_stencil_of_csr(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr, const int32_t* col,
+                        const double* val, double* stencil) {
+    if (!cfg || !rowptr || !col || !val || !stencil || nrow < 1) return fail(nullptr, MGMC_E_INVALID, "null argument");
+    mgmc_config c = *cfg;
+    c.kappa_sq = 0.0;
+    c.fine_operator = MGMC_OPERATOR_FD;
+    const std::string e0 = check_csr_shape(c, nrow, rowptr);
+    if (!e0.empty()) return fail(nullptr, MGMC_E_INVALID, "mgmc_stencil_of_csr: " + e0);
+    const int dim = cfg->dim;
+    const int64_t nxi = cfg->nx - 1, nyi = cfg->ny - 1, nzi = dim == 3 ? cfg->nz - 1 : 1;
+    // the stencil of the lattice's centre row, then every row checked against its truncation
+    double st[27] = {0};
+    bool have[27] = {false};
+    auto slot = [&](int64_t r, int32_t cidx, int* k) {
+        const int64_t ri = r % nxi, rj = (r / nxi) % nyi, rk = r / (nxi * nyi);
+        const int64_t ci = cidx % nxi, cj = (cidx / nxi) % nyi, ck = cidx / (nxi * nyi);
+        const int64_t dx = ci - ri, dy = cj - rj, dz = ck - rk;
+        if (dx < -1 || dx > 1 || dy < -1 || dy > 1 || dz < -1 || dz > 1) return false;
+        *k = dim == 3 ? (int)((dz + 1) * 9 + (dy + 1) * 3 + (dx + 1)) : (int)((dy + 1) * 3 + (dx + 1));
+        return true;
+    };
+    const int64_t rc = ((nzi / 2) * nyi + nyi / 2) * nxi + nxi / 2;
+    for (int64_t q = rowptr[rc]; q < rowptr[rc + 1]; ++q) {
+        int k;
+        if (col[q] < 0 || col[q] >= nrow || !slot(rc, col[q], &k))
+            return fail(nullptr, MGMC_E_UNSUPPORTED, "mgmc_stencil_of_csr: couplings beyond the 3^d box");
+        st[k] = val[q];
+        have[k] = true;
+    }
+    const int zr = dim == 3 ? 1 : 0;
+    for (int64_t r = 0; r < nrow; ++r) {
+        const int64_t ri = r % nxi + 1, rj = (r / nxi) % nyi + 1, rk = r / (nxi * nyi) + 1;
+        int64_t q = rowptr[r];
+        for (int dz = -zr; dz <= zr; ++dz)  // expected entries in ascending column order
+            for (int dy = -1; dy <= 1; ++dy)
+                for (int dx = -1; dx <= 1; ++dx) {
+                    const int k = dim == 3 ? (dz + 1) * 9 + (dy + 1) * 3 + (dx + 1) : (dy + 1) * 3 + (dx + 1);
+                    if (!have[k]) continue;
+                    const int64_t i = ri + dx, j = rj + dy, kk = rk + dz;
+                    if (i < 1 || i > nxi || j < 1 || j > nyi || (dim == 3 && (kk < 1 || kk > nzi))) continue;
+                    const int64_t cexp = ((kk - 1) * nyi + (j - 1)) * nxi + (i - 1);
+                    if (q >= rowptr[r + 1] || col[q] != cexp || val[q] != st[k])
+                        return fail(nullptr, MGMC_E_UNSUPPORTED,
+                                    "mgmc_stencil_of_csr: row " + std::to_string(r) + " is not the constant stencil");
+                    ++q;
+                }
+        if (q != rowptr[r + 1])
+            return fail(nullptr, MGMC_E_UNSUPPORTED,
+                        "mgmc_stencil_of_csr: row " + std::to_string(r) + " has entries outside the stencil");
+    }
+    memcpy(stencil, st, sizeof(st));
+    return MGMC_OK;
+}
+
+int mgmc_create_stencil_batch(const mgmc_config* cfg, const double* fine_stencil, int device, uint64_t seed,
+                              uint64_t chain0, int nchains, mgmc_handle** out) {
+    if (!cfg || !fine_stencil || !out) return fail(nullptr, MGMC_E_INVALID, "null argument");
+    const int dim = cfg->dim;
+    const double centre = fine_stencil[dim == 3 ? 13 : 4];
+    if (!(centre > 0.0)) return fail(nullptr, MGMC_E_INVALID, "mgmc_create_stencil: non-positive centre coefficient");
+    for (int k = 0; k < (dim == 3 ? 27 : 9); ++k)
+        if (!std::isfinite(fine_stencil[k])) return fail(nullptr, MGMC_E_INVALID, "mgmc_create_stencil: non-finite coefficient");
+    mgmc_config c = *cfg;  // the stencil replaces kappa^2 and the fine-operator choice
+    c.kappa_sq = 0.0;
+    c.fine_operator = MGMC_OPERATOR_FD;
+    return create_impl(&c, nullptr, device, seed, chain0, nchains, out, fine_stencil);
 }
 
 int mgmc_operator_csr_size(const mgmc_operator_desc* d, int64_t* nrow, int64_t* nnz) {

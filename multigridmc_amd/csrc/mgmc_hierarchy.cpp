@@ -4,6 +4,8 @@
 #include <math.h>
 #include <string.h>
 
+#include <cstdlib>
+
 #include <sstream>
 
 namespace mgmc {
@@ -200,7 +202,16 @@ void galerkin_stencil(int dim, const double* fine, double* coarse) {
             }
 }
 
-std::vector<LevelSpec> build_hierarchy(const mgmc_config& c) {
+bool stencil_axis_only(int dim, const double* st) {
+    const int zr = dim == 3 ? 1 : 0;
+    for (int dz = -zr; dz <= zr; ++dz)
+        for (int dy = -1; dy <= 1; ++dy)
+            for (int dx = -1; dx <= 1; ++dx)
+                if (std::abs(dx) + std::abs(dy) + std::abs(dz) > 1 && st[sidx(dim, dx, dy, dz)] != 0.0) return false;
+    return true;
+}
+
+std::vector<LevelSpec> build_hierarchy(const mgmc_config& c, const double* fine_st) {
     std::vector<LevelSpec> levels;
     LevelSpec L;
     memset(&L, 0, sizeof(L));
@@ -234,6 +245,13 @@ std::vector<LevelSpec> build_hierarchy(const mgmc_config& c) {
         fem_stencil(c.dim, L.n, c.kappa_sq, L.st);
         L.npoints = (c.dim == 3) ? 27 : 9;
         L.ncolours = 1 << c.dim;
+    }
+    if (fine_st) {  // a given constant stencil (mgmc_create_stencil)
+        memset(L.st, 0, sizeof(L.st));
+        for (int k = 0; k < (c.dim == 3 ? 27 : 9); ++k) L.st[k] = fine_st[k];
+        const bool axis = stencil_axis_only(c.dim, L.st);
+        L.npoints = axis ? 2 * c.dim + 1 : (c.dim == 3 ? 27 : 9);
+        L.ncolours = axis ? 2 : 1 << c.dim;
     }
     for (int level = 0; level < c.nlevel; ++level) {
         L.ndof = 1;

@@ -34,8 +34,13 @@ struct LevelSpec {
 // Returns "" on success, otherwise an error message.
 std::string validate_config(const mgmc_config& cfg);
 
-// Build all levels (cfg must be valid).
-std::vector<LevelSpec> build_hierarchy(const mgmc_config& cfg);
+// Build all levels (cfg must be valid).  fine_st (27 doubles, may be null): the fine level's constant
+// stencil instead of cfg's FD / FEM operator; a stencil whose couplings are all axis neighbours is
+// swept red-black (5/7 points), any other 3^d stencil in 2^d colours.
+std::vector<LevelSpec> build_hierarchy(const mgmc_config& cfg, const double* fine_st = nullptr);
+
+// true if every nonzero of the 3^d stencil is the centre or an axis neighbour
+bool stencil_axis_only(int dim, const double* st);
 
 // Galerkin product of a 3^d stencil with the (1/2,1,1/2)^d linear interpolation.
 void galerkin_stencil(int dim, const double* fine, double* coarse);

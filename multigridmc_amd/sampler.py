@@ -254,6 +254,27 @@ class SparseMatrixOperator(ShiftedLaplaceFDOperator):
     def get_csr(self):
         return self._csr
 
+    def constant_stencil(self, config):
+        """The 3^d stencil every row of the matrix truncates (mgmc_stencil_of_csr), or None: the
+        sampler then builds the stencil hierarchy (mgmc_create_stencil_batch) instead of the matrix
+        path -- the fast path for constant-coefficient operators handed over as matrices."""
+        lib = load_library()
+        rowptr, col, val = self._csr
+        st = np.zeros(27)
+        rc = lib.mgmc_stencil_of_csr(ctypes.byref(config), len(rowptr) - 1,
+                                     rowptr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                     col.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _dp(val), _dp(st))
+        if rc == _native.MGMC_E_UNSUPPORTED:
+            return None
+        check(rc)
+        return st
+
+
+def sampler_csr_matrix(rowptr, col, val, n: int):
+    """(rowptr, col, val) as a scipy CSR matrix of shape (n, n)."""
+    import scipy.sparse as sp
+    return sp.csr_matrix((val, col, rowptr), shape=(n, n))
+
 
 def csr_colour_scheme(lattice: Lattice, rowptr, col, level: int = 0) -> int:
     """Colour classes the device sweeps a matrix level with (mgmc_csr_colour_scheme, host only):
@@ -355,7 +376,13 @@ class MultigridMCSampler:
         self.lib = load_library()
         h = ctypes.c_void_p()
         base = getattr(linear_operator, "base_operator", linear_operator)
-        if getattr(base, "variable_coefficients", False):
+        st = base.constant_stencil(self.config) if isinstance(base, SparseMatrixOperator) else None
+        if st is not None:
+            # a matrix that is one constant stencil (mgmc_stencil_of_csr): the stencil hierarchy
+            check(self.lib.mgmc_create_stencil_batch(ctypes.byref(self.config), _dp(st), int(device),
+                                                     int(seed) & (2**64 - 1), int(chain_id) & (2**64 - 1),
+                                                     self.nchains, ctypes.byref(h)))
+        elif getattr(base, "variable_coefficients", False):
             # per-vertex coefficients: the assembled matrix (A_sparse) and a Galerkin hierarchy of matrices
             rowptr, col, val = base.get_csr()
             check(self.lib.mgmc_create_csr_batch(ctypes.byref(self.config), len(rowptr) - 1,

@@ -1,0 +1,106 @@
+"""The reference-side adapter (include/reference_adapter/hip_multigridmc_sampler.hh) and the host
+entry points it relies on (CPU: no GPU touched).
+
+* mgmc_stencil_of_csr recognises the matrix of a constant-coefficient operator
+  (LinearOperator::get_sparse(), linear_operator.hh:93) as one 3^d stencil truncated at the boundary
+  and returns exactly the stencil mgmc_create builds for that operator; other matrices are
+  MGMC_E_UNSUPPORTED (the adapter then takes the matrix path, mgmc_create_csr).
+* The adapter compiles and links with g++ against declaration headers that restate the reference's
+  interface (tests/cpp/refdecl: Sampler, LinearOperator, Lattice, MultigridParameters and the
+  handful of Eigen members the adapter touches) -- test scaffolding, not the reference itself.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import multigridmc_amd as mg
+from multigridmc_amd import _native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _stencil_of(op, params=None):
+    params = params or mg.MultigridParameters(nlevel=2)
+    cfg = mg.make_config(op, params)
+    rowptr, col, val = op.get_csr()
+    st = np.zeros(27)
+    rc = mg.load_library().mgmc_stencil_of_csr(ctypes.byref(cfg), len(rowptr) - 1,
+                                               rowptr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                               col.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                               val.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                               st.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return rc, st, cfg
+
+
+@pytest.mark.parametrize("cls,shape", [(mg.ShiftedLaplaceFDOperator, (32, 32)),
+                                       (mg.ShiftedLaplaceFDOperator, (16, 8, 24)),
+                                       (mg.ShiftedLaplaceFEMOperator, (16, 16)),
+                                       (mg.ShiftedLaplaceFEMOperator, (8, 16, 8))])
+def test_stencil_of_constant_operator_matrix(cls, shape):
+    """The assembled A_sparse of FD / FEM with a constant correlation length is one stencil, bit for
+    bit the fine stencil of mgmc_describe for that operator."""
+    op = cls(mg.Lattice(*shape), mg.ConstantCorrelationLengthModel(0.2))
+    op.get_csr()
+    rc, st, cfg = _stencil_of(op)
+    assert rc == _native.MGMC_OK
+    ref = mg.describe(cfg)[0]["stencil"]
+    assert np.array_equal(st, ref)
+
+
+@pytest.mark.parametrize("cls,shape", [(mg.ShiftedLaplaceFDOperator, (32, 32)),
+                                       (mg.ShiftedLaplaceFEMOperator, (8, 8, 8)),
+                                       (mg.SquaredShiftedLaplaceFDOperator, (16, 16))])
+def test_stencil_of_variable_matrix_is_unsupported(cls, shape):
+    model = mg.PeriodicCorrelationLengthModel(0.2, 0.4) if cls is not mg.SquaredShiftedLaplaceFDOperator else 25.0
+    op = cls(mg.Lattice(*shape), model)
+    rc, st, cfg = _stencil_of(op)
+    assert rc == _native.MGMC_E_UNSUPPORTED
+
+
+def test_stencil_of_csr_rejects_a_perturbed_row():
+    op = mg.ShiftedLaplaceFDOperator(mg.Lattice(16, 16), 25.0)
+    rowptr, col, val = op.get_csr()
+    val = val.copy()
+    val[rowptr[100] + 1] *= 1.0 + 2.0 ** -50  # one entry off by one ulp-ish
+    op2 = mg.SparseMatrixOperator(op.get_lattice(), mg.sampler_csr_matrix(rowptr, col, val, op.get_ndof()))
+    rc, st, cfg = _stencil_of(op2)
+    assert rc == _native.MGMC_E_UNSUPPORTED
+    assert b"row 100" in mg.load_library().mgmc_last_error(None)
+
+
+def test_sparse_matrix_operator_of_fd_takes_the_stencil_path():
+    op = mg.ShiftedLaplaceFDOperator(mg.Lattice(64, 64, 64), 25.0)
+    sm = mg.SparseMatrixOperator(op.get_lattice(), op.matrix())
+    cfg = mg.make_config(sm, mg.MultigridParameters(nlevel=3))
+    st = sm.constant_stencil(cfg)
+    assert st is not None and np.array_equal(st, mg.describe(mg.make_config(op, mg.MultigridParameters()))[0]["stencil"])
+
+
+def build_adapter_client(out_dir):
+    """g++ the adapter + a small driver against the declaration headers; link libmgmc_hip.so."""
+    exe = os.path.join(out_dir, "adapter_client")
+    lib_dir = os.path.join(ROOT, "multigridmc_amd")
+    cmd = ["g++", "-std=c++17", "-O1", "-Wall", "-Wextra", "-Werror", "-Wno-ignored-qualifiers",
+           "-I", os.path.join(ROOT, "tests", "cpp", "refdecl"), "-I", os.path.join(ROOT, "include"),
+           "-I", os.path.join(ROOT, "include", "reference_adapter"),
+           os.path.join(ROOT, "tests", "cpp", "adapter_client.cpp"), "-o", exe,
+           "-L", lib_dir, "-lmgmc_hip", "-Wl,-rpath," + lib_dir]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    return exe
+
+
+def test_reference_adapter_compiles_and_links(tmp_path):
+    """include/reference_adapter/hip_multigridmc_sampler.hh against the restated reference interface:
+    compiles with -Wall -Wextra -Werror (less -Wignored-qualifiers, which the reference's
+    `const unsigned int get_ndof() const` trips), links, and without a GPU fails loudly the reference's way
+    (message + exit(-1)) at the first device call."""
+    exe = build_adapter_client(str(tmp_path))
+    r = subprocess.run([exe, "describe"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "path stencil" in r.stdout and "path matrix" in r.stdout
+    if not os.path.exists("/dev/kfd"):
+        r = subprocess.run([exe, "sample", "2", "fd"], capture_output=True, text=True)
+        assert r.returncode == 255 and "no HIP device" in r.stderr
