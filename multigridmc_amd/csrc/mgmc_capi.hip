@@ -25,9 +25,6 @@
 #include "mgmc_zrestrict.hpp"
 #include "mgmc_tail.hpp"
 #include "mgmc_gsweep.hpp"
-#ifdef MGMC_Z27_EXPERIMENT  // timing-experiment builds only (scripts/build_exp.sh Z27S)
-#include "mgmc_zsweep27.hpp"
-#endif
 #include "mgmc_rb2d.hpp"
 #include "mgmc_lowrank.hpp"
 #include "mgmc_solver.hpp"
@@ -219,11 +216,10 @@ struct Level {
     bool pairs = false;    // Galerkin level swept in colour-pair passes (mgmc_gsweep.hpp)
     bool quads = false;    // ... two pairs per launch, out of place (k_sweep_quads)
     bool rb2d = false;     // 2D 5-point level: one-launch red-black sweep, out of place (k_rb2d)
-    bool z27 = false;      // 3D 27-point level: z-marching 8-colour sweep (experiment builds only)
     bool field = false;    // per-vertex coefficients (mgmc_create_csr, mgmc_field.hpp)
     FieldArg F;            // ... their device field, pattern and colouring
     double* rbuf = nullptr;  // ... residual scratch (padded layout, zero boundary)
-    bool pingpong() const { return zsweep || quads || rb2d || z27; }  // out-of-place sweeps: x <-> x2
+    bool pingpong() const { return zsweep || quads || rb2d; }  // out-of-place sweeps: x <-> x2
     double* buf(int i) const { return i == 0 ? x : x2; }
     LowRankDev lr;
 };
@@ -531,51 +527,6 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
         }
     }
 }
-
-// one 8-colour sweep of a large 27-point level, xin -> xout (mgmc_zsweep27.hpp; experiment builds:
-// bitwise equal to the pair passes but slower).  The chunk depth minimises (rounds of
-// workgroups) x (steps per chunk, one recomputed K1 plane each): one workgroup per CU (139 KB LDS)
-#ifdef MGMC_Z27_EXPERIMENT
-#ifndef MGMC_Z27_MIN_NX
-#define MGMC_Z27_MIN_NX 64
-#endif
-void launch_z27(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
-                hipStream_t s, int nch = 1) {
-    Z27Args a;
-    a.L = lv.L;
-    a.xin = xin;
-    a.xout = xout;
-    a.f = f;
-    a.S = lv.S;
-    a.G = g;
-    a.cs = lv.L.nstore;
-    a.ntx = (lv.L.nx - 1 + Z27_CX - 1) / Z27_CX;
-    a.nty = (lv.L.ny - 1 + Z27_CY - 1) / Z27_CY;
-    const int nzi = lv.L.nz - 1;
-    const long long txy = (long long)a.ntx * a.nty * nch;
-    double best = 1e300;
-    a.kz = 8;
-    for (int kz = 8; kz <= 128; kz *= 2) {
-        const long long ntz = (nzi + kz - 1) / kz;
-        const double rounds = std::ceil((double)(txy * ntz) / lv.num_cu);
-        const double cost = rounds * (kz / 2 + 2);
-        if (cost < best) {
-            best = cost;
-            a.kz = kz;
-        }
-        if (kz >= nzi) break;
-    }
-    a.ntz = (nzi + a.kz - 1) / a.kz;
-    const int nblk = a.ntx * a.nty * a.ntz;
-    const dim3 grid((nblk + 7) / 8 * 8, 1, nch);
-    if (direction == MGMC_FORWARD)
-        hipLaunchKernelGGL((k_zsweep27<false>), grid, dim3(Z27_NT), z27_lds_bytes(), s, a);
-    else
-        hipLaunchKernelGGL((k_zsweep27<true>), grid, dim3(Z27_NT), z27_lds_bytes(), s, a);
-}
-#else
-void launch_z27(const Level&, const double*, double*, const double*, const GibbsArg&, int, hipStream_t, int = 1) {}
-#endif
 
 void launch_pairs(const Level& lv, double* x, const double* f, const GibbsArg& g, int direction, hipStream_t s,
                   int nch = 1) {
@@ -1369,9 +1320,6 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                     xo = lv.buf(1 - op.src);
                     launch_zsweep(lv, lv.buf(op.src), xo, fs, g, op.direction, lc, lc ? lc->x : nullptr,
                                   h->cfg.coarse_scaling, s, nch);
-                } else if (lv.z27) {
-                    xo = lv.buf(1 - op.src);
-                    launch_z27(lv, lv.buf(op.src), xo, fs, g, op.direction, s, nch);
                 } else if (lv.quads) {
                     xo = lv.buf(1 - op.src);
                     launch_quads(lv, lv.buf(op.src), xo, fs, g, op.direction, s, nch);
@@ -1879,11 +1827,7 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
         lv.pairs = !lv.field && pairs_eligible(lv.spec, lv.L) && !(h->paths & PATH_NO_PAIRS);
         lv.rb2d = !lv.field && cfg->dim == 2 && lv.spec.npoints == 5 && l + 1 < specs.size() &&
                   !(h->paths & PATH_NO_RB2D);
-#ifdef MGMC_Z27_EXPERIMENT
-        lv.z27 = !lv.field && cfg->dim == 3 && lv.spec.npoints == 27 && l + 1 < specs.size() &&
-                 lv.L.nx > MGMC_Z27_MIN_NX && (tail0 < 0 || (int)l < tail0);
-#endif
-        lv.quads = lv.pairs && !lv.z27 && quads_eligible(lv.spec, lv.L, h->paths) && (tail0 < 0 || (int)l < tail0);
+        lv.quads = lv.pairs && quads_eligible(lv.spec, lv.L, h->paths) && (tail0 < 0 || (int)l < tail0);
         if (lv.pingpong()) {
             if (hipMalloc(&lv.x2, cbytes) != hipSuccess) {
                 h->levels.push_back(lv);
@@ -2343,9 +2287,6 @@ static int sweep_component(mgmc_handle* h, int level, int direction, int nsweeps
         if (lr && noise) fb = lr_rhs(h, lv, LR_PATCH_NOISE, lv.scratch[0], tag + (uint32_t)s, h->ctrl + 3, h->stream);
         if (noise && lv.zsweep) {  // the fused z-marching kernel of the V-cycle (out of place)
             launch_zsweep(lv, lv.scratch[cur], lv.scratch[3 - cur], fb, g, direction, nullptr, nullptr, 0.0, h->stream);
-            cur = 3 - cur;
-        } else if (noise && lv.z27) {  // the z-marching 8-colour sweep (out of place)
-            launch_z27(lv, lv.scratch[cur], lv.scratch[3 - cur], fb, g, direction, h->stream);
             cur = 3 - cur;
         } else if (noise && lv.quads) {  // two colour pairs per launch (out of place)
             launch_quads(lv, lv.scratch[cur], lv.scratch[3 - cur], fb, g, direction, h->stream);

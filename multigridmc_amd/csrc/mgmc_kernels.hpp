@@ -224,9 +224,6 @@ __device__ __forceinline__ int colour_of(int i, int j, int k) {
 // evaluated up front by all threads at once (f does not change during the sampler), so a colour pass
 // is only the stencil and the update -- one Philox + Box-Muller latency for the whole sampler instead
 // of one per colour pass.  The same operations as gibbs_point, so the same bits.
-#ifndef MGMC_COARSE_EXP
-#define MGMC_COARSE_EXP 0  // timing experiments only (scripts/build_exp.sh COARSEEXPS); 0 in the product
-#endif
 template <int DIM, int NPTS, bool PRE>
 __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __restrict__ xg,
                                                           const double* __restrict__ fg, StencilArg S, GibbsArg G,
@@ -276,14 +273,9 @@ __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __re
             if (i0 > nxi) continue;
             const int j = row % nyi + 1;
             const int k = (DIM == 3) ? row / nyi + 1 : 0;
-#if MGMC_COARSE_EXP == 1  // timing experiment only (wrong samples): no Philox / Box-Muller
-            pz0[u] = 1e-3 * (double)(t & 7);
-            pz1[u] = 1e-3 * (double)(sw & 7);
-#else
             const Philox4 rnd = philox4x32_10(pair_id<DIM>(L, i0, j, k), G.tag + (uint32_t)sw, (uint32_t)sample,
                                               (uint32_t)(sample >> 32), G.key.k0, G.key.k1);
             normal_pair(rnd, &pz0[u], &pz1[u]);
-#endif
         }
     }
 #pragma unroll
@@ -327,14 +319,9 @@ __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __re
             const int j = row % nyi + 1;
             const int k = (DIM == 3) ? row / nyi + 1 : 0;
             double z0, z1;
-#if MGMC_COARSE_EXP == 1
-            z0 = 1e-3 * (double)(t & 7);
-            z1 = 1e-3 * (double)(sw & 7);
-#else
             const Philox4 rnd = philox4x32_10(pair_id<DIM>(L, i0, j, k), G.tag + (uint32_t)sw, (uint32_t)sample,
                                               (uint32_t)(sample >> 32), G.key.k0, G.key.k1);
             normal_pair(rnd, &z0, &z1);
-#endif
             const long long q = (long long)sw * ndof + (long long)row * nxi + (i0 - 1);
             const long long p = L.at(i0, j, k);
             cs[q] = fma(G.sd, z0, fs[p]);

@@ -30,10 +30,6 @@
 #include "mgmc_kernels.hpp"
 #include "mgmc_lowrank.hpp"
 
-#ifndef MGMC_TAIL_EXP
-#define MGMC_TAIL_EXP 0
-#endif
-
 namespace mgmc {
 
 enum TailKind { TAIL_SWEEP = 0, TAIL_RESTRICT = 1, TAIL_PROLONG = 2, TAIL_COARSE = 3 };
@@ -188,13 +184,8 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             const int i0 = 2 * m + 1;
             if (i0 > G.nx - 1) continue;
             double z0, z1;
-#if MGMC_TAIL_EXP == 1  // timing experiment only (wrong samples): no Philox / Box-Muller in the tail
-            z0 = 1e-3 * (double)(q & 7);
-            z1 = 1e-3 * (double)(tag & 7);
-#else
             const Philox4 rnd = philox4x32_10(pair_id<DIM>(G, i0, j, k), tag, s_lo, s_hi, key.k0, key.k1);
             normal_pair(rnd, &z0, &z1);
-#endif
             const int p = (int)G.at(i0, j, k);
             scr[p] = fma(t.sd, z0, f[p]);
             if (i0 + 1 <= G.nx - 1) scr[p + 1] = fma(t.sd, z1, f[p + 1]);
@@ -213,11 +204,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             // tj << 4 | (tk >> 1) << 7, so a half-wave holds class planes tk and tk+1 (vertex planes
             // 2 apart, 16 bank pairs apart with the padded plane stride of tail_layout): 2-way banks
             const bool fast = DIM == 3 ? (ci <= 8 && cj <= 8 && ck * 64 <= nt) : (ci <= 32 && cj * 32 <= nt);
-#if MGMC_TAIL_EXP == 2  // timing experiment only: colour passes reduced to their barriers
-            if (false) {
-#else
             if (fast) {
-#endif
                 const int ti = DIM == 3 ? (tid & 7) : (tid & 31);
                 const int tj = DIM == 3 ? ((tid >> 4) & 7) : (tid >> 5);
                 const int tk = DIM == 3 ? (((tid >> 3) & 1) | ((tid >> 7) << 1)) : 0;
@@ -226,7 +213,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
                     const double res = stencil_fma<DIM, NPTS>(x, p, G, t.S);
                     x[p] = fma(t.wd, scr[p] - res, x[p]);
                 }
-            } else if (MGMC_TAIL_EXP != 2) {
+            } else {
                 for (int q = tid; q < ci * cj * ck; q += nt) {
                     const int i = fi + 2 * (q % ci), r = q / ci;
                     const int j = fj + 2 * (r % cj), k = DIM == 3 ? fk + 2 * (r / cj) : 0;

@@ -62,21 +62,6 @@ struct ZItem {
     int flags;       // bit0 row interior, bit1 i interior, bit2 i+1 interior, bit3 parity (i+j)&1
 };
 
-// MGMC_ZS_EXP (timing experiments only, scripts/build_exp.sh; 0 in the product): 1 no Box-Muller,
-// 2 no halo ring, 3 no Philox, 4 no stencil, 5 memory skeleton (1 + 2 + 4), 6 no step barriers
-// (wrong results: sync cost only), 8 no prolongation arithmetic, 9 wave-uniform Box-Muller table
-// indices
-#ifndef MGMC_ZS_EXP
-#define MGMC_ZS_EXP 0
-#endif
-#ifndef MGMC_ZS_NT_STORE
-#define MGMC_ZS_NT_STORE 1
-#endif
-#if MGMC_ZS_EXP == 6
-#define ZS_STEP_SYNC() ((void)0)
-#else
-#define ZS_STEP_SYNC() __syncthreads()
-#endif
 // PROLONG: 0 plain sweep; 1 fused prolongation, terms v + (alpha w) x_c (any alpha); 2 the same with
 // v = fma(alpha w, x_c, v), selected when alpha is a power of two: alpha w x_c is then exact, so the
 // fma rounds once like the separate add and the bits are the same.
@@ -273,9 +258,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     const double al0 = a.alpha, al1 = a.alpha * 0.5;
     // KO: k & 1 when known at compile time (the z march: chunks start on odd planes), else -1
     auto prolong_pair = [&](double2 v, int jodd, int k, int cro, auto KO) {
-#if MGMC_ZS_EXP == 8  // timing experiment: coarse ring loads only, no prolongation arithmetic
-        return v;
-#endif
         const int K0 = k >> 1;
         const int kodd = decltype(KO)::value >= 0 ? decltype(KO)::value : (k & 1);
         const double awx = ldexp(al1, -(jodd + kodd)), awy = ldexp(al0, -(jodd + kodd));
@@ -338,7 +320,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     // the even elements of pairs c-1, c (e = 0) or the odd elements of pairs c, c+1 (e = 1)
     // below = the value at (i, j, k-1): from LDS for the first colour, from a register for the second
     auto row_sum = [&](int k, int o, int e, double below) {
-        if (MGMC_ZS_EXP == 4 || MGMC_ZS_EXP == 5) return below;
         const double* s0 = xs + slot(k) * PS;
         const double* sp = xs + slot(k + 1) * PS;
         const int xm = e ? o - WP : o + WP - 1;
@@ -356,22 +337,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         const uint32_t pair = (uint32_t)(k - 1) * plane_pairs + t.pbase;
         uint32_t key0 = a.G.key.k0, key1 = a.G.key.k1;
         asm volatile("" : "+s"(key0), "+s"(key1));  // keep the round-key schedule out of the SGPR budget
-#if MGMC_ZS_EXP == 3  // timing experiment: BM without Philox
-        Philox4 rnd;
-        rnd.v[0] = pair * 2654435761u; rnd.v[1] = pair ^ key0; rnd.v[2] = pair * 40503u; rnd.v[3] = pair + key1;
-#else
         const Philox4 rnd = philox4x32_10(pair, a.G.tag, s_lo, s_hi, key0, key1);
-#endif
         double z0, z1;
-#if MGMC_ZS_EXP == 9  // timing experiment: wave-uniform table indices (no LDS bank conflicts in Box-Muller)
-        Philox4 rnd9 = rnd;
-        rnd9.v[0] &= 0x3FFFFu; rnd9.v[2] &= 0x3FFFFu;
-        normal_pair_t(rnd9, &z0, &z1, tab, tab + 64, tab + 128, tab + 192);
-#elif MGMC_ZS_EXP == 1 || MGMC_ZS_EXP == 5  // timing experiment: no noise generation
-        z0 = (double)(rnd.v[0] & 1); z1 = (double)(rnd.v[2] & 1);
-#else
         normal_pair_t(rnd, &z0, &z1, tab, tab + 64, tab + 128, tab + 192);
-#endif
         return make_double2(z0, z1);
     };
     // One z step p (LDS ring = planes p-2 .. p+1):
@@ -406,10 +374,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
             }
             issue_x(p + 2);
             if (active_wave) fnxt = load_f(p + 1);
-            ZS_STEP_SYNC();
+            __syncthreads();
             // first colour on plane p: c = fma(sd, z, f), x = fma(omega/diag, c - S, x); the second
             // colour's right-hand side of the pair, c' = fma(sd, z', f')
-            if (interior_plane(p) && (MGMC_ZS_EXP != 2 && MGMC_ZS_EXP != 5 ? active_wave : core_wave)) {
+            if (interior_plane(p) && active_wave) {
                 if (inf) {
                     const double res = row_sum(p, o1, e, xs[slot(p - 1) * PS + o1]);
                     const double crhs = fma(sd, e ? z.y : z.x, e ? fcur.y : fcur.x);
@@ -418,7 +386,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
                 }
                 pk_out = fma(sd, e ? z.x : z.y, e ? fcur.x : fcur.y);
             }
-            ZS_STEP_SYNC();
+            __syncthreads();
             // second colour on plane k = p-1 (its element is e: the parity flips with the plane)
             const int k = p - 1;
             if (core_wave) {
@@ -431,12 +399,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
                     double* dst = a.xout + (long long)k * L.sp + t.goff;
                     // (x, y) = (odd, even) element; the second colour is element e here
                     const double2 out = e ? make_double2(fv, sv) : make_double2(sv, fv);
-                    if (MGMC_ZS_NT_STORE) {  // streaming store: keep the write stream out of L2
-                        __builtin_nontemporal_store(out.x, dst);
-                        __builtin_nontemporal_store(out.y, dst + 1);
-                    } else {
-                        *reinterpret_cast<double2*>(dst) = out;
-                    }
+                    // streaming store: keep the write stream out of L2
+                    __builtin_nontemporal_store(out.x, dst);
+                    __builtin_nontemporal_store(out.y, dst + 1);
                 }
                 fb = fv;
             }
@@ -477,13 +442,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     else run(std::integral_constant<int, 0>{});
 }
 
-#ifndef MGMC_ZS_LDS_EXTRA
-#define MGMC_ZS_LDS_EXTRA 0  // timing experiments only: extra LDS bytes of the plain variant (occupancy)
-#endif
 inline size_t zsweep_lds_bytes(int XP, int TY, bool prolong) {
     const int RS = 2 * (XP + 2) + 2, R = TY + 4;
     const int coarse = prolong ? 2 * (TY / 2 + 3) * (XP + 8) : 0;
-    return (size_t)(4 * R * RS + 3 * 64 + 130 + coarse) * sizeof(double) + (prolong ? 0 : MGMC_ZS_LDS_EXTRA);
+    return (size_t)(4 * R * RS + 3 * 64 + 130 + coarse) * sizeof(double);
 }
 
 }  // namespace mgmc

@@ -31,7 +31,7 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in include/mgmc.h but not exported"
         assert s in bound, f"{s} not bound in multigridmc_amd/_native.py"
-    assert lib.mgmc_abi_version() == 4
+    assert lib.mgmc_abi_version() == _native.ABI_VERSION == 5
 
 
 def test_library_is_gfx950_code_object():
@@ -260,7 +260,7 @@ def test_cpp_host_side_describe_and_loud_failure(tmp_path, asan):
     exe = build_client(tmp_path, asan=asan)
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
     out = subprocess.run([exe, "describe"], capture_output=True, text=True, check=True, env=env).stdout.split("\n")
-    assert out[0] == "abi 4"
+    assert out[0] == "abi 5"
     cfg_levels = mg.describe(mg.make_config(mg.ShiftedLaplaceFDOperator(mg.Lattice3d(64, 64, 64), 25.0),
                                             mg.MultigridParameters(nlevel=4)))
     for level, line in enumerate(out[1:5]):
