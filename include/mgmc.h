@@ -156,6 +156,21 @@ int mgmc_csr_colour_scheme(const mgmc_config* cfg, int level, int64_t nrow, cons
 int mgmc_stencil_of_csr(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr, const int32_t* col,
                         const double* val, double* stencil);
 
+/* Host-side bounds check of one level's padded layout (ABI 5; host only; mgmc_create runs it on
+ * every level of every handle).  families: MGMC_LAYOUT_* bits of the kernels that address the level;
+ * reach: 1 (3^d couplings) or 2 (the squared FD operator's levels); zrestrict_cx: coarse points per
+ * tile of the z-marching residual + restriction on this level (0: none).  legacy: bit 0 builds the
+ * round-2 reach-2 layout without its margin rows / planes, bit 1 the unclamped restriction columns
+ * (both out of bounds: kept so the test shows the check catches them).  MGMC_OK, or MGMC_E_INVALID
+ * with the offending offset range in mgmc_last_error(NULL). */
+#define MGMC_LAYOUT_POINT 1u
+#define MGMC_LAYOUT_PAIRS 2u
+#define MGMC_LAYOUT_ZSWEEP 4u
+#define MGMC_LAYOUT_ZSWEEP_COARSE 8u
+#define MGMC_LAYOUT_ZRESTRICT 16u
+#define MGMC_LAYOUT_RB2D 32u
+int mgmc_check_layout(int dim, const int* n, int reach, unsigned families, int zrestrict_cx, int legacy);
+
 /* ---- lifetime ---- */
 int mgmc_create(const mgmc_config* cfg, int device, uint64_t seed, uint64_t chain_id, mgmc_handle** out);
 /* A sampler on a fine operator given as a matrix (LinearOperator::A_sparse, linear_operator.hh:187):

@@ -84,6 +84,7 @@ SIGNATURES = [
     ("mgmc_operator_csr", c_int, [POINTER(MgmcOperatorDesc), POINTER(c_int64), POINTER(ctypes.c_int32), _DP]),
     ("mgmc_csr_colour_scheme", c_int, [POINTER(MgmcConfig), c_int, c_int64, POINTER(c_int64), POINTER(ctypes.c_int32),
                                        POINTER(c_int)]),
+    ("mgmc_check_layout", c_int, [c_int, POINTER(c_int), c_int, ctypes.c_uint, c_int, c_int]),
     ("mgmc_stencil_of_csr", c_int, [POINTER(MgmcConfig), c_int64, POINTER(c_int64), POINTER(ctypes.c_int32), _DP,
                                     _DP]),
     ("mgmc_create_stencil_batch", c_int, [POINTER(MgmcConfig), _DP, c_int, c_uint64, c_uint64, c_int,

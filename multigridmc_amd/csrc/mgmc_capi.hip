@@ -22,6 +22,11 @@
 #include "mgmc_hierarchy.hpp"
 #include "mgmc_kernels.hpp"
 #include "mgmc_zsweep.hpp"
+#include "mgmc_layout_check.hpp"
+static_assert(MGMC_LAYOUT_POINT == mgmc::LF_POINT && MGMC_LAYOUT_PAIRS == mgmc::LF_PAIRS &&
+                  MGMC_LAYOUT_ZSWEEP == mgmc::LF_ZSWEEP && MGMC_LAYOUT_ZSWEEP_COARSE == mgmc::LF_ZSWEEP_C &&
+                  MGMC_LAYOUT_ZRESTRICT == mgmc::LF_ZRESTRICT && MGMC_LAYOUT_RB2D == mgmc::LF_RB2D,
+              "layout family bits");
 #include "mgmc_zrestrict.hpp"
 #include "mgmc_tail.hpp"
 #include "mgmc_gsweep.hpp"
@@ -1712,6 +1717,27 @@ int mgmc_describe(const mgmc_config* cfg, mgmc_level_desc* out, int max_levels) 
     return (int)lv.size();
 }
 
+// the kernel families that address level l (the launch_* dispatch of this handle) and their check
+static int zrestrict_cx_of(const mgmc_handle* h, int l) {  // launch_residual_restrict's tile width
+    if (l + 1 >= (int)h->levels.size()) return 0;
+    const Level& lf = h->levels[l];
+    const Level& lc = h->levels[l + 1];
+    if (lf.spec.dim != 3 || lf.field || (lf.paths & PATH_NO_ZRESTRICT) || lc.L.nx < 8) return 0;
+    return lc.L.nx < 32 ? 16 : 64;
+}
+static std::string check_level_layout_of(const mgmc_handle* h, int l) {
+    const Level& lv = h->levels[l];
+    unsigned fam = LF_POINT;
+    if (lv.pairs || lv.quads) fam |= LF_PAIRS;
+    if (lv.zsweep) fam |= LF_ZSWEEP;
+    if (lv.rb2d) fam |= LF_RB2D;
+    const int cx = zrestrict_cx_of(h, l);
+    if (cx) fam |= LF_ZRESTRICT;
+    if (l > 0 && h->levels[l - 1].zsweep) fam |= LF_ZSWEEP_C;
+    const int reach = lv.field && (lv.F.scheme == 9 || lv.F.scheme == 27) ? 2 : 1;
+    return check_level_layout(lv.L, fam, reach, cx);
+}
+
 // mgmc_create / mgmc_create_csr: csr = the fine operator's matrix (null: the constant-coefficient
 // hierarchy of cfg), every level then built from matrices
 static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, uint64_t seed, uint64_t chain_id,
@@ -1852,6 +1878,14 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
     hipMemsetAsync(h->mom, 0, 4 * sizeof(double) * nchains, h->stream);
     if (cfg->coarse_solver == MGMC_COARSE_CHOLESKY && (rc = build_coarse_chol(h, nullptr, nullptr, 0)) != MGMC_OK)
         return bail(rc);
+    // every level's extreme addresses against its store (mgmc_layout_check.hpp)
+    for (size_t l = 0; l < h->levels.size(); ++l) {
+        const std::string e = check_level_layout_of(h, (int)l);
+        if (!e.empty()) {
+            h->last_error = "internal layout check failed: " + e;
+            return bail(MGMC_E_INVALID);
+        }
+    }
     // op sequence of one sample
     build_ops(h);
     if ((rc = build_tails(h)) != MGMC_OK) return bail(rc);
@@ -1939,6 +1973,15 @@ int mgmc_create_csr_batch(const mgmc_config* cfg, int64_t nrow, const int64_t* r
     A.col.assign(col, col + rowptr[nrow]);
     A.val.assign(val, val + rowptr[nrow]);
     return create_impl(&c, &A, device, seed, chain0, nchains, out);
+}
+
+int mgmc_check_layout(int dim, const int* n, int reach, unsigned families, int zrestrict_cx, int legacy) {
+    if (!n || (dim != 2 && dim != 3) || reach < 1 || reach > 2) return fail(nullptr, MGMC_E_INVALID, "invalid argument");
+    // legacy bit 0: the round-2 layout without the reach-2 margin; bit 1: unclamped restriction columns
+    const Layout L = make_layout(dim, n, reach == 2 && !(legacy & 1));
+    const std::string e = check_level_layout(L, families, reach, zrestrict_cx, (legacy & 2) != 0);
+    if (!e.empty()) return fail(nullptr, MGMC_E_INVALID, e);
+    return MGMC_OK;
 }
 
 int mgmc_stencil_of_csr(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr, const int32_t* col,

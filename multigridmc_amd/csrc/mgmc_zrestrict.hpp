@@ -16,7 +16,7 @@
 // LDS rows are colour-split as in mgmc_zsweep.hpp -- [odd positions | even positions | pad] -- so
 // lanes owning consecutive pairs (residual) or consecutive coarse points (restriction) read
 // consecutive doubles.  All global loads are unconditional: rows / planes outside the level are
-// clamped onto the zero boundary rows / planes, columns past a row end land in the zero padding.
+// clamped onto the zero boundary rows / planes, columns past a row end onto the zero pair (nx+1, nx+2).
 // Global traffic: x and f once (16 B per fine vertex) + f_c, x_c (2 B per fine vertex).
 #pragma once
 #include "mgmc_kernels.hpp"
@@ -78,6 +78,11 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
 
     auto xslot = [](int k) { return (k + 9) % 3; };
     auto clamp_row = [&](int j) { return j < 0 ? 0 : (j > Lf.ny ? Lf.ny : j); };
+    // pairs past the row end read the zero pair (nx+1, nx+2) of the row padding: the last tile's
+    // columns can run up to 2 CX - 2 past nx (nx - 1 = 1 mod CX), beyond the padding; the positions
+    // involved are outside the lattice, their values only reach residuals that are forced to 0
+    // (mgmc_layout_check.hpp)
+    auto clamp_col = [&](int i) { return i > Lf.nx + 1 ? Lf.nx + 1 : i; };
     auto plane_ptr = [&](const double* v, int k) { return v + (long long)(k < 0 ? 0 : (k > Lf.nz ? Lf.nz : k)) * Lf.sp; };
 
     int xoff[NLX], xlds[NLX];
@@ -89,7 +94,7 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
         if (it < XR * XPP) {
             const int r = it / XPP, c2 = it - r * XPP;
             xlds[u] = r * XS + c2;
-            xoff[u] = (int)((long long)clamp_row(xj0 + r) * Lf.sx + (xi0 + 2 * c2) + Lf.off);
+            xoff[u] = (int)((long long)clamp_row(xj0 + r) * Lf.sx + clamp_col(xi0 + 2 * c2) + Lf.off);
         }
     }
     int roff[NLR], rlds[NLR], rflag[NLR], rxo[NLR];
@@ -105,7 +110,7 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
             const int j = rj0 + r, i = ri0 + 2 * c2;
             rlds[u] = r * RSr + c2;
             rxo[u] = (r + 1) * XS + (c2 + 1);  // x LDS offset of the same odd vertex
-            roff[u] = (int)((long long)clamp_row(j) * Lf.sx + i + Lf.off);
+            roff[u] = (int)((long long)clamp_row(j) * Lf.sx + clamp_col(i) + Lf.off);
             const bool rin = j >= 1 && j <= Lf.ny - 1;
             rflag[u] = (rin && i >= 1 && i <= Lf.nx - 1 ? 1 : 0) | (rin && i + 1 <= Lf.nx - 1 ? 2 : 0);
         }

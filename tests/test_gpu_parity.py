@@ -59,6 +59,9 @@ CONFIGS = {
     "3d_zres27": ((512, 16, 24), dict(nlevel=3)),
     # coarse rows / planes ending exactly at a tile / chunk boundary, SSOR pre-sampler
     "3d_zsr_edges": ((128, 34, 18), dict(nlevel=2)),
+    # n/2 - 1 = 1 (mod 64): the residual + restriction's last tile runs past the row end (columns
+    # clamped onto the zero pad pair since round 3, tests/test_layout.py)
+    "3d_zres_lasttile": ((132, 36, 20), dict(nlevel=2)),
     "3d_zsr_ssor_W": ((128, 64, 64), dict(nlevel=3, cycle=2, smoother="SSOR", npresmooth=2, omega=0.9)),
     # dense Cholesky coarse sampler (CholeskySampler, x = G f + U xi on the coarsest level)
     "2d64_chol_W": ((64, 64), dict(nlevel=4, cycle=2, coarse_solver="Cholesky")),
@@ -79,7 +82,8 @@ def test_normals_bitwise(hip_device):
     s.close()
 
 
-@pytest.mark.parametrize("name", ["2d64_template_W", "3d16", "3d_aniso", "2d_aniso_ssor", "3d_zres7", "3d_zres27"])
+@pytest.mark.parametrize("name", ["2d64_template_W", "3d16", "3d_aniso", "2d_aniso_ssor", "3d_zres7", "3d_zres27",
+                                  "3d_zres_lasttile"])
 def test_component_kernels_bitwise(hip_device, name):
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)
