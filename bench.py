@@ -127,7 +127,7 @@ class Collectives:
 
     def __init__(self, sampler, rank, world):
         self.s, self.rank, self.world = sampler, rank, world
-        self.kind, self.rccl_ranks = "none", 0
+        self.kind, self.rccl_ranks, self.n_devices = "none", 0, 1
         if world == 1:
             return
         import threading
@@ -136,6 +136,7 @@ class Collectives:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         buses = [None] * world
         dist.all_gather_object(buses, sampler.comm_info()["pci_bus_id"])
+        self.n_devices = len(set(buses))  # distinct GPUs the ranks run on
         if len(set(buses)) < world:
             if os.environ.get("MGMC_BENCH_DEVICE") is None:
                 raise CommError(f"ranks share GPUs (PCI bus ids {buses}): RCCL cannot run and the line would "
@@ -277,15 +278,19 @@ def main():
             plain3d = args.dim == 3 and not args.fem and not args.posterior
             tr_pre, prov = stored_traffic(args.traffic_file, n, "pre_sweep") if plain3d else (None, None)
             tr_post, prov2 = stored_traffic(args.traffic_file, n, "post_sweep") if plain3d else (None, None)
+            kern = sampler.level_kernels(0)  # the kernels level 0 really runs on (mgmc_level_kernels)
             pre = sweep_roofline(timed["pre_ms"], timed["npre"], 24.0 * n0 * K, tr_pre if K == 1 else None, prov,
-                                 "fine pre-sweep k_zsweep_rb7 (one red-black Gibbs sweep of level 0)")
+                                 f"fine pre-sweep {kern['sweep']} (one Gibbs sweep of level 0)")
             per_kernel["pre_sweep"] = pre
             if timed["npost"] > 0:
                 n1 = mg.Lattice(*((n // 2,) * args.dim)).Nvertex
-                post = sweep_roofline(timed["post_ms"], timed["npost"], (24.0 * n0 + 8.0 * n1) * K,
+                fused = "post_sweep" in kern
+                post = sweep_roofline(timed["post_ms"], timed["npost"], (24.0 * n0 + (8.0 * n1 if fused else 0.0)) * K,
                                       tr_post if K == 1 else None, prov2,
-                                      "fine post-sweep k_zsweep_rb7<PROLONG> (prolongate-add of level 1 fused, "
-                                      "24 B per fine + 8 B per coarse unknown; its own segment of the cycle graph)")
+                                      f"fine post-sweep {kern.get('post_sweep', kern['sweep'])} "
+                                      + ("(prolongate-add of level 1 fused, 24 B per fine + 8 B per coarse unknown; "
+                                         "its own segment of the cycle graph)" if fused else
+                                         "(one Gibbs sweep of level 0; the prolongation is a separate pass)"))
                 per_kernel["post_sweep"] = post
             # the dominant kernel (the longer of the two) is the headline roofline
             roof = dict(max(per_kernel.values(), key=lambda r: r["avg_launch_ms"]))
@@ -306,6 +311,7 @@ def main():
             "value": round(value, 3),
             "unit": "samples/s",
             "n_gpus": world,
+            "n_devices": coll.n_devices,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),

@@ -95,6 +95,7 @@ SIGNATURES = [
     ("mgmc_nchains", c_int, [_H]),
     ("mgmc_destroy", c_int, [_H]),
     ("mgmc_level_desc_get", c_int, [_H, c_int, POINTER(MgmcLevelDesc)]),
+    ("mgmc_level_kernels", c_int, [_H, c_int, ctypes.c_char_p, c_size_t]),
     ("mgmc_set_lowrank", c_int, [_H, c_int, POINTER(c_int64), POINTER(c_int64), _DP, _DP]),
     ("mgmc_lowrank_info", c_int, [_H, c_int, c_int, POINTER(c_int), POINTER(c_int64)]),
     ("mgmc_set_rhs", c_int, [_H, _DP, c_size_t]),

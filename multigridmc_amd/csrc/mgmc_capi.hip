@@ -2115,6 +2115,49 @@ int mgmc_level_desc_get(const mgmc_handle* h, int level, mgmc_level_desc* out) {
     return MGMC_OK;
 }
 
+int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
+    if (!h || !out || n == 0) return fail(nullptr, MGMC_E_INVALID, "null argument");
+    if (level < 0 || level >= (int)h->levels.size()) return fail(nullptr, MGMC_E_INVALID, "level out of range");
+    const Level& lv = h->levels[level];
+    const int dim = lv.spec.dim, np = lv.spec.npoints;
+    const int tl = tail_level(h);
+    const bool last = level + 1 == (int)h->levels.size();
+    std::string sweep, post, res;
+    if (tl >= 0 && level >= tl) {
+        sweep = "k_tail<" + std::to_string(dim) + ">";
+    } else if (last) {
+        sweep = h->cfg.coarse_solver == MGMC_COARSE_CHOLESKY ? "k_coarse_chol" : "k_coarse_ssor_lds (or separate colour passes)";
+    } else if (lv.field) {
+        sweep = "k_fsweep<" + std::to_string(dim) + ">";
+    } else if (lv.zsweep) {
+        sweep = "k_zsweep_rb7<32," + std::to_string(MGMC_ZS_SHAPE_TY) + ",...,0>";
+        if (!(h->paths & PATH_NO_FUSE_PROLONG)) post = "k_zsweep_rb7<32," + std::to_string(MGMC_ZS_SHAPE_TYP) + ",...,PROLONG>";
+    } else if (lv.quads) {
+        sweep = "k_sweep_quads<" + std::to_string(dim) + ">";
+    } else if (lv.rb2d) {
+        sweep = "k_rb2d";
+    } else if (lv.pairs) {
+        sweep = "k_sweep_pairs<" + std::to_string(dim) + ">";
+    } else {
+        sweep = (np == 2 * dim + 1 ? "k_sweep_rb<" : "k_sweep_mc<") + std::to_string(dim) + ">";
+    }
+    if (!last && !(tl >= 0 && level >= tl)) {
+        const int cx = zrestrict_cx_of(h, level);
+        if (lv.field) res = "k_fresidual + k_restrict";
+        else if (cx) {
+            const Level& lc = h->levels[level + 1];
+            const bool wide = np == 7 && cx == 64 &&
+                              (long long)((lc.L.nx + 62) / 64) * ((lc.L.ny + 6) / 8) * (lc.L.nz - 1) >= 16 * 1024;
+            res = "k_zresrestrict<" + std::to_string(np) + "," + std::to_string(cx) + "," + (wide ? "8" : "4") + ">";
+        } else res = "k_residual_restrict<" + std::to_string(dim) + "," + std::to_string(np) + ">";
+    }
+    std::string text = "sweep=" + sweep;
+    if (!post.empty()) text += ";post_sweep=" + post;
+    if (!res.empty()) text += ";residual_restrict=" + res;
+    snprintf(out, n, "%s", text.c_str());
+    return MGMC_OK;
+}
+
 // fine-level vector v of chain c (c < 0: every chain gets the upload of chain 0)
 static int put_fine(mgmc_handle* h, double* v, int c, const double* host, size_t n, const char* what) {
     if (!h || !host) return fail(h, MGMC_E_INVALID, "null argument");

@@ -579,6 +579,13 @@ class MultigridMCSampler:
                 "ndof": int(d.ndof), "stencil": np.array(d.stencil[:]), "varcoef": bool(d.varcoef)}
 
     # -- component operations (reference layout host vectors) --
+    def level_kernels(self, level: int) -> dict:
+        """The kernels the handle runs on a level (mgmc_level_kernels): {"sweep": ..., "post_sweep": ...,
+        "residual_restrict": ...}"""
+        buf = ctypes.create_string_buffer(512)
+        self._chk(self.lib.mgmc_level_kernels(self.handle, int(level), buf, 512))
+        return dict(kv.split("=", 1) for kv in buf.value.decode().split(";"))
+
     def operator_apply(self, level: int, x) -> np.ndarray:
         n = self.level_desc(level)["ndof"]
         x = _as_f64(x, n, "x")

@@ -128,3 +128,14 @@ def test_headline_cycle_and_qoi_series_bitwise(headline):
     assert np.array_equal(z_dev, z_orc)
     assert np.array_equal(s.get_state(), orc.get_state())
     assert s.get_sample_index() == 4
+
+
+def test_headline_kernel_instances(headline):
+    """The instances the tests above ran are the benchmark's (mgmc_level_kernels): the fused z-sweep
+    pair on level 0 with the 64 x 8 residual + restriction, pair passes on level 1, k_tail below."""
+    s, orc, lat, p = headline
+    k0 = s.level_kernels(0)
+    assert k0["sweep"].startswith("k_zsweep_rb7<") and k0["post_sweep"].endswith("PROLONG>")
+    assert k0["residual_restrict"] == "k_zresrestrict<7,64,8>"
+    assert s.level_kernels(1) == {"sweep": "k_sweep_pairs<3>", "residual_restrict": "k_zresrestrict<27,64,4>"}
+    assert s.level_kernels(NLEVEL - 1)["sweep"] == "k_tail<3>"

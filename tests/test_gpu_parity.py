@@ -223,6 +223,16 @@ def test_nonfinite_state_fails_loudly(hip_device, name, qoi):
     s.close()
 
 
+@pytest.mark.parametrize("name,sweep", [("2d64_template_W", "k_rb2d"), ("3d128_zsweep", "k_zsweep_rb7<"),
+                                        ("3d16", "k_sweep_rb<3>")])
+def test_level_kernels_labels(hip_device, name, sweep):
+    """mgmc_level_kernels names the fine sweep each lattice really runs (bench.py's roofline labels)."""
+    shape, kw = CONFIGS[name]
+    s, p, lat = make(shape, **kw)
+    assert s.level_kernels(0)["sweep"].startswith(sweep)
+    s.close()
+
+
 def test_unknown_disable_token_rejected(hip_device, monkeypatch):
     monkeypatch.setenv("MGMC_DISABLE", "tail,no_such_path")
     with pytest.raises(mg.MgmcError, match="no_such_path"):
