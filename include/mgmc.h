@@ -239,6 +239,15 @@ int mgmc_apply(mgmc_handle* h, const double* f, double* x, size_t n);
  * linear_operator/measured_operator.cc:74-91) is appended to a device time series and folded
  * into device-side running moments.  If qoi_out != NULL the nsteps values are copied back. */
 int mgmc_sample(mgmc_handle* h, int nsteps, int64_t qoi_index, double* qoi_out);
+/* qoi_index = MGMC_QOI_VECTOR records z = b^T x with the vector b of mgmc_set_qoi_vector (ABI 5). */
+#define MGMC_QOI_VECTOR (-2)
+/* The QoI vector b for qoi_index = MGMC_QOI_VECTOR: the radius > 0 measurement vector of
+ * MeasuredOperator::measurement_vector (linear_operator/measured_operator.cc:92-171) that
+ * driver_mgmc.cc:58-59, :76 dots with every sample.  nnz entries, rows strictly ascending (reference
+ * vertex indices), values; nnz = 0 removes it.  The dot runs in the cycle graph in a fixed order
+ * (4096-entry blocks, lane-strided sums, xor butterflies -- the low-rank dots' order): the state
+ * stays in HBM.  Rebuilds the handle's graphs. */
+int mgmc_set_qoi_vector(mgmc_handle* h, int64_t nnz, const int64_t* rows, const double* vals);
 /* Enqueue nsteps cycles on the handle's stream without synchronising or copying back. */
 int mgmc_sample_async(mgmc_handle* h, int nsteps, int64_t qoi_index);
 int mgmc_synchronize(mgmc_handle* h);

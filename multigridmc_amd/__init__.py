@@ -5,7 +5,7 @@ residual+restriction, prolongate-add, single-workgroup coarse SSOR sampler) live
 csrc/*.hip behind the C-ABI of include/mgmc.h; this package is the host-side mirror of the
 reference's Sampler / LinearOperator interfaces.
 """
-from ._native import MgmcError, load_library  # noqa: F401
+from ._native import QOI_VECTOR, MgmcError, load_library  # noqa: F401
 from .measured import LowRankUpdate, MeasuredOperator, measurement_vector, synthetic_posterior  # noqa: F401
 from .parameters import MultigridParameters, read_config  # noqa: F401
 from .sampler import (  # noqa: F401

@@ -18,6 +18,7 @@ MGMC_E_HIP = -2
 MGMC_E_NOMEM = -3
 MGMC_E_UNSUPPORTED = -4
 MGMC_E_NONFINITE = -5
+QOI_VECTOR = -2  # mgmc_sample's qoi_index for the vector of mgmc_set_qoi_vector
 
 SMOOTHER_SOR = 0
 SMOOTHER_SSOR = 1
@@ -105,6 +106,7 @@ SIGNATURES = [
     ("mgmc_get_state_chain", c_int, [_H, c_int, _DP, c_size_t]),
     ("mgmc_apply", c_int, [_H, _DP, _DP, c_size_t]),
     ("mgmc_sample", c_int, [_H, c_int, c_int64, _DP]),
+    ("mgmc_set_qoi_vector", c_int, [_H, c_int64, POINTER(c_int64), _DP]),
     ("mgmc_sample_async", c_int, [_H, c_int, c_int64]),
     ("mgmc_synchronize", c_int, [_H]),
     ("mgmc_qoi_moments", c_int, [_H, _DP]),

@@ -262,7 +262,13 @@ struct mgmc_handle {
     hipGraphNode_t timed_node[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     hipEvent_t timed_ev0[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     int unroll = 1;
-    int64_t qoi_store_index = -1;
+    int64_t qoi_store_index = -1;   // padded offset of the QoI vertex, -1 none, -2 the QoI vector
+    // QoI vector b (mgmc_set_qoi_vector): padded offsets, values, block partials [nchains][nblk]
+    long long* qv_off = nullptr;
+    double* qv_val = nullptr;
+    double* qv_part = nullptr;
+    long long qv_n = 0;
+    int qv_nblk = 0;
     std::string last_error;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -1388,6 +1394,16 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 break;
             }
             case OP_QOI: {
+                if (h->qv_n > 0) {  // a QoI vector is installed: its dot (skipped unless ctrl[2] = -2)
+                    hipLaunchKernelGGL(k_qoi_dot, dim3(h->qv_nblk, nch), dim3(64), 0, s, (const double*)h->levels[0].x,
+                                       (const long long*)h->qv_off, (const double*)h->qv_val, h->qv_n,
+                                       (const uint64_t*)h->ctrl, h->qv_part, h->qv_nblk,
+                                       (long long)h->levels[0].L.nstore);
+                    hipLaunchKernelGGL(k_qoi_record_vec, dim3(1), dim3(64 * nch), 0, s, (const double*)h->levels[0].x,
+                                       h->ctrl, h->series, h->series_cap, h->mom, nch, (long long)h->levels[0].L.nstore,
+                                       (const double*)h->qv_part, h->qv_nblk);
+                    break;
+                }
                 hipLaunchKernelGGL(k_qoi_record, dim3(1), dim3(64 * ((nch + 63) / 64)), 0, s,
                                    (const double*)h->levels[0].x, h->ctrl, h->series, h->series_cap, h->mom, nch,
                                    (long long)h->levels[0].L.nstore);
@@ -2102,6 +2118,9 @@ int mgmc_destroy(mgmc_handle* h) {
     if (h->ctrl) hipFree(h->ctrl);
     if (h->mom) hipFree(h->mom);
     if (h->series) hipFree(h->series);
+    if (h->qv_off) hipFree(h->qv_off);
+    if (h->qv_val) hipFree(h->qv_val);
+    if (h->qv_part) hipFree(h->qv_part);
     if (h->lex_tmp) hipFree(h->lex_tmp);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
@@ -2213,14 +2232,21 @@ static int check_finite(mgmc_handle* h) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
     if (flag == 0) return MGMC_OK;
     return fail(h, MGMC_E_NONFINITE,
-                "non-finite chain state: the " + std::string(h->qoi_store_index >= 0 ? "QoI vertex" : "lattice centre") +
+                "non-finite chain state: the " +
+                    std::string(h->qoi_store_index >= 0 ? "QoI vertex"
+                                                        : (h->qoi_store_index == -2 ? "QoI vector's dot" : "lattice centre")) +
                     " became NaN / Inf in sample " + std::to_string(flag - 1) +
                     " (check the right-hand side, the low-rank Sigma and omega; mgmc_set_state clears the guard)");
 }
 
 static int set_qoi(mgmc_handle* h, int64_t qoi_index) {
     int64_t store = -1;
-    if (qoi_index >= 0) {
+    if (qoi_index == MGMC_QOI_VECTOR) {
+        if (h->qv_n == 0) return fail(h, MGMC_E_INVALID, "MGMC_QOI_VECTOR: no QoI vector installed (mgmc_set_qoi_vector)");
+        store = -2;
+    } else if (qoi_index < -1) {
+        return fail(h, MGMC_E_INVALID, "qoi index out of range");
+    } else if (qoi_index >= 0) {
         const Level& lv = h->levels[0];
         if ((uint64_t)qoi_index >= lv.spec.ndof) return fail(h, MGMC_E_INVALID, "qoi index out of range");
         const int nxi = lv.L.nx - 1, nyi = lv.L.ny - 1;
@@ -2273,10 +2299,51 @@ int mgmc_synchronize(mgmc_handle* h) {
 int mgmc_sample(mgmc_handle* h, int nsteps, int64_t qoi_index, double* qoi_out) {
     int rc = mgmc_sample_async(h, nsteps, qoi_index);
     if (rc) return rc;
-    if (qoi_out && nsteps > 0 && qoi_index >= 0)
+    if (qoi_out && nsteps > 0 && (qoi_index >= 0 || qoi_index == MGMC_QOI_VECTOR))
         HIPCHK(h, hipMemcpyAsync(qoi_out, h->series, nsteps * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return check_finite(h);
+}
+
+int mgmc_set_qoi_vector(mgmc_handle* h, int64_t nnz, const int64_t* rows, const double* vals) {
+    if (!h || nnz < 0 || (nnz > 0 && (!rows || !vals))) return fail(h, MGMC_E_INVALID, "invalid argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const Level& lv = h->levels[0];
+    std::vector<long long> off((size_t)nnz);
+    const int64_t nxi = lv.L.nx - 1, nyi = lv.L.ny - 1;
+    for (int64_t e = 0; e < nnz; ++e) {
+        if (rows[e] < 0 || (uint64_t)rows[e] >= lv.spec.ndof || (e > 0 && rows[e] <= rows[e - 1]))
+            return fail(h, MGMC_E_INVALID, "QoI vector rows must be strictly ascending vertex indices");
+        if (!std::isfinite(vals[e])) return fail(h, MGMC_E_INVALID, "non-finite QoI vector value");
+        const int i = (int)(rows[e] % nxi) + 1, j = (int)((rows[e] / nxi) % nyi) + 1;
+        const int k = lv.spec.dim == 3 ? (int)(rows[e] / (nxi * nyi)) + 1 : 0;
+        off[(size_t)e] = lv.L.at(i, j, k);
+    }
+    if (h->qv_off) hipFree(h->qv_off);
+    if (h->qv_val) hipFree(h->qv_val);
+    if (h->qv_part) hipFree(h->qv_part);
+    h->qv_off = nullptr;
+    h->qv_val = nullptr;
+    h->qv_part = nullptr;
+    h->qv_n = 0;
+    h->qv_nblk = 0;
+    if (nnz > 0) {
+        const int nblk = (int)((nnz + QV_BLK - 1) / QV_BLK);
+        if (hipMalloc(&h->qv_off, nnz * sizeof(long long)) != hipSuccess ||
+            hipMalloc(&h->qv_val, nnz * sizeof(double)) != hipSuccess ||
+            hipMalloc(&h->qv_part, (size_t)nblk * h->nchains * sizeof(double)) != hipSuccess)
+            return fail(h, MGMC_E_NOMEM, "device allocation failed (QoI vector)");
+        HIPCHK(h, hipMemcpy(h->qv_off, off.data(), nnz * sizeof(long long), hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(h->qv_val, vals, nnz * sizeof(double), hipMemcpyHostToDevice));
+        h->qv_n = nnz;
+        h->qv_nblk = nblk;
+    }
+    if (h->qoi_store_index == -2) {  // the vector mode ends with the vector
+        int rc = set_qoi(h, -1);
+        if (rc) return rc;
+    }
+    return build_graphs(h);
 }
 
 int mgmc_qoi_moments(mgmc_handle* h, double out[3]) { return mgmc_qoi_moments_chain(h, 0, out); }

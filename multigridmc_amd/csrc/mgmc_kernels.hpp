@@ -623,6 +623,81 @@ __global__ void k_qoi_record(const double* __restrict__ x, uint64_t* ctrl, doubl
     }
 }
 
+// ---- QoI vector z = b^T x per chain (mgmc_set_qoi_vector; the radius > 0 measurement vector of
+// measured_operator.cc:92-171, dotted with the sample as driver_mgmc.cc:76 does) in the fixed order of
+// the low-rank dots: entries ascending in 4096-entry blocks, lane l of a wavefront sums entries
+// l, l+64, ... of its block from 0.0, the lanes combine by the xor butterfly; k_qoi_record_vec combines
+// the block partials the same way.  The oracle's blocked_dot is the same sequence. ----
+constexpr int QV_BLK = 4096;
+__device__ inline double butterfly64(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = v + __shfl_xor(v, o, 64);
+    return v;
+}
+__global__ void __launch_bounds__(64) k_qoi_dot(const double* __restrict__ x, const long long* __restrict__ off,
+                                                const double* __restrict__ val, long long n, const uint64_t* ctrl,
+                                                double* __restrict__ part, int nblk, long long cs) {
+    if ((long long)ctrl[2] != -2) return;  // not recording the vector in this call (uniform)
+    const int b = blockIdx.x, c = blockIdx.y, l = threadIdx.x;
+    const double* xc = x + (long long)c * cs;
+    const long long e0 = (long long)b * QV_BLK, e1 = min(n, e0 + (long long)QV_BLK);
+    double acc = 0.0;
+    constexpr int U = 8;  // products of U entries in flight, then added in entry order
+    for (long long e = e0 + l; e < e1; e += 64 * U) {
+        double pr[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const long long q = e + 64LL * u;
+            pr[u] = q < e1 ? val[q] * xc[off[q]] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (e + 64LL * u < e1) acc = acc + pr[u];
+    }
+    acc = butterfly64(acc);
+    if (l == 0) part[(long long)c * nblk + b] = acc;
+}
+// k_qoi_record with one wavefront per chain: z = x at the QoI vertex (ctrl[2] >= 0), the centre
+// guard (-1), or the combined block partials of k_qoi_dot (-2)
+__global__ void k_qoi_record_vec(const double* __restrict__ x, uint64_t* ctrl, double* series, uint64_t capacity,
+                                 double* mom, int nchains, long long cs, const double* __restrict__ part, int nblk) {
+    __shared__ int bad;
+    const int c = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    const long long q = (long long)ctrl[2];
+    const uint64_t n = ctrl[1], s0 = ctrl[0];
+    if (c < nchains) {
+        double z;
+        if (q == -2) {
+            double acc = 0.0;
+            for (int b = l; b < nblk; b += 64) acc = acc + part[(long long)c * nblk + b];
+            z = butterfly64(acc);
+        } else {
+            z = x[(long long)c * cs + (q >= 0 ? q : (long long)ctrl[6])];
+        }
+        if (l == 0) {
+            if (!isfinite(z)) bad = 1;
+            if (q >= 0 || q == -2) {
+                double* m = mom + 4 * c;
+                if (n < capacity) series[(long long)c * capacity + n] = z;
+                const double cnt = m[0] + 1.0;
+                const double delta = z - m[1];
+                const double mean = m[1] + delta / cnt;
+                m[2] = m[2] + delta * (z - mean);
+                m[1] = mean;
+                m[0] = cnt;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (bad && ctrl[5] == 0) ctrl[5] = s0 + 1;
+        if (q >= 0 || q == -2) ctrl[1] = n + 1;
+        ctrl[0] = s0 + 1;
+    }
+}
+
 // ---- normals for the RNG parity test ----
 __global__ void k_normals(RngKey key, uint64_t pair0, uint64_t npairs, uint32_t tag, uint64_t sample,
                           double* __restrict__ out) {

@@ -30,6 +30,7 @@ import time
 
 import numpy as np
 
+from . import _native as mg_native
 from .measured import MeasuredOperator, measurement_vector
 from .parameters import (ConfigError, ConstantCorrelationLengthModelParameters, GeneralParameters,
                          LatticeParameters, MeasurementFileError, MeasurementParameters, MultigridParameters,
@@ -80,13 +81,15 @@ class ExactTargets:
 
 
 def _qoi_series(sampler: MultigridMCSampler, nsteps: int, rows, vals) -> np.ndarray:
-    if len(rows) == 1 and vals[0] == 1.0:  # radius 0: recorded on the device inside the cycle graph
+    """z = b^T x after every cycle (driver_mgmc.cc:76), recorded on the device inside the cycle graph:
+    radius 0 reads the vertex, radius > 0 the dot with the installed vector (mgmc_set_qoi_vector,
+    blocked order) -- the state never leaves HBM."""
+    if len(rows) == 1 and vals[0] == 1.0:
         return sampler.sample(nsteps, int(rows[0]))
-    z = np.empty(nsteps)  # radius > 0: b^T x per cycle on the host
-    for k in range(nsteps):
-        sampler.sample(1)
-        z[k] = float(np.dot(vals, sampler.get_state()[rows]))
-    return z
+    if getattr(sampler, "_qv", None) is None or not (np.array_equal(sampler._qv[0], rows)
+                                                      and np.array_equal(sampler._qv[1], vals)):
+        sampler.set_qoi_vector(rows, vals)
+    return sampler.sample(nsteps, mg_native.QOI_VECTOR)
 
 
 def measure_sampling_time(sampler, exact: ExactTargets, sampling_params: SamplingParameters,
@@ -125,25 +128,31 @@ def measure_sampling_time(sampler, exact: ExactTargets, sampling_params: Samplin
 def convergence_series(sampler, nsamples: int, nsteps: int, rows, vals, batch: int = 1) -> np.ndarray:
     """QoI series z[k, j] of nsamples chains from x = 0, nsteps cycles each (driver_mgmc.cc:236-254).
     Chain k draws sample indices s0 + k nsteps .. s0 + (k+1) nsteps - 1, exactly as one handle running
-    the chains one after the other.  batch > 1 (radius-0 QoI) runs that many chains at a time on
+    the chains one after the other.  batch > 1 runs that many chains at a time on
     clones of the handle, each on its own HIP stream, with those sample indices: the same draws, so
-    the same series bit for bit, with the small lattices' idle GPU filled by the concurrent chains."""
+    the same series bit for bit, with the small lattices' idle GPU filled by the concurrent chains.
+    A radius > 0 QoI is the device-side dot with the measurement vector on every handle."""
     x0 = np.zeros(sampler.ndof)
     z = np.empty((nsamples, nsteps))
-    if batch <= 1 or not (len(rows) == 1 and vals[0] == 1.0):
+    if batch <= 1:
         for k in range(nsamples):
             sampler.set_state(x0)
             z[k] = _qoi_series(sampler, nsteps, rows, vals)
         return z
     s0 = sampler.get_sample_index()
     handles = [sampler] + [sampler.clone() for _ in range(min(batch, nsamples) - 1)]
+    vertex = len(rows) == 1 and vals[0] == 1.0
+    if not vertex:  # radius > 0: every handle records the dot with the measurement vector
+        for h in handles:
+            h.set_qoi_vector(rows, vals)
+    q = int(rows[0]) if vertex else mg_native.QOI_VECTOR
     try:
         for k0 in range(0, nsamples, len(handles)):
             ks = list(range(k0, min(k0 + len(handles), nsamples)))
             for h, k in zip(handles, ks):
                 h.set_sample_index(s0 + k * nsteps)
                 h.set_state(x0)
-                h.sample_async(nsteps, int(rows[0]))
+                h.sample_async(nsteps, q)
             for h, k in zip(handles, ks):
                 z[k] = h.get_series(nsteps)
         sampler.set_sample_index(s0 + nsamples * nsteps)

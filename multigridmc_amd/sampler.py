@@ -510,16 +510,30 @@ class MultigridMCSampler:
         return x
 
     def sample(self, nsteps: int, qoi_index: int = -1, chain=0) -> np.ndarray:
-        """nsteps cycles of every chain; the QoI series of one chain (chain=None: (nchains, nsteps))"""
-        if chain == 0 or qoi_index < 0:
+        """nsteps cycles of every chain; the QoI series of one chain (chain=None: (nchains, nsteps)).
+        qoi_index: a vertex, -1 (none) or QOI_VECTOR (the dot with set_qoi_vector's vector)."""
+        records = qoi_index >= 0 or qoi_index == _native.QOI_VECTOR
+        if chain == 0 or not records:
             out = np.empty(max(nsteps, 0))
-            self._chk(self.lib.mgmc_sample(self.handle, int(nsteps), int(qoi_index),
-                                           _dp(out) if qoi_index >= 0 else None))
+            self._chk(self.lib.mgmc_sample(self.handle, int(nsteps), int(qoi_index), _dp(out) if records else None))
             return out
         self._chk(self.lib.mgmc_sample(self.handle, int(nsteps), int(qoi_index), None))
         if chain is None:
             return np.stack([self.get_series(nsteps, c) for c in range(self.nchains)])
         return self.get_series(nsteps, chain)
+
+    def set_qoi_vector(self, rows, vals):
+        """The QoI vector b (MeasuredOperator::measurement_vector, radius > 0: measured_operator.cc:92-171)
+        for sample(..., QOI_VECTOR): z = b^T x recorded on the device after every cycle (blocked dot
+        order).  rows strictly ascending; empty rows remove it."""
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        vals = np.ascontiguousarray(vals, dtype=np.float64)
+        if rows.shape != vals.shape:
+            raise ValueError("rows and vals differ in length")
+        self._qv = (rows, vals)
+        self._chk(self.lib.mgmc_set_qoi_vector(self.handle, len(rows),
+                                               rows.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)) if len(rows) else None,
+                                               _dp(vals) if len(rows) else None))
 
     def sample_async(self, nsteps: int, qoi_index: int = -1):
         self._chk(self.lib.mgmc_sample_async(self.handle, int(nsteps), int(qoi_index)))

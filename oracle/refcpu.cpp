@@ -875,6 +875,7 @@ static double butterfly64(double* v) {
     }
     return v[0];
 }
+static double blocked_dot(const std::vector<std::pair<int64_t, double>>& col, double sc, const double* v);
 static double lr_dot(const Level& L, int k, double sc, const double* v, Mode mode) {
     const auto& col = L.lr.cols[k];
     if (mode == FAITHFUL) {
@@ -882,6 +883,10 @@ static double lr_dot(const Level& L, int k, double sc, const double* v, Mode mod
         for (const auto& e : col) s += (sc * e.second) * v[e.first];
         return s;
     }
+    return blocked_dot(col, sc, v);
+}
+// the device's fixed dot order (4096-entry blocks, lane-strided sums, xor butterflies)
+static double blocked_dot(const std::vector<std::pair<int64_t, double>>& col, double sc, const double* v) {
     const int64_t n = (int64_t)col.size();
     const int64_t nblk = (n + LR_BLK - 1) / LR_BLK;
     std::vector<double> part(nblk);
@@ -1644,6 +1649,14 @@ void orc_residual_restrict(orc_handle* h, int level, const double* f, const doub
     std::vector<double> r(A.nrow);
     posterior_residual(*h->mg->levels[level], f, x, r.data(), h->ctx.mode);
     h->mg->ig[level]->restrict_(r.data(), fc);
+}
+
+// sum_e vals[e] x[rows[e]] in the device's blocked order (the low-rank dots' order; the QoI vector
+// record of mgmc_set_qoi_vector)
+double orc_blocked_dot(int64_t n, const int64_t* rows, const double* vals, const double* x) {
+    std::vector<std::pair<int64_t, double>> col((size_t)n);
+    for (int64_t e = 0; e < n; ++e) col[(size_t)e] = {rows[e], vals[e]};
+    return blocked_dot(col, 1.0, x);
 }
 
 void orc_philox_normals(uint64_t seed, uint64_t chain, uint64_t pair0, int64_t n, uint32_t tag, uint64_t sample,

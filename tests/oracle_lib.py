@@ -72,6 +72,7 @@ def lib():
             "orc_lowrank_nnz": (c_int64, [c_void_p, c_int]),
             "orc_get_lowrank": (None, [c_void_p, c_int, POINTER(c_int64), POINTER(c_int64), _DP]),
             "orc_philox_normals": (None, [c_uint64, c_uint64, c_uint64, c_int64, c_uint32, c_uint64, _DP]),
+            "orc_blocked_dot": (c_double, [c_int64, POINTER(c_int64), _DP, _DP]),
             "orc_philox_raw": (None, [POINTER(c_uint32), c_uint32, c_uint32, POINTER(c_uint32)]),
             "orc_ln_unit": (c_double, [c_double]),
             "orc_cos_sin_2pi": (None, [c_double, _DP, _DP]),
@@ -315,6 +316,14 @@ def philox_normals(seed, chain, pair0, n, tag, sample):
     out = np.empty(n)
     lib().orc_philox_normals(seed, chain, pair0, n, tag, sample, dp(out))
     return out
+
+
+def blocked_dot(rows, vals, x):
+    """sum_e vals[e] x[rows[e]] in the device's blocked order (refcpu blocked_dot = lr_dot's order)."""
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    vals = np.ascontiguousarray(vals, dtype=np.float64)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    return float(lib().orc_blocked_dot(len(rows), rows.ctypes.data_as(POINTER(c_int64)), dp(vals), dp(x)))
 
 
 def philox_raw(ctr, key):
