@@ -1940,7 +1940,10 @@ int mgmc_create_csr(const mgmc_config* cfg, int64_t nrow, const int64_t* rowptr,
 // the matrix's shape against cfg's lattice, before anything reads rowptr[nrow] or copies entries:
 // nrow = the interior vertex count, rowptr non-decreasing from 0, at most 125 entries per row (the
 // 5^d box of reach-2 couplings)
-static std::string check_csr_shape(const mgmc_config& cfg, int64_t nrow, const int64_t* rowptr) {
+static std::string check_csr_shape(const mgmc_config& cfg_in, int64_t nrow, const int64_t* rowptr) {
+    mgmc_config cfg = cfg_in;  // the matrix replaces kappa^2 and the fine-operator choice
+    cfg.kappa_sq = 0.0;
+    cfg.fine_operator = MGMC_OPERATOR_FD;
     const std::string err = validate_config(cfg);
     if (!err.empty()) return err;
     int64_t expect = (int64_t)(cfg.nx - 1) * (cfg.ny - 1);
