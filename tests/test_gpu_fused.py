@@ -1,0 +1,37 @@
+"""The fused fine sweeps (mgmc_zsweep2.hpp, -m gpu): one launch = the backward post-sweep of cycle n
+(with the prolongation of the coarse correction) and the forward pre-sweep of cycle n+1, bit for bit
+the oracle's prolongate_add + SORSampler::apply backward (tag_post, sample s) + forward (tag_pre,
+sample s + 1) (sampler/sor_sampler.cc:37-59, multigridmc_sampler.cc:117-128), and the captured
+post-sweep value at the QoI vertex."""
+import numpy as np
+import pytest
+
+import multigridmc_amd as mg
+from tests import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+SEED = 5418513
+
+
+@pytest.mark.parametrize("shape,alpha,omega", [((128, 128, 128), 1.0, 1.0), ((128, 64, 96), 0.9, 1.1),
+                                               ((192, 48, 40), 1.0, 1.0), ((64, 34, 18), 2.0, 0.8)])
+def test_fused_sweeps_bitwise(hip_device, shape, alpha, omega):
+    lat = mg.Lattice(*shape)
+    p = mg.MultigridParameters(nlevel=2, omega=omega)
+    s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), SEED, p, device=0, chain_id=3)
+    st = np.concatenate([s.level_desc(level)["stencil"] for level in range(2)])
+    o = O.Oracle.fd(lat.shape, p, 25.0, mode=O.MULTICOLOUR, seed=SEED, chain=3, override_stencils=st)
+    rng = np.random.default_rng(17)
+    n0, n1 = s.level_desc(0)["ndof"], s.level_desc(1)["ndof"]
+    x = rng.standard_normal(n0)
+    f = rng.standard_normal(n0)
+    xc = rng.standard_normal(n1)
+    for q, (tag_post, tag_pre, sample) in zip([n0 // 2, 7, n0 - 3], [(5, 0, 11), (2, 0, 2 ** 33 + 4), (9, 1, 0)]):
+        d, cap = s.fused_sweeps_apply(tag_post, tag_pre, sample, alpha, xc, f, x, q)
+        y = o.prolongate_add(0, alpha, xc, x)
+        y = o.sor_sampler_apply(0, mg.BACKWARD, tag_post, sample, f, y)
+        assert cap == y[q]
+        y = o.sor_sampler_apply(0, mg.FORWARD, tag_pre, sample + 1, f, y)
+        assert np.array_equal(d, y), f"max diff {np.max(np.abs(d - y))} at {np.argmax(np.abs(d - y))}"
+    s.close()
