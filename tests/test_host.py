@@ -93,19 +93,18 @@ def test_unknown_disable_token_rejected_before_any_device_call(monkeypatch):
 
 def test_product_reads_only_documented_switches():
     """The only environment the library reads: MGMC_DISABLE (kernel-path switches, each covered by
-    tests/test_gpu_parity.py VARIANTS / test_gpu_lowrank.py / test_gpu_fused.py), MGMC_GRAPH_UNROLL
-    (test_unrolled_sample_loop_bitwise) and MGMC_FUSE_CYCLES (fused cycle boundaries below 4 M
-    unknowns, test_gpu_fused.py)."""
+    tests/test_gpu_parity.py VARIANTS / test_gpu_lowrank.py) and MGMC_GRAPH_UNROLL
+    (test_unrolled_sample_loop_bitwise)."""
     src = ""
     csrc = os.path.join(ROOT, "multigridmc_amd", "csrc")
     for fn in os.listdir(csrc):
         if fn.endswith((".hip", ".hpp", ".cpp", ".h")):
             src += open(os.path.join(csrc, fn)).read()
-    assert sorted(set(re.findall(r'getenv\("([A-Z_0-9]+)"\)', src))) == ["MGMC_DISABLE", "MGMC_FUSE_CYCLES", "MGMC_GRAPH_UNROLL"]
+    assert sorted(set(re.findall(r'getenv\("([A-Z_0-9]+)"\)', src))) == ["MGMC_DISABLE", "MGMC_GRAPH_UNROLL"]
     tokens = re.findall(r'\{"([a-z_0-9]+)", PATH_NO_', src)
-    assert len(tokens) == 13
-    tested = "".join(open(os.path.join(ROOT, "tests", f)).read()
-                     for f in ("test_gpu_parity.py", "test_gpu_lowrank.py", "test_gpu_fused.py"))
+    assert len(tokens) == 12
+    tested = open(os.path.join(ROOT, "tests", "test_gpu_parity.py")).read() + \
+        open(os.path.join(ROOT, "tests", "test_gpu_lowrank.py")).read()
     for t in tokens:
         assert re.search(rf'["(,]{t}[",)]', tested), f"MGMC_DISABLE token {t} has no variant test"
 
