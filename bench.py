@@ -65,9 +65,6 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--plain", action="store_true", help="time the single-graph loop instead of the segmented one")
-    ap.add_argument("--unfused", action="store_true",
-                    help="time the cycle graph with separate fine post / pre sweeps (round-2 path) even where the "
-                         "fused cycle boundaries are available")
     ap.add_argument("--posterior", type=int, default=0, metavar="M",
                     help="BASELINE config 5: posterior operator with M point measurements (default lattice 256^3, "
                          "6 levels); not the headline line")
@@ -254,30 +251,21 @@ def main():
         sampler.close()
         sys.exit(2)
 
-    kern = sampler.level_kernels(0)  # the kernels level 0 really runs on (mgmc_level_kernels)
-    fused_loop = "cycle_boundary" in kern and not args.plain and not args.unfused
     # warmup (prior: f = 0, x0 = 0 -- driver_mgmc.cc:61-69 with mean_x_exact = xbar = 0)
     sampler.sample(args.warmup, qoi)
     sampler.reset_moments()
     coll.barrier()  # barrier + device synchronisation
     t0 = time.perf_counter()
-    timed = ftimed = None
     if args.plain:
         sampler.sample_async(args.steps, qoi)
         sampler.synchronize()
-    elif fused_loop:
-        # the sample loop with fused cycle boundaries (k_zsweep2_rb7), HIP events around each fused launch
-        ftimed = sampler.sample_fused_timed(args.steps, qoi)
+        timed = None
     else:
         timed = sampler.sample_timed(args.steps, qoi)
     sampler.synchronize()
     t1 = time.perf_counter()
     coll.barrier()
     elapsed = coll.max(t1 - t0)
-    if fused_loop and rank == 0:
-        # the single fine sweeps, for their own rooflines: a short unfused timed loop after the timed
-        # region (not part of `value`)
-        timed = sampler.sample_timed(min(args.steps, 20), qoi)
 
     from multigridmc_amd.distributed import merge_moments
     parts = coll.allgather_moments()
@@ -290,6 +278,7 @@ def main():
             plain3d = args.dim == 3 and not args.fem and not args.posterior
             tr_pre, prov = stored_traffic(args.traffic_file, n, "pre_sweep") if plain3d else (None, None)
             tr_post, prov2 = stored_traffic(args.traffic_file, n, "post_sweep") if plain3d else (None, None)
+            kern = sampler.level_kernels(0)  # the kernels level 0 really runs on (mgmc_level_kernels)
             pre = sweep_roofline(timed["pre_ms"], timed["npre"], 24.0 * n0 * K, tr_pre if K == 1 else None, prov,
                                  f"fine pre-sweep {kern['sweep']} (one Gibbs sweep of level 0)")
             per_kernel["pre_sweep"] = pre
@@ -303,21 +292,8 @@ def main():
                                          "its own segment of the cycle graph)" if fused else
                                          "(one Gibbs sweep of level 0; the prolongation is a separate pass)"))
                 per_kernel["post_sweep"] = post
-            if ftimed and ftimed["nfused"] > 0:
-                # one launch = two fine sweeps (24 B per unknown per sweep) + the coarse
-                # correction it prolongates (8 B per level-1 unknown)
-                n1 = mg.Lattice(*((n // 2,) * args.dim)).Nvertex
-                fz = sweep_roofline(ftimed["fused_ms"], ftimed["nfused"], (48.0 * n0 + 8.0 * n1) * K,
-                                    None, None,
-                                    f"fused cycle boundary {kern['cycle_boundary']}: the fine post-sweep of cycle n "
-                                    "with its prolongation + the fine pre-sweep of cycle n+1 in one launch "
-                                    "(algorithmic bytes of both sweeps: 48 B per fine + 8 B per coarse unknown)")
-                fz["sweeps_per_launch"] = 2
-                per_kernel["fused_boundary"] = fz
-                roof = dict(fz)
-            else:
-                # the dominant kernel (the longer of the two) is the headline roofline
-                roof = dict(max(per_kernel.values(), key=lambda r: r["avg_launch_ms"]))
+            # the dominant kernel (the longer of the two) is the headline roofline
+            roof = dict(max(per_kernel.values(), key=lambda r: r["avg_launch_ms"]))
             roof["per_kernel"] = per_kernel
             if args.posterior:
                 for r in (roof, pre):
@@ -357,11 +333,7 @@ def main():
             "cpu_baseline": cpu,
             "qoi": {"index": qoi, "samples": nq, "mean": mean, "variance": m2 / nq if nq else None, "chains": len(parts)},
         }
-        if ftimed:
-            line["segments_ms_per_step"] = {"fused_boundary": round(ftimed["fused_ms"] / max(1, ftimed["nfused"]), 4),
-                                            "total": round(ftimed["total_ms"] / args.steps, 4),
-                                            "fused_boundaries": ftimed["nfused"]}
-        elif timed:
+        if timed:
             line["segments_ms_per_step"] = {"pre": round(timed["pre_ms"] / args.steps, 4),
                                             "post": round(timed["post_ms"] / args.steps, 4),
                                             "total": round(timed["total_ms"] / args.steps, 4)}

@@ -318,14 +318,6 @@ int mgmc_time_fine_sweeps(mgmc_handle* h, int nsweeps, float* ms);
 int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* pre_ms, int* npre,
                       double* post_ms, int* npost);
 
-/* The sample loop with fused cycle boundaries (ABI 5), timed: as mgmc_sample_async + synchronize,
- * with event-record nodes around every fused launch (k_zsweep2_rb7: the fine post-sweep of cycle n,
- * its prolongation and the fine pre-sweep of cycle n+1).  *total_ms = the nsteps cycles, *fused_ms =
- * the summed time of the *nfused fused launches.  MGMC_E_UNSUPPORTED if the handle has no fused
- * boundaries (they need the z-swept fine level, SOR 1/1 and no low-rank part). */
-int mgmc_sample_fused_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* fused_ms,
-                            int* nfused);
-
 /* ---- multi-GPU: one chain per rank, RCCL over xGMI for the final QoI reduction ----
  * (the reference is single-process; this is the only collective of the path) */
 #define MGMC_UNIQUE_ID_BYTES 128

@@ -127,7 +127,6 @@ SIGNATURES = [
     ("mgmc_normals", c_int, [_H, c_uint64, c_size_t, c_uint32, c_uint64, _DP]),
     ("mgmc_solve", c_int, [_H, c_int, _DP, _DP, c_double, c_double, c_int, POINTER(c_int), _DP]),
     ("mgmc_time_fine_sweeps", c_int, [_H, c_int, POINTER(c_float)]),
-    ("mgmc_sample_fused_timed", c_int, [_H, c_int, c_int64, _DP, _DP, POINTER(c_int)]),
     ("mgmc_sample_timed", c_int, [_H, c_int, c_int64, _DP, _DP, POINTER(c_int), _DP, POINTER(c_int)]),
     ("mgmc_comm_unique_id", c_int, [ctypes.c_char_p]),
     ("mgmc_comm_init", c_int, [_H, c_int, c_int, ctypes.c_char_p]),

@@ -265,11 +265,6 @@ struct mgmc_handle {
     bool fuse = false;
     double* cap = nullptr;  // [nchains] the post-sweep value at the QoI / guard vertex
     hipGraphExec_t graph_first = nullptr, graph_mid[2] = {nullptr, nullptr}, graph_last = nullptr;
-    // graph_mid with event-record nodes around the fused kernel (mgmc_sample_fused_timed)
-    hipGraph_t graph_mid_timed_src[2] = {nullptr, nullptr};
-    hipGraphExec_t graph_mid_timed[2] = {nullptr, nullptr};
-    hipGraphNode_t mid_node[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
-    hipEvent_t mid_ev0[2] = {nullptr, nullptr};
     // the cycle with four event-record nodes (before the fine pre-sampler, after it, before the fine
     // post-sampler, after the QoI record): mgmc_sample_timed points them at per-step events
     hipGraph_t graph_timed_src = nullptr;
@@ -1475,17 +1470,15 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
 
 // the fused fine post-sweep of this cycle + pre-sweep of the next (reads x2 + alpha P x_1, writes x),
 // then the QoI record of this cycle from the captured post-sweep value
-void enqueue_fused_boundary(mgmc_handle* h, hipStream_t s, const hipEvent_t* ev = nullptr) {
+void enqueue_fused_boundary(mgmc_handle* h, hipStream_t s) {
     const Op& post = h->ops[h->seg_begin_post];
     const Op& pre = h->ops[0];
     Level& l0 = h->levels[0];
     const Level& l1 = h->levels[1];
     const int nch = h->nchains;
     GibbsArg g = make_gibbs(h, l0, post.tag, 1, h->ctrl);
-    if (ev) hipEventRecordWithFlags(ev[0], s, hipEventRecordExternal);
     launch_zsweep2(l0, l1, l0.buf(post.src), l0.buf(1 - post.src), l0.f, l1.x, g, pre.tag, h->cfg.coarse_scaling,
                    h->ctrl, h->cap, s, nch);
-    if (ev) hipEventRecordWithFlags(ev[1], s, hipEventRecordExternal);
     hipLaunchKernelGGL(k_qoi_record, dim3(1), dim3(64 * ((nch + 63) / 64)), 0, s, (const double*)l0.x, h->ctrl,
                        h->series, h->series_cap, h->mom, nch, (long long)l0.L.nstore, (const double*)h->cap);
 }
@@ -1509,14 +1502,9 @@ void destroy_graphs(mgmc_handle* h) {
     h->graph_timed = nullptr;
     if (h->graph_timed_src) hipGraphDestroy(h->graph_timed_src);
     h->graph_timed_src = nullptr;
-    for (hipGraphExec_t* g : {&h->graph_first, &h->graph_mid[0], &h->graph_mid[1], &h->graph_last,
-                              &h->graph_mid_timed[0], &h->graph_mid_timed[1]}) {
+    for (hipGraphExec_t* g : {&h->graph_first, &h->graph_mid[0], &h->graph_mid[1], &h->graph_last}) {
         if (*g) hipGraphExecDestroy(*g);
         *g = nullptr;
-    }
-    for (hipGraph_t& g : h->graph_mid_timed_src) {
-        if (g) hipGraphDestroy(g);
-        g = nullptr;
     }
 }
 
@@ -1591,32 +1579,6 @@ int build_graphs(mgmc_handle* h) {
             if (parity) std::swap(l0.x, l0.x2);
             HIPCHK(h, hipGraphInstantiate(&h->graph_mid[parity], g, nullptr, nullptr, 0));
             HIPCHK(h, hipGraphDestroy(g));
-            // the timed copy: event-record nodes before and after the fused kernel
-            for (auto& e : h->mid_ev0)
-                if (!e) HIPCHK(h, hipEventCreate(&e));
-            if (parity) std::swap(l0.x, l0.x2);
-            HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-            enqueue_ops(h, h->seg_end_pre, h->seg_begin_post, h->stream);
-            enqueue_fused_boundary(h, h->stream, h->mid_ev0);
-            HIPCHK(h, hipStreamEndCapture(h->stream, &h->graph_mid_timed_src[parity]));
-            if (parity) std::swap(l0.x, l0.x2);
-            size_t nn = 0;
-            HIPCHK(h, hipGraphGetNodes(h->graph_mid_timed_src[parity], nullptr, &nn));
-            std::vector<hipGraphNode_t> nodes(nn);
-            HIPCHK(h, hipGraphGetNodes(h->graph_mid_timed_src[parity], nodes.data(), &nn));
-            for (hipGraphNode_t nd : nodes) {
-                hipGraphNodeType ty;
-                HIPCHK(h, hipGraphNodeGetType(nd, &ty));
-                if (ty != hipGraphNodeTypeEventRecord) continue;
-                hipEvent_t e = nullptr;
-                HIPCHK(h, hipGraphEventRecordNodeGetEvent(nd, &e));
-                for (int q = 0; q < 2; ++q)
-                    if (e == h->mid_ev0[q]) h->mid_node[parity][q] = nd;
-            }
-            if (!h->mid_node[parity][0] || !h->mid_node[parity][1])
-                return fail(h, MGMC_E_HIP, "timed fused graph: event-record node not captured");
-            HIPCHK(h, hipGraphInstantiate(&h->graph_mid_timed[parity], h->graph_mid_timed_src[parity], nullptr,
-                                          nullptr, 0));
         }
     }
     return MGMC_OK;
@@ -2256,8 +2218,6 @@ int mgmc_destroy(mgmc_handle* h) {
     destroy_graphs(h);
     for (auto e : h->timed_ev0)
         if (e) hipEventDestroy(e);
-    for (auto e : h->mid_ev0)
-        if (e) hipEventDestroy(e);
     free_tails(h);
     for (auto& lv : h->levels) {
         free_lowrank(lv.lr);
@@ -2335,7 +2295,6 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
     }
     std::string text = "sweep=" + sweep;
     if (!post.empty()) text += ";post_sweep=" + post;
-    if (level == 0 && h->fuse) text += ";cycle_boundary=k_zsweep2_rb7<32," + std::to_string(ZS2_TY) + ",...>";
     if (!res.empty()) text += ";residual_restrict=" + res;
     snprintf(out, n, "%s", text.c_str());
     return MGMC_OK;
@@ -2784,54 +2743,6 @@ int mgmc_time_fine_sweeps(mgmc_handle* h, int nsweeps, float* ms) {
     hipEventDestroy(e0);
     hipEventDestroy(e1);
     return MGMC_OK;
-}
-
-int mgmc_sample_fused_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* fused_ms,
-                            int* nfused) {
-    if (!h || nsteps < 1 || !total_ms || !fused_ms || !nfused) return fail(h, MGMC_E_INVALID, "invalid argument");
-    if (!h->graph_mid_timed[0]) return fail(h, MGMC_E_UNSUPPORTED, "this handle has no fused cycle boundaries");
-    HIPCHK(h, hipSetDevice(h->device));
-    int rc = set_qoi(h, qoi_index);
-    if (rc) return rc;
-    if (qoi_index == MGMC_QOI_VECTOR) return fail(h, MGMC_E_UNSUPPORTED, "fused timing with the QoI vector");
-    HIPCHK(h, hipMemsetAsync(h->ctrl + 1, 0, sizeof(uint64_t), h->stream));
-    if ((rc = ensure_series(h, (uint64_t)nsteps))) return rc;
-    // the loop of mgmc_sample_async, every boundary in the timed copy of its graph
-    int n = nsteps;
-    const bool lead = n >= 2 && (n - 1) % 2;
-    if (lead) --n;
-    const int nb = n >= 2 ? n - 1 : 0;
-    std::vector<hipEvent_t> ev(2 * (size_t)nb + 2);
-    for (auto& e : ev) HIPCHK(h, hipEventCreate(&e));
-    HIPCHK(h, hipEventRecord(ev[0], h->stream));
-    if (lead) HIPCHK(h, hipGraphLaunch(h->graph_all, h->stream));
-    if (nb == 0) {
-        for (int s = 0; s < n; ++s) HIPCHK(h, hipGraphLaunch(h->graph_all, h->stream));
-    } else {
-        HIPCHK(h, hipGraphLaunch(h->graph_first, h->stream));
-        for (int b = 0; b < nb; ++b) {
-            const int par = b & 1;
-            for (int q = 0; q < 2; ++q)
-                HIPCHK(h, hipGraphExecEventRecordNodeSetEvent(h->graph_mid_timed[par], h->mid_node[par][q],
-                                                              ev[1 + 2 * b + q]));
-            HIPCHK(h, hipGraphLaunch(h->graph_mid_timed[par], h->stream));
-        }
-        HIPCHK(h, hipGraphLaunch(h->graph_last, h->stream));
-    }
-    HIPCHK(h, hipEventRecord(ev.back(), h->stream));
-    HIPCHK(h, hipEventSynchronize(ev.back()));
-    float t = 0.f;
-    double fused = 0.0;
-    for (int b = 0; b < nb; ++b) {
-        HIPCHK(h, hipEventElapsedTime(&t, ev[1 + 2 * b], ev[2 + 2 * b]));
-        fused += t;
-    }
-    HIPCHK(h, hipEventElapsedTime(&t, ev[0], ev.back()));
-    *total_ms = t;
-    *fused_ms = fused;
-    *nfused = nb;
-    for (auto& e : ev) hipEventDestroy(e);
-    return check_finite(h);
 }
 
 int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* pre_ms, int* npre,

@@ -541,17 +541,6 @@ class MultigridMCSampler:
     def synchronize(self):
         self._chk(self.lib.mgmc_synchronize(self.handle))
 
-    def sample_fused_timed(self, nsteps: int, qoi_index: int = -1):
-        """The sample loop with fused cycle boundaries, timed (mgmc_sample_fused_timed): {"total_ms",
-        "fused_ms", "nfused"}, or None if this handle has no fused boundaries."""
-        tot, fz, nf = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
-        rc = self.lib.mgmc_sample_fused_timed(self.handle, int(nsteps), int(qoi_index), ctypes.byref(tot),
-                                              ctypes.byref(fz), ctypes.byref(nf))
-        if rc == _native.MGMC_E_UNSUPPORTED:
-            return None
-        self._chk(rc)
-        return {"total_ms": tot.value, "fused_ms": fz.value, "nfused": nf.value}
-
     def sample_timed(self, nsteps: int, qoi_index: int = -1) -> dict:
         """nsteps cycles replayed as [fine pre-sampler | coarse correction | fine post-sampler | QoI]
         graph segments with HIP events on the handle's stream (mgmc_sample_timed)."""
