@@ -98,7 +98,6 @@ enum PathFlag : uint32_t {
     PATH_NO_LR_PREFETCH = 1u << 9,        // low-rank small fix without the up-front loads
     PATH_NO_COARSE_PRECOMPUTE = 1u << 10, // coarse SSOR: right-hand sides inside the colour passes
     PATH_NO_LR_DENSE = 1u << 11,          // dense low-rank column: the row lists over every vertex
-    PATH_NO_FUSE_CYCLES = 1u << 12,       // sample loops: separate fine post / pre sweeps at cycle boundaries
 };
 
 struct PathToken {
@@ -112,7 +111,6 @@ constexpr PathToken kPathTokens[] = {
     {"zrestrict", PATH_NO_ZRESTRICT}, {"lr_small", PATH_NO_LR_SMALL},
     {"lr_merge", PATH_NO_LR_MERGE},   {"lr_prefetch", PATH_NO_LR_PREFETCH},
     {"coarse_precompute", PATH_NO_COARSE_PRECOMPUTE}, {"lr_dense", PATH_NO_LR_DENSE},
-    {"fuse_cycles", PATH_NO_FUSE_CYCLES},
 };
 
 // parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
@@ -258,13 +256,6 @@ struct mgmc_handle {
     size_t seg_end_pre = 0, seg_begin_post = 0, seg_end_post = 0;  // fine-sweep segments
     hipGraphExec_t graph_all = nullptr;
     hipGraphExec_t graph_unroll = nullptr;  // unroll copies of the cycle in one graph (sample loops)
-    // fused cycle boundaries (mgmc_zsweep2.hpp): sample loops of nsteps >= 2 run graph_first (the
-    // fine pre-sweep), nsteps - 1 graph_mid (the rest of a cycle with its fine post-sweep fused to the
-    // next cycle's pre-sweep; [1] = the same with the fine level's two buffers exchanged) and
-    // graph_last (the rest of a cycle, standard)
-    bool fuse = false;
-    double* cap = nullptr;  // [nchains] the post-sweep value at the QoI / guard vertex
-    hipGraphExec_t graph_first = nullptr, graph_mid[2] = {nullptr, nullptr}, graph_last = nullptr;
     // the cycle with four event-record nodes (before the fine pre-sampler, after it, before the fine
     // post-sampler, after the QoI record): mgmc_sample_timed points them at per-step events
     hipGraph_t graph_timed_src = nullptr;
@@ -1461,26 +1452,11 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 }
                 hipLaunchKernelGGL(k_qoi_record, dim3(1), dim3(64 * ((nch + 63) / 64)), 0, s,
                                    (const double*)h->levels[0].x, h->ctrl, h->series, h->series_cap, h->mom, nch,
-                                   (long long)h->levels[0].L.nstore, (const double*)nullptr);
+                                   (long long)h->levels[0].L.nstore);
                 break;
             }
         }
     }
-}
-
-// the fused fine post-sweep of this cycle + pre-sweep of the next (reads x2 + alpha P x_1, writes x),
-// then the QoI record of this cycle from the captured post-sweep value
-void enqueue_fused_boundary(mgmc_handle* h, hipStream_t s) {
-    const Op& post = h->ops[h->seg_begin_post];
-    const Op& pre = h->ops[0];
-    Level& l0 = h->levels[0];
-    const Level& l1 = h->levels[1];
-    const int nch = h->nchains;
-    GibbsArg g = make_gibbs(h, l0, post.tag, 1, h->ctrl);
-    launch_zsweep2(l0, l1, l0.buf(post.src), l0.buf(1 - post.src), l0.f, l1.x, g, pre.tag, h->cfg.coarse_scaling,
-                   h->ctrl, h->cap, s, nch);
-    hipLaunchKernelGGL(k_qoi_record, dim3(1), dim3(64 * ((nch + 63) / 64)), 0, s, (const double*)l0.x, h->ctrl,
-                       h->series, h->series_cap, h->mom, nch, (long long)l0.L.nstore, (const double*)h->cap);
 }
 
 int capture(mgmc_handle* h, size_t begin, size_t end, hipGraphExec_t* out) {
@@ -1502,10 +1478,6 @@ void destroy_graphs(mgmc_handle* h) {
     h->graph_timed = nullptr;
     if (h->graph_timed_src) hipGraphDestroy(h->graph_timed_src);
     h->graph_timed_src = nullptr;
-    for (hipGraphExec_t* g : {&h->graph_first, &h->graph_mid[0], &h->graph_mid[1], &h->graph_last}) {
-        if (*g) hipGraphExecDestroy(*g);
-        *g = nullptr;
-    }
 }
 
 // the timed cycle: the same ops in one graph with an external event-record node at each of the five
@@ -1562,24 +1534,6 @@ int build_graphs(mgmc_handle* h) {
     if (h->levels.size() > 1) {
         rc = capture_timed(h);
         if (rc) return rc;
-    }
-    if (h->fuse && h->qv_n == 0) {
-        if ((rc = capture(h, 0, h->seg_end_pre, &h->graph_first))) return rc;
-        if ((rc = capture(h, h->seg_end_pre, h->ops.size(), &h->graph_last))) return rc;
-        Level& l0 = h->levels[0];
-        for (int parity = 0; parity < 2; ++parity) {
-            // parity 1: the state after the fused kernel of the previous boundary is in the other
-            // buffer; the same ops captured with the fine level's buffers exchanged read it there
-            if (parity) std::swap(l0.x, l0.x2);
-            hipGraph_t g = nullptr;
-            HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-            enqueue_ops(h, h->seg_end_pre, h->seg_begin_post, h->stream);
-            enqueue_fused_boundary(h, h->stream);
-            HIPCHK(h, hipStreamEndCapture(h->stream, &g));
-            if (parity) std::swap(l0.x, l0.x2);
-            HIPCHK(h, hipGraphInstantiate(&h->graph_mid[parity], g, nullptr, nullptr, 0));
-            HIPCHK(h, hipGraphDestroy(g));
-        }
     }
     return MGMC_OK;
 }
@@ -1825,28 +1779,6 @@ int mgmc_describe(const mgmc_config* cfg, mgmc_level_desc* out, int max_levels) 
     return (int)lv.size();
 }
 
-// fused cycle boundaries (mgmc_zsweep2.hpp): the z-swept 3D fine level with its fused prolongation,
-// one SOR pre- and one SOR post-sweep, no low-rank part; lattices above 4 M unknowns (below, the
-// multi-cycle graphs of the sample loop pay more), or any size with MGMC_FUSE_CYCLES=1 (tests)
-static bool fuse_eligible(const mgmc_handle* h) {
-    if (h->levels.size() < 2 || h->field_mode || (h->paths & (PATH_NO_FUSE_CYCLES | PATH_NO_FUSE_PROLONG))) return false;
-    const mgmc_config& c = h->cfg;
-    const Level& l0 = h->levels[0];
-    if (!l0.zsweep || l0.lr.m > 0 || c.smoother != MGMC_SMOOTHER_SOR || c.npresmooth != 1 || c.npostsmooth != 1)
-        return false;
-    if (h->seg_end_pre != 1 || h->seg_end_post != h->seg_begin_post + 1 || h->ops.back().kind != OP_QOI ||
-        h->ops.size() != h->seg_end_post + 1)
-        return false;
-    const Op& pre = h->ops[0];
-    const Op& post = h->ops[h->seg_begin_post];
-    if (pre.kind != OP_SWEEP || pre.level != 0 || pre.direction != MGMC_FORWARD || pre.src != 0) return false;
-    if (post.kind != OP_SWEEP || post.level != 0 || post.direction != MGMC_BACKWARD || !post.prolong || post.src != 1)
-        return false;
-    const char* e = getenv("MGMC_FUSE_CYCLES");
-    if (e && atoi(e) == 1) return true;
-    return l0.spec.ndof > (1u << 22);
-}
-
 // the kernel families that address level l (the launch_* dispatch of this handle) and their check
 static int zrestrict_cx_of(const mgmc_handle* h, int l) {  // launch_residual_restrict's tile width
     if (l + 1 >= (int)h->levels.size()) return 0;
@@ -2018,11 +1950,6 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
     }
     // op sequence of one sample
     build_ops(h);
-    h->fuse = fuse_eligible(h);
-    if (h->fuse && hipMalloc(&h->cap, sizeof(double) * nchains) != hipSuccess) {
-        h->last_error = "device allocation failed";
-        return bail(MGMC_E_NOMEM);
-    }
     if ((rc = build_tails(h)) != MGMC_OK) return bail(rc);
     if ((rc = ensure_series(h, 1024)) != MGMC_OK) return bail(rc);
     if (hipStreamSynchronize(h->stream) != hipSuccess) {
@@ -2240,7 +2167,6 @@ int mgmc_destroy(mgmc_handle* h) {
     if (h->ctrl) hipFree(h->ctrl);
     if (h->mom) hipFree(h->mom);
     if (h->series) hipFree(h->series);
-    if (h->cap) hipFree(h->cap);
     if (h->qv_off) hipFree(h->qv_off);
     if (h->qv_val) hipFree(h->qv_val);
     if (h->qv_part) hipFree(h->qv_part);
@@ -2406,18 +2332,6 @@ int mgmc_sample_async(mgmc_handle* h, int nsteps, int64_t qoi_index) {
     HIPCHK(h, hipMemsetAsync(h->ctrl + 1, 0, sizeof(uint64_t), h->stream));
     if ((rc = ensure_series(h, (uint64_t)std::max(nsteps, 1)))) return rc;
     int s = 0;
-    if (h->graph_mid[0] && h->qoi_store_index != -2 && nsteps >= 2) {
-        // fused cycle boundaries: an even number of them, so the state ends in its own buffer
-        int n = nsteps;
-        if ((n - 1) % 2) {
-            HIPCHK(h, hipGraphLaunch(h->graph_all, h->stream));
-            --n;
-        }
-        HIPCHK(h, hipGraphLaunch(h->graph_first, h->stream));
-        for (int b = 0; b < n - 1; ++b) HIPCHK(h, hipGraphLaunch(h->graph_mid[b & 1], h->stream));
-        HIPCHK(h, hipGraphLaunch(h->graph_last, h->stream));
-        return MGMC_OK;
-    }
     if (h->graph_unroll)
         for (; s + h->unroll <= nsteps; s += h->unroll) HIPCHK(h, hipGraphLaunch(h->graph_unroll, h->stream));
     for (; s < nsteps; ++s) HIPCHK(h, hipGraphLaunch(h->graph_all, h->stream));
@@ -3253,7 +3167,6 @@ int mgmc_set_lowrank(mgmc_handle* h, int m, const int64_t* colptr, const int64_t
         rc = build_coarse_chol(h, m > 0 ? &cols : nullptr, sigma, m);
     HIPCHK(h, hipStreamSynchronize(h->stream));
     build_ops(h);
-    h->fuse = h->cap != nullptr && fuse_eligible(h);  // a low-rank part ends the fused boundaries
     int rc2 = build_tails(h);
     if (!rc2) rc2 = build_graphs(h);
     return rc ? rc : rc2;

@@ -591,10 +591,8 @@ __global__ void __launch_bounds__(256) k_unpack(Layout L, const double* __restri
 // ctrl[0] = sample index, ctrl[1] = series length, ctrl[2] = QoI storage index (int64, <0 = off),
 // ctrl[5] = non-finite guard (0, or 1 + the sample index at which the watched value first was NaN /
 // Inf), ctrl[6] = storage index watched when no QoI is recorded (the lattice centre)
-// cap (the fused cycle boundaries, mgmc_zsweep2.hpp): chain c's value is cap[c] instead of x at the
-// QoI / guard vertex
 __global__ void k_qoi_record(const double* __restrict__ x, uint64_t* ctrl, double* series, uint64_t capacity,
-                             double* mom, int nchains, long long cs, const double* __restrict__ cap) {
+                             double* mom, int nchains, long long cs) {
     // thread c records chain c (series and moments chain c * capacity / c * 4 on); the control words
     // are advanced once, after every chain has read them
     __shared__ int bad;
@@ -604,7 +602,7 @@ __global__ void k_qoi_record(const double* __restrict__ x, uint64_t* ctrl, doubl
     const long long q = (long long)ctrl[2];
     const uint64_t n = ctrl[1], s0 = ctrl[0];
     if (c < nchains) {
-        const double z = cap ? cap[c] : x[(long long)c * cs + (q >= 0 ? q : (long long)ctrl[6])];
+        const double z = x[(long long)c * cs + (q >= 0 ? q : (long long)ctrl[6])];
         if (!isfinite(z)) bad = 1;
         if (q >= 0) {
             double* m = mom + 4 * c;
