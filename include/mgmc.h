@@ -293,13 +293,6 @@ int mgmc_residual_restrict(mgmc_handle* h, int level, const double* f, const dou
 #define MGMC_SOLVER_CG 1
 int mgmc_solve(mgmc_handle* h, int method, const double* b, double* x, double rtol, double atol, int maxiter,
                int* iters, double* rnorm);
-/* The fused fine sweeps of the sample loop (ABI 5; 3D z-sweep fine levels): x <- the forward pre-sweep
- * (tag_pre, sample_index + 1) of the backward post-sweep (tag_post, sample_index) of x + alpha P xc,
- * in one launch; *captured = the post-sweep value at vertex capture_index (what the QoI record of
- * the cycle reads).  Equal to mgmc_prolongate_add(0, alpha, xc, x), then mgmc_sor_sampler_apply
- * backward and forward, bit for bit. */
-int mgmc_fused_sweeps_apply(mgmc_handle* h, uint32_t tag_post, uint32_t tag_pre, uint64_t sample_index, double alpha,
-                            const double* xc, const double* f, double* x, int64_t capture_index, double* captured);
 /* n standard normals of pair ids [pair0, pair0+n/2) for (sweep_tag, sample_index):
  * out[2p] = cos branch, out[2p+1] = sin branch of the Box-Muller pair p */
 int mgmc_normals(mgmc_handle* h, uint64_t pair0, size_t n, uint32_t sweep_tag, uint64_t sample_index,

@@ -123,7 +123,6 @@ SIGNATURES = [
     ("mgmc_restrict", c_int, [_H, c_int, _DP, _DP]),
     ("mgmc_prolongate_add", c_int, [_H, c_int, c_double, _DP, _DP]),
     ("mgmc_residual_restrict", c_int, [_H, c_int, _DP, _DP, _DP]),
-    ("mgmc_fused_sweeps_apply", c_int, [_H, c_uint32, c_uint32, c_uint64, c_double, _DP, _DP, _DP, c_int64, _DP]),
     ("mgmc_normals", c_int, [_H, c_uint64, c_size_t, c_uint32, c_uint64, _DP]),
     ("mgmc_solve", c_int, [_H, c_int, _DP, _DP, c_double, c_double, c_int, POINTER(c_int), _DP]),
     ("mgmc_time_fine_sweeps", c_int, [_H, c_int, POINTER(c_float)]),

@@ -22,7 +22,6 @@
 #include "mgmc_hierarchy.hpp"
 #include "mgmc_kernels.hpp"
 #include "mgmc_zsweep.hpp"
-#include "mgmc_zsweep2.hpp"
 #include "mgmc_layout_check.hpp"
 static_assert(MGMC_LAYOUT_POINT == mgmc::LF_POINT && MGMC_LAYOUT_PAIRS == mgmc::LF_PAIRS &&
                   MGMC_LAYOUT_ZSWEEP == mgmc::LF_ZSWEEP && MGMC_LAYOUT_ZSWEEP_COARSE == mgmc::LF_ZSWEEP_C &&
@@ -431,51 +430,6 @@ void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s,
         hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 1, MINW>), grid, dim3(NT), lds, s, a);
     else
         hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 0, MINW>), grid, dim3(NT), lds, s, a);
-}
-
-// the fused post(n) + pre(n+1) fine sweeps (mgmc_zsweep2.hpp): tile of 32 pairs x ZS2_TY rows
-#ifndef MGMC_ZS2_TY
-#define MGMC_ZS2_TY 12
-#endif
-#ifndef MGMC_ZS2_TZ
-#define MGMC_ZS2_TZ 64
-#endif
-constexpr int ZS2_XP = 32, ZS2_TY = MGMC_ZS2_TY, ZS2_NT = zs2_threads(ZS2_XP, ZS2_TY);
-void launch_zsweep2(const Level& lv, const Level& lc, const double* xin, double* xout, const double* f,
-                    const double* xc, const GibbsArg& g_post, uint32_t tag_pre, double alpha, const uint64_t* ctrl,
-                    double* cap, hipStream_t s, int nch = 1) {
-    ZSweep2Args a;
-    a.L = lv.L;
-    a.Lc = lc.L;
-    a.xin = xin;
-    a.xout = xout;
-    a.f = f;
-    a.xc = xc;
-    a.alpha = alpha;
-    a.S = lv.S;
-    a.G = g_post;
-    a.tag_pre = tag_pre;
-    a.ctrl = ctrl;
-    a.cap = cap;
-    a.cs = lv.L.nstore;
-    a.csc = lc.L.nstore;
-    a.ntx = (lv.L.nx / 2) / ZS2_XP;
-    a.nty = (lv.L.ny - 1 + ZS2_TY - 1) / ZS2_TY;
-    const long long txy = (long long)a.ntx * a.nty;
-    int tz = MGMC_ZS2_TZ;
-    while (tz > 8 && 2 * txy * ((lv.L.nz - 1 + tz - 1) / tz) < 3LL * 2 * lv.num_cu) tz /= 2;
-    a.tz = tz;
-    a.ntz = (lv.L.nz - 1 + tz - 1) / tz;
-    const int ntiles = a.ntx * a.nty * a.ntz;
-    const int nb = (ntiles + 7) / 8 * 8;
-    const size_t lds = zsweep2_lds_bytes(ZS2_XP, ZS2_TY, true);
-    int ex;
-    const bool pow2 = std::isnormal(alpha) && std::frexp(std::fabs(alpha), &ex) == 0.5 && ex > -900 && ex < 900;
-    const dim3 grid(nb, 1, nch);
-    if (pow2)
-        hipLaunchKernelGGL((k_zsweep2_rb7<ZS2_XP, ZS2_TY, ZS2_NT, 2>), grid, dim3(ZS2_NT), lds, s, a);
-    else
-        hipLaunchKernelGGL((k_zsweep2_rb7<ZS2_XP, ZS2_TY, ZS2_NT, 1>), grid, dim3(ZS2_NT), lds, s, a);
 }
 
 void launch_zsweep(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g0,
@@ -2570,41 +2524,6 @@ int mgmc_residual_restrict(mgmc_handle* h, int level, const double* f, const dou
     launch_residual_restrict(lf, lc, lf.scratch[1], fr, lc.scratch[0], lc.scratch[1], 1, h->stream);
     HIPCHK(h, hipGetLastError());
     return download(h, level + 1, lc.scratch[0], fc);
-}
-
-int mgmc_fused_sweeps_apply(mgmc_handle* h, uint32_t tag_post, uint32_t tag_pre, uint64_t sample_index, double alpha,
-                            const double* xc, const double* f, double* x, int64_t capture_index, double* captured) {
-    int rc = check_level(h, 0, true);
-    if (rc) return rc;
-    if (!xc || !f || !x) return fail(h, MGMC_E_INVALID, "null argument");
-    Level& lf = h->levels[0];
-    Level& lc = h->levels[1];
-    if (!lf.zsweep) return fail(h, MGMC_E_UNSUPPORTED, "the fused sweeps need the z-sweep fine level (3D, nx % 64 == 0)");
-    if (capture_index < 0 || (uint64_t)capture_index >= lf.spec.ndof) return fail(h, MGMC_E_INVALID, "capture index out of range");
-    HIPCHK(h, hipSetDevice(h->device));
-    if ((rc = ensure_scratch(h, 0)) || (rc = ensure_scratch(h, 1))) return rc;
-    if ((rc = upload(h, 0, f, lf.scratch[0]))) return rc;
-    if ((rc = upload(h, 0, x, lf.scratch[1]))) return rc;
-    if ((rc = upload(h, 1, xc, lc.scratch[0]))) return rc;
-    // control words of this call: [2] the capture vertex's padded offset, [3] the sample index
-    const int nxi = lf.L.nx - 1, nyi = lf.L.ny - 1;
-    const long long qs = lf.L.at((int)(capture_index % nxi) + 1, (int)((capture_index / nxi) % nyi) + 1,
-                                 (int)(capture_index / ((int64_t)nxi * nyi)) + 1);
-    uint64_t cw[8] = {0, 0, (uint64_t)qs, sample_index, 0, 0, 0, 0};
-    uint64_t* dctrl = nullptr;
-    double* dcap = nullptr;
-    HIPCHK(h, hipMalloc(&dctrl, sizeof(cw)));
-    HIPCHK(h, hipMalloc(&dcap, sizeof(double)));
-    HIPCHK(h, hipMemcpyAsync(dctrl, cw, sizeof(cw), hipMemcpyHostToDevice, h->stream));
-    GibbsArg g = make_gibbs(h, lf, tag_post, 1, dctrl + 3);
-    launch_zsweep2(lf, lc, lf.scratch[1], lf.scratch[2], lf.scratch[0], lc.scratch[0], g, tag_pre, alpha, dctrl, dcap,
-                   h->stream);
-    HIPCHK(h, hipGetLastError());
-    rc = download(h, 0, lf.scratch[2], x);
-    if (!rc && captured) HIPCHK(h, hipMemcpy(captured, dcap, sizeof(double), hipMemcpyDeviceToHost));
-    hipFree(dctrl);
-    hipFree(dcap);
-    return rc;
 }
 
 int mgmc_normals(mgmc_handle* h, uint64_t pair0, size_t n, uint32_t sweep_tag, uint64_t sample_index, double* out) {

@@ -646,19 +646,6 @@ class MultigridMCSampler:
         self._chk(self.lib.mgmc_residual_restrict(self.handle, level, _dp(f), _dp(x), _dp(out)))
         return out
 
-    def fused_sweeps_apply(self, tag_post: int, tag_pre: int, sample_index: int, alpha: float, xc, f, x,
-                           capture_index: int):
-        """mgmc_fused_sweeps_apply: (x after the post-sweep of x + alpha P xc and the next pre-sweep,
-        the post-sweep value at capture_index)"""
-        xc = _as_f64(xc, self.level_desc(1)["ndof"], "xc")
-        f = _as_f64(f, self.ndof, "f")
-        out = _as_f64(x, self.ndof, "x").copy()
-        cap = np.zeros(1)
-        self._chk(self.lib.mgmc_fused_sweeps_apply(self.handle, int(tag_post), int(tag_pre), int(sample_index),
-                                                   float(alpha), _dp(xc), _dp(f), _dp(out), int(capture_index),
-                                                   _dp(cap)))
-        return out, float(cap[0])
-
     def normals(self, pair0: int, n: int, tag: int, sample_index: int) -> np.ndarray:
         out = np.empty(n)
         self._chk(self.lib.mgmc_normals(self.handle, int(pair0), int(n), int(tag), int(sample_index), _dp(out)))
