@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--plain", action="store_true", help="time the single-graph loop instead of the segmented one")
+    ap.add_argument("--timing-stride", type=int, default=4,
+                    help="time the fine-sweep segments (HIP event nodes) of every N-th cycle of the timed loop; the "
+                         "other cycles replay the plain graph (event nodes cost ~5 us each)")
     ap.add_argument("--posterior", type=int, default=0, metavar="M",
                     help="BASELINE config 5: posterior operator with M point measurements (default lattice 256^3, "
                          "6 levels); not the headline line")
@@ -261,7 +264,7 @@ def main():
         sampler.synchronize()
         timed = None
     else:
-        timed = sampler.sample_timed(args.steps, qoi)
+        timed = sampler.sample_timed(args.steps, qoi, stride=args.timing_stride)
     sampler.synchronize()
     t1 = time.perf_counter()
     coll.barrier()

@@ -310,6 +310,10 @@ int mgmc_time_fine_sweeps(mgmc_handle* h, int nsweeps, float* ms);
  * *npre / *npost = number of fine-level sweeps they contain. */
 int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* total_ms, double* pre_ms, int* npre,
                       double* post_ms, int* npost);
+/* The same with the segments timed on every stride-th cycle only (and the last); the other cycles
+ * replay the plain cycle graph (ABI 5).  *npre / *npost count the timed sweeps. */
+int mgmc_sample_timed_stride(mgmc_handle* h, int nsteps, int stride, int64_t qoi_index, double* total_ms,
+                             double* pre_ms, int* npre, double* post_ms, int* npost);
 
 /* ---- multi-GPU: one chain per rank, RCCL over xGMI for the final QoI reduction ----
  * (the reference is single-process; this is the only collective of the path) */

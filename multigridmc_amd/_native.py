@@ -127,6 +127,7 @@ SIGNATURES = [
     ("mgmc_solve", c_int, [_H, c_int, _DP, _DP, c_double, c_double, c_int, POINTER(c_int), _DP]),
     ("mgmc_time_fine_sweeps", c_int, [_H, c_int, POINTER(c_float)]),
     ("mgmc_sample_timed", c_int, [_H, c_int, c_int64, _DP, _DP, POINTER(c_int), _DP, POINTER(c_int)]),
+    ("mgmc_sample_timed_stride", c_int, [_H, c_int, c_int, c_int64, _DP, _DP, POINTER(c_int), _DP, POINTER(c_int)]),
     ("mgmc_comm_unique_id", c_int, [ctypes.c_char_p]),
     ("mgmc_comm_init", c_int, [_H, c_int, c_int, ctypes.c_char_p]),
     ("mgmc_comm_allgather_moments", c_int, [_H, _DP]),

@@ -541,14 +541,15 @@ class MultigridMCSampler:
     def synchronize(self):
         self._chk(self.lib.mgmc_synchronize(self.handle))
 
-    def sample_timed(self, nsteps: int, qoi_index: int = -1) -> dict:
+    def sample_timed(self, nsteps: int, qoi_index: int = -1, stride: int = 1) -> dict:
         """nsteps cycles replayed as [fine pre-sampler | coarse correction | fine post-sampler | QoI]
-        graph segments with HIP events on the handle's stream (mgmc_sample_timed)."""
+        graph segments with HIP events on the handle's stream (mgmc_sample_timed_stride: the segments
+        of every stride-th cycle and the last are timed, the others replay the plain graph)."""
         tot, pre, post = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         npre, npost = ctypes.c_int(), ctypes.c_int()
-        self._chk(self.lib.mgmc_sample_timed(self.handle, int(nsteps), int(qoi_index), ctypes.byref(tot),
-                                             ctypes.byref(pre), ctypes.byref(npre), ctypes.byref(post),
-                                             ctypes.byref(npost)))
+        self._chk(self.lib.mgmc_sample_timed_stride(self.handle, int(nsteps), int(stride), int(qoi_index),
+                                                    ctypes.byref(tot), ctypes.byref(pre), ctypes.byref(npre),
+                                                    ctypes.byref(post), ctypes.byref(npost)))
         return {"total_ms": tot.value, "pre_ms": pre.value, "npre": npre.value, "post_ms": post.value,
                 "npost": npost.value}
 

@@ -426,20 +426,22 @@ def test_unrolled_sample_loop_bitwise(hip_device, monkeypatch, name, unroll):
     s.close()
 
 
-@pytest.mark.parametrize("name", ["3d128_zsweep", "2d64_template_W"])
-def test_sample_timed_segments(hip_device, name):
-    """mgmc_sample_timed (the bench's timing path): one fine pre-sweep and one fine post-sweep per
-    cycle in their own event segments (the post segment ends before the QoI record), positive
-    segment times inside the total, and the same chain as the plain sample loop bit for bit."""
+@pytest.mark.parametrize("name,nsteps,stride,ntimed", [("3d128_zsweep", 4, 1, 4), ("2d64_template_W", 4, 1, 4),
+                                                       ("3d128_zsweep", 7, 3, 3), ("2d64_template_W", 6, 4, 3)])
+def test_sample_timed_segments(hip_device, name, nsteps, stride, ntimed):
+    """mgmc_sample_timed_stride (the bench's timing path): one fine pre-sweep and one fine post-sweep
+    per timed cycle in their own event segments (the post segment ends before the QoI record; every
+    stride-th cycle and the last are timed, the others replay the plain graph), positive segment
+    times inside the total, and the same chain as the plain sample loop bit for bit."""
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)
     t = make(shape, **kw)[0]
     q = mg.measurement_vector_index(lat, [0.5] * lat.dim)
-    r = s.sample_timed(4, q)
-    assert r["npre"] == 4 * (2 if p.smoother == "SSOR" else 1) and r["npost"] == r["npre"]
+    r = s.sample_timed(nsteps, q, stride=stride)
+    assert r["npre"] == ntimed * (2 if p.smoother == "SSOR" else 1) and r["npost"] == r["npre"]
     assert 0 < r["pre_ms"] and 0 < r["post_ms"] and r["pre_ms"] + r["post_ms"] < r["total_ms"]
-    z = s.get_series(4)
-    assert np.array_equal(z, t.sample(4, q))
+    z = s.get_series(nsteps)
+    assert np.array_equal(z, t.sample(nsteps, q))
     assert np.array_equal(s.get_state(), t.get_state())
     s.close()
     t.close()
