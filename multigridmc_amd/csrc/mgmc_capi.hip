@@ -97,6 +97,7 @@ enum PathFlag : uint32_t {
     PATH_NO_LR_PREFETCH = 1u << 9,        // low-rank small fix without the up-front loads
     PATH_NO_COARSE_PRECOMPUTE = 1u << 10, // coarse SSOR: right-hand sides inside the colour passes
     PATH_NO_LR_DENSE = 1u << 11,          // dense low-rank column: the row lists over every vertex
+    PATH_NO_CHOL_DENSE = 1u << 12,        // coarse Cholesky: the blocked banded solves at any size
 };
 
 struct PathToken {
@@ -110,6 +111,7 @@ constexpr PathToken kPathTokens[] = {
     {"zrestrict", PATH_NO_ZRESTRICT}, {"lr_small", PATH_NO_LR_SMALL},
     {"lr_merge", PATH_NO_LR_MERGE},   {"lr_prefetch", PATH_NO_LR_PREFETCH},
     {"coarse_precompute", PATH_NO_COARSE_PRECOMPUTE}, {"lr_dense", PATH_NO_LR_DENSE},
+    {"chol_dense", PATH_NO_CHOL_DENSE},
 };
 
 // parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
@@ -284,9 +286,11 @@ struct mgmc_handle {
     std::vector<double> lr_sigma;
     bool field_mode = false;     // hierarchy built from a matrix (mgmc_create_csr)
     CsrHost coarse_csr;          // ... and its coarsest level (dense Cholesky factors)
-    int chol_n = 0;              // dense Cholesky factors of the coarsest level (mgmc_cholesky.hpp)
-    double* chol_G = nullptr;
+    int chol_n = 0;              // Cholesky factors of the coarsest level (mgmc_cholesky.hpp)
+    double* chol_G = nullptr;    // dense: G and L^{-1}
     double* chol_Li = nullptr;
+    int chol_B = 0, chol_nb = 0; // blocked banded (chol_B > 0): Cf, Cb, Df, Db in one allocation
+    double* chol_blk = nullptr;
 };
 
 #define HIPCHK(h, call)                                                                              \
@@ -950,9 +954,38 @@ void launch_operator_apply(const mgmc_handle* h, const Level& lv, const double* 
     }
 }
 
-// coarsest level: x = G f (+ U xi) with the dense Cholesky factors (mgmc_cholesky.hpp)
+// coarsest level: x = G f (+ U xi) with the dense Cholesky factors, or the blocked banded solves
+// (mgmc_cholesky.hpp)
 void launch_coarse_chol(const mgmc_handle* h, const Level& lv, const double* f, double* x, bool noise, uint32_t tag,
                         const uint64_t* sample, hipStream_t s, int nch = 1) {
+    if (h->chol_B > 0) {
+        CholBlockArgs b;
+        b.L = lv.L;
+        b.n = h->chol_n;
+        b.B = h->chol_B;
+        b.nb = h->chol_nb;
+        const size_t blk = (size_t)h->chol_nb * h->chol_B * h->chol_B;
+        b.Cf = h->chol_blk;
+        b.Cb = h->chol_blk + blk;
+        b.Df = h->chol_blk + 2 * blk;
+        b.Db = h->chol_blk + 3 * blk;
+        b.f = f;
+        b.x = x;
+        b.noise = noise ? 1 : 0;
+        b.key = h->key;
+        b.tag = tag;
+        b.sample = sample;
+        b.cs = lv.L.nstore;
+        b.chain0 = (uint32_t)h->chain;
+        b.seed_hi = (uint32_t)(h->seed >> 32);
+        const dim3 grid(1, 1, nch), block((unsigned)std::min(1024, h->chol_B));
+        const size_t lds = 2 * (size_t)h->chol_B * sizeof(double);
+        if (lv.spec.dim == 3)
+            hipLaunchKernelGGL(k_coarse_chol_blocked<3>, grid, block, lds, s, b);
+        else
+            hipLaunchKernelGGL(k_coarse_chol_blocked<2>, grid, block, lds, s, b);
+        return;
+    }
     CholArgs a;
     a.L = lv.L;
     a.n = h->chol_n;
@@ -1554,54 +1587,104 @@ int check_level(mgmc_handle* h, int level, bool need_coarser) {
     return MGMC_OK;
 }
 
-// dense precision of the coarsest level (+ B Sigma^{-1} B^T: cholesky_sampler.cc:30-36, the oracle's
-// order), its Cholesky factor and the inverses G, L^{-1} (mgmc_cholesky.hpp); O(n^3) on the host
+// banded precision of the coarsest level (+ B Sigma^{-1} B^T: cholesky_sampler.cc:30-36, the oracle's
+// order), its Cholesky factor (mgmc_cholesky.hpp, bitwise the dense loop) and either the dense
+// inverses G, L^{-1} (n <= CHOL_MAX_N, O(n^3) on the host) or the blocked banded solve's blocks
+// (above, or MGMC_DISABLE=chol_dense; O(n bw^2)).  The bandwidth is the widest nonzero coupling:
+// matrix / stencil entries and the row span of each low-rank column (the oracle computes the same).
 int build_coarse_chol(mgmc_handle* h, const std::vector<LRColumn>* cols, const double* sigma, int m) {
     const Level& lv = h->levels.back();
     const long long n = (long long)lv.spec.ndof;
-    if (n > CHOL_MAX_N)
-        return fail(h, MGMC_E_UNSUPPORTED,
-                    "coarse Cholesky needs a coarsest level of at most " + std::to_string(CHOL_MAX_N) + " unknowns");
+    const bool blocked = n > CHOL_MAX_N || (h->paths & PATH_NO_CHOL_DENSE);
     const int dim = lv.spec.dim;
     const int nx = lv.spec.n[0], ny = lv.spec.n[1], nz = dim == 3 ? lv.spec.n[2] : 2;
-    std::vector<double> Q((size_t)n * n, 0.0);
-    if (h->field_mode) {  // the coarsest Galerkin matrix itself
-        const CsrHost& A = h->coarse_csr;
-        for (long long r = 0; r < n; ++r)
-            for (int64_t q = A.rowptr[r]; q < A.rowptr[r + 1]; ++q) Q[(size_t)r * n + A.col[q]] = A.val[q];
+    // the couplings (row, column, value) of the level's matrix, in the dense assembly's order
+    auto for_each_entry = [&](auto&& fn) {
+        if (h->field_mode) {  // the coarsest Galerkin matrix itself
+            const CsrHost& A = h->coarse_csr;
+            for (long long r = 0; r < n; ++r)
+                for (int64_t q = A.rowptr[r]; q < A.rowptr[r + 1]; ++q) fn(r, (long long)A.col[q], A.val[q]);
+            return;
+        }
+        for (long long r = 0; r < n; ++r) {
+            const int i = (int)(r % (nx - 1)) + 1, j = (int)((r / (nx - 1)) % (ny - 1)) + 1;
+            const int k = dim == 3 ? (int)(r / ((long long)(nx - 1) * (ny - 1))) + 1 : 1;
+            for (int dz = (dim == 3 ? -1 : 0); dz <= (dim == 3 ? 1 : 0); ++dz)
+                for (int dy = -1; dy <= 1; ++dy)
+                    for (int dx = -1; dx <= 1; ++dx) {
+                        const int ii = i + dx, jj = j + dy, kk = k + dz;
+                        if (ii < 1 || ii > nx - 1 || jj < 1 || jj > ny - 1 || (dim == 3 && (kk < 1 || kk > nz - 1)))
+                            continue;
+                        const double v = dim == 3 ? lv.spec.st[(dz + 1) * 9 + (dy + 1) * 3 + (dx + 1)]
+                                                  : lv.spec.st[(dy + 1) * 3 + (dx + 1)];
+                        fn(r, ((long long)(dim == 3 ? kk - 1 : 0) * (ny - 1) + (jj - 1)) * (nx - 1) + (ii - 1), v);
+                    }
+        }
+    };
+    long long bw = 0;
+    for_each_entry([&](long long r, long long c, double v) {
+        if (v != 0.0) bw = std::max(bw, r > c ? r - c : c - r);
+    });
+    for (int k = 0; k < m; ++k) {
+        long long lo = n, hi = -1;
+        for (const auto& e : (*cols)[k].ent)
+            if (e.second != 0.0) {
+                lo = std::min(lo, (long long)e.first);
+                hi = std::max(hi, (long long)e.first);
+            }
+        if (hi > lo) bw = std::max(bw, hi - lo);
     }
-    for (long long r = 0; r < (h->field_mode ? 0 : n); ++r) {
-        const int i = (int)(r % (nx - 1)) + 1, j = (int)((r / (nx - 1)) % (ny - 1)) + 1;
-        const int k = dim == 3 ? (int)(r / ((long long)(nx - 1) * (ny - 1))) + 1 : 1;
-        for (int dz = (dim == 3 ? -1 : 0); dz <= (dim == 3 ? 1 : 0); ++dz)
-            for (int dy = -1; dy <= 1; ++dy)
-                for (int dx = -1; dx <= 1; ++dx) {
-                    const int ii = i + dx, jj = j + dy, kk = k + dz;
-                    if (ii < 1 || ii > nx - 1 || jj < 1 || jj > ny - 1 || (dim == 3 && (kk < 1 || kk > nz - 1))) continue;
-                    const double v = dim == 3 ? lv.spec.st[(dz + 1) * 9 + (dy + 1) * 3 + (dx + 1)]
-                                              : lv.spec.st[(dy + 1) * 3 + (dx + 1)];
-                    const long long c = ((long long)(dim == 3 ? kk - 1 : 0) * (ny - 1) + (jj - 1)) * (nx - 1) + (ii - 1);
-                    Q[(size_t)r * n + c] = v;
-                }
-    }
+    const long long B = chol_block_size(bw);
+    if (blocked && B > CHOL_BLOCK_MAX)
+        return fail(h, MGMC_E_UNSUPPORTED,
+                    "coarse Cholesky: " + std::to_string(n) + " unknowns (above " + std::to_string(CHOL_MAX_N) +
+                        ") need a bandwidth of at most " + std::to_string(CHOL_BLOCK_MAX) + ", this level has " +
+                        std::to_string(bw));
+    if (!blocked && n > CHOL_MAX_N)
+        return fail(h, MGMC_E_UNSUPPORTED, "coarse Cholesky: too many unknowns");
+    const long long W = bw + 1;
+    std::vector<double> band((size_t)(n * W), 0.0);
+    for_each_entry([&](long long r, long long c, double v) {
+        if (c <= r && r - c <= bw) band[(size_t)(r * W + (c - r + bw))] = v;
+    });
     if (m > 0) {
         std::vector<double> Bd((size_t)n * m, 0.0);
         for (int k = 0; k < m; ++k)
             for (const auto& e : (*cols)[k].ent) Bd[(size_t)e.first * m + k] = e.second;
         for (long long i = 0; i < n; ++i)
-            for (long long j = 0; j < n; ++j) {
+            for (long long j = std::max(0LL, i - bw); j <= i; ++j) {
                 double s = 0.0;
                 for (int k = 0; k < m; ++k) s += Bd[(size_t)i * m + k] / sigma[k] * Bd[(size_t)j * m + k];
-                Q[(size_t)i * n + j] += s;
+                band[(size_t)(i * W + (j - i + bw))] += s;
             }
     }
-    if (!chol_factor_host(Q, n)) return fail(h, MGMC_E_INVALID, "coarse precision is not positive definite");
-    std::vector<double> Li, G;
-    chol_inverses_host(Q, n, Li, G);
+    if (!chol_band_factor(band, n, bw)) return fail(h, MGMC_E_INVALID, "coarse precision is not positive definite");
     if (h->chol_G) hipFree(h->chol_G);
     if (h->chol_Li) hipFree(h->chol_Li);
-    h->chol_G = h->chol_Li = nullptr;
-    h->chol_n = 0;
+    if (h->chol_blk) hipFree(h->chol_blk);
+    h->chol_G = h->chol_Li = h->chol_blk = nullptr;
+    h->chol_n = h->chol_B = h->chol_nb = 0;
+    if (blocked) {
+        std::vector<double> blk[4];
+        chol_blocks_host(band, n, bw, B, blk[0], blk[1], blk[2], blk[3]);
+        const size_t bytes = blk[0].size() * sizeof(double);
+        if (hipMalloc(&h->chol_blk, 4 * bytes) != hipSuccess) {
+            h->chol_blk = nullptr;
+            return fail(h, MGMC_E_NOMEM, "device allocation failed (blocked coarse Cholesky factors)");
+        }
+        for (int q = 0; q < 4; ++q)
+            HIPCHK(h, hipMemcpy(h->chol_blk + q * blk[0].size(), blk[q].data(), bytes, hipMemcpyHostToDevice));
+        h->chol_B = (int)B;
+        h->chol_nb = (int)((n + B - 1) / B);
+        h->chol_n = (int)n;
+        return MGMC_OK;
+    }
+    std::vector<double> Lm((size_t)n * n, 0.0);
+    for (long long i = 0; i < n; ++i)
+        for (long long c = std::max(0LL, i - bw); c <= i; ++c) Lm[(size_t)i * n + c] = band[(size_t)(i * W + (c - i + bw))];
+    std::vector<double>().swap(band);
+    std::vector<double> Li, G;
+    chol_inverses_host(Lm, n, Li, G);
     const size_t bytes = (size_t)n * n * sizeof(double);
     if (hipMalloc(&h->chol_G, bytes) != hipSuccess || hipMalloc(&h->chol_Li, bytes) != hipSuccess)
         return fail(h, MGMC_E_NOMEM, "device allocation failed (coarse Cholesky factors)");
@@ -2114,6 +2197,7 @@ int mgmc_destroy(mgmc_handle* h) {
         if (p) hipFree(p);
     if (h->chol_G) hipFree(h->chol_G);
     if (h->chol_Li) hipFree(h->chol_Li);
+    if (h->chol_blk) hipFree(h->chol_blk);
     if (h->sv_scal) hipFree(h->sv_scal);
     if (h->sv_part) hipFree(h->sv_part);
     if (h->comm) ncclCommDestroy(h->comm);
@@ -2148,7 +2232,7 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
     if (tl >= 0 && level >= tl) {
         sweep = "k_tail<" + std::to_string(dim) + ">";
     } else if (last) {
-        sweep = h->cfg.coarse_solver == MGMC_COARSE_CHOLESKY ? "k_coarse_chol" : "k_coarse_ssor_lds (or separate colour passes)";
+        sweep = h->cfg.coarse_solver == MGMC_COARSE_CHOLESKY ? (h->chol_B > 0 ? "k_coarse_chol_blocked" : "k_coarse_chol") : "k_coarse_ssor_lds (or separate colour passes)";
     } else if (lv.field) {
         sweep = "k_fsweep<" + std::to_string(dim) + ">";
     } else if (lv.zsweep) {

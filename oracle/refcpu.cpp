@@ -14,7 +14,7 @@
 //   LinearOperator::apply ......... linear_operator/linear_operator.hh:66-76
 //   SORSmoother::apply_sparse ..... smoother/sor_smoother.cc:56-78
 //   SORSampler / SSORSampler ...... sampler/sor_sampler.cc:9-59, sampler/ssor_sampler.cc:9-15
-//   DenseCholeskySampler .......... sampler/cholesky_sampler.{hh,cc} (dense LLT, no permutation)
+//   DenseCholeskySampler .......... sampler/cholesky_sampler.{hh,cc} (LLT, no permutation; banded storage)
 //   MultigridMCSampler ............ sampler/multigridmc_sampler.cc:8-138
 //   RNG plumbing .................. one shared std::mt19937_64, one std::normal_distribution<double>
 //                                   per sampler object (sampler/sampler.hh:31-34, :69-71)
@@ -1173,49 +1173,141 @@ static void dense_factor_inverses(const std::vector<double>& L, int64_t n, std::
         }
 }
 
+// Coarsest levels above 8192 unknowns (or g_chol_blocked, the device's MGMC_DISABLE=chol_dense) use
+// the blocked banded solves of the device (mgmc_cholesky.hpp k_coarse_chol_blocked): Q is banded
+// in lexicographic order, so is L; with B >= bw rows per block L is block lower bidiagonal
+// (diagonal blocks L_kk, coupling blocks C_k) and the two triangular solves become
+//   t = f_k - C_k y_{k-1}, y_k = L_kk^{-1} t;   y' = y + xi;   t = y'_k - C_{k+1}^T x_{k+1}, x_k = L_kk^{-T} t
+// with every row an fma chain in ascending column order.
+static int g_chol_blocked = 0;
+static const int64_t kCholDenseMax = 8192;
+
 struct DenseCholeskySampler : Sampler {
-    int64_t n;
-    std::vector<double> Lmat;  // row-major lower factor
+    int64_t n, bw = 0;
+    std::vector<double> band;  // lower factor, row i holds columns i - bw .. i
     std::vector<double> xi, g;
+    double Lat(int64_t i, int64_t k) const {
+        return (k <= i && i - k <= bw) ? band[(size_t)(i * (bw + 1) + (k - i + bw))] : 0.0;
+    }
     DenseCholeskySampler(Ctx* c, const Level* L) : Sampler(c) {
         lev = L;
         n = L->A.nrow;
-        Lmat.assign((size_t)n * n, 0.0);
+        const int m = L->lr.m;
+        // bandwidth: the widest nonzero coupling of the matrix and the row span of each low-rank column
         for (int64_t r = 0; r < n; ++r)
-            for (int64_t q = L->A.rowptr[r]; q < L->A.rowptr[r + 1]; ++q) Lmat[(size_t)r * n + L->A.col[q]] = L->A.val[q];
-        if (L->lr.m > 0) {  // A += B Sigma^{-1} B^T (cholesky_sampler.cc:30-36)
-            std::vector<double> Bd((size_t)n * L->lr.m, 0.0);
-            for (int k = 0; k < L->lr.m; ++k)
-                for (const auto& e : L->lr.cols[k]) Bd[(size_t)e.first * L->lr.m + k] = e.second;
+            for (int64_t q = L->A.rowptr[r]; q < L->A.rowptr[r + 1]; ++q)
+                if (L->A.val[q] != 0.0) bw = std::max(bw, std::abs(r - (int64_t)L->A.col[q]));
+        for (int k = 0; k < m; ++k) {
+            int64_t lo = n, hi = -1;
+            for (const auto& e : L->lr.cols[k])
+                if (e.second != 0.0) {
+                    lo = std::min(lo, (int64_t)e.first);
+                    hi = std::max(hi, (int64_t)e.first);
+                }
+            if (hi > lo) bw = std::max(bw, hi - lo);
+        }
+        const int64_t W = bw + 1;
+        band.assign((size_t)(n * W), 0.0);
+        for (int64_t r = 0; r < n; ++r)
+            for (int64_t q = L->A.rowptr[r]; q < L->A.rowptr[r + 1]; ++q) {
+                const int64_t col = L->A.col[q];
+                if (col <= r && r - col <= bw) band[(size_t)(r * W + (col - r + bw))] = L->A.val[q];
+            }
+        if (m > 0) {  // A += B Sigma^{-1} B^T (cholesky_sampler.cc:30-36); lower triangle, zero outside the band
+            std::vector<double> Bd((size_t)n * m, 0.0);
+            for (int k = 0; k < m; ++k)
+                for (const auto& e : L->lr.cols[k]) Bd[(size_t)e.first * m + k] = e.second;
             for (int64_t i = 0; i < n; ++i)
-                for (int64_t j = 0; j < n; ++j) {
+                for (int64_t j = std::max<int64_t>(0, i - bw); j <= i; ++j) {
                     double s = 0.0;
-                    for (int k = 0; k < L->lr.m; ++k) s += Bd[(size_t)i * L->lr.m + k] / L->lr.sigma[k] * Bd[(size_t)j * L->lr.m + k];
-                    Lmat[(size_t)i * n + j] += s;
+                    for (int k = 0; k < m; ++k) s += Bd[(size_t)i * m + k] / L->lr.sigma[k] * Bd[(size_t)j * m + k];
+                    band[(size_t)(i * W + (j - i + bw))] += s;
                 }
         }
+        // the dense LLT loop (column j: diagonal, then the rows below), its skipped products being zeros
         for (int64_t j = 0; j < n; ++j) {
-            double d = Lmat[(size_t)j * n + j];
-            for (int64_t k = 0; k < j; ++k) d -= Lmat[(size_t)j * n + k] * Lmat[(size_t)j * n + k];
+            double& djj = band[(size_t)(j * W + bw)];
+            double d = djj;
+            for (int64_t k = std::max<int64_t>(0, j - bw); k < j; ++k) d -= Lat(j, k) * Lat(j, k);
             d = sqrt(d);
-            Lmat[(size_t)j * n + j] = d;
-            for (int64_t i = j + 1; i < n; ++i) {
-                double s = Lmat[(size_t)i * n + j];
-                for (int64_t k = 0; k < j; ++k) s -= Lmat[(size_t)i * n + k] * Lmat[(size_t)j * n + k];
-                Lmat[(size_t)i * n + j] = s / d;
+            djj = d;
+            for (int64_t i = j + 1; i <= std::min(n - 1, j + bw); ++i) {
+                double& lij = band[(size_t)(i * W + (j - i + bw))];
+                double s = lij;
+                for (int64_t k = std::max<int64_t>(0, i - bw); k < j; ++k) s -= Lat(i, k) * Lat(j, k);
+                lij = s / d;
             }
-            for (int64_t k = j + 1; k < n; ++k) Lmat[(size_t)j * n + k] = 0.0;
         }
+        blocked = n > kCholDenseMax || g_chol_blocked;
         xi.resize(n);
         g.resize(n);
     }
     // cholesky_sampler.hh:50-66: xi ~ N(0, I), x = L^{-T} (xi + L^{-1} f).  MULTICOLOUR (device order):
     // xi from the Philox pair / branch of each vertex under the op's sweep tag, as a Gibbs sweep of
-    // this level would draw it, and the two triangular solves replaced by products with the
-    // precomputed U = L^{-T} and G = Q^{-1} = U U^T (dense_factor_inverses): x = G f + U xi, each
-    // row an fma chain in ascending column order -- every row independent, as the device computes it.
+    // this level would draw it; up to 8192 unknowns the two triangular solves are replaced by products
+    // with the precomputed U = L^{-T} and G = Q^{-1} = U U^T (dense_factor_inverses): x = G f + U xi,
+    // each row an fma chain in ascending column order -- every row independent, as the device
+    // computes it; above, the blocked solves (blocked_solve).
     const Level* lev = nullptr;
-    std::vector<double> U, G;  // row-major n x n (MULTICOLOUR)
+    bool blocked = false;
+    std::vector<double> U, G;  // row-major n x n (MULTICOLOUR, dense)
+    int64_t B = 0, nb = 0;
+    std::vector<double> Cb, Db;  // blocked: C_k(r, j) at Cb[k B^2 + r B + j], L_kk^{-1}(r, j) at Db[...]
+    void make_blocks() {
+        B = std::max<int64_t>(64, (std::max<int64_t>(bw, 1) + 63) / 64 * 64);
+        nb = (n + B - 1) / B;
+        const size_t BB = (size_t)(B * B);
+        Cb.assign(nb * BB, 0.0);
+        Db.assign(nb * BB, 0.0);
+        for (int64_t k = 0; k < nb; ++k) {
+            const int64_t base = k * B, Bk = std::min(B, n - base);
+            if (k > 0)
+                for (int64_t r = 0; r < Bk; ++r)
+                    for (int64_t j = 0; j < B; ++j) Cb[k * BB + r * B + j] = Lat(base + r, base - B + j);
+            double* D = &Db[k * BB];
+            for (int64_t c = 0; c < Bk; ++c)  // L_kk^{-1} column by column (dense_factor_inverses' loop)
+                for (int64_t r = c; r < Bk; ++r) {
+                    double s = r == c ? 1.0 : 0.0;
+                    for (int64_t q = c; q < r; ++q) s -= Lat(base + r, base + q) * D[q * B + c];
+                    D[r * B + c] = s / Lat(base + r, base + r);
+                }
+        }
+    }
+    void blocked_solve(const double* f, double* x, bool noise) {
+        if (Db.empty()) make_blocks();
+        const size_t BB = (size_t)(B * B);
+        std::vector<double> t(B), y(n);
+        for (int64_t k = 0; k < nb; ++k) {
+            const int64_t base = k * B, Bk = std::min(B, n - base);
+            for (int64_t r = 0; r < Bk; ++r) {
+                double s = 0.0;
+                if (k > 0)
+                    for (int64_t j = 0; j < B; ++j) s = fma(Cb[k * BB + r * B + j], y[base - B + j], s);
+                t[r] = f[base + r] - s;
+            }
+            for (int64_t r = 0; r < Bk; ++r) {
+                double a = 0.0;
+                for (int64_t j = 0; j <= r; ++j) a = fma(Db[k * BB + r * B + j], t[j], a);
+                y[base + r] = a;
+                x[base + r] = noise ? a + xi[base + r] : a;
+            }
+        }
+        for (int64_t k = nb - 1; k >= 0; --k) {
+            const int64_t base = k * B, Bk = std::min(B, n - base);
+            for (int64_t r = 0; r < Bk; ++r) {
+                double s = 0.0;
+                if (k + 1 < nb)
+                    for (int64_t j = 0; j < std::min(B, n - base - B); ++j)
+                        s = fma(Cb[(k + 1) * BB + j * B + r], x[base + B + j], s);
+                t[r] = x[base + r] - s;
+            }
+            for (int64_t r = 0; r < Bk; ++r) {
+                double a = 0.0;
+                for (int64_t j = r; j < Bk; ++j) a = fma(Db[k * BB + j * B + r], t[j], a);
+                x[base + r] = a;
+            }
+        }
+    }
     void apply(const double* f, double* x) override { solve(f, x, true); }
     void solve(const double* f, double* x, bool noise) {
         if (noise) {
@@ -1230,8 +1322,17 @@ struct DenseCholeskySampler : Sampler {
                 }
             }
         }
+        if (ctx->mode == MULTICOLOUR && blocked) {
+            blocked_solve(f, x, noise);
+            return;
+        }
         if (ctx->mode == MULTICOLOUR) {
-            if (U.empty()) dense_factor_inverses(Lmat, n, U, G);
+            if (U.empty()) {
+                std::vector<double> Lmat((size_t)n * n, 0.0);
+                for (int64_t i = 0; i < n; ++i)
+                    for (int64_t k = std::max<int64_t>(0, i - bw); k <= i; ++k) Lmat[(size_t)i * n + k] = Lat(i, k);
+                dense_factor_inverses(Lmat, n, U, G);
+            }
             for (int64_t i = 0; i < n; ++i) {
                 double a = 0.0;
                 for (int64_t j = 0; j < n; ++j) a = fma(G[(size_t)i * n + j], f[j], a);
@@ -1242,15 +1343,15 @@ struct DenseCholeskySampler : Sampler {
             }
             return;
         }
-        for (int64_t i = 0; i < n; ++i) {  // L g = f
+        for (int64_t i = 0; i < n; ++i) {  // L g = f (banded forward substitution)
             double s = f[i];
-            for (int64_t k = 0; k < i; ++k) s -= Lmat[(size_t)i * n + k] * g[k];
-            g[i] = s / Lmat[(size_t)i * n + i];
+            for (int64_t k = std::max<int64_t>(0, i - bw); k < i; ++k) s -= Lat(i, k) * g[k];
+            g[i] = s / Lat(i, i);
         }
         for (int64_t i = n - 1; i >= 0; --i) {  // L^T x = xi + g
             double s = noise ? xi[i] + g[i] : g[i];
-            for (int64_t k = i + 1; k < n; ++k) s -= Lmat[(size_t)k * n + i] * x[k];
-            x[i] = s / Lmat[(size_t)i * n + i];
+            for (int64_t k = i + 1; k <= std::min(n - 1, i + bw); ++k) s -= Lat(k, i) * x[k];
+            x[i] = s / Lat(i, i);
         }
     }
 };
@@ -1453,6 +1554,8 @@ void orc_destroy(orc_handle* h) { delete h; }
 
 // worker threads of the row-parallel loops (see g_threads); results do not depend on it
 void orc_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
+// coarse Cholesky: the blocked banded solves at any size (read when a sampler is built)
+void orc_set_chol_blocked(int on) { g_chol_blocked = on ? 1 : 0; }
 int orc_get_threads(void) { return g_threads; }
 
 // the reference's fine operators (any correlation-length model) as CSR: pde 0 FD, 1 FEM, 2 squared

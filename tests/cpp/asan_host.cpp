@@ -27,6 +27,7 @@ orc_handle* orc_create_fem(const orc_params* q, int mode, uint64_t seed, uint64_
 orc_handle* orc_create_csr(const orc_params* q, int mode, uint64_t seed, int64_t nrow, const int64_t* rowptr,
                            const int32_t* col, const double* val);
 void orc_destroy(orc_handle* h);
+void orc_set_chol_blocked(int on);
 int64_t orc_ndof(orc_handle* h, int level);
 int orc_nlevel(orc_handle* h);
 int64_t orc_nnz(orc_handle* h, int level);
@@ -199,6 +200,24 @@ int main() {
                 orc_destroy(h);
             }
             orc_handle* h = orc_create_fem(&p3, mode, 11ull, 0, nullptr);
+            exercise(h, false);
+            orc_destroy(h);
+        }
+        // the blocked banded Cholesky: forced on small coarsest levels, and by size (127^2 unknowns)
+        orc_set_chol_blocked(1);
+        for (int lr = 0; lr <= 1; ++lr) {
+            const orc_params p2 = params(2, 32, 3, 2, 0, 1), p3 = params(3, 16, 2, 1, 1, 1);
+            orc_handle* h = orc_create_fd(&p2, mode, 5418513ull, 1, nullptr);
+            exercise(h, lr);
+            orc_destroy(h);
+            h = orc_create_fd(&p3, mode, 5418513ull, 2, nullptr);
+            exercise(h, lr);
+            orc_destroy(h);
+        }
+        orc_set_chol_blocked(0);
+        {
+            const orc_params pb = params(2, 128, 1, 1, 0, 1);
+            orc_handle* h = orc_create_fd(&pb, mode, 7ull, 0, nullptr);
             exercise(h, false);
             orc_destroy(h);
         }

@@ -44,6 +44,7 @@ def lib():
                                           POINTER(c_int32), _DP]),
             "orc_destroy": (None, [c_void_p]),
             "orc_set_threads": (None, [c_int]),
+            "orc_set_chol_blocked": (None, [c_int]),
             "orc_get_threads": (c_int, []),
             "orc_ndof": (c_int64, [c_void_p, c_int]),
             "orc_nlevel": (c_int, [c_void_p]),
@@ -301,6 +302,12 @@ def operator_csr(shape, pde, periodic=False, Lambda=0.2, Lambda_min=0.2, Lambda_
 def set_threads(n: int) -> None:
     """Worker threads of the oracle's row-parallel loops (bitwise the same results; default 1)."""
     lib().orc_set_threads(int(n))
+
+
+def set_chol_blocked(on: bool) -> None:
+    """Coarse Cholesky: the blocked banded solves at any size (the device's MGMC_DISABLE=chol_dense);
+    read when an oracle is built."""
+    lib().orc_set_chol_blocked(1 if on else 0)
 
 
 def cpu_share() -> int:

@@ -171,7 +171,8 @@ VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_
             ("coarse_precompute", "3d16"), ("coarse_precompute", "2d64_template_W"),
             ("coarse_precompute", "3d32_W_ssor"), ("coarse_precompute,tail", "3d64_4lvl"),
             (ALL_PATHS, "3d128_zsweep"), (ALL_PATHS, "3d_aniso_zsweep_ssor"), (ALL_PATHS, "2d64_template_W"),
-            (ALL_PATHS, "2d_aniso_ssor"), (ALL_PATHS, "3d_zres27")]
+            (ALL_PATHS, "2d_aniso_ssor"), (ALL_PATHS, "3d_zres27"),
+            ("chol_dense", "2d64_chol_W"), ("chol_dense", "3d32_chol_ssor"), ("chol_dense", "3d128_zsweep_chol")]
 
 
 @pytest.mark.parametrize("paths,name", VARIANTS)
@@ -181,12 +182,17 @@ def test_variant_cycles_bitwise(hip_device, monkeypatch, paths, name):
     prolongate-add pass instead of the fold into the first post-sweep's plane loads; quads = one
     colour pair per launch; rb2d / zsweep = the 2D / 3D fine level in colour passes; pairs = one
     colour per pass on Galerkin levels; zrestrict = the per-point residual + restriction;
-    coarse_precompute = the coarse SSOR sampler's right-hand sides inside its colour passes.  Every
-    combination gives the oracle's cycle exactly."""
+    coarse_precompute = the coarse SSOR sampler's right-hand sides inside its colour passes;
+    chol_dense = the coarse Cholesky's blocked banded solves on a small coarsest level (the oracle's
+    blocked mode).  Every combination gives the oracle's cycle exactly."""
     monkeypatch.setenv("MGMC_DISABLE", paths)
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)
-    mc = oracle_for(s, p, lat)
+    O.set_chol_blocked("chol_dense" in paths.split(","))
+    try:
+        mc = oracle_for(s, p, lat)
+    finally:
+        O.set_chol_blocked(False)
     f = np.random.default_rng(7).standard_normal(lat.Nvertex)
     x_dev, x_orc = np.zeros(lat.Nvertex), np.zeros(lat.Nvertex)
     for _ in range(2):
@@ -363,8 +369,8 @@ def test_invalid_level_and_sizes_raise(hip_device):
     with pytest.raises(mg.MgmcError):
         s.sample(3, lat.Nvertex + 5)
     s.close()
-    with pytest.raises(mg.MgmcError):  # dense coarse Cholesky needs a small coarsest level
-        make((128, 128), nlevel=1, coarse_solver="Cholesky")
+    with pytest.raises(mg.MgmcError, match="bandwidth"):  # coarse Cholesky: rows of at most 4096 above 8192 dofs
+        make((8192, 8), nlevel=1, coarse_solver="Cholesky")
 
 
 def test_cpp_host_side_sample_matches_python_path(hip_device, tmp_path):

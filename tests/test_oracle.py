@@ -301,3 +301,45 @@ def test_host_code_clean_under_address_sanitizer():
                        timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "asan_host OK" in r.stdout
+
+
+# ---------------------------------------------------------------- blocked banded Cholesky
+@pytest.mark.parametrize("shape,nlevel", [((16, 16), 1), ((32, 32), 2), ((8, 8, 8), 1), ((12, 10), 1)])
+def test_blocked_cholesky_equals_dense_products(shape, nlevel):
+    """The oracle's two multicolour Cholesky sampler forms (refcpu.cpp DenseCholeskySampler): the
+    dense products x = G f + U xi (up to 8,192 unknowns) and the blocked banded solves (above, or
+    forced) compute the same x = L^-T (xi + L^-1 f) from the same Philox xi: equal to rounding."""
+    p = MultigridParameters(nlevel=nlevel, coarse_solver="Cholesky")
+    f = np.random.default_rng(5).standard_normal(int(np.prod([n - 1 for n in shape])))
+    out = []
+    for blocked in (False, True):
+        O.set_chol_blocked(blocked)
+        try:
+            o = O.Oracle.fd(shape, p, kappa_sq=4.0, mode=O.MULTICOLOUR, seed=77)
+        finally:
+            O.set_chol_blocked(False)
+        x = np.zeros_like(f)
+        o.apply(f, x)
+        out.append(x)
+    assert np.max(np.abs(out[0] - out[1])) <= 1e-12 * np.max(np.abs(out[0]))
+    assert not np.array_equal(out[0], np.zeros_like(f))
+
+
+def test_blocked_cholesky_is_exact_sampler():
+    """Above 8,192 unknowns (2D 128^2, one level: 16,129, the blocked mode by size) the oracle's
+    Cholesky sampler is exact: 400 independent draws of the centre vertex against (Q^-1)_cc and
+    (Q^-1 f)_c (5 sigma)."""
+    p = MultigridParameters(nlevel=1, coarse_solver="Cholesky")
+    o = O.Oracle.fd((128, 128), p, kappa_sq=25.0, mode=O.MULTICOLOUR, seed=3)
+    Q = o.csr_matrix(0).tocsc()
+    import scipy.sparse.linalg as spla
+    n = Q.shape[0]
+    c = n // 2
+    f = np.random.default_rng(1).standard_normal(n)
+    e = np.zeros(n)
+    e[c] = 1.0
+    var, mean = spla.spsolve(Q, e)[c], spla.spsolve(Q, f)[c]
+    o.set_rhs(f)
+    z = o.sample(400, c)
+    assert abs(z.mean() - mean) < 5 * np.sqrt(var / 400)
+    assert abs(z.var() - var) < 5 * var * np.sqrt(2.0 / 400)
