@@ -57,7 +57,9 @@ def test_blocked_coarse_cholesky_cycles_bitwise(hip_device, name):
         assert np.array_equal(x_dev, x_orc)
     qoi = mg.measurement_vector_index(lat, [0.5] * lat.dim)
     s.fix_rhs(f)
+    s.set_state(x_dev)
     mc.set_rhs(f)
+    mc.set_state(x_orc)
     assert np.array_equal(s.sample(4, qoi), mc.sample(4, qoi))
     assert np.array_equal(s.get_state(), mc.get_state())
     s.close()
