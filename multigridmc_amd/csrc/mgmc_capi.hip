@@ -30,6 +30,7 @@ static_assert(MGMC_LAYOUT_POINT == mgmc::LF_POINT && MGMC_LAYOUT_PAIRS == mgmc::
 #include "mgmc_zrestrict.hpp"
 #include "mgmc_tail.hpp"
 #include "mgmc_gsweep.hpp"
+#include "mgmc_jsweep.hpp"
 #include "mgmc_rb2d.hpp"
 #include "mgmc_lowrank.hpp"
 #include "mgmc_solver.hpp"
@@ -98,6 +99,7 @@ enum PathFlag : uint32_t {
     PATH_NO_COARSE_PRECOMPUTE = 1u << 10, // coarse SSOR: right-hand sides inside the colour passes
     PATH_NO_LR_DENSE = 1u << 11,          // dense low-rank column: the row lists over every vertex
     PATH_NO_CHOL_DENSE = 1u << 12,        // coarse Cholesky: the blocked banded solves at any size
+    PATH_NO_JSWEEP = 1u << 13,            // 3D Galerkin levels of 64 / 128 pairs: colour-pair passes, not j-marching halves
 };
 
 struct PathToken {
@@ -111,7 +113,7 @@ constexpr PathToken kPathTokens[] = {
     {"zrestrict", PATH_NO_ZRESTRICT}, {"lr_small", PATH_NO_LR_SMALL},
     {"lr_merge", PATH_NO_LR_MERGE},   {"lr_prefetch", PATH_NO_LR_PREFETCH},
     {"coarse_precompute", PATH_NO_COARSE_PRECOMPUTE}, {"lr_dense", PATH_NO_LR_DENSE},
-    {"chol_dense", PATH_NO_CHOL_DENSE},
+    {"chol_dense", PATH_NO_CHOL_DENSE}, {"jsweep", PATH_NO_JSWEEP},
 };
 
 // parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
@@ -221,7 +223,8 @@ struct Level {
     uint32_t paths = 0;    // PathFlag bits of the handle (MGMC_DISABLE)
     bool zsweep = false;   // fused z-marching red-black sweep available
     bool pairs = false;    // Galerkin level swept in colour-pair passes (mgmc_gsweep.hpp)
-    bool quads = false;    // ... two pairs per launch, out of place (k_sweep_quads)
+    bool quads = false;    // ... two pairs per launch, out of place (k_sweep_quads, or k_jsweep_half:)
+    bool jsweep = false;   // ... j-marching half-sweeps (mgmc_jsweep.hpp)
     bool rb2d = false;     // 2D 5-point level: one-launch red-black sweep, out of place (k_rb2d)
     bool field = false;    // per-vertex coefficients (mgmc_create_csr, mgmc_field.hpp)
     FieldArg F;            // ... their device field, pattern and colouring
@@ -503,8 +506,51 @@ void launch_rb2d(const Level& lv, const double* xin, double* xout, const double*
         hipLaunchKernelGGL((k_rb2d<false>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx, cs);
 }
 
+// j-marching half-sweeps (k_jsweep_half): 3D 27-point levels with rows of 128 pairs (nx = 256: level 1 at
+// 512^3), x read about 1.5 times per half instead of once per colour-pair pass
+bool jsweep_eligible(const LevelSpec& sp, const Layout& L, uint32_t paths) {
+    return sp.dim == 3 && sp.npoints == 27 && L.nx == 2 * JS_NP && L.ny >= 2 && L.nz >= 2 && !(paths & PATH_NO_JSWEEP);
+}
+
+#ifndef MGMC_JS_TILES  // target workgroups per half: one round at 3 per CU (timing builds override it)
+#define MGMC_JS_TILES 768
+#endif
+
+void launch_jsweep(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
+                   hipStream_t s, int nch) {
+    JSweepArgs a;
+    a.cs = lv.L.nstore;
+    a.L = lv.L;
+    a.xo = xin;
+    a.xout = xout;
+    a.f = f;
+    a.S = lv.S;
+    a.G = g;
+    const bool fwd = direction == MGMC_FORWARD;
+    a.jA = fwd ? 0 : 1;  // first pair of a half: colours (0,1) / (4,5) forward, (7,6) / (3,2) backward
+    a.nsteps = (lv.L.ny - a.jA) / 2 + 1;
+    for (int h = 0; h < 2; ++h) {
+        a.kp = fwd ? h : 1 - h;
+        a.xz = h == 0 ? xin : xout;  // the second half reads the first half's new planes
+        const int first = 2 - a.kp;
+        a.nk = first > lv.L.nz - 1 ? 0 : (lv.L.nz - 1 - first) / 2 + 1;
+        if (a.nk == 0) continue;
+        const int nchunk = std::max(1, std::min(a.nsteps, MGMC_JS_TILES / a.nk));
+        a.spc = (a.nsteps + nchunk - 1) / nchunk;
+        a.nchunk = (a.nsteps + a.spc - 1) / a.spc;
+        const int nb = (a.nk * a.nchunk + 7) / 8 * 8;
+        const dim3 grid(nb, 1, nch), block(JS_NT);
+        if (fwd) hipLaunchKernelGGL((k_jsweep_half<false>), grid, block, jsweep_lds_bytes(), s, a);
+        else hipLaunchKernelGGL((k_jsweep_half<true>), grid, block, jsweep_lds_bytes(), s, a);
+    }
+}
+
 void launch_quads(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
                   hipStream_t s, int nch = 1) {
+    if (lv.jsweep) {
+        launch_jsweep(lv, xin, xout, f, g, direction, s, nch);
+        return;
+    }
     QuadPassArgs a;
     a.cs = lv.L.nstore;
     a.L = lv.L;
@@ -633,6 +679,9 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
         const long long nchunk = std::max(1LL, (2 * slots + per_chunk - 1) / per_chunk);
         a.kz = std::max(8, (int)((lc.L.nz - 1 + nchunk - 1) / nchunk));
     }
+#ifdef MGMC_ZR27_KZ  // (timing builds: scripts/build_exp.sh VARIANTS)
+    if (NPTS == 27 && CX == 64) a.kz = MGMC_ZR27_KZ;
+#endif
     a.ntz = (lc.L.nz - 1 + a.kz - 1) / a.kz;
     const int nt = a.ntx * a.nty * a.ntz;
     const int nb = (nt + 7) / 8 * 8;
@@ -677,7 +726,12 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
                 launch_zresrestrict_t<7, 64, 8, 512>(lf, lc, x, f, fc, xc, s, nch);
             else launch_zresrestrict_t<7, 64, 4, 256>(lf, lc, x, f, fc, xc, s, nch);
         } else {
+#ifndef MGMC_ZR27_CY  // (timing builds: scripts/build_exp.sh VARIANTS)
+#define MGMC_ZR27_CY 4
+#endif
             if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch);
+            else if (MGMC_ZR27_CY == 8 && lc.L.nx >= 128)
+                launch_zresrestrict_t<27, 64, 8, 512>(lf, lc, x, f, fc, xc, s, nch);
             else launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s, nch);
         }
         return;
@@ -1952,7 +2006,8 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
         lv.pairs = !lv.field && pairs_eligible(lv.spec, lv.L) && !(h->paths & PATH_NO_PAIRS);
         lv.rb2d = !lv.field && cfg->dim == 2 && lv.spec.npoints == 5 && l + 1 < specs.size() &&
                   !(h->paths & PATH_NO_RB2D);
-        lv.quads = lv.pairs && quads_eligible(lv.spec, lv.L, h->paths) && (tail0 < 0 || (int)l < tail0);
+        lv.jsweep = lv.pairs && jsweep_eligible(lv.spec, lv.L, h->paths) && (tail0 < 0 || (int)l < tail0);
+        lv.quads = lv.jsweep || (lv.pairs && quads_eligible(lv.spec, lv.L, h->paths) && (tail0 < 0 || (int)l < tail0));
         if (lv.pingpong()) {
             if (hipMalloc(&lv.x2, cbytes) != hipSuccess) {
                 h->levels.push_back(lv);
@@ -2238,6 +2293,8 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
     } else if (lv.zsweep) {
         sweep = "k_zsweep_rb7<32," + std::to_string(MGMC_ZS_SHAPE_TY) + ",...,0>";
         if (!(h->paths & PATH_NO_FUSE_PROLONG)) post = "k_zsweep_rb7<32," + std::to_string(MGMC_ZS_SHAPE_TYP) + ",...,PROLONG>";
+    } else if (lv.jsweep) {
+        sweep = "k_jsweep_half";
     } else if (lv.quads) {
         sweep = "k_sweep_quads<" + std::to_string(dim) + ">";
     } else if (lv.rb2d) {

@@ -3,7 +3,7 @@ V-cycle, one chain -- the hierarchy bench.py times.
 
 The kernel instances this configuration selects exist only at this size (mgmc_capi.hip): the fine
 residual + restriction `k_zresrestrict<7,64,8,512>` (chosen when the coarse level has >= 16 K tile
-planes), the fused-prolongation post-sweep's 128-plane z chunks, the level-1 colour-pair passes at
+planes), the fused-prolongation post-sweep's 128-plane z chunks, the level-1 j-marching half-sweeps (k_jsweep_half) at
 their full 128-pair row width and the 512^3 `k_tail`.  Every one of them is compared here bit for
 bit (np.array_equal) with the CPU oracle's MULTICOLOUR replay of the same hierarchy (the device's
 level stencils, Philox key (5418513, 0)).  The residual + restriction components are also the
@@ -85,7 +85,7 @@ def test_headline_residual_restrict_bitwise(headline, level):
 @pytest.mark.parametrize("level,direction", [(0, mg.FORWARD), (1, mg.BACKWARD)])
 def test_headline_noisy_sweep_bitwise(headline, level, direction):
     """One Gibbs sweep (SORSampler::apply, sor_sampler.cc:37-59) at full width: the fine z-marching
-    red-black sweep (512^3) and the level-1 colour-pair passes (255^3, 128-pair rows)."""
+    red-black sweep (512^3) and the level-1 j-marching half-sweeps (255^3, 128-pair rows)."""
     s, orc, lat, p = headline
     rng = np.random.default_rng(200 + level)
     n = s.level_desc(level)["ndof"]
@@ -103,7 +103,7 @@ def test_headline_cycle_and_qoi_series_bitwise(headline):
     device-resident measure_sampling_time loop (driver_mgmc.cc:66-78) for 3 samples with the QoI at
     the lattice centre: cycle state, QoI series and final state equal the oracle's exactly.  This
     runs the benchmark's graph: fused-prolongation post-sweep (128-plane chunks), k_zresrestrict
-    <7,64,8,512>, the level-1 pair passes, the 512^3 k_tail and the QoI record."""
+    <7,64,8,512>, the level-1 and level-2 j-marching half-sweeps, the 512^3 k_tail and the QoI record."""
     s, orc, lat, p = headline
     f = np.random.default_rng(11).standard_normal(lat.Nvertex)
     x_dev = np.zeros(lat.Nvertex)
@@ -132,10 +132,10 @@ def test_headline_cycle_and_qoi_series_bitwise(headline):
 
 def test_headline_kernel_instances(headline):
     """The instances the tests above ran are the benchmark's (mgmc_level_kernels): the fused z-sweep
-    pair on level 0 with the 64 x 8 residual + restriction, pair passes on level 1, k_tail below."""
+    pair on level 0 with the 64 x 8 residual + restriction, j-marching half-sweeps on level 1, k_tail below."""
     s, orc, lat, p = headline
     k0 = s.level_kernels(0)
     assert k0["sweep"].startswith("k_zsweep_rb7<") and k0["post_sweep"].endswith("PROLONG>")
     assert k0["residual_restrict"] == "k_zresrestrict<7,64,8>"
-    assert s.level_kernels(1) == {"sweep": "k_sweep_pairs<3>", "residual_restrict": "k_zresrestrict<27,64,4>"}
+    assert s.level_kernels(1) == {"sweep": "k_jsweep_half", "residual_restrict": "k_zresrestrict<27,64,4>"}
     assert s.level_kernels(NLEVEL - 1)["sweep"] == "k_tail<3>"

@@ -63,6 +63,8 @@ CONFIGS = {
     # clamped onto the zero pad pair since round 3, tests/test_layout.py)
     "3d_zres_lasttile": ((132, 36, 20), dict(nlevel=2)),
     "3d_zsr_ssor_W": ((128, 64, 64), dict(nlevel=3, cycle=2, smoother="SSOR", npresmooth=2, omega=0.9)),
+    # j-marching half-sweeps (k_jsweep_half) on a short level 1 of 128-pair rows, SSOR, W-cycle
+    "3d_jsweep_ssor_W": ((512, 44, 60), dict(nlevel=3, cycle=2, smoother="SSOR", npresmooth=2, omega=1.1)),
     # dense Cholesky coarse sampler (CholeskySampler, x = G f + U xi on the coarsest level)
     "2d64_chol_W": ((64, 64), dict(nlevel=4, cycle=2, coarse_solver="Cholesky")),
     "3d32_chol_ssor": ((32, 32, 32), dict(nlevel=3, smoother="SSOR", coarse_solver="Cholesky")),
@@ -158,7 +160,7 @@ def test_mgmc_cycles_bitwise(hip_device, name):
 
 # every MGMC_DISABLE token of mgmc_capi.hip (PathFlag), alone and all together, on configurations
 # where the fast path it turns off would run
-ALL_PATHS = "tail,fuse_prolong,quads,rb2d,zsweep,pairs,zrestrict,lr_small,lr_merge,lr_prefetch,coarse_precompute"
+ALL_PATHS = "tail,fuse_prolong,quads,rb2d,zsweep,pairs,zrestrict,lr_small,lr_merge,lr_prefetch,coarse_precompute,jsweep"
 VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_ssor"),
             ("fuse_prolong", "3d128_zsweep_odd"),
             ("tail", "3d16"), ("tail", "3d64_4lvl"), ("tail", "2d64_template_W"), ("tail", "3d32_W_ssor"),
@@ -172,7 +174,8 @@ VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_
             ("coarse_precompute", "3d32_W_ssor"), ("coarse_precompute,tail", "3d64_4lvl"),
             (ALL_PATHS, "3d128_zsweep"), (ALL_PATHS, "3d_aniso_zsweep_ssor"), (ALL_PATHS, "2d64_template_W"),
             (ALL_PATHS, "2d_aniso_ssor"), (ALL_PATHS, "3d_zres27"),
-            ("chol_dense", "2d64_chol_W"), ("chol_dense", "3d32_chol_ssor"), ("chol_dense", "3d128_zsweep_chol")]
+            ("chol_dense", "2d64_chol_W"), ("chol_dense", "3d32_chol_ssor"), ("chol_dense", "3d128_zsweep_chol"),
+            ("jsweep", "3d_zres27"), ("jsweep", "3d_jsweep_ssor_W")]
 
 
 @pytest.mark.parametrize("paths,name", VARIANTS)
@@ -181,7 +184,8 @@ def test_variant_cycles_bitwise(hip_device, monkeypatch, paths, name):
     levels as separate launches instead of one k_tail workgroup; fuse_prolong = the separate
     prolongate-add pass instead of the fold into the first post-sweep's plane loads; quads = one
     colour pair per launch; rb2d / zsweep = the 2D / 3D fine level in colour passes; pairs = one
-    colour per pass on Galerkin levels; zrestrict = the per-point residual + restriction;
+    colour per pass on Galerkin levels; jsweep = colour-pair passes instead of the j-marching half-sweeps
+    on 3D Galerkin levels of 64 / 128 pairs per row; zrestrict = the per-point residual + restriction;
     coarse_precompute = the coarse SSOR sampler's right-hand sides inside its colour passes;
     chol_dense = the coarse Cholesky's blocked banded solves on a small coarsest level (the oracle's
     blocked mode).  Every combination gives the oracle's cycle exactly."""
@@ -229,13 +233,15 @@ def test_nonfinite_state_fails_loudly(hip_device, name, qoi):
     s.close()
 
 
-@pytest.mark.parametrize("name,sweep", [("2d64_template_W", "k_rb2d"), ("3d128_zsweep", "k_zsweep_rb7<"),
-                                        ("3d16", "k_sweep_rb<3>")])
-def test_level_kernels_labels(hip_device, name, sweep):
-    """mgmc_level_kernels names the fine sweep each lattice really runs (bench.py's roofline labels)."""
+@pytest.mark.parametrize("name,level,sweep", [("2d64_template_W", 0, "k_rb2d"), ("3d128_zsweep", 0, "k_zsweep_rb7<"),
+                                              ("3d16", 0, "k_sweep_rb<3>"), ("3d_jsweep_ssor_W", 1, "k_jsweep_half"),
+                                              ("3d_zres27", 1, "k_jsweep_half"), ("3d128_zsweep", 1, "k_sweep_quads<3>"),
+                                              ("3d_aniso_zsweep_ssor", 1, "k_sweep_pairs<3>")])
+def test_level_kernels_labels(hip_device, name, level, sweep):
+    """mgmc_level_kernels names the sweep each level really runs (bench.py's roofline labels)."""
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)
-    assert s.level_kernels(0)["sweep"].startswith(sweep)
+    assert s.level_kernels(level)["sweep"].startswith(sweep)
     s.close()
 
 
