@@ -507,13 +507,16 @@ void launch_rb2d(const Level& lv, const double* xin, double* xout, const double*
 }
 
 // j-marching half-sweeps (k_jsweep_half): 3D 27-point levels with rows of 128 pairs (nx = 256: level 1 at
-// 512^3), x read about 1.5 times per half instead of once per colour-pair pass
+// 512^3), x read about 1.5 times per half instead of once per colour-pair pass.
+// With 64-pair rows (512^3 level 2, 256^3 level 1) the kernel is slower than the pair passes (2 x 21 against
+// 4 x 8 us per sweep at 127^3, 256^3 cycle 0.484 -> 0.503 ms): those levels are latency-bound, and the
+// march's chunks are short.
 bool jsweep_eligible(const LevelSpec& sp, const Layout& L, uint32_t paths) {
-    return sp.dim == 3 && sp.npoints == 27 && L.nx == 2 * JS_NP && L.ny >= 2 && L.nz >= 2 && !(paths & PATH_NO_JSWEEP);
+    return sp.dim == 3 && sp.npoints == 27 && L.nx == 256 && L.ny >= 2 && L.nz >= 2 && !(paths & PATH_NO_JSWEEP);
 }
 
-#ifndef MGMC_JS_TILES  // target workgroups per half: one round at 3 per CU (timing builds override it)
-#define MGMC_JS_TILES 768
+#ifndef MGMC_JS_ROUNDS  // workgroups per half: this many rounds of the resident slots (timing builds override it)
+#define MGMC_JS_ROUNDS 1
 #endif
 
 void launch_jsweep(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
@@ -526,6 +529,10 @@ void launch_jsweep(const Level& lv, const double* xin, double* xout, const doubl
     a.f = f;
     a.S = lv.S;
     a.G = g;
+    const int np = lv.L.nx / 2;
+    const size_t lds = jsweep_lds_bytes(np);
+    // resident workgroups: LDS-bound (160 KB per CU), one round of them per half
+    const int slots = (int)std::max<size_t>(1, (160 * 1024) / lds) * lv.num_cu * MGMC_JS_ROUNDS;
     const bool fwd = direction == MGMC_FORWARD;
     a.jA = fwd ? 0 : 1;  // first pair of a half: colours (0,1) / (4,5) forward, (7,6) / (3,2) backward
     a.nsteps = (lv.L.ny - a.jA) / 2 + 1;
@@ -535,13 +542,13 @@ void launch_jsweep(const Level& lv, const double* xin, double* xout, const doubl
         const int first = 2 - a.kp;
         a.nk = first > lv.L.nz - 1 ? 0 : (lv.L.nz - 1 - first) / 2 + 1;
         if (a.nk == 0) continue;
-        const int nchunk = std::max(1, std::min(a.nsteps, MGMC_JS_TILES / a.nk));
+        const int nchunk = std::max(1, std::min(a.nsteps, slots / a.nk));
         a.spc = (a.nsteps + nchunk - 1) / nchunk;
         a.nchunk = (a.nsteps + a.spc - 1) / a.spc;
         const int nb = (a.nk * a.nchunk + 7) / 8 * 8;
-        const dim3 grid(nb, 1, nch), block(JS_NT);
-        if (fwd) hipLaunchKernelGGL((k_jsweep_half<false>), grid, block, jsweep_lds_bytes(), s, a);
-        else hipLaunchKernelGGL((k_jsweep_half<true>), grid, block, jsweep_lds_bytes(), s, a);
+        const dim3 grid(nb, 1, nch), block(2 * np);
+        if (fwd) hipLaunchKernelGGL((k_jsweep_half<128, false>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((k_jsweep_half<128, true>), grid, block, lds, s, a);
     }
 }
 
@@ -2294,7 +2301,7 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
         sweep = "k_zsweep_rb7<32," + std::to_string(MGMC_ZS_SHAPE_TY) + ",...,0>";
         if (!(h->paths & PATH_NO_FUSE_PROLONG)) post = "k_zsweep_rb7<32," + std::to_string(MGMC_ZS_SHAPE_TYP) + ",...,PROLONG>";
     } else if (lv.jsweep) {
-        sweep = "k_jsweep_half";
+        sweep = "k_jsweep_half<" + std::to_string(lv.L.nx / 2) + ">";
     } else if (lv.quads) {
         sweep = "k_sweep_quads<" + std::to_string(dim) + ">";
     } else if (lv.rb2d) {

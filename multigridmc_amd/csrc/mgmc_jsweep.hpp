@@ -34,11 +34,10 @@
 
 namespace mgmc {
 
-constexpr int JS_NP = 128;           // pairs per row (nx = 256)
-constexpr int JS_NT = 2 * JS_NP;     // threads: A-row pairs, B-row pairs
+// NP pairs per row (nx = 2 NP; the library runs NP = 128: level 1 at 512^3); 2 NP threads
+// (A-row pairs, B-row pairs); ring rows of stride 2 NP + 8: odd pairs [0, NP) and the guard at NP, then
+// the even block from NP + 1: its guard (position 0) first, even pair m at NP + 2 + m
 constexpr int JS_RING = 8;           // rows per plane in the LDS ring
-constexpr int JS_RS = 2 * JS_NP + 8; // ring row stride: odd [0, 128] (guard at 128), even [129, 258] (guard at 129)
-constexpr int JS_EV = JS_NP + 1;     // offset of the even block; even pair m at JS_EV + 1 + m
 #ifndef MGMC_JS_D  // (timing builds override it)
 #define MGMC_JS_D 3
 #endif
@@ -67,10 +66,11 @@ struct JSweepArgs {
 __device__ __forceinline__ void js_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 constexpr int JS_TAB = 322;  // Box-Muller tables in LDS: log reduction (rc, hi, lo) x 64 + cos/sin 130
-inline size_t jsweep_lds_bytes() { return (size_t)(JS_RING * 3 * JS_RS + JS_TAB) * sizeof(double); }
+inline size_t jsweep_lds_bytes(int np) { return (size_t)(JS_RING * 3 * (2 * np + 8) + JS_TAB) * sizeof(double); }
 
-template <bool FIRST_ODD>
-__global__ void __launch_bounds__(JS_NT) k_jsweep_half(JSweepArgs a) {
+template <int NP, bool FIRST_ODD>
+__global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
+    constexpr int JS_NP = NP, JS_NT = 2 * NP, JS_RS = 2 * NP + 8, JS_EV = NP + 1;
     {
         const int ch = batch_chain();
         a.xo += ch * a.cs;
@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(JS_NT) k_jsweep_half(JSweepArgs a) {
     const int k = 2 - a.kp + 2 * kk;
     const int s0 = chunk * a.spc, s1 = min(s0 + a.spc, a.nsteps);
     const int tid = threadIdx.x;
-    const int role = tid >> 7;        // 0: A-row, 1: B-row
+    const int role = tid / JS_NP;     // 0: A-row, 1: B-row
     const int m = tid & (JS_NP - 1);  // pair of the row
     const int i0 = 2 * m + 1;
     const uint64_t sample = *a.G.sample;

@@ -137,5 +137,5 @@ def test_headline_kernel_instances(headline):
     k0 = s.level_kernels(0)
     assert k0["sweep"].startswith("k_zsweep_rb7<") and k0["post_sweep"].endswith("PROLONG>")
     assert k0["residual_restrict"] == "k_zresrestrict<7,64,8>"
-    assert s.level_kernels(1) == {"sweep": "k_jsweep_half", "residual_restrict": "k_zresrestrict<27,64,4>"}
+    assert s.level_kernels(1) == {"sweep": "k_jsweep_half<128>", "residual_restrict": "k_zresrestrict<27,64,4>"}
     assert s.level_kernels(NLEVEL - 1)["sweep"] == "k_tail<3>"

@@ -234,9 +234,10 @@ def test_nonfinite_state_fails_loudly(hip_device, name, qoi):
 
 
 @pytest.mark.parametrize("name,level,sweep", [("2d64_template_W", 0, "k_rb2d"), ("3d128_zsweep", 0, "k_zsweep_rb7<"),
-                                              ("3d16", 0, "k_sweep_rb<3>"), ("3d_jsweep_ssor_W", 1, "k_jsweep_half"),
-                                              ("3d_zres27", 1, "k_jsweep_half"), ("3d128_zsweep", 1, "k_sweep_quads<3>"),
-                                              ("3d_aniso_zsweep_ssor", 1, "k_sweep_pairs<3>")])
+                                              ("3d16", 0, "k_sweep_rb<3>"), ("3d_jsweep_ssor_W", 1, "k_jsweep_half<128>"),
+                                              ("3d_zres27", 1, "k_jsweep_half<128>"), ("3d128_zsweep", 1, "k_sweep_quads<3>"),
+                                              ("3d_aniso_zsweep_ssor", 1, "k_sweep_pairs<3>"),
+                                              ("3d64_4lvl", 1, "k_sweep_quads<3>")])
 def test_level_kernels_labels(hip_device, name, level, sweep):
     """mgmc_level_kernels names the sweep each level really runs (bench.py's roofline labels)."""
     shape, kw = CONFIGS[name]
