@@ -162,7 +162,7 @@ def test_mgmc_cycles_bitwise(hip_device, name):
 # where the fast path it turns off would run
 ALL_PATHS = "tail,fuse_prolong,quads,rb2d,zsweep,pairs,zrestrict,lr_small,lr_merge,lr_prefetch,coarse_precompute,jsweep"
 VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_ssor"),
-            ("fuse_prolong", "3d128_zsweep_odd"),
+            ("fuse_prolong", "3d128_zsweep_odd"), ("fuse_prolong", "3d_zres27"), ("fuse_prolong", "3d_jsweep_ssor_W"),
             ("tail", "3d16"), ("tail", "3d64_4lvl"), ("tail", "2d64_template_W"), ("tail", "3d32_W_ssor"),
             ("quads", "3d64_4lvl"), ("quads", "3d_zres27"), ("quads", "2d256_global_coarse"),
             ("quads", "2d_aniso_ssor"),
