@@ -56,7 +56,8 @@ extern "C" {
 
 /* coarse solvers (MultigridParameters::coarse_solver) */
 #define MGMC_COARSE_SSOR 0
-#define MGMC_COARSE_CHOLESKY 1 /* dense Cholesky factors of the coarsest level (cholesky_sampler.hh:50-66) */
+#define MGMC_COARSE_CHOLESKY 1 /* Cholesky factors of the coarsest level (cholesky_sampler.cc:9-41): dense inverses up to
+                                  8192 unknowns, blocked banded solves above (rows of at most 4096 unknowns) */
 
 /* fine-level operators (driver_mgmc.cc:414-425, PriorParameters::pde_model) */
 #define MGMC_OPERATOR_FD 0  /* ShiftedLaplaceFDOperator: 5/7-point (shiftedlaplace_fd_operator.cc:9-57) */
@@ -283,8 +284,10 @@ int mgmc_residual_restrict(mgmc_handle* h, int level, const double* f, const dou
 /* ---- exact-statistics engine (linear_operator.hh:119-174 targets at any lattice size) ----
  * x = Q^{-1} b with the multigrid preconditioner of MultigridPreconditioner
  * (preconditioner/multigrid_preconditioner.cc:74-109): one deterministic cycle of the handle's
- * hierarchy from x = 0 (its smoothers without noise, with the B_bar fix; ncoarsesmooth SSOR sweeps
- * on the coarsest level in place of the reference's Cholesky).  method MGMC_SOLVER_LOOP is the
+ * hierarchy from x = 0 (its smoothers without noise, with the B_bar fix).  The coarsest level is
+ * solved exactly with its Cholesky factors, as the reference's CholeskySolver, when the handle has
+ * them (coarse_solver Cholesky, or a coarsest level of at most 2048 unknowns); otherwise it takes
+ * ncoarsesmooth SSOR sweeps.  method MGMC_SOLVER_LOOP is the
  * reference's LoopSolver (solver/loop_solver.cc:9-53, x -= M(Qx - b)); MGMC_SOLVER_CG wraps the
  * same (symmetric) cycle in conjugate gradients.  Stops when ||r||/||b|| < rtol and ||r|| < atol
  * (the reference's test) or after maxiter iterations; *iters and *rnorm report the outcome.
