@@ -506,13 +506,15 @@ void launch_rb2d(const Level& lv, const double* xin, double* xout, const double*
         hipLaunchKernelGGL((k_rb2d<false>), grid, block, 0, s, lv.L, xin, xout, f, lv.S, g, c1, ntx, cs);
 }
 
-// j-marching half-sweeps (k_jsweep_half): 3D 27-point levels with rows of 128 pairs (nx = 256: level 1 at
-// 512^3), x read about 1.5 times per half instead of once per colour-pair pass.
+// j-marching half-sweeps (k_jsweep_half): 3D 27-point levels with rows of 128 or 256 pairs (nx = 256: level 1
+// at 512^3; nx = 512: the FEM prior's fine level at 512^3), x read about 1.5 times per half instead of once
+// per colour-pair pass (DESIGN.md sections 3a, 3c; 512^3 FEM cycle 4.65 -> 3.76 ms).
 // With 64-pair rows (512^3 level 2, 256^3 level 1) the kernel is slower than the pair passes (2 x 21 against
 // 4 x 8 us per sweep at 127^3, 256^3 cycle 0.484 -> 0.503 ms): those levels are latency-bound, and the
 // march's chunks are short.
 bool jsweep_eligible(const LevelSpec& sp, const Layout& L, uint32_t paths) {
-    return sp.dim == 3 && sp.npoints == 27 && L.nx == 256 && L.ny >= 2 && L.nz >= 2 && !(paths & PATH_NO_JSWEEP);
+    return sp.dim == 3 && sp.npoints == 27 && (L.nx == 256 || L.nx == 512) && L.ny >= 2 && L.nz >= 2 &&
+           !(paths & PATH_NO_JSWEEP);
 }
 
 #ifndef MGMC_JS_ROUNDS  // workgroups per half: this many rounds of the resident slots (timing builds override it)
@@ -547,8 +549,13 @@ void launch_jsweep(const Level& lv, const double* xin, double* xout, const doubl
         a.nchunk = (a.nsteps + a.spc - 1) / a.spc;
         const int nb = (a.nk * a.nchunk + 7) / 8 * 8;
         const dim3 grid(nb, 1, nch), block(2 * np);
-        if (fwd) hipLaunchKernelGGL((k_jsweep_half<128, false>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((k_jsweep_half<128, true>), grid, block, lds, s, a);
+        if (np == 256) {  // FEM prior's 27-point fine level at 512^3
+            if (fwd) hipLaunchKernelGGL((k_jsweep_half<256, false>), grid, block, lds, s, a);
+            else hipLaunchKernelGGL((k_jsweep_half<256, true>), grid, block, lds, s, a);
+        } else {
+            if (fwd) hipLaunchKernelGGL((k_jsweep_half<128, false>), grid, block, lds, s, a);
+            else hipLaunchKernelGGL((k_jsweep_half<128, true>), grid, block, lds, s, a);
+        }
     }
 }
 

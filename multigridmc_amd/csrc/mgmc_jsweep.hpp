@@ -34,7 +34,7 @@
 
 namespace mgmc {
 
-// NP pairs per row (nx = 2 NP; the library runs NP = 128: level 1 at 512^3); 2 NP threads
+// NP pairs per row (nx = 2 NP; the library runs NP = 128, 256: 512^3 level 1, FEM fine level); 2 NP threads
 // (A-row pairs, B-row pairs); ring rows of stride 2 NP + 8: odd pairs [0, NP) and the guard at NP, then
 // the even block from NP + 1: its guard (position 0) first, even pair m at NP + 2 + m
 constexpr int JS_RING = 8;           // rows per plane in the LDS ring

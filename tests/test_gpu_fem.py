@@ -24,6 +24,8 @@ CONFIGS = {
     "3d128_zres": ((128, 128, 128), dict(nlevel=3, omega=1.1)),  # pairs, 27-point z-marching zres
     "3d_aniso": ((64, 32, 48), dict(nlevel=3, smoother="SSOR", coarse_scaling=0.9)),
     "3d32_chol": ((32, 32, 32), dict(nlevel=3, coarse_solver="Cholesky")),
+    # j-marching half-sweeps on the 27-point fine level (256-pair rows) and level 1 (128-pair rows)
+    "3d_jsweep": ((512, 24, 20), dict(nlevel=3, smoother="SSOR")),
 }
 
 
@@ -107,4 +109,12 @@ def test_fem_statistics_vs_exact_covariance(hip_device, shape, kw, nsamples, tol
     scale = np.max(np.abs(Qinv))
     assert np.max(np.abs(ex - mu)) < 2 * tol * scale
     assert np.max(np.abs(cov - Qinv)) < tol * scale
+    s.close()
+
+
+def test_fem_jsweep_kernel_instances(hip_device):
+    """The 27-point fine level of 256-pair rows and its 128-pair level 1 run the j-marching half-sweeps."""
+    s, mc, p, lat = make("3d_jsweep")
+    assert s.level_kernels(0)["sweep"] == "k_jsweep_half<256>"
+    assert s.level_kernels(1)["sweep"] == "k_jsweep_half<128>"
     s.close()
