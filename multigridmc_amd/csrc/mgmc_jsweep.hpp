@@ -1,6 +1,7 @@
-// mgmc_jsweep.hpp -- j-marching half-sweeps of the 8-colour Gibbs sweep of a 3D Galerkin (27-point)
-// level whose rows are 128 pairs long (nx = 256: level 1 of the 512^3 hierarchy): both colour pairs of
-// one k parity in one launch, x read about 1.5 times per half instead of once per colour-pair pass.
+// mgmc_jsweep.hpp -- j-marching half-sweeps of the 8-colour Gibbs sweep of a 3D Galerkin-shaped
+// (27-point) level with rows of NP = 128 or 256 pairs (level 1 of the 512^3 hierarchy; the FEM prior's
+// fine level at 512^3): both colour pairs of one k parity in one launch, x read about 1.5 times per
+// half instead of once per colour-pair pass.
 //
 // A sweep's four colour-pair passes (mgmc_gsweep.hpp: forward (0,1), (2,3) | (4,5), (6,7), backward
 // reversed) come in k-parity halves.  Within a half (own planes k of parity kp), the second pair's rows
@@ -8,16 +9,18 @@
 // is old in the half (rows of their own parity, planes k +- 1 of the other parity).  One workgroup
 // marches a chunk of one own plane in j, two rows per step, pipelined:
 //
-//   step s, a = 2 s + jA:  A-row a       first pair  (threads 0..127: rows a-1, a, a+1, old)
-//                          B-row a - 3   second pair (threads 128..255: rows a-4 and a-2 new, a-3 old)
+//   step s, a = 2 s + jA:  A-row a       first pair  (threads 0..NP-1: rows a-1, a, a+1, old)
+//                          B-row a - 3   second pair (threads NP..2NP-1: rows a-4 and a-2 new, a-3 old)
 //
 // Both rows run in the same two phases (first colour | barrier | second colour with the new values of
 // the first, exchanged through LDS | barrier), one pair per thread, as the pair passes do within a row.
 // The rows a-4 .. a+1 of planes k-1, k, k+1 sit in an 8-row LDS ring (colour-split rows: odd positions,
-// then even ones, zero guards at both ends, so consecutive lanes read consecutive doubles).  The next
-// step's rows a+2, a+3 are written into the ring's free slots at the end of a step; their loads were
-// issued into registers JS_D - 1 steps earlier.  New first-pair values are written into the ring (the second
-// pair and the chunk's later steps read them); every row of the chunk is stored to xout.
+// then even ones, zero guards at both ends, so consecutive lanes read consecutive doubles); each thread
+// reads its pair's 9 x 4 window once per step.  The next step's rows a+2, a+3 are written into the
+// ring's free slots at the end of a step; their loads were issued into registers JS_D - 1 steps
+// earlier.  New first-pair values are written into the ring (the second pair and the chunk's later
+// steps read them); every row of the chunk is stored to xout.  Barriers wait for LDS only (js_barrier),
+// and the Box-Muller tables sit in LDS, so nothing drains the prefetched loads early.
 //
 // Tiles are (own plane, chunk of steps).  A chunk that stores the A-rows of steps [s0, s1) and the
 // B-rows below them runs steps s0 - 1 .. s1: step s0 - 1 recomputes the A-row the chunk's first B-row
@@ -34,8 +37,7 @@
 
 namespace mgmc {
 
-// NP pairs per row (nx = 2 NP; the library runs NP = 128, 256: 512^3 level 1, FEM fine level); 2 NP threads
-// (A-row pairs, B-row pairs); ring rows of stride 2 NP + 8: odd pairs [0, NP) and the guard at NP, then
+// NP pairs per row (nx = 2 NP); 2 NP threads (A-row pairs, B-row pairs); ring rows of stride 2 NP + 8: odd pairs [0, NP) and the guard at NP, then
 // the even block from NP + 1: its guard (position 0) first, even pair m at NP + 2 + m
 constexpr int JS_RING = 8;           // rows per plane in the LDS ring
 #ifndef MGMC_JS_D  // (timing builds override it)
@@ -96,7 +98,7 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
 
     auto slot = [](int j) { return ((j % JS_RING) + JS_RING) % JS_RING; };
     auto rowp = [&](int j, int dz) { return ring + (slot(j) * 3 + dz) * JS_RS; };  // dz: plane index 0..2
-    // staging: thread t moves pair (t & 127) of rows 2 q + (t >> 7), q = 0..2 (6 rows: 2 rows x 3 planes)
+    // staging: thread t moves pair t % NP of item 2 q + t / NP, q = 0..2 (6 items: 2 rows x 3 planes)
     // Loads are unconditional (rows clamped onto the lattice, out-of-range rows zeroed when they are
     // written to the ring): a conditional load merges into its register through a copy, and the copy
     // waits for the load right away
