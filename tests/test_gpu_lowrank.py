@@ -33,6 +33,8 @@ CONFIGS = {
     "2d128_points_tail": ((128, 128), dict(nlevel=5), (0.0, 4, False)),
     # dense-column path on the fine level (> 4096 vertices), the global column as an entry list below
     "2d128_point_global_W": ((128, 128), dict(nlevel=4, cycle=2), (0.0, 4, True)),
+    # j-marching half-sweeps on level 1 (128-pair rows) with the low-rank patch / fix around them
+    "3d_jsweep_points_ssor": ((512, 24, 20), dict(nlevel=3, smoother="SSOR"), (0.0, 5, False)),
 }
 TAIL_CONFIGS = ["2d64_ball_ssor_W", "3d32_points_tail_W", "3d48_ball_tail_ssor", "2d128_points_tail"]
 
