@@ -291,18 +291,24 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     }
 
     // ---- global <-> LDS / registers ----
-    double2 px[NLX];
-    auto issue_x = [&](int k) {
+    // The fused-prolongation sweep (PF2) loads x planes two steps ahead (one register set per plane
+    // parity, chosen at compile time from the step's parity) and f unconditionally (idle waves load a
+    // zero pad pair): its 0.686 -> 0.677 ms (round 3, interleaved A/B).  The plain sweep has no
+    // registers to spare for the second set (it spills at its 80-VGPR budget).
+    constexpr bool PF2 = PROLONG != 0;
+    double2 pxb[PF2 ? 2 : 1][NLX];
+#define ZS_PX(B) pxb[PF2 ? (B) : 0]
+    auto issue_x = [&](int k, auto Bc) {
         const double* base = plane_base(a.xin, k);
 #pragma unroll
-        for (int u = 0; u < NLX; ++u) px[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
+        for (int u = 0; u < NLX; ++u) ZS_PX(decltype(Bc)::value)[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
     };
-    auto deposit_x = [&](int k, auto KO) {
+    auto deposit_x = [&](int k, auto KO, auto Bc) {
         double* dst = xs + slot(k) * PS;
 #pragma unroll
         for (int u = 0; u < NLX; ++u) {
             if (xlds[u] < 0) continue;
-            double2 v = px[u];
+            double2 v = ZS_PX(decltype(Bc)::value)[u];
             if (PROLONG && interior_plane(k)) v = prolong_pair(v, pcro[u] & 1, k, pcro[u] >> 1, KO);
             dst[xlds[u]] = v.x;
             dst[xlds[u] + WP] = v.y;
@@ -310,7 +316,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     };
     // f of the item on plane k: (first-colour element, other element) -- two 8-byte loads at
     // wave-uniform element offsets instead of a pair load and per-lane selects
-    auto load_f = [&](int k) { return *reinterpret_cast<const double2*>(plane_base(a.f, k) + t.goff); };
+    const int foff = PF2 ? (active_wave ? t.goff : L.off + 1) : t.goff;  // (PF2: idle waves load a zero pad pair)
+    auto load_f = [&](int k) { return *reinterpret_cast<const double2*>(plane_base(a.f, k) + foff); };
 
     // fma-chain stencil sum (ascending column order) at LDS offset o of plane k.  The fine FD
     // stencil is symmetric (launch_zsweep checks a[4]=a[22], a[10]=a[16], a[12]=a[14]), so four
@@ -344,6 +351,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     };
     // One z step p (LDS ring = planes p-2 .. p+1):
     //   deposit x(p+1) (into the slot plane p-3 left), issue x(p+2) and f(p+1)   | barrier
+    //   (PF2: issue x(p+3); f(p+2) is issued once this step has used f(p))
     //   first colour on plane p (core + halo ring)                              | barrier
     //   second colour on plane p-1 (core); plane p-1 is final: store it from the new second-colour
     //   values (registers) and the first-colour values (LDS), and keep the latter as the next
@@ -367,13 +375,20 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
             const int e = odd_step ? 1 - E0c_v : E0c_v;  // first-colour element on plane p
             const int o1 = t.lds + e * WP, o2 = t.lds + (1 - e) * WP;
             const bool inf = e ? in1 : in0;  // (compile-time choice)
-            deposit_x(p + 1, std::integral_constant<int, odd_step ? 0 : 1>{});  // p even on even steps
+            // p even on even steps: plane p+1 odd (register set 1), p+3 too
+            using Bp = std::integral_constant<int, odd_step ? 0 : 1>;
+            deposit_x(p + 1, std::integral_constant<int, odd_step ? 0 : 1>{}, Bp{});
             if (PROLONG) {
                 if (odd_step) deposit_c((p + 3) / 2);
                 else issue_c((p + 4) / 2);
             }
-            issue_x(p + 2);
-            if (active_wave) fnxt = load_f(p + 1);
+            if constexpr (PF2) {
+                issue_x(p + 3, Bp{});  // (past the chunk: clamped planes, loaded and never used)
+                (void)fnxt;
+            } else {
+                issue_x(p + 2, Bp{});
+                if (active_wave) fnxt = load_f(p + 1);
+            }
             __syncthreads();
             // first colour on plane p: c = fma(sd, z, f), x = fma(omega/diag, c - S, x); the second
             // colour's right-hand side of the pair, c' = fma(sd, z', f')
@@ -386,6 +401,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
                 }
                 pk_out = fma(sd, e ? z.x : z.y, e ? fcur.x : fcur.y);
             }
+            if constexpr (PF2) fcur = load_f(p + 2);  // this step's f is used up: the registers take f(p+2)
             __syncthreads();
             // second colour on plane k = p-1 (its element is e: the parity flips with the plane)
             const int k = p - 1;
@@ -409,7 +425,12 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         };
         double2 fA = make_double2(0.0, 0.0), fB = make_double2(0.0, 0.0);
         double pkA = 0.0, pkB = 0.0;
-        if (active_wave) fA = load_f(k0 - 1);
+        if constexpr (PF2) {
+            fA = load_f(k0 - 1);
+            fB = load_f(k0);
+        } else if (active_wave) {
+            fA = load_f(k0 - 1);
+        }
         if (active_wave && interior_plane(k0 - 1)) z = noise(k0 - 1);
         for (int p = k0 - 1; p <= k1; p += 2) {
             step(p, std::integral_constant<bool, false>{}, fA, fB, pkB, pkA);
@@ -426,21 +447,27 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         deposit_c((k0 - 1) / 2);
         __syncthreads();
     }
-    issue_x(k0 - 2);
-    deposit_x(k0 - 2, std::integral_constant<int, -1>{});
-    issue_x(k0 - 1);
-    deposit_x(k0 - 1, std::integral_constant<int, -1>{});
+    // (k0 odd: planes k0-2, k0 take register set 1, k0-1, k0+1 set 0)
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    issue_x(k0 - 2, B1{});
+    deposit_x(k0 - 2, std::integral_constant<int, -1>{}, B1{});
+    issue_x(k0 - 1, B0{});
+    deposit_x(k0 - 1, std::integral_constant<int, -1>{}, B0{});
     if (PROLONG) {
         __syncthreads();
         issue_c((k0 + 1) / 2);
         deposit_c((k0 + 1) / 2);
         __syncthreads();
     }
-    issue_x(k0);
+    issue_x(k0, B1{});
+    if constexpr (PF2) issue_x(k0 + 1, B0{});
     if (PROLONG) run(RunE0{E0});
     else if (E0) run(std::integral_constant<int, 1>{});  // wave-uniform branch
     else run(std::integral_constant<int, 0>{});
 }
+
+#undef ZS_PX
 
 inline size_t zsweep_lds_bytes(int XP, int TY, bool prolong) {
     const int RS = 2 * (XP + 2) + 2, R = TY + 4;
