@@ -1710,6 +1710,14 @@ int build_coarse_chol(mgmc_handle* h, const std::vector<LRColumn>* cols, const d
                         std::to_string(bw));
     if (!blocked && n > CHOL_MAX_N)
         return fail(h, MGMC_E_UNSUPPORTED, "coarse Cholesky: too many unknowns");
+    // the banded host factor costs n bw^2 / 2 multiply-adds: refuse what would take more than a few
+    // minutes on one core (3D 128^3 nlevel 2: 63^3 unknowns, bandwidth 4033 -- a fill-reducing sparse
+    // factorisation, the reference's CHOLMOD, is the tool for such levels)
+    if (blocked && (double)n * (double)bw * (double)bw > CHOL_HOST_WORK_MAX)
+        return fail(h, MGMC_E_UNSUPPORTED,
+                    "coarse Cholesky: " + std::to_string(n) + " unknowns of bandwidth " + std::to_string(bw) +
+                        " exceed the banded factor's host work limit (n bw^2 <= " +
+                        std::to_string((long long)CHOL_HOST_WORK_MAX) + "); use more levels");
     const long long W = bw + 1;
     std::vector<double> band((size_t)(n * W), 0.0);
     for_each_entry([&](long long r, long long c, double v) {

@@ -90,6 +90,7 @@ __global__ void __launch_bounds__(256) k_coarse_chol(CholArgs a) {
 //   Cf[k][j][r] = C_k(r, j)   Cb[k][j][r] = C_k(j, r)   Df[k][j][r] = D_k(r, j)   Db[k][j][r] = D_k(j, r)
 // Work per solve O(n B) sequential in B-row steps: latency-bound, as the reference's two solves.
 constexpr int CHOL_BLOCK_MAX = 4096;  // 2 B doubles of LDS (64 KB), <= 4 rows per thread
+constexpr double CHOL_HOST_WORK_MAX = 1e11;  // n bw^2 of the banded host factor (about a minute)
 
 struct CholBlockArgs {
     Layout L;

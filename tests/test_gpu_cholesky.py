@@ -99,7 +99,8 @@ def test_blocked_coarse_cholesky_batched_chains(hip_device):
 def test_dense_lowrank_column_band_unsupported(hip_device):
     """A global-average measurement couples every coarse unknown: a bandwidth of n - 1 has no blocked
     factor above 8,192 unknowns (MGMC_E_UNSUPPORTED naming the bandwidth), nor has a lattice whose
-    rows are longer than 4,096."""
+    rows are longer than 4,096; a 3D level whose banded factor would take the host hours is refused
+    too."""
     op, lat = LR.measured((256, 256), 25.0, 0.0, 2, True)
     p = mg.MultigridParameters(nlevel=2, coarse_solver="Cholesky")
     s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), SEED, p)
@@ -109,6 +110,8 @@ def test_dense_lowrank_column_band_unsupported(hip_device):
     s.close()
     with pytest.raises(mg.MgmcError, match="bandwidth"):  # lexicographic band of 8191 unknowns
         _make((8192, 8), dict(nlevel=1))
+    with pytest.raises(mg.MgmcError, match="host work limit"):  # 63^3 unknowns, bandwidth 4033
+        _make((128, 128, 128), dict(nlevel=2))
 
 
 @pytest.mark.parametrize("shape,nlevel,tol", [((16, 16), 1, 0.04), ((32, 32), 2, 0.05)])
