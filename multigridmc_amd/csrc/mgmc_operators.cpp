@@ -222,22 +222,47 @@ CsrHost assemble_fem(const mgmc_operator_desc& d, const Lat& L) {
     return A;
 }
 
-// SquaredShiftedLaplaceFDOperator, 2D (squared_shiftedlaplace_fd_operator.cc:9-96): the 13-point
-// diamond of (kappa^2 - Laplace)^2 with homogeneous Neumann corrections on the diagonal
+// SquaredShiftedLaplaceFDOperator, 2D (squared_shiftedlaplace_fd_operator.cc:9-96): the row of
+// (kappa^2 - Laplace)^2 at a vertex is the 13-point diamond of the squared 5-point Laplacian (weights
+// `bilap` by |offset|) plus -2 kappa^2 times the Laplacian on the 4 axis neighbours; an axis neighbour
+// outside the domain folds the point mirrored two steps beyond it back onto the centre (homogeneous
+// Neumann).  Entries in the assembly order of the reference (x offset outer, y inner, ascending),
+// each with its expression order, so the CSR is bit for bit the reference's (tests/test_varcoef.py).
+struct DiamondPoint {
+    int dx, dy;
+    bool axis;     // |dx| + |dy| == 1
+    double bilap;  // squared-Laplacian weight of the offset
+    double lap;    // Laplacian weight (axis neighbours)
+    double fold;   // Neumann fold-back weight onto the centre (axis neighbours)
+};
+
 CsrHost assemble_squared_fd(const mgmc_operator_desc& d, const Lat& L) {
     double h[3], hinv2[3], cv;
     spacing(L, h, hinv2, &cv);
-    double sl[2][2] = {{0, 0}, {0, 0}};
-    sl[0][0] = -2 * (hinv2[0] + hinv2[1]);
-    sl[1][0] = hinv2[0];
-    sl[0][1] = hinv2[1];
-    double ss[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-    ss[0][0] = 6 * (hinv2[0] * hinv2[0] + hinv2[1] * hinv2[1]) + 8 * hinv2[0] * hinv2[1];
-    ss[1][0] = -4 * hinv2[0] * (hinv2[0] + hinv2[1]);
-    ss[0][1] = -4 * hinv2[1] * (hinv2[0] + hinv2[1]);
-    ss[2][0] = hinv2[0] * hinv2[0];
-    ss[0][2] = hinv2[1] * hinv2[1];
-    ss[1][1] = 2 * hinv2[0] * hinv2[1];
+    const double gx = hinv2[0], gy = hinv2[1];
+    // squared-Laplacian weights by (|dx|, |dy|) and the Laplacian's centre
+    auto bilap = [&](int ax, int ay) -> double {
+        if (ax == 0 && ay == 0) return 6 * (gx * gx + gy * gy) + 8 * gx * gy;
+        if (ax == 1 && ay == 0) return -4 * gx * (gx + gy);
+        if (ax == 0 && ay == 1) return -4 * gy * (gx + gy);
+        if (ax == 2 && ay == 0) return gx * gx;
+        if (ax == 0 && ay == 2) return gy * gy;
+        if (ax == 1 && ay == 1) return 2 * gx * gy;
+        return 0.0;
+    };
+    const double lap_centre = -2 * (gx + gy);
+    std::vector<DiamondPoint> pts;
+    for (int dx = -2; dx <= 2; ++dx)
+        for (int dy = -2; dy <= 2; ++dy) {
+            const int ax = abs(dx), ay = abs(dy);
+            if (ax + ay > 2 || ax + ay == 0) continue;
+            DiamondPoint q{dx, dy, ax + ay == 1, bilap(ax, ay), 0.0, 0.0};
+            if (q.axis) {
+                q.lap = ax ? gx : gy;
+                q.fold = bilap(2 * ax, 2 * ay);
+            }
+            pts.push_back(q);
+        }
     CsrHost A;
     A.nrow = L.nvertex();
     A.rowptr.push_back(0);
@@ -245,23 +270,21 @@ CsrHost assemble_squared_fd(const mgmc_operator_desc& d, const Lat& L) {
     for (int64_t ell = 0; ell < A.nrow; ++ell) {
         double x[3];
         vertex_coordinates(L, ell, h, x);
-        const double alpha_b = kappa_sq_at(d, x);
-        double diagonal = (alpha_b * alpha_b - 2. * alpha_b * sl[0][0] + ss[0][0]) * cv;
+        const double k2 = kappa_sq_at(d, x);
+        double centre = (k2 * k2 - 2. * k2 * lap_centre + bilap(0, 0)) * cv;
         int idx[3];
         L.lin2euc(ell, idx);
-        for (int j = -2; j <= 2; ++j)
-            for (int k = -2; k <= 2; ++k) {
-                if ((abs(j) + abs(k) > 2) || (j == 0 && k == 0)) continue;
-                const int s[3] = {idx[0] + j, idx[1] + k, 0};
-                if (L.interior(s)) {
-                    double e = ss[abs(j)][abs(k)];
-                    if (abs(j) + abs(k) == 1) e += -2. * alpha_b * sl[abs(j)][abs(k)];
-                    rb.add(L.euc2lin(s), e * cv);
-                } else if (abs(j) + abs(k) == 1) {
-                    diagonal += ss[2 * abs(j)][2 * abs(k)] * cv;
-                }
+        for (const DiamondPoint& q : pts) {
+            const int nb[3] = {idx[0] + q.dx, idx[1] + q.dy, 0};
+            if (L.interior(nb)) {
+                double w = q.bilap;
+                if (q.axis) w += -2. * k2 * q.lap;
+                rb.add(L.euc2lin(nb), w * cv);
+            } else if (q.axis) {
+                centre += q.fold * cv;
             }
-        rb.add(ell, diagonal);
+        }
+        rb.add(ell, centre);
         rb.flush(A);
     }
     return A;
@@ -395,13 +418,15 @@ std::string validate_operator(const mgmc_operator_desc& d) {
 double kappa_sq_at(const mgmc_operator_desc& d, const double* x) {
     if (d.kappa_model == MGMC_KAPPA_CONSTANT) return 1. / pow(d.Lambda, 2);  // correlationlength_model.hh:52
     if (d.kappa_model == MGMC_KAPPA_GIVEN) return d.kappa_sq;
-    // PeriodicCorrelationLengthModel (correlationlength_model.hh:90-104)
-    const double Lambda_1 = 0.5 * (d.Lambda_max + d.Lambda_min);
-    const double Lambda_2 = 0.5 * (d.Lambda_max - d.Lambda_min);
-    double Lambda_ = Lambda_2;
-    for (int q = 0; q < d.dim; ++q) Lambda_ *= cos(M_PI * x[q]);
-    Lambda_ += Lambda_1;
-    return 1. / (Lambda_ * Lambda_);
+    // PeriodicCorrelationLengthModel (correlationlength_model.hh:90-104): the correlation length
+    // oscillates around the middle of [Lambda_min, Lambda_max] with half its width as amplitude,
+    // ell(x) = mid + amp prod_d cos(pi x_d), and kappa^2 = ell^-2 (the reference's operation order)
+    const double mid = 0.5 * (d.Lambda_max + d.Lambda_min);
+    const double amp = 0.5 * (d.Lambda_max - d.Lambda_min);
+    double ell = amp;
+    for (int axis = 0; axis < d.dim; ++axis) ell *= cos(M_PI * x[axis]);
+    ell += mid;
+    return 1. / (ell * ell);
 }
 
 CsrHost assemble_operator(const mgmc_operator_desc& d) {
