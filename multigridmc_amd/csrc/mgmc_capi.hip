@@ -30,6 +30,7 @@ static_assert(MGMC_LAYOUT_POINT == mgmc::LF_POINT && MGMC_LAYOUT_PAIRS == mgmc::
 #include "mgmc_zrestrict.hpp"
 #include "mgmc_tail.hpp"
 #include "mgmc_gsweep.hpp"
+#include "mgmc_qrestrict.hpp"
 #include "mgmc_jsweep.hpp"
 #include "mgmc_rb2d.hpp"
 #include "mgmc_lowrank.hpp"
@@ -58,7 +59,9 @@ enum OpKind {
     OP_QOI = 4,
     OP_COPY = 5,
     OP_COARSE_CHOL = 6,
-    OP_TAIL = 7      // the sub-cycle of the coarsest levels in one workgroup (mgmc_tail.hpp)
+    OP_TAIL = 7,     // the sub-cycle of the coarsest levels in one workgroup (mgmc_tail.hpp)
+    OP_SWEEP_RESTRICT = 8,  // 2D Galerkin level: last pre-sweep + residual + restriction (mgmc_qrestrict.hpp)
+    OP_PROLONG_SWEEP = 9    // 2D Galerkin level: prolongate-add + first post-sweep (mgmc_qrestrict.hpp)
 };
 
 struct Op {
@@ -77,7 +80,6 @@ struct Op {
     int lr_coarse_patch = 0;  // OP_RESIDUAL_RESTRICT: ... and the coarse level's first pre-sweep
     uint32_t lr_coarse_tag = 0;
     int tail = -1;           // OP_TAIL: index into mgmc_handle::tail_args
-                             // OP_RESIDUAL_RESTRICT: done by the previous sweep (no launch)
 };
 
 
@@ -100,6 +102,8 @@ enum PathFlag : uint32_t {
     PATH_NO_LR_DENSE = 1u << 11,          // dense low-rank column: the row lists over every vertex
     PATH_NO_CHOL_DENSE = 1u << 12,        // coarse Cholesky: the blocked banded solves at any size
     PATH_NO_JSWEEP = 1u << 13,            // 3D Galerkin levels of 64 / 128 pairs: colour-pair passes, not j-marching halves
+    PATH_NO_QRESTRICT = 1u << 14,         // 2D Galerkin levels: last pre-sweep and residual + restriction as two launches
+    PATH_NO_QPROLONG = 1u << 15,          // 2D Galerkin levels: prolongate-add and first post-sweep as two launches
 };
 
 struct PathToken {
@@ -114,6 +118,7 @@ constexpr PathToken kPathTokens[] = {
     {"lr_merge", PATH_NO_LR_MERGE},   {"lr_prefetch", PATH_NO_LR_PREFETCH},
     {"coarse_precompute", PATH_NO_COARSE_PRECOMPUTE}, {"lr_dense", PATH_NO_LR_DENSE},
     {"chol_dense", PATH_NO_CHOL_DENSE}, {"jsweep", PATH_NO_JSWEEP},
+    {"qrestrict", PATH_NO_QRESTRICT}, {"qprolong", PATH_NO_QPROLONG},
 };
 
 // parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
@@ -763,6 +768,87 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
         hipLaunchKernelGGL((k_residual_restrict<2, 9>), grid, block, 0, s, lf.L, lc.L, x, f, fc, xc, lf.S, zero_xc);
 }
 
+// 2D Galerkin level: its last pre-sweep and the residual + restriction onto lc in one launch
+// (mgmc_qrestrict.hpp).  One pair item per thread per colour phase: NT >= (CJ + 3) nx / 2 with CJ
+// coarse rows per workgroup, CJ as small as the thread count allows (the most workgroups: these levels
+// are launch-bound, the recomputed edge rows cost little)
+int qrestrict_threads(int npair) {
+    const int nt = 4 * npair <= 256 ? 256 : (4 * npair <= 512 ? 512 : 1024);
+    return 4 * npair <= nt ? nt : 0;
+}
+
+bool qrestrict_ok(const mgmc_handle* h, int level);
+
+// k_prolong_quads2d: NT >= (CJ + 2) nx / 2
+int qprolong_threads(int npair) {
+    for (int nt = 256; nt <= 1024; nt += 256)
+        if (3 * npair <= nt) return nt;
+    return 0;
+}
+
+void launch_qprolong(const Level& lv, const Level& lc, const double* xin, double* xout, const double* f,
+                     const double* xc, double alpha, const GibbsArg& g, int direction, hipStream_t s, int nch = 1) {
+    QProlongArgs a;
+    a.L = lv.L;
+    a.Lc = lc.L;
+    a.xin = xin;
+    a.xout = xout;
+    a.f = f;
+    a.xc = xc;
+    a.alpha = alpha;
+    a.S = lv.S;
+    a.G = g;
+    a.cs = lv.L.nstore;
+    a.csc = lc.L.nstore;
+    const int npair = lv.L.nx / 2;
+    const int nt = qprolong_threads(npair);
+    a.CJ = nt / npair - 2;
+    const dim3 grid((lc.L.ny - 1 + a.CJ - 1) / a.CJ, 1, nch);
+    const size_t lds = qprolong_lds_bytes(lv.L.nx, a.CJ);
+    const bool fwd = direction == MGMC_FORWARD;
+#define MGMC_QP_LAUNCH(NT)                                                                               \
+    do {                                                                                                   \
+        if (fwd) hipLaunchKernelGGL((k_prolong_quads2d<NT, false>), grid, dim3(NT), lds, s, a);            \
+        else hipLaunchKernelGGL((k_prolong_quads2d<NT, true>), grid, dim3(NT), lds, s, a);                 \
+    } while (0)
+    if (nt == 256) MGMC_QP_LAUNCH(256);
+    else if (nt == 512) MGMC_QP_LAUNCH(512);
+    else if (nt == 768) MGMC_QP_LAUNCH(768);
+    else MGMC_QP_LAUNCH(1024);
+#undef MGMC_QP_LAUNCH
+}
+
+void launch_qrestrict(const Level& lv, const Level& lc, const double* xin, double* xout, const double* f, double* fc,
+                      double* xc, const GibbsArg& g, int direction, hipStream_t s, int nch = 1) {
+    QRestrictArgs a;
+    a.L = lv.L;
+    a.Lc = lc.L;
+    a.xin = xin;
+    a.xout = xout;
+    a.f = f;
+    a.fc = fc;
+    a.xc = xc;
+    a.S = lv.S;
+    a.G = g;
+    a.cs = lv.L.nstore;
+    a.csc = lc.L.nstore;
+    const int npair = lv.L.nx / 2;
+    const int nt = qrestrict_threads(npair);
+    a.CJ = nt / npair - 3;
+    const dim3 grid((lc.L.ny - 1 + a.CJ - 1) / a.CJ, 1, nch);
+    const size_t lds = qrestrict_lds_bytes(lv.L.nx, a.CJ);
+    const bool fwd = direction == MGMC_FORWARD;
+#define MGMC_QR_LAUNCH(NT)                                                                               \
+    do {                                                                                                   \
+        if (fwd) hipLaunchKernelGGL((k_quads_restrict2d<NT, false>), grid, dim3(NT), lds, s, a);           \
+        else hipLaunchKernelGGL((k_quads_restrict2d<NT, true>), grid, dim3(NT), lds, s, a);                \
+    } while (0)
+    if (nt == 256) MGMC_QR_LAUNCH(256);
+    else if (nt == 512) MGMC_QR_LAUNCH(512);
+    else MGMC_QR_LAUNCH(1024);
+#undef MGMC_QR_LAUNCH
+}
+
 void launch_prolongate(const Level& lf, const Level& lc, double* x, const double* xc, double alpha, hipStream_t s,
                        int nch = 1) {
     dim3 block(64, 4, 1);
@@ -1301,7 +1387,7 @@ void free_tails(mgmc_handle* h) {
 }
 
 // replace every maximal run of ops on levels >= lt (one call of build_ops_level(lt)) by one OP_TAIL
-int build_tails(mgmc_handle* h) {
+int build_tails_only(mgmc_handle* h) {
     free_tails(h);
     const int lt = tail_level(h);
     if (lt < 0) return MGMC_OK;
@@ -1413,6 +1499,86 @@ int build_tails(mgmc_handle* h) {
     return MGMC_OK;
 }
 
+// a level whose last pre-sweep and residual + restriction can run as one k_quads_restrict2d launch:
+// 2D 9-point Galerkin level swept by quad passes (out of place), no low-rank part, not the coarsest,
+// rows of at most 256 pairs (one pair item per thread of a 1024-thread workgroup)
+bool qrestrict_ok(const mgmc_handle* h, int level) {
+    if (h->paths & PATH_NO_QRESTRICT) return false;
+    if (level < 1 || level + 1 >= (int)h->levels.size()) return false;
+    const Level& lv = h->levels[level];
+    if (lv.spec.dim != 2 || lv.spec.npoints != 9 || !lv.quads || lv.jsweep || lv.field || lv.lr.m > 0 ||
+        !lv.pingpong())
+        return false;
+    if (qrestrict_threads(lv.L.nx / 2) == 0) return false;
+    const int CJ = qrestrict_threads(lv.L.nx / 2) / (lv.L.nx / 2) - 3;
+    return qrestrict_lds_bytes(lv.L.nx, CJ) <= 150 * 1024;
+}
+
+// the same for the prolongate-add and the first post-sweep (k_prolong_quads2d)
+bool qprolong_ok(const mgmc_handle* h, int level) {
+    if (h->paths & PATH_NO_QPROLONG) return false;
+    if (level < 1 || level + 1 >= (int)h->levels.size()) return false;
+    const Level& lv = h->levels[level];
+    if (lv.spec.dim != 2 || lv.spec.npoints != 9 || !lv.quads || lv.jsweep || lv.field || lv.lr.m > 0 ||
+        !lv.pingpong())
+        return false;
+    const int nt = qprolong_threads(lv.L.nx / 2);
+    return nt > 0 && qprolong_lds_bytes(lv.L.nx, nt / (lv.L.nx / 2) - 2) <= 150 * 1024;
+}
+
+// fuse every (sweep, residual + restriction) pair of ops on a qrestrict_ok level into one
+// OP_SWEEP_RESTRICT (the restriction reads the buffer the sweep writes), and every (prolongate-add,
+// sweep) pair on a qprolong_ok level into one OP_PROLONG_SWEEP (the sweep reads the buffer the
+// prolongation updates in place; the fused kernel leaves that buffer as it was, and nothing reads it
+// before the sweep's output replaces it); the fine level (level 0) keeps its ops, so the timed
+// fine-sweep segments are unchanged
+void fuse_sweep_restrict(mgmc_handle* h) {
+    std::vector<Op> out;
+    std::vector<size_t> removed;  // original indices of the dropped restriction ops
+    for (size_t q = 0; q < h->ops.size(); ++q) {
+        const Op& op = h->ops[q];
+        if (op.kind == OP_PROLONGATE && q + 1 < h->ops.size() && qprolong_ok(h, op.level)) {
+            const Op& nx = h->ops[q + 1];
+            if (nx.kind == OP_SWEEP && nx.level == op.level && nx.src == op.src && !nx.prolong) {
+                Op f = nx;
+                f.kind = OP_PROLONG_SWEEP;
+                out.push_back(f);
+                removed.push_back(q);
+                ++q;
+                continue;
+            }
+        }
+        if (op.kind == OP_SWEEP && q + 1 < h->ops.size() && qrestrict_ok(h, op.level) && !op.prolong) {
+            const Op& nx = h->ops[q + 1];
+            if (nx.kind == OP_RESIDUAL_RESTRICT && nx.level == op.level && nx.src == 1 - op.src) {
+                Op f = op;
+                f.kind = OP_SWEEP_RESTRICT;
+                out.push_back(f);
+                removed.push_back(q + 1);
+                ++q;
+                continue;
+            }
+        }
+        out.push_back(op);
+    }
+    auto shift = [&](size_t& seg) {
+        size_t d = 0;
+        for (size_t r : removed)
+            if (r < seg) ++d;
+        seg -= d;
+    };
+    shift(h->seg_end_pre);
+    shift(h->seg_begin_post);
+    shift(h->seg_end_post);
+    h->ops.swap(out);
+}
+
+int build_tails(mgmc_handle* h) {
+    const int rc = build_tails_only(h);
+    if (rc == MGMC_OK) fuse_sweep_restrict(h);
+    return rc;
+}
+
 void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
     const uint64_t* sample = h->ctrl;  // ctrl[0]
     const int nch = h->nchains;        // batched chains: every launch covers all of them
@@ -1447,6 +1613,19 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                     lr_small(h, lv, xo, op.direction, op.lr_next, op.lr_next_tag, sample, s, nch);
                 else if (lr)
                     lr_fix(lv, xo, op.direction, lv.lr.dense_path ? nullptr : lv.f, s, nch);
+                break;
+            }
+            case OP_SWEEP_RESTRICT: {  // (2D Galerkin level, no low-rank part: qrestrict_ok)
+                GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
+                Level& lc = h->levels[op.level + 1];
+                launch_qrestrict(lv, lc, lv.buf(op.src), lv.buf(1 - op.src), lv.f, lc.f, lc.x, g, op.direction, s, nch);
+                break;
+            }
+            case OP_PROLONG_SWEEP: {  // (2D Galerkin level, no low-rank part: qprolong_ok)
+                GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
+                Level& lc = h->levels[op.level + 1];
+                launch_qprolong(lv, lc, lv.buf(op.src), lv.buf(1 - op.src), lv.f, lc.x, h->cfg.coarse_scaling, g,
+                                op.direction, s, nch);
                 break;
             }
             case OP_COARSE_CHOL: {
@@ -2334,8 +2513,13 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
             const bool wide = np == 7 && cx == 64 &&
                               (long long)((lc.L.nx + 62) / 64) * ((lc.L.ny + 6) / 8) * (lc.L.nz - 1) >= 16 * 1024;
             res = "k_zresrestrict<" + std::to_string(np) + "," + std::to_string(cx) + "," + (wide ? "8" : "4") + ">";
+        } else if (qrestrict_ok(h, level)) {
+            sweep = "k_sweep_quads<2> (last pre-sweep: k_quads_restrict2d)";
+            res = "k_quads_restrict2d";
+
         } else res = "k_residual_restrict<" + std::to_string(dim) + "," + std::to_string(np) + ">";
     }
+    if (qprolong_ok(h, level)) post = "k_prolong_quads2d";  // (first post-sweep with the prolongation)
     std::string text = "sweep=" + sweep;
     if (!post.empty()) text += ";post_sweep=" + post;
     if (!res.empty()) text += ";residual_restrict=" + res;

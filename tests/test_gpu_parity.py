@@ -69,6 +69,14 @@ CONFIGS = {
     "2d64_chol_W": ((64, 64), dict(nlevel=4, cycle=2, coarse_solver="Cholesky")),
     "3d32_chol_ssor": ((32, 32, 32), dict(nlevel=3, smoother="SSOR", coarse_solver="Cholesky")),
     "3d128_zsweep_chol": ((128, 128, 128), dict(nlevel=5, coarse_solver="Cholesky")),
+    # 2D Galerkin levels' last pre-sweep + residual + restriction in one launch (k_quads_restrict2d):
+    # 255^2 (1024-thread workgroups... 128 pairs: 512) and 127^2 levels, one coarse row per workgroup
+    "2d512_qrestrict": ((512, 512), dict(nlevel=4)),
+    # ... backward last pre-sweep (SSOR), two pre-sweeps, W-cycle, non-square (64-pair rows)
+    "2d_qr_aniso_ssor_W": ((256, 128), dict(nlevel=3, cycle=2, smoother="SSOR", npresmooth=2, omega=1.1)),
+    # ... 32-pair rows: 5 coarse rows per workgroup, the last workgroup partial (23 coarse rows); the
+    # level sits in k_tail unless MGMC_DISABLE=tail (variant below)
+    "2d_qr_cj5": ((128, 96), dict(nlevel=3, ncoarsesmooth=2)),
 }
 
 
@@ -160,7 +168,8 @@ def test_mgmc_cycles_bitwise(hip_device, name):
 
 # every MGMC_DISABLE token of mgmc_capi.hip (PathFlag), alone and all together, on configurations
 # where the fast path it turns off would run
-ALL_PATHS = "tail,fuse_prolong,quads,rb2d,zsweep,pairs,zrestrict,lr_small,lr_merge,lr_prefetch,coarse_precompute,jsweep"
+ALL_PATHS = ("tail,fuse_prolong,quads,rb2d,zsweep,pairs,zrestrict,lr_small,lr_merge,lr_prefetch,coarse_precompute,jsweep,"
+             "qrestrict,qprolong")
 VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_ssor"),
             ("fuse_prolong", "3d128_zsweep_odd"), ("fuse_prolong", "3d_zres27"), ("fuse_prolong", "3d_jsweep_ssor_W"),
             ("tail", "3d16"), ("tail", "3d64_4lvl"), ("tail", "2d64_template_W"), ("tail", "3d32_W_ssor"),
@@ -175,7 +184,11 @@ VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_
             (ALL_PATHS, "3d128_zsweep"), (ALL_PATHS, "3d_aniso_zsweep_ssor"), (ALL_PATHS, "2d64_template_W"),
             (ALL_PATHS, "2d_aniso_ssor"), (ALL_PATHS, "3d_zres27"),
             ("chol_dense", "2d64_chol_W"), ("chol_dense", "3d32_chol_ssor"), ("chol_dense", "3d128_zsweep_chol"),
-            ("jsweep", "3d_zres27"), ("jsweep", "3d_jsweep_ssor_W")]
+            ("jsweep", "3d_zres27"), ("jsweep", "3d_jsweep_ssor_W"),
+            ("qrestrict", "2d512_qrestrict"), ("qrestrict", "2d_qr_aniso_ssor_W"), ("tail", "2d_qr_cj5"),
+            ("tail,qrestrict", "2d_qr_cj5"), (ALL_PATHS, "2d512_qrestrict"),
+            ("qprolong", "2d512_qrestrict"), ("qprolong", "2d_qr_aniso_ssor_W"), ("tail,qprolong", "2d_qr_cj5"),
+            ("qrestrict,qprolong", "2d_qr_aniso_ssor_W")]
 
 
 @pytest.mark.parametrize("paths,name", VARIANTS)
@@ -186,6 +199,9 @@ def test_variant_cycles_bitwise(hip_device, monkeypatch, paths, name):
     colour pair per launch; rb2d / zsweep = the 2D / 3D fine level in colour passes; pairs = one
     colour per pass on Galerkin levels; jsweep = colour-pair passes instead of the j-marching half-sweeps
     on 3D Galerkin levels of 64 / 128 pairs per row; zrestrict = the per-point residual + restriction;
+    qrestrict = a 2D Galerkin level's last pre-sweep and its residual + restriction as two launches
+    instead of one k_quads_restrict2d; qprolong = its prolongate-add and first post-sweep as two
+    launches instead of one k_prolong_quads2d;
     coarse_precompute = the coarse SSOR sampler's right-hand sides inside its colour passes;
     chol_dense = the coarse Cholesky's blocked banded solves on a small coarsest level (the oracle's
     blocked mode).  Every combination gives the oracle's cycle exactly."""
@@ -243,6 +259,21 @@ def test_level_kernels_labels(hip_device, name, level, sweep):
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)
     assert s.level_kernels(level)["sweep"].startswith(sweep)
+    s.close()
+
+
+@pytest.mark.parametrize("name,levels", [("2d512_qrestrict", (1, 2)), ("2d_qr_aniso_ssor_W", (1,))])
+def test_qrestrict_labels(hip_device, name, levels):
+    """2D Galerkin levels outside k_tail run their last pre-sweep and residual + restriction as one
+    k_quads_restrict2d launch, and their prolongate-add and first post-sweep as one k_prolong_quads2d
+    launch (mgmc_qrestrict.hpp); MGMC_DISABLE=qrestrict / qprolong are covered above."""
+    shape, kw = CONFIGS[name]
+    s, p, lat = make(shape, **kw)
+    for level in levels:
+        k = s.level_kernels(level)
+        assert k["residual_restrict"] == "k_quads_restrict2d"
+        assert k["post_sweep"] == "k_prolong_quads2d"
+    assert s.level_kernels(0)["residual_restrict"].startswith("k_residual_restrict<2")
     s.close()
 
 
