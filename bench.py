@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -65,9 +66,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--plain", action="store_true", help="time the single-graph loop instead of the segmented one")
-    ap.add_argument("--timing-stride", type=int, default=4,
+    ap.add_argument("--timing-stride", type=int, default=0,
                     help="time the fine-sweep segments (HIP event nodes) of every N-th cycle of the timed loop; the "
-                         "other cycles replay the plain graph (event nodes cost ~5 us each)")
+                         "other cycles replay the plain graph.  0 (default): N = max(4, ceil(10 ms / cycle)), the "
+                         "cycle estimated from the warm-up, so the event nodes (about 0.05-0.1 ms per timed cycle) "
+                         "stay near 1% of the loop: 4 at 512^3, 21 at 256^3, ~100 for the 2D 1024^2 cycle")
     ap.add_argument("--posterior", type=int, default=0, metavar="M",
                     help="BASELINE config 5: posterior operator with M point measurements (default lattice 256^3, "
                          "6 levels); not the headline line")
@@ -255,7 +258,18 @@ def main():
         sys.exit(2)
 
     # warmup (prior: f = 0, x0 = 0 -- driver_mgmc.cc:61-69 with mean_x_exact = xbar = 0)
-    sampler.sample(args.warmup, qoi)
+    if args.warmup // 2 > 0:
+        sampler.sample(args.warmup // 2, qoi)
+    stride = args.timing_stride
+    if args.warmup - args.warmup // 2 > 0:  # the second half of the warm-up estimates the cycle time
+        tw = time.perf_counter()
+        sampler.sample(args.warmup - args.warmup // 2, qoi)
+        sampler.synchronize()
+        est_ms = (time.perf_counter() - tw) * 1e3 / (args.warmup - args.warmup // 2)
+    else:
+        est_ms = 1.0
+    if stride <= 0:
+        stride = max(4, int(math.ceil(10.0 / max(est_ms, 1e-3))))
     sampler.reset_moments()
     coll.barrier()  # barrier + device synchronisation
     t0 = time.perf_counter()
@@ -264,7 +278,7 @@ def main():
         sampler.synchronize()
         timed = None
     else:
-        timed = sampler.sample_timed(args.steps, qoi, stride=args.timing_stride)
+        timed = sampler.sample_timed(args.steps, qoi, stride=stride)
     sampler.synchronize()
     t1 = time.perf_counter()
     coll.barrier()
@@ -282,11 +296,11 @@ def main():
             tr_pre, prov = stored_traffic(args.traffic_file, n, "pre_sweep") if plain3d else (None, None)
             tr_post, prov2 = stored_traffic(args.traffic_file, n, "post_sweep") if plain3d else (None, None)
             kern = sampler.level_kernels(0)  # the kernels level 0 really runs on (mgmc_level_kernels)
+            n1 = mg.Lattice(*((n // 2,) * args.dim)).Nvertex
             pre = sweep_roofline(timed["pre_ms"], timed["npre"], 24.0 * n0 * K, tr_pre if K == 1 else None, prov,
                                  f"fine pre-sweep {kern['sweep']} (one Gibbs sweep of level 0)")
             per_kernel["pre_sweep"] = pre
             if timed["npost"] > 0:
-                n1 = mg.Lattice(*((n // 2,) * args.dim)).Nvertex
                 fused = "post_sweep" in kern
                 post = sweep_roofline(timed["post_ms"], timed["npost"], (24.0 * n0 + (8.0 * n1 if fused else 0.0)) * K,
                                       tr_post if K == 1 else None, prov2,
@@ -339,7 +353,8 @@ def main():
         if timed:
             line["segments_ms_per_step"] = {"pre": round(timed["pre_ms"] / args.steps, 4),
                                             "post": round(timed["post_ms"] / args.steps, 4),
-                                            "total": round(timed["total_ms"] / args.steps, 4)}
+                                            "total": round(timed["total_ms"] / args.steps, 4),
+                                            "timing_stride": stride, "timed_pre_sweeps": timed["npre"]}
         if args.dim == 2:
             line["metric"] = "MGMC V-cycle samples/sec, 2D (BASELINE config 2)"
         if args.posterior:

@@ -1530,8 +1530,9 @@ bool qprolong_ok(const mgmc_handle* h, int level) {
 // OP_SWEEP_RESTRICT (the restriction reads the buffer the sweep writes), and every (prolongate-add,
 // sweep) pair on a qprolong_ok level into one OP_PROLONG_SWEEP (the sweep reads the buffer the
 // prolongation updates in place; the fused kernel leaves that buffer as it was, and nothing reads it
-// before the sweep's output replaces it); the fine level (level 0) keeps its ops, so the timed
-// fine-sweep segments are unchanged
+// before the sweep's output replaces it).  The fine level (level 0) keeps its ops, so the timed
+// fine-sweep segments are unchanged (the same fusions around the 2D fine level's k_rb2d were built,
+// bitwise, and measured slower: DESIGN.md section 3)
 void fuse_sweep_restrict(mgmc_handle* h) {
     std::vector<Op> out;
     std::vector<size_t> removed;  // original indices of the dropped restriction ops
@@ -2519,7 +2520,7 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
 
         } else res = "k_residual_restrict<" + std::to_string(dim) + "," + std::to_string(np) + ">";
     }
-    if (qprolong_ok(h, level)) post = "k_prolong_quads2d";  // (first post-sweep with the prolongation)
+    if (qprolong_ok(h, level)) post = "k_prolong_quads2d";  // (the first post-sweep, with the prolongation)
     std::string text = "sweep=" + sweep;
     if (!post.empty()) text += ";post_sweep=" + post;
     if (!res.empty()) text += ";residual_restrict=" + res;
@@ -2978,7 +2979,8 @@ int mgmc_sample_timed_stride(mgmc_handle* h, int nsteps, int stride, int64_t qoi
     *post_ms = post;
     int cpre = 0, cpost = 0;
     for (size_t q = 0; q < h->ops.size(); ++q)
-        if (h->ops[q].kind == OP_SWEEP && h->ops[q].level == 0) {
+        if ((h->ops[q].kind == OP_SWEEP || h->ops[q].kind == OP_SWEEP_RESTRICT || h->ops[q].kind == OP_PROLONG_SWEEP) &&
+            h->ops[q].level == 0) {
             if (q < h->seg_end_pre) ++cpre;
             else if (q >= h->seg_begin_post && q < h->seg_end_post) ++cpost;
         }
