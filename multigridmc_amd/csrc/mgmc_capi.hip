@@ -60,8 +60,7 @@ enum OpKind {
     OP_COPY = 5,
     OP_COARSE_CHOL = 6,
     OP_TAIL = 7,     // the sub-cycle of the coarsest levels in one workgroup (mgmc_tail.hpp)
-    OP_SWEEP_RESTRICT = 8,  // 2D Galerkin level: last pre-sweep + residual + restriction (mgmc_qrestrict.hpp)
-    OP_PROLONG_SWEEP = 9    // 2D Galerkin level: prolongate-add + first post-sweep (mgmc_qrestrict.hpp)
+    OP_SWEEP_RESTRICT = 8   // 2D Galerkin level: last pre-sweep + residual + restriction (mgmc_qrestrict.hpp)
 };
 
 struct Op {
@@ -103,7 +102,6 @@ enum PathFlag : uint32_t {
     PATH_NO_CHOL_DENSE = 1u << 12,        // coarse Cholesky: the blocked banded solves at any size
     PATH_NO_JSWEEP = 1u << 13,            // 3D Galerkin levels of 64 / 128 pairs: colour-pair passes, not j-marching halves
     PATH_NO_QRESTRICT = 1u << 14,         // 2D Galerkin levels: last pre-sweep and residual + restriction as two launches
-    PATH_NO_QPROLONG = 1u << 15,          // 2D Galerkin levels: prolongate-add and first post-sweep as two launches
 };
 
 struct PathToken {
@@ -118,7 +116,7 @@ constexpr PathToken kPathTokens[] = {
     {"lr_merge", PATH_NO_LR_MERGE},   {"lr_prefetch", PATH_NO_LR_PREFETCH},
     {"coarse_precompute", PATH_NO_COARSE_PRECOMPUTE}, {"lr_dense", PATH_NO_LR_DENSE},
     {"chol_dense", PATH_NO_CHOL_DENSE}, {"jsweep", PATH_NO_JSWEEP},
-    {"qrestrict", PATH_NO_QRESTRICT}, {"qprolong", PATH_NO_QPROLONG},
+    {"qrestrict", PATH_NO_QRESTRICT},
 };
 
 // parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
@@ -779,44 +777,6 @@ int qrestrict_threads(int npair) {
 
 bool qrestrict_ok(const mgmc_handle* h, int level);
 
-// k_prolong_quads2d: NT >= (CJ + 2) nx / 2
-int qprolong_threads(int npair) {
-    for (int nt = 256; nt <= 1024; nt += 256)
-        if (3 * npair <= nt) return nt;
-    return 0;
-}
-
-void launch_qprolong(const Level& lv, const Level& lc, const double* xin, double* xout, const double* f,
-                     const double* xc, double alpha, const GibbsArg& g, int direction, hipStream_t s, int nch = 1) {
-    QProlongArgs a;
-    a.L = lv.L;
-    a.Lc = lc.L;
-    a.xin = xin;
-    a.xout = xout;
-    a.f = f;
-    a.xc = xc;
-    a.alpha = alpha;
-    a.S = lv.S;
-    a.G = g;
-    a.cs = lv.L.nstore;
-    a.csc = lc.L.nstore;
-    const int npair = lv.L.nx / 2;
-    const int nt = qprolong_threads(npair);
-    a.CJ = nt / npair - 2;
-    const dim3 grid((lc.L.ny - 1 + a.CJ - 1) / a.CJ, 1, nch);
-    const size_t lds = qprolong_lds_bytes(lv.L.nx, a.CJ);
-    const bool fwd = direction == MGMC_FORWARD;
-#define MGMC_QP_LAUNCH(NT)                                                                               \
-    do {                                                                                                   \
-        if (fwd) hipLaunchKernelGGL((k_prolong_quads2d<NT, false>), grid, dim3(NT), lds, s, a);            \
-        else hipLaunchKernelGGL((k_prolong_quads2d<NT, true>), grid, dim3(NT), lds, s, a);                 \
-    } while (0)
-    if (nt == 256) MGMC_QP_LAUNCH(256);
-    else if (nt == 512) MGMC_QP_LAUNCH(512);
-    else if (nt == 768) MGMC_QP_LAUNCH(768);
-    else MGMC_QP_LAUNCH(1024);
-#undef MGMC_QP_LAUNCH
-}
 
 void launch_qrestrict(const Level& lv, const Level& lc, const double* xin, double* xout, const double* f, double* fc,
                       double* xc, const GibbsArg& g, int direction, hipStream_t s, int nch = 1) {
@@ -1514,41 +1474,16 @@ bool qrestrict_ok(const mgmc_handle* h, int level) {
     return qrestrict_lds_bytes(lv.L.nx, CJ) <= 150 * 1024;
 }
 
-// the same for the prolongate-add and the first post-sweep (k_prolong_quads2d)
-bool qprolong_ok(const mgmc_handle* h, int level) {
-    if (h->paths & PATH_NO_QPROLONG) return false;
-    if (level < 1 || level + 1 >= (int)h->levels.size()) return false;
-    const Level& lv = h->levels[level];
-    if (lv.spec.dim != 2 || lv.spec.npoints != 9 || !lv.quads || lv.jsweep || lv.field || lv.lr.m > 0 ||
-        !lv.pingpong())
-        return false;
-    const int nt = qprolong_threads(lv.L.nx / 2);
-    return nt > 0 && qprolong_lds_bytes(lv.L.nx, nt / (lv.L.nx / 2) - 2) <= 150 * 1024;
-}
-
 // fuse every (sweep, residual + restriction) pair of ops on a qrestrict_ok level into one
-// OP_SWEEP_RESTRICT (the restriction reads the buffer the sweep writes), and every (prolongate-add,
-// sweep) pair on a qprolong_ok level into one OP_PROLONG_SWEEP (the sweep reads the buffer the
-// prolongation updates in place; the fused kernel leaves that buffer as it was, and nothing reads it
-// before the sweep's output replaces it).  The fine level (level 0) keeps its ops, so the timed
-// fine-sweep segments are unchanged (the same fusions around the 2D fine level's k_rb2d were built,
-// bitwise, and measured slower: DESIGN.md section 3)
+// OP_SWEEP_RESTRICT (the restriction reads the buffer the sweep writes).  The fine level (level 0)
+// keeps its ops, so the timed fine-sweep segments are unchanged.  (Measured and not kept, DESIGN.md
+// section 3: the same fusion around the 2D fine level's k_rb2d, and the mirror image on the way up --
+// prolongate-add + first post-sweep in one launch -- both bitwise, neither faster.)
 void fuse_sweep_restrict(mgmc_handle* h) {
     std::vector<Op> out;
     std::vector<size_t> removed;  // original indices of the dropped restriction ops
     for (size_t q = 0; q < h->ops.size(); ++q) {
         const Op& op = h->ops[q];
-        if (op.kind == OP_PROLONGATE && q + 1 < h->ops.size() && qprolong_ok(h, op.level)) {
-            const Op& nx = h->ops[q + 1];
-            if (nx.kind == OP_SWEEP && nx.level == op.level && nx.src == op.src && !nx.prolong) {
-                Op f = nx;
-                f.kind = OP_PROLONG_SWEEP;
-                out.push_back(f);
-                removed.push_back(q);
-                ++q;
-                continue;
-            }
-        }
         if (op.kind == OP_SWEEP && q + 1 < h->ops.size() && qrestrict_ok(h, op.level) && !op.prolong) {
             const Op& nx = h->ops[q + 1];
             if (nx.kind == OP_RESIDUAL_RESTRICT && nx.level == op.level && nx.src == 1 - op.src) {
@@ -1620,13 +1555,6 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
                 Level& lc = h->levels[op.level + 1];
                 launch_qrestrict(lv, lc, lv.buf(op.src), lv.buf(1 - op.src), lv.f, lc.f, lc.x, g, op.direction, s, nch);
-                break;
-            }
-            case OP_PROLONG_SWEEP: {  // (2D Galerkin level, no low-rank part: qprolong_ok)
-                GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
-                Level& lc = h->levels[op.level + 1];
-                launch_qprolong(lv, lc, lv.buf(op.src), lv.buf(1 - op.src), lv.f, lc.x, h->cfg.coarse_scaling, g,
-                                op.direction, s, nch);
                 break;
             }
             case OP_COARSE_CHOL: {
@@ -2520,7 +2448,6 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
 
         } else res = "k_residual_restrict<" + std::to_string(dim) + "," + std::to_string(np) + ">";
     }
-    if (qprolong_ok(h, level)) post = "k_prolong_quads2d";  // (the first post-sweep, with the prolongation)
     std::string text = "sweep=" + sweep;
     if (!post.empty()) text += ";post_sweep=" + post;
     if (!res.empty()) text += ";residual_restrict=" + res;
@@ -2954,14 +2881,21 @@ int mgmc_sample_timed_stride(mgmc_handle* h, int nsteps, int stride, int64_t qoi
     const int nt = (int)timed_steps.size();
     std::vector<hipEvent_t> ev(NSEG * (size_t)nt);
     for (auto& e : ev) HIPCHK(h, hipEventCreate(&e));
-    for (int s = 0, ti = 0; s < nsteps; ++s) {
+    // (runs of untimed cycles replay the unrolled graph where there is one, as the plain sample loop
+    // does: one graph launch per cycle costs host time comparable to a small lattice's cycle)
+    for (int s = 0, ti = 0; s < nsteps;) {
         if (ti < nt && timed_steps[ti] == s) {
             for (int q = 0; q < NSEG; ++q)
                 HIPCHK(h, hipGraphExecEventRecordNodeSetEvent(h->graph_timed, h->timed_node[q], ev[NSEG * ti + q]));
             HIPCHK(h, hipGraphLaunch(h->graph_timed, h->stream));
             ++ti;
+            ++s;
+        } else if (h->graph_unroll && s + h->unroll <= (ti < nt ? timed_steps[ti] : nsteps)) {
+            HIPCHK(h, hipGraphLaunch(h->graph_unroll, h->stream));
+            s += h->unroll;
         } else {
             HIPCHK(h, hipGraphLaunch(h->graph_all, h->stream));
+            ++s;
         }
     }
     HIPCHK(h, hipEventSynchronize(ev[NSEG * nt - 1]));
@@ -2979,7 +2913,7 @@ int mgmc_sample_timed_stride(mgmc_handle* h, int nsteps, int stride, int64_t qoi
     *post_ms = post;
     int cpre = 0, cpost = 0;
     for (size_t q = 0; q < h->ops.size(); ++q)
-        if ((h->ops[q].kind == OP_SWEEP || h->ops[q].kind == OP_SWEEP_RESTRICT || h->ops[q].kind == OP_PROLONG_SWEEP) &&
+        if ((h->ops[q].kind == OP_SWEEP || h->ops[q].kind == OP_SWEEP_RESTRICT) &&
             h->ops[q].level == 0) {
             if (q < h->seg_end_pre) ++cpre;
             else if (q >= h->seg_begin_post && q < h->seg_end_post) ++cpost;

@@ -169,7 +169,7 @@ def test_mgmc_cycles_bitwise(hip_device, name):
 # every MGMC_DISABLE token of mgmc_capi.hip (PathFlag), alone and all together, on configurations
 # where the fast path it turns off would run
 ALL_PATHS = ("tail,fuse_prolong,quads,rb2d,zsweep,pairs,zrestrict,lr_small,lr_merge,lr_prefetch,coarse_precompute,jsweep,"
-             "qrestrict,qprolong")
+             "qrestrict")
 VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_ssor"),
             ("fuse_prolong", "3d128_zsweep_odd"), ("fuse_prolong", "3d_zres27"), ("fuse_prolong", "3d_jsweep_ssor_W"),
             ("tail", "3d16"), ("tail", "3d64_4lvl"), ("tail", "2d64_template_W"), ("tail", "3d32_W_ssor"),
@@ -186,9 +186,7 @@ VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_
             ("chol_dense", "2d64_chol_W"), ("chol_dense", "3d32_chol_ssor"), ("chol_dense", "3d128_zsweep_chol"),
             ("jsweep", "3d_zres27"), ("jsweep", "3d_jsweep_ssor_W"),
             ("qrestrict", "2d512_qrestrict"), ("qrestrict", "2d_qr_aniso_ssor_W"), ("tail", "2d_qr_cj5"),
-            ("tail,qrestrict", "2d_qr_cj5"), (ALL_PATHS, "2d512_qrestrict"),
-            ("qprolong", "2d512_qrestrict"), ("qprolong", "2d_qr_aniso_ssor_W"), ("tail,qprolong", "2d_qr_cj5"),
-            ("qrestrict,qprolong", "2d_qr_aniso_ssor_W")]
+            ("tail,qrestrict", "2d_qr_cj5"), (ALL_PATHS, "2d512_qrestrict")]
 
 
 @pytest.mark.parametrize("paths,name", VARIANTS)
@@ -200,8 +198,7 @@ def test_variant_cycles_bitwise(hip_device, monkeypatch, paths, name):
     colour per pass on Galerkin levels; jsweep = colour-pair passes instead of the j-marching half-sweeps
     on 3D Galerkin levels of 64 / 128 pairs per row; zrestrict = the per-point residual + restriction;
     qrestrict = a 2D Galerkin level's last pre-sweep and its residual + restriction as two launches
-    instead of one k_quads_restrict2d; qprolong = its prolongate-add and first post-sweep as two
-    launches instead of one k_prolong_quads2d;
+    instead of one k_quads_restrict2d;
     coarse_precompute = the coarse SSOR sampler's right-hand sides inside its colour passes;
     chol_dense = the coarse Cholesky's blocked banded solves on a small coarsest level (the oracle's
     blocked mode).  Every combination gives the oracle's cycle exactly."""
@@ -265,14 +262,12 @@ def test_level_kernels_labels(hip_device, name, level, sweep):
 @pytest.mark.parametrize("name,levels", [("2d512_qrestrict", (1, 2)), ("2d_qr_aniso_ssor_W", (1,))])
 def test_qrestrict_labels(hip_device, name, levels):
     """2D Galerkin levels outside k_tail run their last pre-sweep and residual + restriction as one
-    k_quads_restrict2d launch, and their prolongate-add and first post-sweep as one k_prolong_quads2d
-    launch (mgmc_qrestrict.hpp); MGMC_DISABLE=qrestrict / qprolong are covered above."""
+    k_quads_restrict2d launch (mgmc_qrestrict.hpp); MGMC_DISABLE=qrestrict is covered above."""
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)
     for level in levels:
         k = s.level_kernels(level)
-        assert k["residual_restrict"] == "k_quads_restrict2d"
-        assert k["post_sweep"] == "k_prolong_quads2d"
+        assert k["residual_restrict"] == "k_quads_restrict2d" and "post_sweep" not in k
     assert s.level_kernels(0) == {"sweep": "k_rb2d", "residual_restrict": "k_residual_restrict<2,5>"}
     s.close()
 
