@@ -79,6 +79,8 @@ struct Op {
     int lr_coarse_patch = 0;  // OP_RESIDUAL_RESTRICT: ... and the coarse level's first pre-sweep
     uint32_t lr_coarse_tag = 0;
     int tail = -1;           // OP_TAIL: index into mgmc_handle::tail_args
+    int zpre = 0;            // OP_SWEEP_RESTRICT: also draws the next OP_COARSE_LDS's noise into mgmc_handle::zbuf;
+                             // OP_COARSE_LDS: reads it from there
 };
 
 
@@ -283,6 +285,8 @@ struct mgmc_handle {
     double* comm_buf = nullptr;  // device scratch for collectives
     uint32_t paths = 0;          // PathFlag bits (MGMC_DISABLE)
     int unroll_override = 0;     // MGMC_GRAPH_UNROLL (cycles per sample-loop graph launch; 0 = by size)
+    double2* zbuf = nullptr;           // the coarse SSOR sampler's pre-drawn Box-Muller pairs [chain][item]
+    long long zbuf_n = 0;              // items per chain
     std::vector<TailArgs*> tail_args;  // device copies, one per OP_TAIL
     std::vector<size_t> tail_lds;      // dynamic LDS bytes per OP_TAIL
     double* sv[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // solver: b x r z p q (level 0)
@@ -643,23 +647,34 @@ void launch_pairs(const Level& lv, double* x, const double* f, const GibbsArg& g
     }
 }
 
-void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStream_t s, int nch = 1) {
+// the coarse SSOR sampler's right-hand sides are precomputed when they fit next to x and f
+bool coarse_precompute(const Level& lv, int nsweeps) {
+    const long long ndof = (long long)(lv.L.nx - 1) * (lv.L.ny - 1) * (lv.spec.dim == 3 ? lv.L.nz - 1 : 1);
+    return lv.lds_bytes + (size_t)nsweeps * ndof * sizeof(double) <= 150 * 1024 &&
+           !(lv.paths & PATH_NO_COARSE_PRECOMPUTE);
+}
+
+// zb: its Box-Muller pairs drawn by the launch before (nullptr: drawn here)
+void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStream_t s, int nch = 1,
+                       const double2* zb = nullptr, long long zs = 0) {
     const int dim = lv.spec.dim, np = lv.spec.npoints, nc = lv.spec.ncolours;
     dim3 block(1024), grid(1, 1, nch);
     const long long chs = lv.L.nstore;
-    // precomputed right hand sides (k_coarse_ssor_lds) when they fit next to x and f
     const long long ndof = (long long)(lv.L.nx - 1) * (lv.L.ny - 1) * (dim == 3 ? lv.L.nz - 1 : 1);
     const size_t lds_pre = lv.lds_bytes + (size_t)nsweeps * ndof * sizeof(double);
-    const int pre = lds_pre <= 150 * 1024 && !(lv.paths & PATH_NO_COARSE_PRECOMPUTE);
+    const int pre = coarse_precompute(lv, nsweeps);
     const size_t lds = pre ? lds_pre : lv.lds_bytes;
 #define MGMC_COARSE_LAUNCH(D, P)                                                                                 \
     do {                                                                                                           \
-        if (pre)                                                                                                   \
+        if (pre && zb)                                                                                             \
+            hipLaunchKernelGGL((k_coarse_ssor_lds<D, P, true, true>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, \
+                               g, nsweeps, nc, chs, zb, zs);                                                       \
+        else if (pre)                                                                                              \
             hipLaunchKernelGGL((k_coarse_ssor_lds<D, P, true>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g,   \
-                               nsweeps, nc, chs);                                                                  \
+                               nsweeps, nc, chs, nullptr, 0);                                                      \
         else                                                                                                       \
             hipLaunchKernelGGL((k_coarse_ssor_lds<D, P, false>), grid, block, lds, s, lv.L, lv.x, lv.f, lv.S, g,  \
-                               nsweeps, nc, chs);                                                                  \
+                               nsweeps, nc, chs, nullptr, 0);                                                      \
     } while (0)
     if (dim == 3 && np == 27) MGMC_COARSE_LAUNCH(3, 27);
     else if (dim == 3 && np == 7) MGMC_COARSE_LAUNCH(3, 7);
@@ -778,9 +793,16 @@ int qrestrict_threads(int npair) {
 bool qrestrict_ok(const mgmc_handle* h, int level);
 
 
+// zc != nullptr: spare workgroups also draw the coarsest level's SSOR-sampler noise (nsweeps sweeps from
+// tag zc_tag) into zc, zcs items per chain
 void launch_qrestrict(const Level& lv, const Level& lc, const double* xin, double* xout, const double* f, double* fc,
-                      double* xc, const GibbsArg& g, int direction, hipStream_t s, int nch = 1) {
+                      double* xc, const GibbsArg& g, int direction, hipStream_t s, int nch = 1, double2* zc = nullptr,
+                      int zc_nsweeps = 0, uint32_t zc_tag = 0, long long zcs = 0) {
     QRestrictArgs a;
+    a.zc = zc;
+    a.zc_nsweeps = zc_nsweeps;
+    a.zc_tag = zc_tag;
+    a.zcs = zcs;
     a.L = lv.L;
     a.Lc = lc.L;
     a.xin = xin;
@@ -795,7 +817,9 @@ void launch_qrestrict(const Level& lv, const Level& lc, const double* xin, doubl
     const int npair = lv.L.nx / 2;
     const int nt = qrestrict_threads(npair);
     a.CJ = nt / npair - 3;
-    const dim3 grid((lc.L.ny - 1 + a.CJ - 1) / a.CJ, 1, nch);
+    a.nblk_main = (lc.L.ny - 1 + a.CJ - 1) / a.CJ;
+    const int nextra = zc ? (int)std::min<long long>((zcs + nt - 1) / nt, 64) : 0;
+    const dim3 grid(a.nblk_main + nextra, 1, nch);
     const size_t lds = qrestrict_lds_bytes(lv.L.nx, a.CJ);
     const bool fwd = direction == MGMC_FORWARD;
 #define MGMC_QR_LAUNCH(NT)                                                                               \
@@ -1507,6 +1531,28 @@ void fuse_sweep_restrict(mgmc_handle* h) {
     shift(h->seg_begin_post);
     shift(h->seg_end_post);
     h->ops.swap(out);
+    // a fused restriction onto the coarsest level draws the coarse SSOR sampler's noise in spare
+    // workgroups (QRestrictArgs::zc): the sampler's one workgroup then only reads it (4.5 of its ~19 us
+    // were the draws at 2D 1024^2).  The pairs are adjacent ops, so one buffer serves every visit
+    if (h->zbuf) hipFree(h->zbuf);
+    h->zbuf = nullptr;
+    h->zbuf_n = 0;
+    for (size_t q = 0; q + 1 < h->ops.size(); ++q) {
+        Op& op = h->ops[q];
+        Op& co = h->ops[q + 1];
+        if (op.kind != OP_SWEEP_RESTRICT || co.kind != OP_COARSE_LDS || co.level != op.level + 1 ||
+            co.level + 1 != (int)h->levels.size() || !coarse_precompute(h->levels[co.level], co.nsweeps))
+            continue;
+        const Level& lc = h->levels[co.level];
+        const long long n = (long long)co.nsweeps * (lc.L.ny - 1) * (lc.L.nx / 2);
+        if (!h->zbuf) {
+            if (hipMalloc(&h->zbuf, (size_t)h->nchains * n * sizeof(double2)) != hipSuccess) return;  // (draws stay in place)
+            h->zbuf_n = n;
+        }
+        if (n != h->zbuf_n) continue;
+        op.zpre = 1;
+        co.zpre = 1;
+    }
 }
 
 int build_tails(mgmc_handle* h) {
@@ -1554,7 +1600,14 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
             case OP_SWEEP_RESTRICT: {  // (2D Galerkin level, no low-rank part: qrestrict_ok)
                 GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
                 Level& lc = h->levels[op.level + 1];
-                launch_qrestrict(lv, lc, lv.buf(op.src), lv.buf(1 - op.src), lv.f, lc.f, lc.x, g, op.direction, s, nch);
+                if (op.zpre) {  // + the next op's (the coarse sampler's) noise
+                    const Op& co = h->ops[q + 1];
+                    launch_qrestrict(lv, lc, lv.buf(op.src), lv.buf(1 - op.src), lv.f, lc.f, lc.x, g, op.direction, s,
+                                     nch, h->zbuf, co.nsweeps, co.tag, h->zbuf_n);
+                } else {
+                    launch_qrestrict(lv, lc, lv.buf(op.src), lv.buf(1 - op.src), lv.f, lc.f, lc.x, g, op.direction, s,
+                                     nch);
+                }
                 break;
             }
             case OP_COARSE_CHOL: {
@@ -1563,7 +1616,8 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
             }
             case OP_COARSE_LDS: {
                 GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
-                launch_coarse_lds(lv, g, op.nsweeps, s, nch);
+                if (op.zpre) launch_coarse_lds(lv, g, op.nsweeps, s, nch, h->zbuf, h->zbuf_n);
+                else launch_coarse_lds(lv, g, op.nsweeps, s, nch);
                 break;
             }
             case OP_RESIDUAL_RESTRICT: {
@@ -2394,6 +2448,7 @@ int mgmc_destroy(mgmc_handle* h) {
     if (h->qv_val) hipFree(h->qv_val);
     if (h->qv_part) hipFree(h->qv_part);
     if (h->lex_tmp) hipFree(h->lex_tmp);
+    if (h->zbuf) hipFree(h->zbuf);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
     return MGMC_OK;

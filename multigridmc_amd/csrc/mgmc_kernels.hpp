@@ -224,16 +224,21 @@ __device__ __forceinline__ int colour_of(int i, int j, int k) {
 // evaluated up front by all threads at once (f does not change during the sampler), so a colour pass
 // is only the stencil and the update -- one Philox + Box-Muller latency for the whole sampler instead
 // of one per colour pass.  The same operations as gibbs_point, so the same bits.
-template <int DIM, int NPTS, bool PRE>
+// ZBUF (with PRE): the Box-Muller pairs come from zb[t] (t = the item index below; chains zs apart),
+// drawn by spare workgroups of the launch before (k_quads_restrict2d) with the same Philox blocks and
+// normal_pair, so the bits are the same
+template <int DIM, int NPTS, bool PRE, bool ZBUF = false>
 __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __restrict__ xg,
                                                           const double* __restrict__ fg, StencilArg S, GibbsArg G,
-                                                          int nsweeps, int ncolours, long long chs) {
+                                                          int nsweeps, int ncolours, long long chs,
+                                                          const double2* __restrict__ zb = nullptr, long long zs = 0) {
     constexpr bool precompute = PRE;  // a template parameter: the colour passes carry no Philox code
     {  // batched chains (blockIdx.z)
         const int ch = batch_chain();
         xg += ch * chs;
         fg += ch * chs;
         G.key = chain_key(G, ch);
+        if (ZBUF) zb += ch * zs;
     }
     extern __shared__ __attribute__((aligned(16))) double smem[];
     double* xs = smem;
@@ -273,6 +278,12 @@ __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __re
             if (i0 > nxi) continue;
             const int j = row % nyi + 1;
             const int k = (DIM == 3) ? row / nyi + 1 : 0;
+            if (ZBUF) {
+                const double2 zz = zb[t];
+                pz0[u] = zz.x;
+                pz1[u] = zz.y;
+                continue;
+            }
             const Philox4 rnd = philox4x32_10(pair_id<DIM>(L, i0, j, k), G.tag + (uint32_t)sw, (uint32_t)sample,
                                               (uint32_t)(sample >> 32), G.key.k0, G.key.k1);
             normal_pair(rnd, &pz0[u], &pz1[u]);
@@ -319,9 +330,15 @@ __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __re
             const int j = row % nyi + 1;
             const int k = (DIM == 3) ? row / nyi + 1 : 0;
             double z0, z1;
-            const Philox4 rnd = philox4x32_10(pair_id<DIM>(L, i0, j, k), G.tag + (uint32_t)sw, (uint32_t)sample,
-                                              (uint32_t)(sample >> 32), G.key.k0, G.key.k1);
-            normal_pair(rnd, &z0, &z1);
+            if (ZBUF) {
+                const double2 zz = zb[t];
+                z0 = zz.x;
+                z1 = zz.y;
+            } else {
+                const Philox4 rnd = philox4x32_10(pair_id<DIM>(L, i0, j, k), G.tag + (uint32_t)sw, (uint32_t)sample,
+                                                  (uint32_t)(sample >> 32), G.key.k0, G.key.k1);
+                normal_pair(rnd, &z0, &z1);
+            }
             const long long q = (long long)sw * ndof + (long long)row * nxi + (i0 - 1);
             const long long p = L.at(i0, j, k);
             cs[q] = fma(G.sd, z0, fs[p]);

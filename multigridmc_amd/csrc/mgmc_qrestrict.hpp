@@ -43,6 +43,14 @@ struct QRestrictArgs {
     GibbsArg G;
     int CJ;             // coarse rows per workgroup
     long long cs, csc;  // batched chains: doubles between chains of the level / the coarse level
+    // when the coarse level is the coarsest and its SSOR sampler follows (k_coarse_ssor_lds<..., ZBUF>):
+    // workgroups nblk_main .. of the grid draw that sampler's Box-Muller pairs into zc (its item
+    // order; tags zc_tag, zc_tag + 1, ...), in parallel with the restriction -- they depend on no data
+    int nblk_main;
+    double2* zc;
+    int zc_nsweeps;
+    uint32_t zc_tag;
+    long long zcs;      // zc doubles2 per chain
 };
 
 // rows of the LDS buffers for CJ coarse rows: old / swept x, f, residual
@@ -65,6 +73,26 @@ __global__ void __launch_bounds__(NT) k_quads_restrict2d(QRestrictArgs a) {
         a.fc += ch * a.csc;
         a.xc += ch * a.csc;
         a.G.key = chain_key(a.G, ch);
+    }
+    if ((int)blockIdx.x >= a.nblk_main) {  // the coarsest level's noise (see QRestrictArgs)
+        const Layout& Lc = a.Lc;
+        const uint64_t sample = *a.G.sample;
+        const int nxi = Lc.nx - 1, nyi = Lc.ny - 1, npair = Lc.nx / 2;
+        const int n = a.zc_nsweeps * nyi * npair;
+        double2* z = a.zc + batch_chain() * a.zcs;
+        for (int t = ((int)blockIdx.x - a.nblk_main) * NT + (int)threadIdx.x; t < n;
+             t += ((int)gridDim.x - a.nblk_main) * NT) {
+            const int m = t % npair, rt = t / npair;
+            const int row = rt % nyi, sw = rt / nyi;
+            const int i0 = 2 * m + 1;
+            if (i0 > nxi) continue;
+            const Philox4 rnd = philox4x32_10(pair_id<2>(Lc, i0, row + 1, 0), a.zc_tag + (uint32_t)sw,
+                                              (uint32_t)sample, (uint32_t)(sample >> 32), a.G.key.k0, a.G.key.k1);
+            double z0, z1;
+            normal_pair(rnd, &z0, &z1);
+            z[t] = make_double2(z0, z1);
+        }
+        return;
     }
     extern __shared__ __attribute__((aligned(16))) double qsm[];
     const Layout& L = a.L;
