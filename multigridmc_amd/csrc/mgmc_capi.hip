@@ -80,7 +80,8 @@ struct Op {
     uint32_t lr_coarse_tag = 0;
     int tail = -1;           // OP_TAIL: index into mgmc_handle::tail_args
     int zpre = 0;            // OP_SWEEP_RESTRICT: also draws the next OP_COARSE_LDS's noise into mgmc_handle::zbuf;
-                             // OP_COARSE_LDS: reads it from there
+                             // OP_COARSE_LDS: reads it from there; OP_RESIDUAL_RESTRICT: 1 + the index of
+                             // the OP_TAIL after it whose noise its spare workgroups draw
 };
 
 
@@ -104,6 +105,7 @@ enum PathFlag : uint32_t {
     PATH_NO_CHOL_DENSE = 1u << 12,        // coarse Cholesky: the blocked banded solves at any size
     PATH_NO_JSWEEP = 1u << 13,            // 3D Galerkin levels of 64 / 128 pairs: colour-pair passes, not j-marching halves
     PATH_NO_QRESTRICT = 1u << 14,         // 2D Galerkin levels: last pre-sweep and residual + restriction as two launches
+    PATH_NO_TAIL_NOISE = 1u << 15,        // k_tail draws its sweeps' noise itself (not the restriction launch before it)
 };
 
 struct PathToken {
@@ -118,7 +120,7 @@ constexpr PathToken kPathTokens[] = {
     {"lr_merge", PATH_NO_LR_MERGE},   {"lr_prefetch", PATH_NO_LR_PREFETCH},
     {"coarse_precompute", PATH_NO_COARSE_PRECOMPUTE}, {"lr_dense", PATH_NO_LR_DENSE},
     {"chol_dense", PATH_NO_CHOL_DENSE}, {"jsweep", PATH_NO_JSWEEP},
-    {"qrestrict", PATH_NO_QRESTRICT},
+    {"qrestrict", PATH_NO_QRESTRICT}, {"tail_noise", PATH_NO_TAIL_NOISE},
 };
 
 // parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
@@ -289,6 +291,12 @@ struct mgmc_handle {
     long long zbuf_n = 0;              // items per chain
     std::vector<TailArgs*> tail_args;  // device copies, one per OP_TAIL
     std::vector<size_t> tail_lds;      // dynamic LDS bytes per OP_TAIL
+    // per OP_TAIL: its sweeps' Box-Muller pairs, drawn by spare workgroups of the restriction launch
+    // before it (nullptr: the tail draws them); the jobs (device) and items per chain
+    std::vector<double2*> tail_zb;
+    std::vector<TailNoiseJob*> tail_jobs;
+    std::vector<int> tail_njobs;
+    std::vector<long long> tail_zn;
     double* sv[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // solver: b x r z p q (level 0)
     double* sv_scal = nullptr;   // solver scalars
     double* sv_part = nullptr;   // reduction partials
@@ -683,10 +691,21 @@ void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStrea
 #undef MGMC_COARSE_LAUNCH
 }
 
+struct TailNoiseLaunch {  // spare workgroups of the launch draw a tail's noise (ZRestrictArgs)
+    const TailNoiseJob* jobs;
+    int njobs;
+    double2* zb;
+    long long zbs;
+    RngKey key;
+    uint32_t chain0, seed_hi;
+    const uint64_t* sample;
+};
+
 template <int NPTS, int CX, int CY, int NT>
 void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, const double* f, double* fc, double* xc,
-                           hipStream_t s, int nch) {
+                           hipStream_t s, int nch, const TailNoiseLaunch* tn = nullptr) {
     ZRestrictArgs a;
+    memset(&a, 0, sizeof(a));
     a.csf = lf.L.nstore;
     a.csc = lc.L.nstore;
     a.Lf = lf.L;
@@ -717,12 +736,28 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
     a.ntz = (lc.L.nz - 1 + a.kz - 1) / a.kz;
     const int nt = a.ntx * a.nty * a.ntz;
     const int nb = (nt + 7) / 8 * 8;
+    if (tn) {
+        a.nblk_main = nb;
+        a.jobs = tn->jobs;
+        a.njobs = tn->njobs;
+        a.zb = tn->zb;
+        a.zbs = tn->zbs;
+        a.key = tn->key;
+        a.chain0 = tn->chain0;
+        a.seed_hi = tn->seed_hi;
+        a.sample = tn->sample;
+        const int nextra = (int)std::min<long long>((tn->zbs + NT - 1) / NT, 64);
+        hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT, true>), dim3(nb + nextra, 1, nch), dim3(NT),
+                           zrestrict_lds_bytes(CX, CY), s, a);
+        return;
+    }
     hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT>), dim3(nb, 1, nch), dim3(NT), zrestrict_lds_bytes(CX, CY), s,
                        a);
 }
 
+// tn: the small z-marching kernel also draws a tail's noise (zr_small_path; ignored elsewhere)
 void launch_residual_restrict(const Level& lf, const Level& lc, const double* x, const double* f, double* fc,
-                              double* xc, int zero_xc, hipStream_t s, int nch = 1) {
+                              double* xc, int zero_xc, hipStream_t s, int nch = 1, const TailNoiseLaunch* tn = nullptr) {
     const bool zr = lf.spec.dim == 3 && zero_xc && !lf.field && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8;
     if (nch > 1 && !zr) {  // batched chains on the generic kernels: one launch per chain
         for (int c = 0; c < nch; ++c)
@@ -750,7 +785,7 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
     if (lf.spec.dim == 3 && zero_xc && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8) {
         const bool small = lc.L.nx < 32;
         if (lf.spec.npoints == 7) {
-            if (small) launch_zresrestrict_t<7, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch);
+            if (small) launch_zresrestrict_t<7, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch, tn);
             // 64 x 8 coarse points, 512 threads, 80 KB of LDS (2 workgroups per CU): half the y halo
             // of 64 x 4 (19 x planes rows per 16 fine rows instead of 11 per 8); 512^3 with kz 32:
             // 505-525 -> 488-502 us (interleaved A/B); at 256^3 too few tiles (73 against 66 us)
@@ -761,7 +796,7 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
 #ifndef MGMC_ZR27_CY  // (timing builds: scripts/build_exp.sh VARIANTS)
 #define MGMC_ZR27_CY 4
 #endif
-            if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch);
+            if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch, tn);
             else if (MGMC_ZR27_CY == 8 && lc.L.nx >= 128)
                 launch_zresrestrict_t<27, 64, 8, 512>(lf, lc, x, f, fc, xc, s, nch);
             else launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s, nch);
@@ -1366,8 +1401,24 @@ int tail_level(const mgmc_handle* h) {
 void free_tails(mgmc_handle* h) {
     for (auto p : h->tail_args)
         if (p) hipFree(p);
+    for (auto p : h->tail_zb)
+        if (p) hipFree(p);
+    for (auto p : h->tail_jobs)
+        if (p) hipFree(p);
     h->tail_args.clear();
     h->tail_lds.clear();
+    h->tail_zb.clear();
+    h->tail_jobs.clear();
+    h->tail_njobs.clear();
+    h->tail_zn.clear();
+}
+
+// the residual + restriction from level lf onto lf + 1 runs as the small z-marching kernel
+// (k_zresrestrict<., 16, 4, 64>): launch_residual_restrict's choice for zero_xc = 1
+bool zr_small_path(const mgmc_handle* h, int lf) {
+    const Level& f = h->levels[lf];
+    const Level& c = h->levels[lf + 1];
+    return f.spec.dim == 3 && !f.field && !(f.paths & PATH_NO_ZRESTRICT) && c.L.nx >= 8 && c.L.nx < 32;
 }
 
 // replace every maximal run of ops on levels >= lt (one call of build_ops_level(lt)) by one OP_TAIL
@@ -1464,6 +1515,39 @@ int build_tails_only(mgmc_handle* h) {
         A.cs = h->levels[lt].L.nstore;  // batched chains: one workgroup per chain
         A.chain0 = (uint32_t)h->chain;
         A.seed_hi = (uint32_t)(h->seed >> 32);
+        // the sweeps' Box-Muller pairs: drawn by spare workgroups of the restriction before the tail when
+        // that is the small z-marching kernel (3D; k_zresrestrict<..., ZN>), else here
+        std::vector<TailNoiseJob> jobs;
+        long long zn = 0;
+        const bool pre_zr = !out.empty() && out.back().kind == OP_RESIDUAL_RESTRICT && out.back().level == lt - 1 &&
+                            zr_small_path(h, lt - 1) && h->levels[lt - 1].lr.m == 0 && !(h->paths & PATH_NO_TAIL_NOISE);
+        for (int o = 0; o < A.nops; ++o) {
+            TailOp& t = A.ops[o];
+            t.zoff = -1;
+            if (t.kind != TAIL_SWEEP && t.kind != TAIL_COARSE) continue;
+            const Layout& G = A.lv[t.level].G;
+            const long long items = (long long)(G.nx / 2) * (G.ny - 1) * (G.dim == 3 ? G.nz - 1 : 1);
+            const int ns = t.kind == TAIL_SWEEP ? 1 : t.nsweeps;
+            t.zoff = (int)zn;
+            for (int sw = 0; sw < ns; ++sw) {
+                jobs.push_back(TailNoiseJob{G.nx, G.ny, G.nz, t.tag + (uint32_t)sw, (int)zn});
+                zn += items;
+            }
+        }
+        double2* zb = nullptr;
+        TailNoiseJob* dj = nullptr;
+        if (pre_zr && !jobs.empty() && (int)jobs.size() <= TAIL_MAX_NOISE_JOBS && zn < (1LL << 30)) {
+            HIPCHK(h, hipMalloc(&zb, (size_t)h->nchains * zn * sizeof(double2)));
+            HIPCHK(h, hipMalloc(&dj, jobs.size() * sizeof(TailNoiseJob)));
+            HIPCHK(h, hipMemcpy(dj, jobs.data(), jobs.size() * sizeof(TailNoiseJob), hipMemcpyHostToDevice));
+            A.zb = zb;
+            A.zbs = zn;
+            out.back().zpre = (int)h->tail_args.size() + 1;  // the restriction draws for tail #(zpre - 1)
+        }
+        h->tail_zb.push_back(zb);
+        h->tail_jobs.push_back(dj);
+        h->tail_njobs.push_back(zb ? (int)jobs.size() : 0);
+        h->tail_zn.push_back(zb ? zn : 0);
         TailArgs* d = nullptr;
         HIPCHK(h, hipMalloc(&d, sizeof(TailArgs)));
         HIPCHK(h, hipMemcpy(d, &A, sizeof(TailArgs), hipMemcpyHostToDevice));
@@ -1629,7 +1713,14 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                     fr = lr_rhs(h, lv, LR_PATCH_RESIDUAL, lv.f, 0, sample, s, nch,
                                 lv.lr.dense_path && op.lr_post_patch ? (int64_t)op.lr_post_tag : -1);
                 }
-                launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch);
+                if (op.zpre > 0) {  // + the next op's (k_tail's) noise
+                    const int ti = op.zpre - 1;
+                    const TailNoiseLaunch tn{h->tail_jobs[ti], h->tail_njobs[ti], h->tail_zb[ti], h->tail_zn[ti],
+                                             h->key, (uint32_t)h->chain, (uint32_t)(h->seed >> 32), sample};
+                    launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch, &tn);
+                } else {
+                    launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch);
+                }
                 if (lr && lv.lr.dense_path)
                     ;  // f was never patched; the post-sweep's rhs went to lr.fe2 above
                 else if (lr && (op.lr_post_patch || op.lr_coarse_patch))

@@ -42,7 +42,18 @@ struct TailOp {
     int dir;       // sweeps: 1 forward, 2 backward (MGMC_FORWARD / MGMC_BACKWARD)
     uint32_t tag;  // first sweep tag
     int nsweeps;   // TAIL_COARSE: forward/backward sweeps, tags tag, tag+1, ...
+    int zoff;      // sweeps, with TailArgs::zb: this op's Box-Muller pairs start at zb[zoff] (one sweep's
+                   // npair x nrow items after the other, the item order of the right-hand-side loop)
 };
+
+// one job of the tail's pre-drawn noise: the pairs of one sweep of one tail level (drawn by spare
+// workgroups of the residual + restriction launch before the tail, mgmc_zrestrict.hpp)
+struct TailNoiseJob {
+    int nx, ny, nz;    // the level's cells (pair ids: pair_id<3>)
+    uint32_t tag;
+    int zoff;          // first item in zb
+};
+constexpr int TAIL_MAX_NOISE_JOBS = 24;
 
 struct TailLevel {
     Layout G;      // LDS layout (off 0, sx = nx+1, sp = sx (ny+1), 3D padded to 8 mod 16)
@@ -76,6 +87,8 @@ struct TailArgs {
     Layout Lg;
     long long cs;          // batched chains: doubles between chains of level lt (one workgroup per chain)
     uint32_t chain0, seed_hi;  // chain c's Philox key: (key.k0, lo32(chain0 + c) ^ seed_hi)
+    const double2* zb;     // pre-drawn Box-Muller pairs of the sweeps (nullptr: drawn here), zbs per chain
+    long long zbs;
     TailLevel lv[TAIL_MAX_LEVELS];
     TailOp ops[TAIL_MAX_OPS];
 };
@@ -159,8 +172,9 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
     }
     __syncthreads();
 
+    const double2* zb = A->zb ? A->zb + ch * A->zbs : nullptr;
     // one Gibbs sweep of level t: right hand sides of every vertex, then the colour passes
-    auto sweep = [&](const TailLevel& t, int dir, uint32_t tag) {
+    auto sweep = [&](const TailLevel& t, int dir, uint32_t tag, int zoff) {
         const Layout& G = t.G;
         double* x = lds + t.ox;
         double* f = lds + t.of;
@@ -184,8 +198,14 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             const int i0 = 2 * m + 1;
             if (i0 > G.nx - 1) continue;
             double z0, z1;
-            const Philox4 rnd = philox4x32_10(pair_id<DIM>(G, i0, j, k), tag, s_lo, s_hi, key.k0, key.k1);
-            normal_pair(rnd, &z0, &z1);
+            if (zb) {
+                const double2 zz = zb[zoff + q];
+                z0 = zz.x;
+                z1 = zz.y;
+            } else {
+                const Philox4 rnd = philox4x32_10(pair_id<DIM>(G, i0, j, k), tag, s_lo, s_hi, key.k0, key.k1);
+                normal_pair(rnd, &z0, &z1);
+            }
             const int p = (int)G.at(i0, j, k);
             scr[p] = fma(t.sd, z0, f[p]);
             if (i0 + 1 <= G.nx - 1) scr[p + 1] = fma(t.sd, z1, f[p + 1]);
@@ -246,9 +266,12 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
         const TailOp op = A->ops[o];
         const TailLevel& t = A->lv[op.level];
         if (op.kind == TAIL_SWEEP) {
-            sweep(t, op.dir, op.tag);
+            sweep(t, op.dir, op.tag, op.zoff);
         } else if (op.kind == TAIL_COARSE) {
-            for (int s = 0; s < op.nsweeps; ++s) sweep(t, (s & 1) ? 2 : 1, op.tag + (uint32_t)s);
+            for (int s = 0; s < op.nsweeps; ++s) {
+                const int npair = t.G.nx / 2, nrow = (t.G.ny - 1) * (DIM == 3 ? t.G.nz - 1 : 1);
+                sweep(t, (s & 1) ? 2 : 1, op.tag + (uint32_t)s, op.zoff + s * npair * nrow);
+            }
         } else if (op.kind == TAIL_RESTRICT) {
             const TailLevel& c = A->lv[op.level + 1];
             const Layout& G = t.G;

@@ -20,6 +20,7 @@
 // Global traffic: x and f once (16 B per fine vertex) + f_c, x_c (2 B per fine vertex).
 #pragma once
 #include "mgmc_kernels.hpp"
+#include "mgmc_tail.hpp"
 
 namespace mgmc {
 
@@ -33,10 +34,47 @@ struct ZRestrictArgs {
     int kz;            // coarse planes per chunk
     int ntx, nty, ntz;
     long long csf, csc;  // batched chains: doubles between chains on the fine / coarse level
+    // ZN: workgroups nblk_main .. of the grid draw the next op's (k_tail's) Box-Muller pairs instead
+    // (they depend on no data): jobs[0 .. njobs) into zb (zbs items per chain)
+    int nblk_main;
+    const TailNoiseJob* jobs;
+    int njobs;
+    double2* zb;
+    long long zbs;
+    RngKey key;                // chain c's key: (key.k0, lo32(chain0 + c) ^ seed_hi)
+    uint32_t chain0, seed_hi;
+    const uint64_t* sample;
 };
 
-template <int NPTS, int CX, int CY, int NT>
+template <int NPTS, int CX, int CY, int NT, bool ZN = false>
 __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
+    if (ZN && (int)blockIdx.x >= a.nblk_main) {  // the tail's noise (see ZRestrictArgs)
+        const int ch = batch_chain();
+        RngKey key = a.key;
+        if (ch) key.k1 = (a.chain0 + (uint32_t)ch) ^ a.seed_hi;
+        const uint64_t sample = *a.sample;
+        double2* z = a.zb + ch * a.zbs;
+        const int nw = ((int)gridDim.x - a.nblk_main) * NT;
+        const int w0 = ((int)blockIdx.x - a.nblk_main) * NT + (int)threadIdx.x;
+        for (int jb = 0; jb < a.njobs; ++jb) {
+            const TailNoiseJob J = a.jobs[jb];
+            const int npair = J.nx / 2, nyi = J.ny - 1;
+            const int n = npair * nyi * (J.nz - 1);
+            for (int q = w0; q < n; q += nw) {
+                const int m = q % npair, row = q / npair;
+                const int i0 = 2 * m + 1;
+                if (i0 > J.nx - 1) continue;
+                const int j = row % nyi + 1, k = row / nyi + 1;
+                const uint32_t pair = (uint32_t)(((uint64_t)(k - 1) * (uint64_t)nyi + (uint64_t)(j - 1)) * (uint64_t)npair +
+                                                 (uint64_t)m);  // pair_id<3>
+                const Philox4 rnd = philox4x32_10(pair, J.tag, (uint32_t)sample, (uint32_t)(sample >> 32), key.k0, key.k1);
+                double z0, z1;
+                normal_pair(rnd, &z0, &z1);
+                z[J.zoff + q] = make_double2(z0, z1);
+            }
+        }
+        return;
+    }
     // fine x range of the residual region: [2*I0-1, 2*I0+2*CX-1] = RP pairs from an odd position.
     // x is staged with one more vertex on each side: positions [2*I0-3, 2*I0+2*CX+2] = XPP pairs.
     constexpr int RP = CX + 1;                   // residual pairs per row
@@ -62,7 +100,7 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
     }
     const Layout& Lf = a.Lf;
     const Layout& Lc = a.Lc;
-    const int nb = gridDim.x, b = blockIdx.x, per = nb >> 3;
+    const int nb = ZN ? a.nblk_main : (int)gridDim.x, b = blockIdx.x, per = nb >> 3;
     const int tile = (nb & 7) ? b : (b & 7) * per + (b >> 3);
     const int txi = tile % a.ntx;
     const int tyi = (tile / a.ntx) % a.nty;

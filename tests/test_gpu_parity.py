@@ -169,7 +169,7 @@ def test_mgmc_cycles_bitwise(hip_device, name):
 # every MGMC_DISABLE token of mgmc_capi.hip (PathFlag), alone and all together, on configurations
 # where the fast path it turns off would run
 ALL_PATHS = ("tail,fuse_prolong,quads,rb2d,zsweep,pairs,zrestrict,lr_small,lr_merge,lr_prefetch,coarse_precompute,jsweep,"
-             "qrestrict")
+             "qrestrict,tail_noise")
 VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_ssor"),
             ("fuse_prolong", "3d128_zsweep_odd"), ("fuse_prolong", "3d_zres27"), ("fuse_prolong", "3d_jsweep_ssor_W"),
             ("tail", "3d16"), ("tail", "3d64_4lvl"), ("tail", "2d64_template_W"), ("tail", "3d32_W_ssor"),
@@ -186,7 +186,8 @@ VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_
             ("chol_dense", "2d64_chol_W"), ("chol_dense", "3d32_chol_ssor"), ("chol_dense", "3d128_zsweep_chol"),
             ("jsweep", "3d_zres27"), ("jsweep", "3d_jsweep_ssor_W"),
             ("qrestrict", "2d512_qrestrict"), ("qrestrict", "2d_qr_aniso_ssor_W"), ("tail", "2d_qr_cj5"),
-            ("tail,qrestrict", "2d_qr_cj5"), (ALL_PATHS, "2d512_qrestrict")]
+            ("tail,qrestrict", "2d_qr_cj5"), (ALL_PATHS, "2d512_qrestrict"),
+            ("tail_noise", "3d16"), ("tail_noise", "3d64_4lvl"), ("tail_noise", "3d32_W_ssor")]
 
 
 @pytest.mark.parametrize("paths,name", VARIANTS)
@@ -198,7 +199,8 @@ def test_variant_cycles_bitwise(hip_device, monkeypatch, paths, name):
     colour per pass on Galerkin levels; jsweep = colour-pair passes instead of the j-marching half-sweeps
     on 3D Galerkin levels of 64 / 128 pairs per row; zrestrict = the per-point residual + restriction;
     qrestrict = a 2D Galerkin level's last pre-sweep and its residual + restriction as two launches
-    instead of one k_quads_restrict2d;
+    instead of one k_quads_restrict2d; tail_noise = k_tail draws its sweeps' Box-Muller pairs itself
+    instead of the restriction launch before it;
     coarse_precompute = the coarse SSOR sampler's right-hand sides inside its colour passes;
     chol_dense = the coarse Cholesky's blocked banded solves on a small coarsest level (the oracle's
     blocked mode).  Every combination gives the oracle's cycle exactly."""
