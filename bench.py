@@ -94,10 +94,24 @@ def cpu_baseline(dim, n, nlevel, warmup, samples, posterior_args=None):
            "--nlevel", str(nlevel), "--warmup", str(warmup), "--samples", str(samples)]
     if posterior_args:
         cmd += posterior_args
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=1500)
-    if r.returncode != 0:
-        raise RuntimeError(f"CPU baseline failed (rc {r.returncode}): {r.stderr[-800:]}")
-    b = json.loads(r.stdout.strip().splitlines()[-1])
+    # a progress line on stderr every 30 s: the CPU baseline runs for minutes at 512^3, and a GPU box
+    # takes a command that stays silent for 3 minutes to be hung
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    t0 = time.perf_counter()
+    while True:
+        try:
+            stdout, stderr = proc.communicate(timeout=30)
+            break
+        except subprocess.TimeoutExpired:
+            el = time.perf_counter() - t0
+            print(f"bench: CPU baseline running ({el:.0f} s)", file=sys.stderr, flush=True)
+            if el > 1500:
+                proc.kill()
+                stdout, stderr = proc.communicate()
+                raise RuntimeError("CPU baseline timed out")
+    if proc.returncode != 0:
+        raise RuntimeError(f"CPU baseline failed (rc {proc.returncode}): {stderr[-800:]}")
+    b = json.loads(stdout.strip().splitlines()[-1])
     agg = ""
     if "cores_aggregate" in b:
         agg = (f"; all cores: {b['cores_aggregate']} chains forked after the setup (shared CSR operators, own "
@@ -247,6 +261,8 @@ def main():
     K = args.chains
     sampler = mg.MultigridMCSampler(op, SEED, params, device=device, chain_id=rank * K, nchains=K)
     t_setup = time.perf_counter() - t_setup
+    if rank == 0:
+        print(f"bench: setup {t_setup:.1f} s", file=sys.stderr, flush=True)
     qoi = mg.measurement_vector_index(lat, [0.5] * args.dim)
     n0 = lat.Nvertex
 
