@@ -367,10 +367,13 @@ def main():
             "qoi": {"index": qoi, "samples": nq, "mean": mean, "variance": m2 / nq if nq else None, "chains": len(parts)},
         }
         if timed:
-            line["segments_ms_per_step"] = {"pre": round(timed["pre_ms"] / args.steps, 4),
-                                            "post": round(timed["post_ms"] / args.steps, 4),
+            # pre / post: summed over the timed cycles only (every stride-th), so per timed cycle
+            nct = timed["ncycles_timed"]
+            line["segments_ms_per_step"] = {"pre": round(timed["pre_ms"] / nct, 4),
+                                            "post": round(timed["post_ms"] / nct, 4),
                                             "total": round(timed["total_ms"] / args.steps, 4),
-                                            "timing_stride": stride, "timed_pre_sweeps": timed["npre"]}
+                                            "timing_stride": stride, "timed_cycles": nct,
+                                            "timed_pre_sweeps": timed["npre"]}
         if args.dim == 2:
             line["metric"] = "MGMC V-cycle samples/sec, 2D (BASELINE config 2)"
         if args.posterior:

@@ -170,6 +170,8 @@ int mgmc_stencil_of_csr(const mgmc_config* cfg, int64_t nrow, const int64_t* row
 #define MGMC_LAYOUT_ZSWEEP_COARSE 8u
 #define MGMC_LAYOUT_ZRESTRICT 16u
 #define MGMC_LAYOUT_RB2D 32u
+#define MGMC_LAYOUT_JSWEEP 64u     /* + a replay of the j-marching half-sweeps' whole grid (256 CUs) */
+#define MGMC_LAYOUT_QRESTRICT 128u /* 2D fused last pre-sweep + residual + restriction */
 int mgmc_check_layout(int dim, const int* n, int reach, unsigned families, int zrestrict_cx, int legacy);
 
 /* ---- lifetime ---- */
@@ -218,7 +220,10 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n);
  * (linear_operator.cc:10-23); every SOR smoother sets up its B_bar (sor_smoother.cc:17-37) here,
  * so the call costs 2 m noise-free sweeps per level.  From then on every sweep applies the
  * low-rank fix and noise, and residuals / operator applications include B Sigma^{-1} B^T.
- * m = 0 restores the prior operator.  1 <= m <= 64. */
+ * m = 0 restores the prior operator.  1 <= m <= 64.  Invalid arguments (MGMC_E_INVALID from the
+ * checks of m, colptr, rows, vals, sigma) leave the handle unchanged; a failure after them (a coarse
+ * band the blocked Cholesky cannot take, the host work limit, an allocation) leaves the prior operator
+ * (no low-rank part on any level, the prior's coarse factors) and returns the error code. */
 int mgmc_set_lowrank(mgmc_handle* h, int m, const int64_t* colptr, const int64_t* rows, const double* vals,
                      const double* sigma);
 /* m of the current low-rank part (LinearOperator::get_m_lowrank); *nrows_bbar = rows stored for
@@ -272,6 +277,13 @@ int mgmc_operator_apply(mgmc_handle* h, int level, const double* x, double* y);
 /* deterministic multicolour SOR sweeps (SORSmoother::apply, no noise; with the B_bar fix) */
 int mgmc_smoother_apply(mgmc_handle* h, int level, int direction, int nsweeps,
                         const double* b, double* x);
+/* The Smoother drop-ins (include/reference_adapter/hip_sor_smoother.hh), noise-free multicolour sweeps:
+ * SORSmoother::apply exactly as the reference nests it -- nsmooth x (nsmooth sweeps of apply_sparse,
+ * then the B_bar fix once), smoother/sor_smoother.cc:41-53 over :56-78 -- so nsmooth^2 sweeps ... */
+int mgmc_sor_smoother_apply(mgmc_handle* h, int level, int direction, int nsmooth, const double* b, double* x);
+/* ... and SSORSmoother::apply (smoother/ssor_smoother.cc:9-15): nsmooth x (forward sweep + fix,
+ * backward sweep + fix) */
+int mgmc_ssor_smoother_apply(mgmc_handle* h, int level, int nsmooth, const double* b, double* x);
 /* one noisy multicolour SOR Gibbs sweep with explicit RNG counter (SORSampler::apply, nsmooth=1) */
 int mgmc_sor_sampler_apply(mgmc_handle* h, int level, int direction, uint32_t sweep_tag,
                            uint64_t sample_index, const double* f, double* x);

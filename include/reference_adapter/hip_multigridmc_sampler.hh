@@ -25,9 +25,13 @@
 // the CSC form mgmc_set_lowrank takes) and get_Sigma().diagonal().
 //
 // Noise: the reference's sampler draws from the shared std::mt19937_64; the device stream is
-// counter-based (Philox keyed by seed and chain id), so the constructor takes
-// the seed as one draw of the shared engine -- a run is still a deterministic function of the
-// driver's seed.  Errors print and exit(-1) like the reference (multigridmc_sampler.cc:47-49).
+// counter-based (Philox keyed by seed and chain id).  The constructor takes the
+// Philox seed as an explicit argument (default 5418513, the driver's literal seed, driver_mgmc.cc:448)
+// and never draws from the shared engine: the reference's MultigridMCSampler consumes none at
+// construction (multigridmc_sampler.cc:8-100), so the SSOR / Cholesky samplers driver_mgmc builds
+// after it (driver_mgmc.cc:450-501) see the engine state they see in an unmodified reference.  A
+// caller that wants the seed tied to the engine passes rng() itself.  Errors print and exit(-1) like
+// the reference (multigridmc_sampler.cc:47-49).
 #pragma once
 
 #include <cstdint>
@@ -45,20 +49,18 @@
 class HipMultigridMCSampler : public Sampler {
    public:
     enum class Path { stencil, matrix };
+    static constexpr uint64_t default_seed = 5418513;  // driver_mgmc.cc:448
 
     // The reference's MultigridMCSampler(linear_operator, rng, params, cholesky_params) plus where to
-    // run: the HIP device and the chain id of the Philox key (one chain per rank, nchains per handle).
+    // run: the HIP device, the chain id of the Philox key (one chain per rank, nchains per handle) and
+    // the Philox seed.  rng_ is kept as the Sampler base keeps it and is not drawn from.
     HipMultigridMCSampler(const std::shared_ptr<LinearOperator> linear_operator_, std::mt19937_64& rng_,
-                          const MultigridParameters params_, int device = 0, uint64_t chain_id = 0, int nchains = 1)
-        : Sampler(linear_operator_, rng_), seed(rng_()) {
-        const Plan plan = classify(*linear_operator_, params_);
-        if (plan.path == Path::stencil)
-            impl.reset(new mgmc::HipMultigridMCSampler(plan.cfg, plan.stencil, device, seed, chain_id, nchains));
-        else
-            impl.reset(new mgmc::HipMultigridMCSampler(plan.cfg, (int64_t)plan.outer.size() - 1, plan.outer.data(),
-                                                       plan.inner, plan.values, device, seed, chain_id, nchains));
-        path_ = plan.path;
-        if (linear_operator_->get_m_lowrank() > 0) install_lowrank(*linear_operator_);
+                          const MultigridParameters params_, int device = 0, uint64_t chain_id = 0, int nchains = 1,
+                          uint64_t seed_ = default_seed)
+        : Sampler(linear_operator_, rng_), seed(seed_) {
+        Path path = Path::matrix;
+        impl = make_impl(*linear_operator_, params_, device, seed, chain_id, nchains, &path);
+        path_ = path;
     }
 
     // sampler.hh:41 -- one call = one MGMC cycle (multigridmc_sampler.cc:132-138), x in/out on the host
@@ -126,6 +128,24 @@ class HipMultigridMCSampler : public Sampler {
         return plan;
     }
 
+    // A device sampler for the operator: the stencil or the matrix path (classify), with a
+    // MeasuredOperator's low-rank part installed.  The Smoother drop-ins (hip_sor_smoother.hh) build
+    // their one-level handle through it too.
+    static std::unique_ptr<mgmc::HipMultigridMCSampler> make_impl(const LinearOperator& op, const MultigridParameters& p,
+                                                                  int device, uint64_t seed, uint64_t chain_id,
+                                                                  int nchains, Path* path = nullptr) {
+        const Plan plan = classify(op, p);
+        std::unique_ptr<mgmc::HipMultigridMCSampler> impl;
+        if (plan.path == Path::stencil)
+            impl.reset(new mgmc::HipMultigridMCSampler(plan.cfg, plan.stencil, device, seed, chain_id, nchains));
+        else
+            impl.reset(new mgmc::HipMultigridMCSampler(plan.cfg, (int64_t)plan.outer.size() - 1, plan.outer.data(),
+                                                       plan.inner, plan.values, device, seed, chain_id, nchains));
+        if (path) *path = plan.path;
+        if (op.get_m_lowrank() > 0) install_lowrank(op, *impl);
+        return impl;
+    }
+
    private:
     static mgmc::MultigridParameters to_mgmc(const MultigridParameters& p) {
         mgmc::MultigridParameters q;
@@ -159,13 +179,13 @@ class HipMultigridMCSampler : public Sampler {
 
     // MeasuredOperator (measured_operator.cc:9-49): B (ColMajor: colptr / row index / values, the CSC
     // form of mgmc_set_lowrank) and Sigma's diagonal
-    void install_lowrank(const LinearOperator& op) {
+    static void install_lowrank(const LinearOperator& op, mgmc::HipMultigridMCSampler& impl) {
         const LinearOperator::SparseMatrixType& B = op.get_B();
         const int m = (int)B.cols();
         std::vector<int64_t> colptr(B.outerIndexPtr(), B.outerIndexPtr() + m + 1);
         std::vector<int64_t> rows(B.innerIndexPtr(), B.innerIndexPtr() + B.nonZeros());
         const Eigen::VectorXd sigma = op.get_Sigma().diagonal();
-        impl->set_lowrank(m, colptr.data(), rows.data(), B.valuePtr(), sigma.data());
+        impl.set_lowrank(m, colptr.data(), rows.data(), B.valuePtr(), sigma.data());
     }
 
     const uint64_t seed;

@@ -20,6 +20,10 @@ from .sampler import (  # noqa: F401
     ShiftedLaplaceFEMOperator,
     SquaredShiftedLaplaceFDOperator,
     SparseMatrixOperator,
+    SORSmoother,
+    SORSmootherFactory,
+    SSORSmoother,
+    SSORSmootherFactory,
     ConstantCorrelationLengthModel,
     PeriodicCorrelationLengthModel,
     comm_unique_id,

@@ -119,6 +119,8 @@ SIGNATURES = [
     ("mgmc_get_stream", c_int, [_H, POINTER(c_void_p)]),
     ("mgmc_operator_apply", c_int, [_H, c_int, _DP, _DP]),
     ("mgmc_smoother_apply", c_int, [_H, c_int, c_int, c_int, _DP, _DP]),
+    ("mgmc_sor_smoother_apply", c_int, [_H, c_int, c_int, c_int, _DP, _DP]),
+    ("mgmc_ssor_smoother_apply", c_int, [_H, c_int, c_int, _DP, _DP]),
     ("mgmc_sor_sampler_apply", c_int, [_H, c_int, c_int, c_uint32, c_uint64, _DP, _DP]),
     ("mgmc_restrict", c_int, [_H, c_int, _DP, _DP]),
     ("mgmc_prolongate_add", c_int, [_H, c_int, c_double, _DP, _DP]),

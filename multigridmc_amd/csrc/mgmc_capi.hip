@@ -25,7 +25,8 @@
 #include "mgmc_layout_check.hpp"
 static_assert(MGMC_LAYOUT_POINT == mgmc::LF_POINT && MGMC_LAYOUT_PAIRS == mgmc::LF_PAIRS &&
                   MGMC_LAYOUT_ZSWEEP == mgmc::LF_ZSWEEP && MGMC_LAYOUT_ZSWEEP_COARSE == mgmc::LF_ZSWEEP_C &&
-                  MGMC_LAYOUT_ZRESTRICT == mgmc::LF_ZRESTRICT && MGMC_LAYOUT_RB2D == mgmc::LF_RB2D,
+                  MGMC_LAYOUT_ZRESTRICT == mgmc::LF_ZRESTRICT && MGMC_LAYOUT_RB2D == mgmc::LF_RB2D &&
+                  MGMC_LAYOUT_JSWEEP == mgmc::LF_JSWEEP && MGMC_LAYOUT_QRESTRICT == mgmc::LF_QRESTRICT,
               "layout family bits");
 #include "mgmc_zrestrict.hpp"
 #include "mgmc_tail.hpp"
@@ -309,9 +310,10 @@ struct mgmc_handle {
     double* chol_Li = nullptr;
     int chol_B = 0, chol_nb = 0; // blocked banded (chol_B > 0): Cf, Cb, Df, Db in one allocation
     double* chol_blk = nullptr;
+    bool poison = false;         // MGMC_POISON=1: NaN-filled scratch allocations and LDS (debug, poison_fill)
 };
 
-#define HIPCHK(h, call)                                                                              \
+#define HIPCHK(h, call)                                                                            \
     do {                                                                                             \
         hipError_t e_ = (call);                                                                      \
         if (e_ != hipSuccess) {                                                                      \
@@ -327,6 +329,28 @@ static int fail(mgmc_handle* h, int code, const std::string& msg) {
     set_global_error(msg);
     return code;
 }
+
+// Debug poison (MGMC_POISON=1, read at mgmc_create*): every device buffer the library does not zero
+// or fill completely at allocation (noise buffers, the QoI series, dot partials, staging, solver
+// scratch) is filled with 0xFF bytes (a NaN pattern), and every op of a captured cycle graph is
+// preceded by k_lds_poison, which fills the LDS of every CU with NaN.  A kernel that reads device
+// memory or LDS that no kernel of the cycle wrote -- recycled allocations, the previous kernel's LDS
+// -- then carries a NaN into the chain and the non-finite guard reports it (MGMC_E_NONFINITE).
+static void poison_fill(const mgmc_handle* h, void* p, size_t bytes) {
+    if (h && h->poison && p && bytes) (void)hipMemsetAsync(p, 0xFF, bytes, h->stream);
+}
+
+namespace {
+constexpr int LDS_POISON_DOUBLES = 80 * 1024 / 8;  // two 1024-thread workgroups of 80 KB fill a CU's 160 KB
+__global__ void __launch_bounds__(1024) k_lds_poison() {
+    extern __shared__ double lds[];
+    const double nan = __builtin_nan("");
+    for (int q = threadIdx.x; q < LDS_POISON_DOUBLES; q += blockDim.x) lds[q] = nan;
+    __syncthreads();
+    // a read the compiler cannot drop keeps the stores alive
+    if (lds[(threadIdx.x * 7) % LDS_POISON_DOUBLES] == 0.0) asm volatile("" ::: "memory");
+}
+}  // namespace
 
 // ------------------------------------------------------------------------------------------
 // launch helpers
@@ -548,22 +572,20 @@ void launch_jsweep(const Level& lv, const double* xin, double* xout, const doubl
     a.G = g;
     const int np = lv.L.nx / 2;
     const size_t lds = jsweep_lds_bytes(np);
-    // resident workgroups: LDS-bound (160 KB per CU), one round of them per half
-    const int slots = (int)std::max<size_t>(1, (160 * 1024) / lds) * lv.num_cu * MGMC_JS_ROUNDS;
     const bool fwd = direction == MGMC_FORWARD;
-    a.jA = fwd ? 0 : 1;  // first pair of a half: colours (0,1) / (4,5) forward, (7,6) / (3,2) backward
-    a.nsteps = (lv.L.ny - a.jA) / 2 + 1;
     for (int h = 0; h < 2; ++h) {
-        a.kp = fwd ? h : 1 - h;
+        // resident workgroups: LDS-bound (160 KB per CU), one round of them per half (jsweep_plan; the
+        // host check mgmc_layout_check.hpp jsweep_grid_check replays the same plan)
+        const JSweepPlan p = jsweep_plan(lv.L, fwd, h, lv.num_cu, lds, MGMC_JS_ROUNDS);
+        if (p.nk == 0) continue;
+        a.kp = p.kp;
+        a.jA = p.jA;  // first pair of a half: colours (0,1) / (4,5) forward, (7,6) / (3,2) backward
+        a.nsteps = p.nsteps;
+        a.nk = p.nk;
+        a.spc = p.spc;
+        a.nchunk = p.nchunk;
         a.xz = h == 0 ? xin : xout;  // the second half reads the first half's new planes
-        const int first = 2 - a.kp;
-        a.nk = first > lv.L.nz - 1 ? 0 : (lv.L.nz - 1 - first) / 2 + 1;
-        if (a.nk == 0) continue;
-        const int nchunk = std::max(1, std::min(a.nsteps, slots / a.nk));
-        a.spc = (a.nsteps + nchunk - 1) / nchunk;
-        a.nchunk = (a.nsteps + a.spc - 1) / a.spc;
-        const int nb = (a.nk * a.nchunk + 7) / 8 * 8;
-        const dim3 grid(nb, 1, nch), block(2 * np);
+        const dim3 grid(p.nb, 1, nch), block(2 * np);
         if (np == 256) {  // FEM prior's 27-point fine level at 512^3
             if (fwd) hipLaunchKernelGGL((k_jsweep_half<256, false>), grid, block, lds, s, a);
             else hipLaunchKernelGGL((k_jsweep_half<256, true>), grid, block, lds, s, a);
@@ -1537,7 +1559,15 @@ int build_tails_only(mgmc_handle* h) {
         double2* zb = nullptr;
         TailNoiseJob* dj = nullptr;
         if (pre_zr && !jobs.empty() && (int)jobs.size() <= TAIL_MAX_NOISE_JOBS && zn < (1LL << 30)) {
+            std::vector<long long> zo, zi;  // the restriction's writes / the tail's reads stay in the buffer
+            for (const TailNoiseJob& J : jobs) {
+                zo.push_back(J.zoff);
+                zi.push_back((long long)(J.nx / 2) * (J.ny - 1) * (J.nz - 1));
+            }
+            const std::string e = tail_noise_check(zo, zi, zn);
+            if (!e.empty()) return fail(h, MGMC_E_INVALID, "internal layout check failed: " + e);
             HIPCHK(h, hipMalloc(&zb, (size_t)h->nchains * zn * sizeof(double2)));
+            poison_fill(h, zb, (size_t)h->nchains * zn * sizeof(double2));
             HIPCHK(h, hipMalloc(&dj, jobs.size() * sizeof(TailNoiseJob)));
             HIPCHK(h, hipMemcpy(dj, jobs.data(), jobs.size() * sizeof(TailNoiseJob), hipMemcpyHostToDevice));
             A.zb = zb;
@@ -1631,6 +1661,7 @@ void fuse_sweep_restrict(mgmc_handle* h) {
         const long long n = (long long)co.nsweeps * (lc.L.ny - 1) * (lc.L.nx / 2);
         if (!h->zbuf) {
             if (hipMalloc(&h->zbuf, (size_t)h->nchains * n * sizeof(double2)) != hipSuccess) return;  // (draws stay in place)
+            poison_fill(h, h->zbuf, (size_t)h->nchains * n * sizeof(double2));
             h->zbuf_n = n;
         }
         if (n != h->zbuf_n) continue;
@@ -1651,6 +1682,8 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
     for (size_t q = begin; q < end; ++q) {
         const Op& op = h->ops[q];
         Level& lv = h->levels[op.level];
+        if (h->poison)  // (debug: poison_fill) the op's kernels start on NaN-filled LDS
+            hipLaunchKernelGGL(k_lds_poison, dim3(8 * lv.num_cu), dim3(1024), LDS_POISON_DOUBLES * sizeof(double), s);
         switch (op.kind) {
             case OP_SWEEP: {
                 GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
@@ -1852,6 +1885,7 @@ int ensure_series(mgmc_handle* h, uint64_t needed) {
     double* p = nullptr;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipMalloc(&p, cap * h->nchains * sizeof(double)));  // chain c's series c * cap on
+    poison_fill(h, p, cap * h->nchains * sizeof(double));
     if (h->series) HIPCHK(h, hipFree(h->series));
     h->series = p;
     h->series_cap = cap;
@@ -1863,6 +1897,7 @@ int ensure_lex(mgmc_handle* h, size_t n) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
     if (h->lex_tmp) HIPCHK(h, hipFree(h->lex_tmp));
     HIPCHK(h, hipMalloc(&h->lex_tmp, n * sizeof(double)));
+    poison_fill(h, h->lex_tmp, n * sizeof(double));
     h->lex_cap = n;
     return MGMC_OK;
 }
@@ -2153,6 +2188,16 @@ static int zrestrict_cx_of(const mgmc_handle* h, int l) {  // launch_residual_re
     if (lf.spec.dim != 3 || lf.field || (lf.paths & PATH_NO_ZRESTRICT) || lc.L.nx < 8) return 0;
     return lc.L.nx < 32 ? 16 : 64;
 }
+// both directions and both halves of a j-marching level, with launch_jsweep's plan
+static std::string jsweep_grid_check_level(const Layout& L, int num_cu) {
+    const size_t lds = jsweep_lds_bytes(L.nx / 2);
+    for (int d = 0; d < 2; ++d)
+        for (int half = 0; half < 2; ++half) {
+            const std::string e = jsweep_grid_check(L, jsweep_plan(L, d == 0, half, num_cu, lds, MGMC_JS_ROUNDS), JS_D);
+            if (!e.empty()) return e;
+        }
+    return "";
+}
 static std::string check_level_layout_of(const mgmc_handle* h, int l) {
     const Level& lv = h->levels[l];
     unsigned fam = LF_POINT;
@@ -2162,8 +2207,12 @@ static std::string check_level_layout_of(const mgmc_handle* h, int l) {
     const int cx = zrestrict_cx_of(h, l);
     if (cx) fam |= LF_ZRESTRICT;
     if (l > 0 && h->levels[l - 1].zsweep) fam |= LF_ZSWEEP_C;
+    if (lv.jsweep) fam |= LF_JSWEEP;
+    if (qrestrict_ok(h, l)) fam |= LF_QRESTRICT;
     const int reach = lv.field && (lv.F.scheme == 9 || lv.F.scheme == 27) ? 2 : 1;
-    return check_level_layout(lv.L, fam, reach, cx);
+    std::string e = check_level_layout(lv.L, fam, reach, cx);
+    if (e.empty() && lv.jsweep) e = jsweep_grid_check_level(lv.L, lv.num_cu);
+    return e;
 }
 
 // mgmc_create / mgmc_create_csr: csr = the fine operator's matrix (null: the constant-coefficient
@@ -2197,6 +2246,7 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
     mgmc_handle* h = new mgmc_handle();
     h->paths = paths;
     if (const char* u = getenv("MGMC_GRAPH_UNROLL")) h->unroll_override = std::max(1, std::min(64, atoi(u)));
+    if (const char* u = getenv("MGMC_POISON")) h->poison = atoi(u) != 0;
     h->cfg = *cfg;
     h->device = device;
     h->seed = seed;
@@ -2411,7 +2461,8 @@ int mgmc_check_layout(int dim, const int* n, int reach, unsigned families, int z
     if (!n || (dim != 2 && dim != 3) || reach < 1 || reach > 2) return fail(nullptr, MGMC_E_INVALID, "invalid argument");
     // legacy bit 0: the round-2 layout without the reach-2 margin; bit 1: unclamped restriction columns
     const Layout L = make_layout(dim, n, reach == 2 && !(legacy & 1));
-    const std::string e = check_level_layout(L, families, reach, zrestrict_cx, (legacy & 2) != 0);
+    std::string e = check_level_layout(L, families, reach, zrestrict_cx, (legacy & 2) != 0);
+    if (e.empty() && (families & LF_JSWEEP)) e = jsweep_grid_check_level(L, 256);  // MI355X: 256 CUs
     if (!e.empty()) return fail(nullptr, MGMC_E_INVALID, e);
     return MGMC_OK;
 }
@@ -2760,6 +2811,7 @@ int mgmc_set_qoi_vector(mgmc_handle* h, int64_t nnz, const int64_t* rows, const 
             return fail(h, MGMC_E_NOMEM, "device allocation failed (QoI vector)");
         HIPCHK(h, hipMemcpy(h->qv_off, off.data(), nnz * sizeof(long long), hipMemcpyHostToDevice));
         HIPCHK(h, hipMemcpy(h->qv_val, vals, nnz * sizeof(double), hipMemcpyHostToDevice));
+        poison_fill(h, h->qv_part, (size_t)nblk * h->nchains * sizeof(double));
         h->qv_n = nnz;
         h->qv_nblk = nblk;
     }
@@ -2884,6 +2936,48 @@ static int sweep_component(mgmc_handle* h, int level, int direction, int nsweeps
 
 int mgmc_smoother_apply(mgmc_handle* h, int level, int direction, int nsweeps, const double* b, double* x) {
     return sweep_component(h, level, direction, nsweeps, false, 0, 0, b, x);
+}
+
+// noise-free sweeps on one level in a given order, the low-rank fix after the marked ones
+// (the Smoother drop-ins below); x stays on the device between the sweeps
+static int smoother_sequence(mgmc_handle* h, int level, const std::vector<std::pair<int, bool>>& seq,
+                             const double* b, double* x) {
+    int rc = check_level(h, level, false);
+    if (rc) return rc;
+    if (!b || !x) return fail(h, MGMC_E_INVALID, "null argument");
+    HIPCHK(h, hipSetDevice(h->device));
+    if ((rc = ensure_scratch(h, level))) return rc;
+    Level& lv = h->levels[level];
+    if ((rc = upload(h, level, b, lv.scratch[0]))) return rc;
+    if ((rc = upload(h, level, x, lv.scratch[1]))) return rc;
+    for (const auto& st : seq) {
+        GibbsArg g = make_gibbs(h, lv, 0, 0, h->ctrl + 3);
+        launch_sweep(lv, lv.scratch[1], lv.scratch[0], g, st.first, false, h->stream);
+        if (st.second && lv.lr.m > 0) lr_fix(lv, lv.scratch[1], st.first, nullptr, h->stream);
+    }
+    HIPCHK(h, hipGetLastError());
+    return download(h, level, lv.scratch[1], x);
+}
+
+int mgmc_sor_smoother_apply(mgmc_handle* h, int level, int direction, int nsmooth, const double* b, double* x) {
+    if (direction != MGMC_FORWARD && direction != MGMC_BACKWARD) return fail(h, MGMC_E_INVALID, "invalid direction");
+    if (nsmooth < 0) return fail(h, MGMC_E_INVALID, "nsmooth must be >= 0");
+    // SORSmoother::apply (sor_smoother.cc:41-53) over apply_sparse (:56-78): both loop nsmooth times
+    std::vector<std::pair<int, bool>> seq;
+    for (int k = 0; k < nsmooth; ++k)
+        for (int j = 0; j < nsmooth; ++j) seq.push_back({direction, j == nsmooth - 1});
+    return smoother_sequence(h, level, seq, b, x);
+}
+
+int mgmc_ssor_smoother_apply(mgmc_handle* h, int level, int nsmooth, const double* b, double* x) {
+    if (nsmooth < 0) return fail(h, MGMC_E_INVALID, "nsmooth must be >= 0");
+    // SSORSmoother::apply (ssor_smoother.cc:9-15): its SORSmoothers have nsmooth 1 (ssor_smoother.hh:47-48)
+    std::vector<std::pair<int, bool>> seq;
+    for (int k = 0; k < nsmooth; ++k) {
+        seq.push_back({MGMC_FORWARD, true});
+        seq.push_back({MGMC_BACKWARD, true});
+    }
+    return smoother_sequence(h, level, seq, b, x);
 }
 
 int mgmc_sor_sampler_apply(mgmc_handle* h, int level, int direction, uint32_t sweep_tag, uint64_t sample_index,
@@ -3166,8 +3260,14 @@ int mgmc_solve(mgmc_handle* h, int method, const double* b, double* x, double rt
                                     (int)h->lr_cols.size())))
             return rc;
     }
-    if (!h->sv_scal) HIPCHK(h, hipMalloc(&h->sv_scal, 16 * sizeof(double)));
-    if (!h->sv_part) HIPCHK(h, hipMalloc(&h->sv_part, SOLVE_NB * sizeof(double)));
+    if (!h->sv_scal) {
+        HIPCHK(h, hipMalloc(&h->sv_scal, 16 * sizeof(double)));
+        poison_fill(h, h->sv_scal, 16 * sizeof(double));
+    }
+    if (!h->sv_part) {
+        HIPCHK(h, hipMalloc(&h->sv_part, SOLVE_NB * sizeof(double)));
+        poison_fill(h, h->sv_part, SOLVE_NB * sizeof(double));
+    }
     double *vb = h->sv[0], *vx = h->sv[1], *vr = h->sv[2], *vz = h->sv[3], *vp = h->sv[4], *vq = h->sv[5];
     hipStream_t s = h->stream;
     const dim3 gv(4096), bv(256);
@@ -3530,6 +3630,19 @@ int mgmc_set_lowrank(mgmc_handle* h, int m, const int64_t* colptr, const int64_t
     }
     if (!rc && h->chol_n > 0)  // the coarse factors carry B_c Sigma^{-1} B_c^T
         rc = build_coarse_chol(h, m > 0 ? &cols : nullptr, sigma, m);
+    if (rc) {
+        // no half-installed posterior: a failure (a coarse band the blocked Cholesky cannot take, the
+        // host work limit, an allocation) leaves the handle with the prior -- no low-rank part on any
+        // level and the prior's coarse factors -- and the error code.  The levels' low-rank parts are
+        // installed before the coarse factor is built, so they are removed again here.
+        const std::string err = h->last_error;
+        for (auto& lv : h->levels) free_lowrank(lv.lr);
+        h->lr_cols.clear();
+        h->lr_sigma.clear();
+        if (h->chol_n > 0) (void)build_coarse_chol(h, nullptr, nullptr, 0);  // (succeeded at mgmc_create)
+        h->last_error = err;
+        set_global_error(err);
+    }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     build_ops(h);
     int rc2 = build_tails(h);

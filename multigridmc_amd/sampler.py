@@ -550,8 +550,10 @@ class MultigridMCSampler:
         self._chk(self.lib.mgmc_sample_timed_stride(self.handle, int(nsteps), int(stride), int(qoi_index),
                                                     ctypes.byref(tot), ctypes.byref(pre), ctypes.byref(npre),
                                                     ctypes.byref(post), ctypes.byref(npost)))
+        # the timed cycles: every stride-th and the last (mgmc_sample_timed_stride's selection)
+        ncyc = sum(1 for s in range(int(nsteps)) if s % int(stride) == 0 or s == int(nsteps) - 1)
         return {"total_ms": tot.value, "pre_ms": pre.value, "npre": npre.value, "post_ms": post.value,
-                "npost": npost.value}
+                "npost": npost.value, "ncycles_timed": ncyc}
 
     def qoi_moments(self, chain: int = 0):
         out = np.zeros(3)
@@ -613,6 +615,21 @@ class MultigridMCSampler:
         b = _as_f64(b, n, "b")
         out = _as_f64(x, n, "x").copy()
         self._chk(self.lib.mgmc_smoother_apply(self.handle, level, direction, nsweeps, _dp(b), _dp(out)))
+        return out
+
+    def sor_smoother_apply(self, level: int, direction: int, nsmooth: int, b, x) -> np.ndarray:
+        """SORSmoother::apply (sor_smoother.cc:41-53 over apply_sparse :56-78): nsmooth x (nsmooth
+        noise-free multicolour sweeps, then the B_bar fix once)."""
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        out = np.ascontiguousarray(x, dtype=np.float64).copy()
+        self._chk(self.lib.mgmc_sor_smoother_apply(self.handle, level, direction, nsmooth, _dp(b), _dp(out)))
+        return out
+
+    def ssor_smoother_apply(self, level: int, nsmooth: int, b, x) -> np.ndarray:
+        """SSORSmoother::apply (ssor_smoother.cc:9-15): nsmooth x (forward sweep + fix, backward + fix)."""
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        out = np.ascontiguousarray(x, dtype=np.float64).copy()
+        self._chk(self.lib.mgmc_ssor_smoother_apply(self.handle, level, nsmooth, _dp(b), _dp(out)))
         return out
 
     def sor_sampler_apply(self, level: int, direction: int, tag: int, sample_index: int, f, x) -> np.ndarray:
@@ -708,8 +725,79 @@ class HipMulticolourSORSmoother:
         x[:] = self.sampler.smoother_apply(self.level, self.direction, self.nsmooth, b, x)
 
 
+class _OneLevelSmoother:
+    """A Smoother (smoother/smoother.hh:15-34) on its own device handle: the operator as a one-level
+    hierarchy (MultigridMCSampler with nlevel 1; a MeasuredOperator's B / Sigma installed, so the
+    B_bar fix of sor_smoother.cc:17-51 runs), the state uploaded per apply (host vectors, like the
+    reference's Eigen vectors)."""
+
+    def __init__(self, linear_operator, omega: float, device: int):
+        self.linear_operator = linear_operator
+        self.omega = float(omega)
+        p = MultigridParameters(nlevel=1, smoother="SOR", coarse_solver="SSOR", npresmooth=1, npostsmooth=1,
+                                ncoarsesmooth=1, omega=self.omega, cycle=1, coarse_scaling=1.0)
+        self._s = MultigridMCSampler(linear_operator, 0, p, device=device)
+
+    def close(self):
+        self._s.close()
+
+    def _check(self, b, x):
+        n = self.linear_operator.get_ndof()
+        if len(b) != n or len(x) != n:
+            raise ValueError(f"vector sizes {len(b)} / {len(x)}, operator {n}")
+
+
+class SORSmoother(_OneLevelSmoother):
+    """SORSmoother(linear_operator, omega, nsmooth, direction) (smoother/sor_smoother.hh:53-60):
+    apply(b, x) is the reference's SORSmoother::apply -- nsmooth x (nsmooth sweeps, then the
+    low-rank fix), sor_smoother.cc:41-78 -- with multicolour sweeps."""
+
+    def __init__(self, linear_operator, omega: float, nsmooth: int, direction: int, device: int = 0):
+        if direction not in (FORWARD, BACKWARD):
+            raise ValueError("direction must be FORWARD (1) or BACKWARD (2)")
+        super().__init__(linear_operator, omega, device)
+        self.nsmooth, self.direction = int(nsmooth), int(direction)
+
+    def apply(self, b, x: np.ndarray):
+        self._check(b, x)
+        x[:] = self._s.sor_smoother_apply(0, self.direction, self.nsmooth, b, x)
+
+
+class SSORSmoother(_OneLevelSmoother):
+    """SSORSmoother(linear_operator, omega, nsmooth) (smoother/ssor_smoother.hh:31-48): nsmooth x
+    (forward SOR sweep + fix, backward SOR sweep + fix), ssor_smoother.cc:9-15."""
+
+    def __init__(self, linear_operator, omega: float, nsmooth: int, device: int = 0):
+        super().__init__(linear_operator, omega, device)
+        self.nsmooth = int(nsmooth)
+
+    def apply(self, b, x: np.ndarray):
+        self._check(b, x)
+        x[:] = self._s.ssor_smoother_apply(0, self.nsmooth, b, x)
+
+
+class SORSmootherFactory:
+    """SmootherFactory (smoother/smoother.hh:39-44) of SORSmoother (sor_smoother.hh:91-125)."""
+
+    def __init__(self, omega: float, nsmooth: int, direction: int, device: int = 0):
+        self.omega, self.nsmooth, self.direction, self.device = omega, nsmooth, direction, device
+
+    def get(self, linear_operator) -> SORSmoother:
+        return SORSmoother(linear_operator, self.omega, self.nsmooth, self.direction, self.device)
+
+
+class SSORSmootherFactory:
+    """SmootherFactory of SSORSmoother (ssor_smoother.hh:70-100)."""
+
+    def __init__(self, omega: float, nsmooth: int, device: int = 0):
+        self.omega, self.nsmooth, self.device = omega, nsmooth, device
+
+    def get(self, linear_operator) -> SSORSmoother:
+        return SSORSmoother(linear_operator, self.omega, self.nsmooth, self.device)
+
+
 __all__ = [
     "Lattice", "Lattice2d", "Lattice3d", "ShiftedLaplaceFDOperator", "MultigridMCSampler",
-    "HipMulticolourSORSmoother", "measurement_vector_index", "ConstantCorrelationLengthModel",
+    "HipMulticolourSORSmoother", "SORSmoother", "SSORSmoother", "SORSmootherFactory", "SSORSmootherFactory", "measurement_vector_index", "ConstantCorrelationLengthModel",
     "PeriodicCorrelationLengthModel", "SquaredShiftedLaplaceFDOperator", "comm_unique_id", "make_config", "describe", "FORWARD", "BACKWARD",
 ]

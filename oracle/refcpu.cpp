@@ -1029,9 +1029,13 @@ struct SORSmoother {
             }
         bbar_mode = mode;
     }
-    // SORSmoother::apply (sor_smoother.cc:41-53): sweep, then x -= bar(B) (B^T x)
+    // SORSmoother::apply (sor_smoother.cc:41-53) with nsmooth = 1: sweep, then x -= bar(B) (B^T x)
     void apply(Mode mode, const double* b, double* x) const {
         sweep(mode, b, x);
+        fix(mode, x);
+    }
+    // the low-rank update after apply_sparse (sor_smoother.cc:46-51): x -= bar(B) (B^T x)
+    void fix(Mode mode, double* x) const {
         const int m = L->lr.m;
         if (m == 0) return;
         if (bbar.empty() || bbar_mode != mode) build_bbar(mode);
@@ -1727,6 +1731,28 @@ void orc_get_lowrank(orc_handle* h, int level, int64_t* colptr, int64_t* rows, d
 void orc_smoother_apply(orc_handle* h, int level, int direction, int nsweeps, const double* b, double* x) {
     SORSmoother s(h->mg->levels[level].get(), h->mg->p.omega, (Direction)direction);
     for (int k = 0; k < nsweeps; ++k) s.apply(h->ctx.mode, b, x);
+}
+
+// SORSmoother::apply as the reference nests it (sor_smoother.cc:41-53 loops nsmooth times over
+// apply_sparse, which loops nsmooth times over the sweep itself, :64): nsmooth x (nsmooth sweeps, then
+// the low-rank fix once)
+void orc_sor_smoother_apply(orc_handle* h, int level, int direction, int nsmooth, const double* b, double* x) {
+    SORSmoother s(h->mg->levels[level].get(), h->mg->p.omega, (Direction)direction);
+    for (int k = 0; k < nsmooth; ++k) {
+        for (int j = 0; j < nsmooth; ++j) s.sweep(h->ctx.mode, b, x);
+        s.fix(h->ctx.mode, x);
+    }
+}
+
+// SSORSmoother::apply (ssor_smoother.cc:9-15; smoothers built with nsmooth 1, ssor_smoother.hh:47-48):
+// nsmooth x (forward sweep + fix, backward sweep + fix)
+void orc_ssor_smoother_apply(orc_handle* h, int level, int nsmooth, const double* b, double* x) {
+    SORSmoother fw(h->mg->levels[level].get(), h->mg->p.omega, FORWARD);
+    SORSmoother bw(h->mg->levels[level].get(), h->mg->p.omega, BACKWARD);
+    for (int k = 0; k < nsmooth; ++k) {
+        fw.apply(h->ctx.mode, b, x);
+        bw.apply(h->ctx.mode, b, x);
+    }
 }
 
 // one noisy sweep with explicit (tag, sample) in multicolour mode (SORSampler, nsmooth = 1)

@@ -5,6 +5,13 @@
 //
 //   adapter_client describe                  which path each operator takes (host only)
 //   adapter_client sample <n> <fd|fem|periodic>   seed, path, then n QoI values of apply() cycles
+//   adapter_client rngcheck                  constructs a sampler on the driver's shared engine and
+//                                            reports (also from an atexit handler, so a failed device
+//                                            call's exit(-1) reports too) whether the engine moved
+//   adapter_client smoother <fd|fem|periodic> <sor|ssor> <nsmooth> <fwd|bwd> [lowrank]
+//                                            b, x and x after one Smoother::apply(b, x) of the Smoother
+//                                            drop-in (b, x from a fixed mt19937_64 stream); "lowrank" adds two
+//                                            point measurements (MeasuredOperator-like B, Sigma)
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -14,6 +21,7 @@
 #include <vector>
 
 #include "hip_multigridmc_sampler.hh"
+#include "hip_sor_smoother.hh"
 
 namespace {
 
@@ -45,7 +53,8 @@ class TestLattice : public Lattice {
 // its CSR arrays are its ColMajor arrays)
 class AssembledOperator : public LinearOperator {
    public:
-    AssembledOperator(std::shared_ptr<Lattice> lat, int pde, bool periodic) : LinearOperator(lat, 0) {
+    AssembledOperator(std::shared_ptr<Lattice> lat, int pde, bool periodic, bool lowrank = false)
+        : LinearOperator(lat, lowrank ? 2 : 0) {
         const Eigen::VectorXi s = lat->shape();
         mgmc_operator_desc d{};
         d.dim = lat->dim();
@@ -65,6 +74,12 @@ class AssembledOperator : public LinearOperator {
         mgmc::check(mgmc_operator_csr(&d, rowptr.data(), col.data(), val.data()), nullptr, "mgmc_operator_csr");
         A_sparse.assign_compressed(std::vector<int>(rowptr.begin(), rowptr.end()), std::vector<int>(col.begin(), col.end()),
                                    std::move(val));
+        if (lowrank) {  // two point measurements (rows N/3, 2N/3), Sigma = diag(1e-3, 2e-3)
+            const int n = (int)nrow;
+            B.assign_compressed({0, 1, 2}, {n / 3, 2 * n / 3}, {1.0, 1.0});
+            Sigma_diag.diagonal()[0] = 1e-3;
+            Sigma_diag.diagonal()[1] = 2e-3;
+        }
     }
 };
 
@@ -83,15 +98,20 @@ MultigridParameters params(unsigned nlevel) {
     return p;
 }
 
-std::shared_ptr<LinearOperator> make_op(const std::string& kind) {
-    if (kind == "fd") return std::make_shared<AssembledOperator>(std::make_shared<TestLattice>(std::vector<int>{16, 16, 16}), MGMC_OPERATOR_FD, false);
-    if (kind == "fem") return std::make_shared<AssembledOperator>(std::make_shared<TestLattice>(std::vector<int>{16, 16, 16}), MGMC_OPERATOR_FEM, false);
-    if (kind == "periodic") return std::make_shared<AssembledOperator>(std::make_shared<TestLattice>(std::vector<int>{32, 32}), MGMC_OPERATOR_FD, true);
+std::shared_ptr<LinearOperator> make_op(const std::string& kind, bool lowrank = false) {
+    if (kind == "fd") return std::make_shared<AssembledOperator>(std::make_shared<TestLattice>(std::vector<int>{16, 16, 16}), MGMC_OPERATOR_FD, false, lowrank);
+    if (kind == "fem") return std::make_shared<AssembledOperator>(std::make_shared<TestLattice>(std::vector<int>{16, 16, 16}), MGMC_OPERATOR_FEM, false, lowrank);
+    if (kind == "periodic") return std::make_shared<AssembledOperator>(std::make_shared<TestLattice>(std::vector<int>{32, 32}), MGMC_OPERATOR_FD, true, lowrank);
     std::fprintf(stderr, "unknown operator %s\n", kind.c_str());
     std::exit(2);
 }
 
 const char* name(HipMultigridMCSampler::Path p) { return p == HipMultigridMCSampler::Path::stencil ? "stencil" : "matrix"; }
+
+// rngcheck: the driver's engine and a copy of its state at construction time
+std::mt19937_64 g_rng(5418513);  // driver_mgmc.cc:448-449
+std::mt19937_64 g_rng_before;
+void report_engine() { std::printf("engine %s\n", g_rng == g_rng_before ? "unchanged" : "CHANGED"); std::fflush(stdout); }
 
 }  // namespace
 
@@ -122,6 +142,38 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
-    std::fprintf(stderr, "usage: adapter_client describe | sample <n> <fd|fem|periodic>\n");
+    if (mode == "rngcheck") {
+        g_rng_before = g_rng;
+        std::atexit(report_engine);  // runs on the exit(-1) of a failed device call too
+        HipMultigridMCSampler sampler(make_op("fd"), g_rng, params(3), /*device=*/0, /*chain_id=*/0);
+        std::printf("seed %llu\n", (unsigned long long)sampler.get_seed());
+        return 0;
+    }
+    if (mode == "smoother" && argc > 5) {
+        const bool lowrank = argc > 6 && std::string(argv[6]) == "lowrank";
+        const std::shared_ptr<LinearOperator> op = make_op(argv[2], lowrank);
+        const std::string kind = argv[3];
+        const int nsmooth = std::atoi(argv[4]);
+        const Direction dir = std::string(argv[5]) == "bwd" ? backward : forward;
+        std::shared_ptr<SmootherFactory> factory;
+        if (kind == "sor")
+            factory = std::make_shared<HipSORSmootherFactory>(1.0, nsmooth, dir);
+        else
+            factory = std::make_shared<HipSSORSmootherFactory>(1.0, nsmooth);
+        const std::shared_ptr<Smoother> smoother = factory->get(op);  // multigrid_preconditioner.cc:18-33
+        const std::ptrdiff_t ndof = (std::ptrdiff_t)op->get_ndof();
+        Eigen::VectorXd b(ndof), x(ndof);
+        std::mt19937_64 r(7);
+        std::uniform_real_distribution<double> u(-1.0, 1.0);
+        for (std::ptrdiff_t i = 0; i < ndof; ++i) b[i] = u(r);
+        for (std::ptrdiff_t i = 0; i < ndof; ++i) x[i] = u(r);
+        for (std::ptrdiff_t i = 0; i < ndof; ++i) std::printf("%.17g\n", b[i]);
+        for (std::ptrdiff_t i = 0; i < ndof; ++i) std::printf("%.17g\n", x[i]);
+        smoother->apply(b, x);
+        for (std::ptrdiff_t i = 0; i < ndof; ++i) std::printf("%.17g\n", x[i]);
+        return 0;
+    }
+    std::fprintf(stderr, "usage: adapter_client describe | sample <n> <fd|fem|periodic> | rngcheck | "
+                         "smoother <fd|fem|periodic> <sor|ssor> <nsmooth> <fwd|bwd> [lowrank]\n");
     return 2;
 }

@@ -55,6 +55,8 @@ def lib():
             "orc_set_state": (None, [c_void_p, _DP]),
             "orc_get_state": (None, [c_void_p, _DP]),
             "orc_set_sample_index": (None, [c_void_p, c_uint64]),
+            "orc_sor_smoother_apply": (None, [c_void_p, c_int, c_int, c_int, _DP, _DP]),
+            "orc_ssor_smoother_apply": (None, [c_void_p, c_int, c_int, _DP, _DP]),
             "orc_reseed": (None, [c_void_p, c_uint64, c_uint64]),
             "orc_operator_nnz": (c_int64, [c_int, POINTER(c_int), c_int, c_int, c_double, c_double, c_double]),
             "orc_operator_csr": (None, [c_int, POINTER(c_int), c_int, c_int, c_double, c_double, c_double,
@@ -207,6 +209,9 @@ class Oracle:
         x = np.ascontiguousarray(x, dtype=np.float64)
         self.L.orc_set_state(self.h, dp(x))
 
+    def set_sample_index(self, index):
+        self.L.orc_set_sample_index(self.h, int(index))
+
     def get_state(self):
         x = np.empty(self.ndof())
         self.L.orc_get_state(self.h, dp(x))
@@ -238,6 +243,20 @@ class Oracle:
         b = np.ascontiguousarray(b, dtype=np.float64)
         out = np.ascontiguousarray(x, dtype=np.float64).copy()
         self.L.orc_smoother_apply(self.h, level, direction, nsweeps, dp(b), dp(out))
+        return out
+
+    def sor_smoother_apply(self, level, direction, nsmooth, b, x):
+        """SORSmoother::apply with the reference's nesting: nsmooth x (nsmooth sweeps, low-rank fix)."""
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        out = np.ascontiguousarray(x, dtype=np.float64).copy()
+        self.L.orc_sor_smoother_apply(self.h, level, direction, nsmooth, dp(b), dp(out))
+        return out
+
+    def ssor_smoother_apply(self, level, nsmooth, b, x):
+        """SSORSmoother::apply: nsmooth x (forward + fix, backward + fix)."""
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        out = np.ascontiguousarray(x, dtype=np.float64).copy()
+        self.L.orc_ssor_smoother_apply(self.h, level, nsmooth, dp(b), dp(out))
         return out
 
     def sor_sampler_apply(self, level, direction, tag, sample, f, x):

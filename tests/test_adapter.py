@@ -104,3 +104,29 @@ def test_reference_adapter_compiles_and_links(tmp_path):
     if not os.path.exists("/dev/kfd"):
         r = subprocess.run([exe, "sample", "2", "fd"], capture_output=True, text=True)
         assert r.returncode == 255 and "no HIP device" in r.stderr
+
+
+def test_adapter_construction_leaves_the_shared_engine_alone(tmp_path):
+    """HipMultigridMCSampler takes its Philox seed as an argument (default 5418513,
+    driver_mgmc.cc:448) and never draws from the driver's std::mt19937_64, as the reference's
+    MultigridMCSampler draws none at construction -- so the SSOR / Cholesky samplers driver_mgmc builds
+    after it (driver_mgmc.cc:450-501) see an unmodified engine.  The client compares the engine with a
+    copy from before the construction, from an atexit handler too (without a GPU the construction ends
+    in the adapter's exit(-1))."""
+    exe = build_adapter_client(str(tmp_path))
+    r = subprocess.run([exe, "rngcheck"], capture_output=True, text=True)
+    assert "engine unchanged" in r.stdout, (r.stdout, r.stderr)
+    assert "engine CHANGED" not in r.stdout
+    if r.returncode == 0:
+        assert "seed 5418513" in r.stdout
+
+
+def test_smoother_adapter_compiles(tmp_path):
+    """include/reference_adapter/hip_sor_smoother.hh (HipSORSmoother / HipSSORSmoother : public
+    Smoother and their SmootherFactory classes) compiles and links in the same client, against the
+    restated smoother/smoother.hh and sor_smoother.hh declarations; without a GPU the first device call
+    fails the reference's way."""
+    exe = build_adapter_client(str(tmp_path))
+    if not os.path.exists("/dev/kfd"):
+        r = subprocess.run([exe, "smoother", "fd", "sor", "1", "fwd"], capture_output=True, text=True)
+        assert r.returncode == 255 and "no HIP device" in r.stderr

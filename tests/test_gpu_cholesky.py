@@ -107,7 +107,16 @@ def test_dense_lowrank_column_band_unsupported(hip_device):
     with pytest.raises(mg.MgmcError, match="bandwidth") as e:
         s.set_lowrank(op.get_B())
     assert e.value.code == _native.MGMC_E_UNSUPPORTED
+    # the failed call leaves the prior: the handle samples exactly what a fresh prior handle
+    # samples -- no posterior smoothers left on the levels with a prior-only coarse factor
+    q = mg.measurement_vector_index(lat, [0.5, 0.5])
+    z = s.sample(5, q)
+    x = s.get_state()
     s.close()
+    fresh = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), SEED, p)
+    assert np.array_equal(z, fresh.sample(5, q))
+    assert np.array_equal(x, fresh.get_state())
+    fresh.close()
     with pytest.raises(mg.MgmcError, match="bandwidth"):  # lexicographic band of 8191 unknowns
         _make((8192, 8), dict(nlevel=1))
     with pytest.raises(mg.MgmcError, match="host work limit"):  # 63^3 unknowns, bandwidth 4033

@@ -103,7 +103,8 @@ def test_headline_cycle_and_qoi_series_bitwise(headline):
     device-resident measure_sampling_time loop (driver_mgmc.cc:66-78) for 3 samples with the QoI at
     the lattice centre: cycle state, QoI series and final state equal the oracle's exactly.  This
     runs the benchmark's graph: fused-prolongation post-sweep (128-plane chunks), k_zresrestrict
-    <7,64,8,512>, the level-1 and level-2 j-marching half-sweeps, the 512^3 k_tail and the QoI record."""
+    <7,64,8,512>, the level-1 j-marching half-sweeps, the level-2 colour-pair passes, the 512^3 k_tail and
+    the QoI record."""
     s, orc, lat, p = headline
     f = np.random.default_rng(11).standard_normal(lat.Nvertex)
     x_dev = np.zeros(lat.Nvertex)
@@ -130,6 +131,36 @@ def test_headline_cycle_and_qoi_series_bitwise(headline):
     assert s.get_sample_index() == 4
 
 
+def test_headline_same_seed_handles_match_oracle(headline):
+    """Determinism at the headline size, pinned to the oracle: three fresh handles
+    with the same (seed, chain) -- each allocated after the previous one was freed, so each runs on
+    recycled device memory -- start from one state (x, f, sample index) and run 4 prior cycles of the
+    benchmark graph; every QoI series and final state equals the MULTICOLOUR oracle's, not just each
+    other.  With MGMC_POISON=1 (scripts/determinism_512.py) unzeroed buffers and the LDS start as NaN."""
+    s, orc, lat, p = headline
+    qoi = mg.measurement_vector_index(lat, [0.5, 0.5, 0.5])
+    rng = np.random.default_rng(12)
+    x0 = 0.01 * rng.standard_normal(lat.Nvertex)
+    f = np.zeros(lat.Nvertex)  # prior (driver_mgmc configs 2-4: f = 0)
+    t0 = time.time()
+    orc.set_rhs(f)
+    orc.set_state(x0)
+    orc.set_sample_index(7)
+    z_orc = orc.sample(4, qoi)
+    x_orc = orc.get_state()
+    _log(f"oracle 4 cycles: {time.time() - t0:.1f} s")
+    for r in range(3):
+        h = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), SEED, p, device=0, chain_id=0)
+        h.fix_rhs(f)
+        h.set_state(x0)
+        h.set_sample_index(7)
+        z = h.sample(4, qoi)
+        same_z, same_x = bool(np.array_equal(z, z_orc)), bool(np.array_equal(h.get_state(), x_orc))
+        _log(f"handle {r}: series {'==' if same_z else '!='} oracle, state {'==' if same_x else '!='} oracle")
+        h.close()
+        assert same_z and same_x, (r, z.tolist(), z_orc.tolist())
+
+
 def test_headline_kernel_instances(headline):
     """The instances the tests above ran are the benchmark's (mgmc_level_kernels): the fused z-sweep
     pair on level 0 with the 64 x 8 residual + restriction, j-marching half-sweeps on level 1, k_tail below."""
@@ -138,4 +169,5 @@ def test_headline_kernel_instances(headline):
     assert k0["sweep"].startswith("k_zsweep_rb7<") and k0["post_sweep"].endswith("PROLONG>")
     assert k0["residual_restrict"] == "k_zresrestrict<7,64,8>"
     assert s.level_kernels(1) == {"sweep": "k_jsweep_half<128>", "residual_restrict": "k_zresrestrict<27,64,4>"}
+    assert s.level_kernels(2)["sweep"] == "k_sweep_pairs<3>"  # 64-pair rows: neither j-marching nor quads
     assert s.level_kernels(NLEVEL - 1)["sweep"] == "k_tail<3>"

@@ -3,6 +3,7 @@ include/mgmc.h, configuration validation, Galerkin stencils vs the oracle's SpGE
 libconfig-subset parser, QoI indexing, and the rank-order moment merge (gloo, world_size 2)."""
 import ctypes
 import os
+import sys
 import re
 
 import numpy as np
@@ -93,14 +94,15 @@ def test_unknown_disable_token_rejected_before_any_device_call(monkeypatch):
 
 def test_product_reads_only_documented_switches():
     """The only environment the library reads: MGMC_DISABLE (kernel-path switches, each covered by
-    tests/test_gpu_parity.py VARIANTS / test_gpu_lowrank.py) and MGMC_GRAPH_UNROLL
-    (test_unrolled_sample_loop_bitwise)."""
+    tests/test_gpu_parity.py VARIANTS / test_gpu_lowrank.py), MGMC_GRAPH_UNROLL
+    (test_unrolled_sample_loop_bitwise) and MGMC_POISON (debug: NaN-filled scratch and LDS,
+    scripts/gpu_r4a.sh runs the headline determinism test with it)."""
     src = ""
     csrc = os.path.join(ROOT, "multigridmc_amd", "csrc")
     for fn in os.listdir(csrc):
         if fn.endswith((".hip", ".hpp", ".cpp", ".h")):
             src += open(os.path.join(csrc, fn)).read()
-    assert sorted(set(re.findall(r'getenv\("([A-Z_0-9]+)"\)', src))) == ["MGMC_DISABLE", "MGMC_GRAPH_UNROLL"]
+    assert sorted(set(re.findall(r'getenv\("([A-Z_0-9]+)"\)', src))) == ["MGMC_DISABLE", "MGMC_GRAPH_UNROLL", "MGMC_POISON"]
     tokens = re.findall(r'\{"([a-z_0-9]+)", PATH_NO_', src)
     assert len(tokens) == 16
     tested = open(os.path.join(ROOT, "tests", "test_gpu_parity.py")).read() + \
@@ -380,3 +382,50 @@ def test_bench_collectives_world2(mode):
                 assert "share GPUs" in msg
             if mode == "short":
                 assert "spans 1 ranks" in msg
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("mode", ["shared", "rehearsal", "distinct"])
+def test_bench_world2_through_torchrun(mode):
+    """the driver's N > 1 launch line itself --
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1
+    --master-port P bench.py --gpus 2 --steps K --warmup W -- end to end through bench.main() on two
+    gloo ranks (tests/bench_rehearsal.py stands in only for the device sampler).  Ranks sharing one
+    device without MGMC_BENCH_DEVICE exit 2 ("share GPUs"); with it they rehearse on gloo collectives
+    and the line says so; on distinct devices the line reports the RCCL communicator's 2 ranks.  The
+    JSON line's value is the whole job's rate (2 chains x K / max-over-ranks time)."""
+    import json
+    import subprocess
+    env = dict(os.environ)
+    env.pop("MGMC_BENCH_DEVICE", None)
+    env["MGMC_FAKE_MODE"] = "distinct" if mode == "distinct" else "shared"
+    if mode == "rehearsal":
+        env["MGMC_BENCH_DEVICE"] = "0"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "tests", "bench_rehearsal.py"),
+           "--gpus", "2", "--steps", "6", "--warmup", "2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, cwd=ROOT, timeout=240)
+    if mode == "shared":
+        assert r.returncode != 0
+        assert "share GPUs" in r.stderr and "(exitcode: 2)" in r.stderr  # bench.main's sys.exit(2)
+        return
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["steps"] == 6 and line["warmup"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["chains"] == 2
+    assert line["config"]["collectives"] == ("gloo" if mode == "rehearsal" else "rccl")
+    assert line["config"]["rccl_ranks"] == (0 if mode == "rehearsal" else 2)
+    assert line["n_devices"] == (1 if mode == "rehearsal" else 2)
+    assert line["qoi"]["chains"] == 2 and line["qoi"]["samples"] == 12
+    assert line["value"] == pytest.approx(12 / (6 * line["ms_per_step"] / 1e3), rel=1e-3)
+    assert line["cpu_baseline"] is None  # rank 0 at N = 1 only

@@ -14,8 +14,9 @@ import pytest
 import multigridmc_amd as mg
 from multigridmc_amd import _native
 
-ALL2 = 1 | 2 | 32           # point, pairs, rb2d
+ALL2 = 1 | 2 | 32 | 128     # point, pairs, rb2d, fused last pre-sweep + residual + restriction
 ALL3 = 1 | 2 | 4 | 8 | 16   # point, pairs, zsweep (+ coarse side), z-marching residual + restriction
+JSWEEP = 64                 # j-marching half-sweeps (levels with nx = 256 / 512): box + whole-grid replay
 
 
 def check(shape, reach=1, families=None, cx=None, legacy=0):
@@ -23,6 +24,8 @@ def check(shape, reach=1, families=None, cx=None, legacy=0):
     n = (ctypes.c_int * 3)(*(list(shape) + [0] * (3 - dim)))
     if families is None:
         families = ALL3 if dim == 3 else ALL2
+        if dim == 3 and shape[0] in (256, 512):
+            families |= JSWEEP
     if cx is None:
         cx = 0 if dim == 2 else (16 if shape[0] // 2 < 32 else 64)
     return mg.load_library().mgmc_check_layout(dim, n, reach, families, cx, legacy)
@@ -66,3 +69,14 @@ def test_restriction_last_tile_columns_clamped(n):
     assert check(shape, legacy=2) == _native.MGMC_E_INVALID
     assert b"residual + restriction" in mg.load_library().mgmc_last_error(None)
     assert check((512, 16, 16), legacy=2) == _native.MGMC_OK  # powers of two never reached it
+
+
+@pytest.mark.parametrize("shape", [(256, 256, 256), (512, 512, 512), (256, 24, 20), (512, 24, 20), (256, 2, 2),
+                                   (256, 4, 6), (512, 130, 66), (256, 256, 6)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_jsweep_grid_replay(shape):
+    """k_jsweep_half (round 3): the host replay of its whole grid -- XCD tile order, chunk steps
+    s0-1 .. s1, the idle steps of the unrolled loop, loads JS_D steps ahead, f loads, stores -- with
+    launch_jsweep's own plan (both directions, both k-parity halves) stays inside rows [0, ny] and
+    planes [0, nz], stores only interior rows, and covers every (plane, chunk) tile exactly once."""
+    assert check(shape, families=JSWEEP) == _native.MGMC_OK, mg.load_library().mgmc_last_error(None)
