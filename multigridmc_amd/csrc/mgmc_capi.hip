@@ -821,6 +821,8 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
             if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch, tn);
             else if (MGMC_ZR27_CY == 8 && lc.L.nx >= 128)
                 launch_zresrestrict_t<27, 64, 8, 512>(lf, lc, x, f, fc, xc, s, nch);
+            else if (MGMC_ZR27_CY == 3)
+                launch_zresrestrict_t<27, 64, 3, 256>(lf, lc, x, f, fc, xc, s, nch);
             else launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s, nch);
         }
         return;

@@ -120,11 +120,14 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     const int nb = gridDim.x;
     const int b = blockIdx.x;
     const int per = nb >> 3;
-    const int tile = (nb & 7) ? b : (b & 7) * per + (b >> 3);
+#ifndef MGMC_ZS_ORDER  // (timing builds: 1 = y fastest within the XCD's range, 2 = no XCD remap)
+#define MGMC_ZS_ORDER 0
+#endif
+    const int tile = (nb & 7) || MGMC_ZS_ORDER == 2 ? b : (b & 7) * per + (b >> 3);
     // x fastest: a workgroup's x neighbours run next to it on the same XCD and share the partial
     // 128-B lines of the x halo through L2 (y fastest: 1.49x algorithmic traffic against 1.21x)
-    const int txi = tile % a.ntx;
-    const int tyi = (tile / a.ntx) % a.nty;
+    const int txi = MGMC_ZS_ORDER == 1 ? (tile / a.nty) % a.ntx : tile % a.ntx;
+    const int tyi = MGMC_ZS_ORDER == 1 ? tile % a.nty : (tile / a.ntx) % a.nty;
     const int tzi = tile / (a.ntx * a.nty);
     if (tzi >= a.ntz) return;
     const int q0 = txi * XP;              // first core pair; core positions 2q0+1 .. 2q0+2XP

@@ -486,3 +486,24 @@ def test_sample_timed_segments(hip_device, name, nsteps, stride, ntimed):
     assert np.array_equal(s.get_state(), t.get_state())
     s.close()
     t.close()
+
+
+def test_poison_switch_fills_unwritten_memory_and_leaves_results_alone(hip_device, monkeypatch):
+    """MGMC_POISON=1: the QoI series buffer starts as NaN bytes -- entries past
+    the recorded samples read NaN (positive control of the allocation poison) -- while the recorded
+    series and the state, with NaN-filled LDS before every op of the cycle graph, equal an unpoisoned
+    handle's bit for bit (no kernel of the cycle reads memory it did not write)."""
+    lat = mg.Lattice(32, 32, 32)
+    q = mg.measurement_vector_index(lat, [0.5] * 3)
+    p = mg.MultigridParameters(nlevel=4)
+    ref = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 7, p, device=0)
+    z_ref = ref.sample(5, q)
+    x_ref = ref.get_state()
+    ref.close()
+    monkeypatch.setenv("MGMC_POISON", "1")
+    s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 7, p, device=0)
+    z = s.sample(5, q)
+    tail = s.get_series(12)[5:]
+    assert np.array_equal(z, z_ref) and np.array_equal(s.get_state(), x_ref)
+    assert np.all(np.isnan(tail))
+    s.close()
