@@ -107,6 +107,7 @@ enum PathFlag : uint32_t {
     PATH_NO_JSWEEP = 1u << 13,            // 3D Galerkin levels of 64 / 128 pairs: colour-pair passes, not j-marching halves
     PATH_NO_QRESTRICT = 1u << 14,         // 2D Galerkin levels: last pre-sweep and residual + restriction as two launches
     PATH_NO_TAIL_NOISE = 1u << 15,        // k_tail draws its sweeps' noise itself (not the restriction launch before it)
+    PATH_NO_SYM = 1u << 16,               // 27-point kernels read all 27 coefficients even when the stencil is symmetric
 };
 
 struct PathToken {
@@ -122,6 +123,7 @@ constexpr PathToken kPathTokens[] = {
     {"coarse_precompute", PATH_NO_COARSE_PRECOMPUTE}, {"lr_dense", PATH_NO_LR_DENSE},
     {"chol_dense", PATH_NO_CHOL_DENSE}, {"jsweep", PATH_NO_JSWEEP},
     {"qrestrict", PATH_NO_QRESTRICT}, {"tail_noise", PATH_NO_TAIL_NOISE},
+    {"sym", PATH_NO_SYM},
 };
 
 // parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
@@ -235,6 +237,7 @@ struct Level {
     bool jsweep = false;   // ... j-marching half-sweeps (mgmc_jsweep.hpp)
     bool rb2d = false;     // 2D 5-point level: one-launch red-black sweep, out of place (k_rb2d)
     bool field = false;    // per-vertex coefficients (mgmc_create_csr, mgmc_field.hpp)
+    bool sym = false;      // 27-point stencil bitwise reflection-symmetric: kernels fold it (stencil_coef<true>)
     FieldArg F;            // ... their device field, pattern and colouring
     double* rbuf = nullptr;  // ... residual scratch (padded layout, zero boundary)
     bool pingpong() const { return zsweep || quads || rb2d; }  // out-of-place sweeps: x <-> x2
@@ -292,6 +295,7 @@ struct mgmc_handle {
     long long zbuf_n = 0;              // items per chain
     std::vector<TailArgs*> tail_args;  // device copies, one per OP_TAIL
     std::vector<size_t> tail_lds;      // dynamic LDS bytes per OP_TAIL
+    std::vector<char> tail_sym;        // ... every level of it has a symmetric 27-point stencil (k_tail<3, true>)
     // per OP_TAIL: its sweeps' Box-Muller pairs, drawn by spare workgroups of the restriction launch
     // before it (nullptr: the tail draws them); the jobs (device) and items per chain
     std::vector<double2*> tail_zb;
@@ -586,13 +590,19 @@ void launch_jsweep(const Level& lv, const double* xin, double* xout, const doubl
         a.nchunk = p.nchunk;
         a.xz = h == 0 ? xin : xout;  // the second half reads the first half's new planes
         const dim3 grid(p.nb, 1, nch), block(2 * np);
-        if (np == 256) {  // FEM prior's 27-point fine level at 512^3
-            if (fwd) hipLaunchKernelGGL((k_jsweep_half<256, false>), grid, block, lds, s, a);
-            else hipLaunchKernelGGL((k_jsweep_half<256, true>), grid, block, lds, s, a);
+#define MGMC_JS_LAUNCH(NPV, SYMV)                                                                   \
+    do {                                                                                            \
+        if (fwd) hipLaunchKernelGGL((k_jsweep_half<NPV, false, SYMV>), grid, block, lds, s, a);     \
+        else hipLaunchKernelGGL((k_jsweep_half<NPV, true, SYMV>), grid, block, lds, s, a);          \
+    } while (0)
+        if (np == 256) {  // FEM prior's 27-point fine level at 512^3 (not symmetric bit for bit)
+            MGMC_JS_LAUNCH(256, false);
+        } else if (lv.sym) {  // the cubic FD hierarchies' 255^3 level: 8 distinct coefficients
+            MGMC_JS_LAUNCH(128, true);
         } else {
-            if (fwd) hipLaunchKernelGGL((k_jsweep_half<128, false>), grid, block, lds, s, a);
-            else hipLaunchKernelGGL((k_jsweep_half<128, true>), grid, block, lds, s, a);
+            MGMC_JS_LAUNCH(128, false);
         }
+#undef MGMC_JS_LAUNCH
     }
 }
 
@@ -1431,6 +1441,7 @@ void free_tails(mgmc_handle* h) {
         if (p) hipFree(p);
     h->tail_args.clear();
     h->tail_lds.clear();
+    h->tail_sym.clear();
     h->tail_zb.clear();
     h->tail_jobs.clear();
     h->tail_njobs.clear();
@@ -1587,6 +1598,9 @@ int build_tails_only(mgmc_handle* h) {
         t.tail = (int)h->tail_args.size();
         h->tail_args.push_back(d);
         h->tail_lds.push_back((size_t)A.lds_doubles * sizeof(double));
+        bool tsym = true;
+        for (int l = lt; l < lt + A.nlev; ++l) tsym = tsym && h->levels[l].sym;
+        h->tail_sym.push_back(tsym ? 1 : 0);
         out.push_back(t);
         if (r <= pre_end) removed_before_pre += r - q - 1;
         q = r;
@@ -1776,7 +1790,10 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
             }
             case OP_TAIL: {  // one workgroup per chain
                 const size_t lds = h->tail_lds[op.tail];
-                if (lv.spec.dim == 3)
+                if (lv.spec.dim == 3 && h->tail_sym[op.tail])
+                    hipLaunchKernelGGL((k_tail<3, true>), dim3(nch), dim3(TAIL_NT), lds, s,
+                                       (const TailArgs*)h->tail_args[op.tail]);
+                else if (lv.spec.dim == 3)
                     hipLaunchKernelGGL(k_tail<3>, dim3(nch), dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
                 else
                     hipLaunchKernelGGL(k_tail<2>, dim3(nch), dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
@@ -2292,6 +2309,7 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
         lv.L = make_layout(cfg->dim, specs[l].n,
                            h->field_mode && (fields[l].scheme == 9 || fields[l].scheme == 27));
         memcpy(lv.S.a, specs[l].st, sizeof(lv.S.a));
+        lv.sym = !h->field_mode && stencil_reflection_symmetric(lv.S.a, lv.spec.npoints) && !(h->paths & PATH_NO_SYM);
         const size_t bytes = lv.L.nstore * sizeof(double);
         const size_t cbytes = bytes * nchains;  // x, x2, f of every chain, L.nstore apart
         if (hipMalloc(&lv.x, cbytes) != hipSuccess || hipMalloc(&lv.f, cbytes) != hipSuccess) {
@@ -2623,7 +2641,7 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
         sweep = "k_zsweep_rb7<32," + std::to_string(MGMC_ZS_SHAPE_TY) + ",...,0>";
         if (!(h->paths & PATH_NO_FUSE_PROLONG)) post = "k_zsweep_rb7<32," + std::to_string(MGMC_ZS_SHAPE_TYP) + ",...,PROLONG>";
     } else if (lv.jsweep) {
-        sweep = "k_jsweep_half<" + std::to_string(lv.L.nx / 2) + ">";
+        sweep = "k_jsweep_half<" + std::to_string(lv.L.nx / 2) + (lv.sym && lv.L.nx == 256 ? ",sym" : "") + ">";
     } else if (lv.quads) {
         sweep = "k_sweep_quads<" + std::to_string(dim) + ">";
     } else if (lv.rb2d) {

@@ -70,7 +70,7 @@ __device__ __forceinline__ void js_barrier() { asm volatile("s_waitcnt lgkmcnt(0
 constexpr int JS_TAB = 322;  // Box-Muller tables in LDS: log reduction (rc, hi, lo) x 64 + cos/sin 130
 inline size_t jsweep_lds_bytes(int np) { return (size_t)(JS_RING * 3 * (2 * np + 8) + JS_TAB) * sizeof(double); }
 
-template <int NP, bool FIRST_ODD>
+template <int NP, bool FIRST_ODD, bool SYM = false>
 __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
     constexpr int JS_NP = NP, JS_NT = 2 * NP, JS_RS = 2 * NP + 8, JS_EV = NP + 1;
     {
@@ -159,9 +159,9 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
     // 27-term chain of window element e (1: odd position 2m+1, 2: even 2m+2)
     auto chain = [&](auto ec) {
         constexpr int e = decltype(ec)::value;
-        double res = a.S.a[0] * w[0][e - 1];
+        double res = stencil_coef<SYM>(a.S, 0) * w[0][e - 1];
 #pragma unroll
-        for (int t = 1; t < 27; ++t) res = fma(a.S.a[t], w[t / 3][e + t % 3 - 1], res);
+        for (int t = 1; t < 27; ++t) res = fma(stencil_coef<SYM>(a.S, t), w[t / 3][e + t % 3 - 1], res);
         return res;
     };
 

@@ -63,6 +63,30 @@ struct StencilArg {
     double a[27];
 };
 
+// Reflection-symmetric 27-point stencils (a[dz][dy][dx] bitwise equal under each of dx, dy, dz -> 2 - d:
+// the Galerkin levels of the cubic FD hierarchies, checked on the host by stencil_reflection_symmetric)
+// hold at most 8 distinct values.  A kernel instantiated with SYM reads coefficient t from the lowest
+// index of its class: the same bits, but only 8 doubles live in SGPRs instead of 27 (the full set
+// spills into VGPR lanes and costs a v_readlane per use).
+constexpr int sym_rep(int t) {
+    const int dz = t / 9, dy = (t / 3) % 3, dx = t % 3;
+    return (dz == 2 ? 0 : dz) * 9 + (dy == 2 ? 0 : dy) * 3 + (dx == 2 ? 0 : dx);
+}
+template <bool SYM>
+__host__ __device__ inline double stencil_coef(const StencilArg& S, int t) {
+    return S.a[SYM ? sym_rep(t) : t];
+}
+inline bool stencil_reflection_symmetric(const double* a, int npoints) {
+    if (npoints != 27) return false;
+    for (int t = 0; t < 27; ++t) {  // bit for bit (a +0 / -0 pair would not do)
+        uint64_t u, v;
+        __builtin_memcpy(&u, a + t, 8);
+        __builtin_memcpy(&v, a + sym_rep(t), 8);
+        if (u != v) return false;
+    }
+    return true;
+}
+
 struct GibbsArg {
     double omega;
     double sd;  // sqrt(diag*(2-omega)/omega)
@@ -84,8 +108,8 @@ __device__ __forceinline__ RngKey chain_key(const GibbsArg& G, int c) {
     return k;
 }
 
-// ascending-column-order row sum  sum_k a_k x_k  starting from 0.0
-template <int DIM, int NPTS>
+// ascending-column-order row sum  sum_k a_k x_k  starting from 0.0 (SYM: stencil_coef's fold)
+template <int DIM, int NPTS, bool SYM = false>
 __device__ __forceinline__ double stencil_sum(const double* __restrict__ x, long long p, const Layout& L,
                                               const StencilArg& S) {
     double res = 0.0;
@@ -110,7 +134,7 @@ __device__ __forceinline__ double stencil_sum(const double* __restrict__ x, long
             for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
                 for (int dx = -1; dx <= 1; ++dx)
-                    res += S.a[(dz + 1) * 9 + (dy + 1) * 3 + (dx + 1)] * x[p + dz * L.sp + dy * L.sx + dx];
+                    res += stencil_coef<SYM>(S, (dz + 1) * 9 + (dy + 1) * 3 + (dx + 1)) * x[p + dz * L.sp + dy * L.sx + dx];
     } else {  // 9
 #pragma unroll
         for (int dy = -1; dy <= 1; ++dy)
@@ -121,7 +145,7 @@ __device__ __forceinline__ double stencil_sum(const double* __restrict__ x, long
 }
 
 // the same row sum as an fma chain (Gibbs updates): a_0 x_0, then fma(a_k, x_k, .) ascending
-template <int DIM, int NPTS>
+template <int DIM, int NPTS, bool SYM = false>
 __device__ __forceinline__ double stencil_fma(const double* __restrict__ x, long long p, const Layout& L,
                                               const StencilArg& S) {
     double res;
@@ -140,11 +164,11 @@ __device__ __forceinline__ double stencil_fma(const double* __restrict__ x, long
         res = fma(S.a[5], x[p + 1], res);
         res = fma(S.a[7], x[p + L.sx], res);
     } else if (NPTS == 27) {
-        res = S.a[0] * x[p - L.sp - L.sx - 1];
+        res = stencil_coef<SYM>(S, 0) * x[p - L.sp - L.sx - 1];
 #pragma unroll
         for (int q = 1; q < 27; ++q) {
             const int dz = q / 9 - 1, dy = (q / 3) % 3 - 1, dx = q % 3 - 1;
-            res = fma(S.a[q], x[p + dz * L.sp + dy * L.sx + dx], res);
+            res = fma(stencil_coef<SYM>(S, q), x[p + dz * L.sp + dy * L.sx + dx], res);
         }
     } else {  // 9
         res = S.a[0] * x[p - L.sx - 1];

@@ -93,7 +93,8 @@ struct TailArgs {
     TailOp ops[TAIL_MAX_OPS];
 };
 
-template <int DIM>
+// SYM: every 27-point level of the tail has a reflection-symmetric stencil (stencil_coef)
+template <int DIM, bool SYM = false>
 __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
     constexpr int NPTS = DIM == 3 ? 27 : 9;
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -230,7 +231,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
                 const int tk = DIM == 3 ? (((tid >> 3) & 1) | ((tid >> 7) << 1)) : 0;
                 if (ti < ci && tj < cj && tk < ck) {
                     const int p = (int)G.at(fi + 2 * ti, fj + 2 * tj, DIM == 3 ? fk + 2 * tk : 0);
-                    const double res = stencil_fma<DIM, NPTS>(x, p, G, t.S);
+                    const double res = stencil_fma<DIM, NPTS, SYM>(x, p, G, t.S);
                     x[p] = fma(t.wd, scr[p] - res, x[p]);
                 }
             } else {
@@ -238,7 +239,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
                     const int i = fi + 2 * (q % ci), r = q / ci;
                     const int j = fj + 2 * (r % cj), k = DIM == 3 ? fk + 2 * (r / cj) : 0;
                     const long long p = G.at(i, j, k);
-                    const double res = stencil_fma<DIM, NPTS>(x, p, G, t.S);
+                    const double res = stencil_fma<DIM, NPTS, SYM>(x, p, G, t.S);
                     x[p] = fma(t.wd, scr[p] - res, x[p]);
                 }
             }
@@ -288,7 +289,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
                 int i, j, k;
                 coords(G, q, i, j, k);
                 const long long p = G.at(i, j, k);
-                scr[p] = f[p] - stencil_sum<DIM, NPTS>(x, p, G, t.S);
+                scr[p] = f[p] - stencil_sum<DIM, NPTS, SYM>(x, p, G, t.S);
             }
             __syncthreads();
             const Layout& Gc = c.G;

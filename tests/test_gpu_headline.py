@@ -168,6 +168,7 @@ def test_headline_kernel_instances(headline):
     k0 = s.level_kernels(0)
     assert k0["sweep"].startswith("k_zsweep_rb7<") and k0["post_sweep"].endswith("PROLONG>")
     assert k0["residual_restrict"] == "k_zresrestrict<7,64,8>"
-    assert s.level_kernels(1) == {"sweep": "k_jsweep_half<128>", "residual_restrict": "k_zresrestrict<27,64,4>"}
+    # the 255^3 Galerkin stencil is reflection-symmetric bit for bit: the folded instance (stencil_coef)
+    assert s.level_kernels(1) == {"sweep": "k_jsweep_half<128,sym>", "residual_restrict": "k_zresrestrict<27,64,4>"}
     assert s.level_kernels(2)["sweep"] == "k_sweep_pairs<3>"  # 64-pair rows: neither j-marching nor quads
     assert s.level_kernels(NLEVEL - 1)["sweep"] == "k_tail<3>"
