@@ -641,8 +641,13 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
         if (nk == 0) continue;
         const dim3 grid(a.nblk_y * nk, 1, nch);
         if (dim == 3) {
-            if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false>), grid, dim3(nt), lds, s, a);
-            else hipLaunchKernelGGL((k_sweep_quads<3, true>), grid, dim3(nt), lds, s, a);
+            if (lv.sym) {
+                if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false, true>), grid, dim3(nt), lds, s, a);
+                else hipLaunchKernelGGL((k_sweep_quads<3, true, true>), grid, dim3(nt), lds, s, a);
+            } else {
+                if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false>), grid, dim3(nt), lds, s, a);
+                else hipLaunchKernelGGL((k_sweep_quads<3, true>), grid, dim3(nt), lds, s, a);
+            }
         } else {
             if (fwd) hipLaunchKernelGGL((k_sweep_quads<2, false>), grid, dim3(nt), lds, s, a);
             else hipLaunchKernelGGL((k_sweep_quads<2, true>), grid, dim3(nt), lds, s, a);
@@ -678,8 +683,13 @@ void launch_pairs(const Level& lv, double* x, const double* f, const GibbsArg& g
         const int nt = a.rows_per_block * npair;
         const bool odd = c & 1;
         if (dim == 3) {
-            if (odd) hipLaunchKernelGGL((k_sweep_pairs<3, true>), grid, dim3(nt), 0, s, a);
-            else hipLaunchKernelGGL((k_sweep_pairs<3, false>), grid, dim3(nt), 0, s, a);
+            if (lv.sym) {
+                if (odd) hipLaunchKernelGGL((k_sweep_pairs<3, true, true>), grid, dim3(nt), 0, s, a);
+                else hipLaunchKernelGGL((k_sweep_pairs<3, false, true>), grid, dim3(nt), 0, s, a);
+            } else {
+                if (odd) hipLaunchKernelGGL((k_sweep_pairs<3, true>), grid, dim3(nt), 0, s, a);
+                else hipLaunchKernelGGL((k_sweep_pairs<3, false>), grid, dim3(nt), 0, s, a);
+            }
         } else {
             if (odd) hipLaunchKernelGGL((k_sweep_pairs<2, true>), grid, dim3(nt), 0, s, a);
             else hipLaunchKernelGGL((k_sweep_pairs<2, false>), grid, dim3(nt), 0, s, a);
@@ -733,7 +743,7 @@ struct TailNoiseLaunch {  // spare workgroups of the launch draw a tail's noise 
     const uint64_t* sample;
 };
 
-template <int NPTS, int CX, int CY, int NT>
+template <int NPTS, int CX, int CY, int NT, bool SYM = false>
 void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, const double* f, double* fc, double* xc,
                            hipStream_t s, int nch, const TailNoiseLaunch* tn = nullptr) {
     ZRestrictArgs a;
@@ -779,12 +789,12 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
         a.seed_hi = tn->seed_hi;
         a.sample = tn->sample;
         const int nextra = (int)std::min<long long>((tn->zbs + NT - 1) / NT, 64);
-        hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT, true>), dim3(nb + nextra, 1, nch), dim3(NT),
+        hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT, true, SYM>), dim3(nb + nextra, 1, nch), dim3(NT),
                            zrestrict_lds_bytes(CX, CY), s, a);
         return;
     }
-    hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT>), dim3(nb, 1, nch), dim3(NT), zrestrict_lds_bytes(CX, CY), s,
-                       a);
+    hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT, false, SYM>), dim3(nb, 1, nch), dim3(NT),
+                       zrestrict_lds_bytes(CX, CY), s, a);
 }
 
 // tn: the small z-marching kernel also draws a tail's noise (zr_small_path; ignored elsewhere)
@@ -828,7 +838,9 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
 #ifndef MGMC_ZR27_CY  // (timing builds: scripts/build_exp.sh VARIANTS)
 #define MGMC_ZR27_CY 4
 #endif
-            if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch, tn);
+            if (small && lf.sym) launch_zresrestrict_t<27, 16, 4, 64, true>(lf, lc, x, f, fc, xc, s, nch, tn);
+            else if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch, tn);
+            else if (MGMC_ZR27_CY == 4 && lf.sym) launch_zresrestrict_t<27, 64, 4, 256, true>(lf, lc, x, f, fc, xc, s, nch);
             else if (MGMC_ZR27_CY == 8 && lc.L.nx >= 128)
                 launch_zresrestrict_t<27, 64, 8, 512>(lf, lc, x, f, fc, xc, s, nch);
             else if (MGMC_ZR27_CY == 3)

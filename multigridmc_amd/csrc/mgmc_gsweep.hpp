@@ -36,7 +36,7 @@ struct PairPassArgs {
 
 // FIRST_ODD: the odd position (i parity 1) is updated first (backward sweeps).  A template parameter,
 // so every index into the register window below is static.
-template <int DIM, bool FIRST_ODD>
+template <int DIM, bool FIRST_ODD, bool SYM = false>  // SYM: stencil_coef's fold (3D, same bits)
 __global__ void __launch_bounds__(256) k_sweep_pairs(PairPassArgs a) {
     constexpr int NPTS = DIM == 3 ? 27 : 9;
     __shared__ double xnew[256 + 2];  // new first-colour values, [1 + tid]; zero guards at both ends
@@ -82,11 +82,11 @@ __global__ void __launch_bounds__(256) k_sweep_pairs(PairPassArgs a) {
     // stencil fma chain of the vertex at window position s (1: odd 2m+1, 2: even 2m+2)
     auto chain = [&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        double res = a.S.a[0] * w[0][s - 1];
+        double res = stencil_coef<SYM>(a.S, 0) * w[0][s - 1];
 #pragma unroll
         for (int q = 1; q < NPTS; ++q) {
             const int rr = q / 3, dx = q % 3 - 1;
-            res = fma(a.S.a[q], w[rr][s + dx], res);
+            res = fma(stencil_coef<SYM>(a.S, q), w[rr][s + dx], res);
         }
         return res;
     };
@@ -159,7 +159,7 @@ struct QuadPassArgs {
     long long cs;       // batched chains: doubles between chains (blockIdx.z = chain)
 };
 
-template <int DIM, bool FIRST_ODD>
+template <int DIM, bool FIRST_ODD, bool SYM = false>  // SYM: stencil_coef's fold (3D, same bits)
 __global__ void __launch_bounds__(1024) k_sweep_quads(QuadPassArgs a) {
     {
         const int ch = batch_chain();
@@ -195,11 +195,11 @@ __global__ void __launch_bounds__(1024) k_sweep_quads(QuadPassArgs a) {
     double w[NR][4];
     auto chain = [&](auto sc) {
         constexpr int s = decltype(sc)::value;
-        double res = a.S.a[0] * w[0][s - 1];
+        double res = stencil_coef<SYM>(a.S, 0) * w[0][s - 1];
 #pragma unroll
         for (int q = 1; q < NPTS; ++q) {
             const int rr = q / 3, dx = q % 3 - 1;
-            res = fma(a.S.a[q], w[rr][s + dx], res);
+            res = fma(stencil_coef<SYM>(a.S, q), w[rr][s + dx], res);
         }
         return res;
     };

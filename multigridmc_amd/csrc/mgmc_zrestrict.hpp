@@ -46,7 +46,8 @@ struct ZRestrictArgs {
     const uint64_t* sample;
 };
 
-template <int NPTS, int CX, int CY, int NT, bool ZN = false>
+// SYM: a reflection-symmetric 27-point stencil, read by class (stencil_coef; same bits)
+template <int NPTS, int CX, int CY, int NT, bool ZN = false, bool SYM = false>
 __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
     if (ZN && (int)blockIdx.x >= a.nblk_main) {  // the tail's noise (see ZRestrictArgs)
         const int ch = batch_chain();
@@ -220,12 +221,12 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
                     for (int dy = -1; dy <= 1; ++dy) {
                         const double* rowp = pl[dz] + dy * XS;
                         const int c = dz * 9 + (dy + 1) * 3;
-                        y0 += a.S.a[c] * rowp[m0];
-                        y1 += a.S.a[c] * rowp[m1];
-                        y0 += a.S.a[c + 1] * rowp[o0];
-                        y1 += a.S.a[c + 1] * rowp[o1];
-                        y0 += a.S.a[c + 2] * rowp[m0 + 1];
-                        y1 += a.S.a[c + 2] * rowp[m1 + 1];
+                        y0 += stencil_coef<SYM>(a.S, c) * rowp[m0];
+                        y1 += stencil_coef<SYM>(a.S, c) * rowp[m1];
+                        y0 += stencil_coef<SYM>(a.S, c + 1) * rowp[o0];
+                        y1 += stencil_coef<SYM>(a.S, c + 1) * rowp[o1];
+                        y0 += stencil_coef<SYM>(a.S, c + 2) * rowp[m0 + 1];
+                        y1 += stencil_coef<SYM>(a.S, c + 2) * rowp[m1 + 1];
                     }
             }
             rs[rlds[u]] = (kin && (rflag[u] & 1)) ? fv[u].x - y0 : 0.0;
