@@ -315,6 +315,8 @@ struct mgmc_handle {
     int chol_B = 0, chol_nb = 0; // blocked banded (chol_B > 0): Cf, Cb, Df, Db in one allocation
     double* chol_blk = nullptr;
     bool poison = false;         // MGMC_POISON=1: NaN-filled scratch allocations and LDS (debug, poison_fill)
+    unsigned long long* tail_prof = nullptr;  // (timing builds, MGMC_TAIL_PROF: the first tail's phase stamps)
+    std::vector<TailOp> tail_prof_ops;
 };
 
 #define HIPCHK(h, call)                                                                            \
@@ -1562,6 +1564,13 @@ int build_tails_only(mgmc_handle* h) {
         A.cs = h->levels[lt].L.nstore;  // batched chains: one workgroup per chain
         A.chain0 = (uint32_t)h->chain;
         A.seed_hi = (uint32_t)(h->seed >> 32);
+#ifdef MGMC_TAIL_PROF
+        if (h->tail_args.empty()) {
+            if (!h->tail_prof) HIPCHK(h, hipMalloc(&h->tail_prof, 256 * sizeof(unsigned long long)));
+            A.prof = h->tail_prof;
+            h->tail_prof_ops.assign(A.ops, A.ops + A.nops);
+        }
+#endif
         // the sweeps' Box-Muller pairs: drawn by spare workgroups of the restriction before the tail when
         // that is the small z-marching kernel (3D; k_zresrestrict<..., ZN>), else here
         std::vector<TailNoiseJob> jobs;
@@ -2614,6 +2623,7 @@ int mgmc_destroy(mgmc_handle* h) {
     if (h->sv_scal) hipFree(h->sv_scal);
     if (h->sv_part) hipFree(h->sv_part);
     if (h->comm) ncclCommDestroy(h->comm);
+    if (h->tail_prof) hipFree(h->tail_prof);
     if (h->comm_buf) hipFree(h->comm_buf);
     if (h->ctrl) hipFree(h->ctrl);
     if (h->mom) hipFree(h->mom);
@@ -3129,6 +3139,22 @@ int mgmc_sample_timed(mgmc_handle* h, int nsteps, int64_t qoi_index, double* tot
                       double* post_ms, int* npost) {
     return mgmc_sample_timed_stride(h, nsteps, 1, qoi_index, total_ms, pre_ms, npre, post_ms, npost);
 }
+
+#ifdef MGMC_TAIL_PROF
+// timing builds only: the phase stamps of the last run of the first k_tail (wall clock, rate in kHz):
+// out[0] start, out[1] after the LDS fill from HBM, out[2 + 2 o] after op o's right-hand sides (sweeps),
+// out[3 + 2 o] after op o, out[2 + 2 nops] after the store; kinds[o] = 16 * level + TailKind
+extern "C" int mgmc_debug_tail_profile(mgmc_handle* h, unsigned long long* out, int n, int* kinds, int* nops,
+                                       int* rate_khz) {
+    if (!h || !h->tail_prof) return fail(h, MGMC_E_UNSUPPORTED, "no tail profile");
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(out, h->tail_prof, std::min(n, 256) * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    *nops = (int)h->tail_prof_ops.size();
+    for (int o = 0; o < *nops; ++o) kinds[o] = 16 * h->tail_prof_ops[o].level + h->tail_prof_ops[o].kind;
+    HIPCHK(h, hipDeviceGetAttribute(rate_khz, hipDeviceAttributeWallClockRate, h->device));
+    return MGMC_OK;
+}
+#endif
 
 int mgmc_sample_timed_stride(mgmc_handle* h, int nsteps, int stride, int64_t qoi_index, double* total_ms,
                              double* pre_ms, int* npre, double* post_ms, int* npost) {

@@ -91,7 +91,19 @@ struct TailArgs {
     long long zbs;
     TailLevel lv[TAIL_MAX_LEVELS];
     TailOp ops[TAIL_MAX_OPS];
+    unsigned long long* prof;  // (timing builds, MGMC_TAIL_PROF: wall-clock stamps per phase; else null)
 };
+
+#ifdef MGMC_TAIL_PROF  // timing builds only: one wall-clock stamp per phase from thread 0
+#define TAIL_STAMP(slot)                                                          \
+    do {                                                                          \
+        if (A->prof && threadIdx.x == 0 && blockIdx.x == 0) A->prof[slot] = wall_clock64(); \
+    } while (0)
+#else
+#define TAIL_STAMP(slot) \
+    do {                 \
+    } while (0)
+#endif
 
 // SYM: every 27-point level of the tail has a reflection-symmetric stencil (stencil_coef)
 template <int DIM, bool SYM = false>
@@ -110,6 +122,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
     if (ch) key.k1 = (A->chain0 + (uint32_t)ch) ^ A->seed_hi;
     const uint32_t s_lo = (uint32_t)sample, s_hi = (uint32_t)(sample >> 32);
     double* scr = lds + A->oscr;
+    TAIL_STAMP(0);
 
     __shared__ double lr_s[LR_MAX_M];
     const int wave = tid >> 6, lane = tid & 63, nwave = nt >> 6;
@@ -173,7 +186,9 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
     }
     __syncthreads();
 
+    TAIL_STAMP(1);
     const double2* zb = A->zb ? A->zb + ch * A->zbs : nullptr;
+    int stamp_op = 0;  // (MGMC_TAIL_PROF: the op being run)
     // one Gibbs sweep of level t: right hand sides of every vertex, then the colour passes
     auto sweep = [&](const TailLevel& t, int dir, uint32_t tag, int zoff) {
         const Layout& G = t.G;
@@ -212,6 +227,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             if (i0 + 1 <= G.nx - 1) scr[p + 1] = fma(t.sd, z1, f[p + 1]);
         }
         __syncthreads();
+        TAIL_STAMP(2 + 2 * stamp_op);
         const int nc = t.ncolours;
         for (int cc = 0; cc < nc; ++cc) {
             const int c = dir == 1 ? cc : nc - 1 - cc;
@@ -266,6 +282,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
     for (int o = 0; o < A->nops; ++o) {
         const TailOp op = A->ops[o];
         const TailLevel& t = A->lv[op.level];
+        stamp_op = o;
         if (op.kind == TAIL_SWEEP) {
             sweep(t, op.dir, op.tag, op.zoff);
         } else if (op.kind == TAIL_COARSE) {
@@ -352,6 +369,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             }
             __syncthreads();
         }
+        TAIL_STAMP(3 + 2 * o);
     }
 
     {  // level lt back to HBM
@@ -363,6 +381,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             xg[A->Lg.at(i, j, k)] = lds[t0.ox + (int)t0.G.at(i, j, k)];
         }
     }
+    TAIL_STAMP(2 + 2 * A->nops);
 }
 
 }  // namespace mgmc

@@ -3,6 +3,9 @@
 # height (zc3, zc3k4: cycle times).  Interleaved repetitions in one box call.
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/r4b && export TMPDIR=/tmp
 O=gpurun_out/r4b
+# k_tail phase times (timing build with wall-clock stamps; never the product)
+MGMC_LIBRARY=$GRAFT_REPO_ROOT/build/libmgmc_exptprof.so timeout -k 10 120 python scripts/tail_prof.py 512 7 > $O/tail_prof512.log 2>&1; rc=$?
+echo "tail prof rc=$rc"; cat $O/tail_prof512.log; [ $rc -eq 0 ] || exit $rc
 # correctness first: the symmetric-stencil kernels (k_jsweep_half<128,.,true>, k_tail<3,true>) at the
 # headline and config-3 sizes and their MGMC_DISABLE=sym variants, bitwise against the oracle
 timeout -k 10 600 python -u -m pytest -x -q --timeout 900 --timeout-method thread tests/test_gpu_headline.py tests/test_gpu_config3.py "tests/test_gpu_parity.py::test_variant_cycles_bitwise" -k "headline or config3 or sym" > $O/sym_parity.log 2>&1; rc=$?
