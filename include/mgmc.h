@@ -161,8 +161,8 @@ int mgmc_stencil_of_csr(const mgmc_config* cfg, int64_t nrow, const int64_t* row
  * every level of every handle).  families: MGMC_LAYOUT_* bits of the kernels that address the level;
  * reach: 1 (3^d couplings) or 2 (the squared FD operator's levels); zrestrict_cx: coarse points per
  * tile of the z-marching residual + restriction on this level (0: none).  legacy: bit 0 builds the
- * round-2 reach-2 layout without its margin rows / planes, bit 1 the unclamped restriction columns
- * (both out of bounds: kept so the test shows the check catches them).  MGMC_OK, or MGMC_E_INVALID
+ * round-2 reach-2 layout without its margin rows / planes, bit 1 the unclamped restriction columns,
+ * bit 2 a j-sweep grid 8 workgroups short (all wrong: kept so the test shows the check catches them).  MGMC_OK, or MGMC_E_INVALID
  * with the offending offset range in mgmc_last_error(NULL). */
 #define MGMC_LAYOUT_POINT 1u
 #define MGMC_LAYOUT_PAIRS 2u

@@ -2228,12 +2228,15 @@ static int zrestrict_cx_of(const mgmc_handle* h, int l) {  // launch_residual_re
     if (lf.spec.dim != 3 || lf.field || (lf.paths & PATH_NO_ZRESTRICT) || lc.L.nx < 8) return 0;
     return lc.L.nx < 32 ? 16 : 64;
 }
-// both directions and both halves of a j-marching level, with launch_jsweep's plan
-static std::string jsweep_grid_check_level(const Layout& L, int num_cu) {
+// both directions and both halves of a j-marching level, with launch_jsweep's plan (short_grid: the plan
+// with its last 8 workgroups dropped -- a negative control for the test, which the replay must reject)
+static std::string jsweep_grid_check_level(const Layout& L, int num_cu, bool short_grid = false) {
     const size_t lds = jsweep_lds_bytes(L.nx / 2);
     for (int d = 0; d < 2; ++d)
         for (int half = 0; half < 2; ++half) {
-            const std::string e = jsweep_grid_check(L, jsweep_plan(L, d == 0, half, num_cu, lds, MGMC_JS_ROUNDS), JS_D);
+            JSweepPlan p = jsweep_plan(L, d == 0, half, num_cu, lds, MGMC_JS_ROUNDS);
+            if (short_grid && p.nb > 8) p.nb -= 8;
+            const std::string e = jsweep_grid_check(L, p, JS_D);
             if (!e.empty()) return e;
         }
     return "";
@@ -2503,7 +2506,7 @@ int mgmc_check_layout(int dim, const int* n, int reach, unsigned families, int z
     // legacy bit 0: the round-2 layout without the reach-2 margin; bit 1: unclamped restriction columns
     const Layout L = make_layout(dim, n, reach == 2 && !(legacy & 1));
     std::string e = check_level_layout(L, families, reach, zrestrict_cx, (legacy & 2) != 0);
-    if (e.empty() && (families & LF_JSWEEP)) e = jsweep_grid_check_level(L, 256);  // MI355X: 256 CUs
+    if (e.empty() && (families & LF_JSWEEP)) e = jsweep_grid_check_level(L, 256, (legacy & 4) != 0);  // 256 CUs
     if (!e.empty()) return fail(nullptr, MGMC_E_INVALID, e);
     return MGMC_OK;
 }

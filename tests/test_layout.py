@@ -80,3 +80,10 @@ def test_jsweep_grid_replay(shape):
     launch_jsweep's own plan (both directions, both k-parity halves) stays inside rows [0, ny] and
     planes [0, nz], stores only interior rows, and covers every (plane, chunk) tile exactly once."""
     assert check(shape, families=JSWEEP) == _native.MGMC_OK, mg.load_library().mgmc_last_error(None)
+
+
+def test_jsweep_grid_replay_rejects_a_short_grid():
+    """Negative control: the same replay with the plan's last 8 workgroups dropped reports the
+    (plane, chunk) tiles nobody sweeps."""
+    assert check((512, 512, 512), families=JSWEEP, legacy=4) == _native.MGMC_E_INVALID
+    assert b"not covered by the grid" in mg.load_library().mgmc_last_error(None)
