@@ -90,7 +90,13 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
     const int k = 2 - a.kp + 2 * kk;
     const int s0 = chunk * a.spc, s1 = min(s0 + a.spc, a.nsteps);
     const int tid = threadIdx.x;
-    const int role = tid / JS_NP;     // 0: A-row, 1: B-row
+    // 0: A-row, 1: B-row -- uniform across a wavefront (NP is a multiple of 64): readfirstlane lets the
+    // compiler keep everything that depends only on the role (rows, ring slots, row offsets, the step's
+    // go / store flags) in SGPRs, so the per-lane work is the pair's column arithmetic
+#ifndef MGMC_JS_UNIFORM_ROLE  // (timing builds: 0 = the round-3 per-lane role)
+#define MGMC_JS_UNIFORM_ROLE 1
+#endif
+    const int role = MGMC_JS_UNIFORM_ROLE ? __builtin_amdgcn_readfirstlane(tid / JS_NP) : tid / JS_NP;
     const int m = tid & (JS_NP - 1);  // pair of the row
     const int i0 = 2 * m + 1;
     const uint64_t sample = *a.G.sample;
@@ -99,19 +105,19 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
     auto slot = [](int j) { return ((j % JS_RING) + JS_RING) % JS_RING; };
     auto rowp = [&](int j, int dz) { return ring + (slot(j) * 3 + dz) * JS_RS; };  // dz: plane index 0..2
     // staging: thread t moves pair t % NP of item 2 q + t / NP, q = 0..2 (6 items: 2 rows x 3 planes)
-    // Loads are unconditional (rows clamped onto the lattice, out-of-range rows zeroed when they are
-    // written to the ring): a conditional load merges into its register through a copy, and the copy
-    // waits for the load right away
+    // Loads are unconditional (rows clamped onto the lattice: an out-of-range row reads the zero
+    // boundary row, exactly its zeros): a conditional load merges into its register through a copy,
+    // and the copy waits for the load right away
     auto load_pair = [&](int j, int dz) -> double2 {
         const int jc = j < 0 ? 0 : (j > L.ny ? L.ny : j);
         const double* src = (dz == 1 ? a.xo : a.xz) + L.at(i0, jc, k + dz - 1);
         return *reinterpret_cast<const double2*>(src);
     };
+    // (rows outside [0, ny] were loaded from the clamped boundary rows 0 / ny: already zeros)
     auto deposit = [&](int j, int dz, double2 v) {
-        const bool in = j >= 0 && j <= L.ny;
         double* r = rowp(j, dz);
-        r[m] = in ? v.x : 0.0;               // odd position 2m+1
-        r[JS_EV + 1 + m] = in ? v.y : 0.0;   // even position 2m+2
+        r[m] = v.x;               // odd position 2m+1
+        r[JS_EV + 1 + m] = v.y;   // even position 2m+2
     };
     auto guards = [&](int j) {  // zero guards of a ring row index (positions 0 and nx + 1)
         if (tid < 3) {

@@ -18,7 +18,7 @@ for lib in 0 o1 o2; do
   done
 done
 unset MGMC_LIBRARY
-REPS=2 timeout -k 10 700 python scripts/lib_cycle_bench.py 0,0+MGMC_DISABLE=sym,o1,o2,zc3,zc3k4,jd4,jr2 > $O/cycle.log 2>&1; rc=$?
+REPS=2 timeout -k 10 700 python scripts/lib_cycle_bench.py 0,0+MGMC_DISABLE=sym,jrole0,o1,o2,zc3,jd4,jr2 > $O/cycle.log 2>&1; rc=$?
 echo "cycle rc=$rc"; cat $O/cycle.log; [ $rc -eq 0 ] || exit $rc
 # config 3 (256^3, 6 levels): fine-sweep tile heights / chunk depths (the 512^3-tuned TY 20, TZ 32 leaves
 # 416 tiles on 512 workgroup slots at 256^3)
