@@ -108,7 +108,12 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
     // Loads are unconditional (rows clamped onto the lattice: an out-of-range row reads the zero
     // boundary row, exactly its zeros): a conditional load merges into its register through a copy,
     // and the copy waits for the load right away
+    // Rows past the chunk's last window row a(s1) + 1 are never deposited (the loop's idle steps and the
+    // prefetches JS_D steps past s1): they are loaded from that last row instead of the next chunk's
+    // rows, which would be fetched from HBM only to be dropped (their values are never used)
+    const int jlast = 2 * s1 + a.jA + 1, flast = 2 * s1 + a.jA;
     auto load_pair = [&](int j, int dz) -> double2 {
+        j = MGMC_CHUNK_CLAMP && j > jlast ? jlast : j;
         const int jc = j < 0 ? 0 : (j > L.ny ? L.ny : j);
         const double* src = (dz == 1 ? a.xo : a.xz) + L.at(i0, jc, k + dz - 1);
         return *reinterpret_cast<const double2*>(src);
@@ -177,7 +182,8 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
     // loop is unrolled by JS_D so that the buffers are static registers.
     double2 P[JS_D][3], F[JS_D];
     auto frow = [&](int s) { return role == 0 ? 2 * s + a.jA : 2 * s + a.jA - 3; };
-    auto load_f = [&](int j) -> double2 {  // (rows outside the lattice: never used)
+    auto load_f = [&](int j) -> double2 {  // (rows outside the lattice or past flast: never used)
+        j = MGMC_CHUNK_CLAMP && j > flast ? flast : j;
         const int jc = j < 1 ? 1 : (j > L.ny - 1 ? L.ny - 1 : j);
         return *reinterpret_cast<const double2*>(a.f + L.at(i0, jc, k));
     };

@@ -59,6 +59,12 @@ inline Layout make_layout(int dim, const int n[3], bool reach2 = false) {
     return L;
 }
 
+// the sweeps' loads past the end of a workgroup's chunk reload its last needed row / plane instead of
+// fetching the next chunk's (timing builds: 0 = the round-3 loads)
+#ifndef MGMC_CHUNK_CLAMP
+#define MGMC_CHUNK_CLAMP 1
+#endif
+
 struct StencilArg {
     double a[27];
 };

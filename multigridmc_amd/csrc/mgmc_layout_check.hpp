@@ -98,13 +98,16 @@ inline std::string jsweep_grid_check(const Layout& L, const JSweepPlan& p, int j
         const int k = 2 - p.kp + 2 * kk;
         const int s0 = chunk * p.spc, s1 = std::min(s0 + p.spc, p.nsteps);
         const int a0 = 2 * (s0 - 1) + p.jA;
+        const int jlast = 2 * s1 + p.jA + 1, flast = 2 * s1 + p.jA;  // (the kernel's clamps past the chunk)
         auto xrow = [&](int j, int dz) -> std::string {  // load_pair: clamped row, plane k + dz - 1
+            j = j > jlast ? jlast : j;
             const int jc = j < 0 ? 0 : (j > L.ny ? L.ny : j);
             const int kz = k + dz - 1;
             if (jc < 0 || jc > L.ny || kz < 0 || kz > L.nz) return bad("x load", jc, kz);
             return "";
         };
         auto frow_ok = [&](int j) -> std::string {  // load_f: row clamped onto [1, ny - 1], plane k
+            j = j > flast ? flast : j;
             const int jc = j < 1 ? 1 : (j > L.ny - 1 ? L.ny - 1 : j);
             if (jc < 1 || jc > L.ny - 1 || k < 1 || k > L.nz - 1) return bad("f load", jc, k);
             return "";

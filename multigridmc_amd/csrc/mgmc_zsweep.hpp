@@ -301,8 +301,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     constexpr bool PF2 = PROLONG != 0;
     double2 pxb[PF2 ? 2 : 1][NLX];
 #define ZS_PX(B) pxb[PF2 ? (B) : 0]
+    // planes past the chunk's last deposited plane k1 + 1 (the loads issued one / two steps ahead in the
+    // chunk's last steps) are never used: they load plane k1 + 1 again (an L2 hit) instead of the next
+    // chunk's planes from HBM; likewise f past k1
     auto issue_x = [&](int k, auto Bc) {
-        const double* base = plane_base(a.xin, k);
+        const double* base = plane_base(a.xin, MGMC_CHUNK_CLAMP && k > k1 + 1 ? k1 + 1 : k);
 #pragma unroll
         for (int u = 0; u < NLX; ++u) ZS_PX(decltype(Bc)::value)[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
     };
@@ -320,7 +323,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     // f of the item on plane k: (first-colour element, other element) -- two 8-byte loads at
     // wave-uniform element offsets instead of a pair load and per-lane selects
     const int foff = PF2 ? (active_wave ? t.goff : L.off + 1) : t.goff;  // (PF2: idle waves load a zero pad pair)
-    auto load_f = [&](int k) { return *reinterpret_cast<const double2*>(plane_base(a.f, k) + foff); };
+    auto load_f = [&](int k) { return *reinterpret_cast<const double2*>(plane_base(a.f, MGMC_CHUNK_CLAMP && k > k1 ? k1 : k) + foff); };
 
     // fma-chain stencil sum (ascending column order) at LDS offset o of plane k.  The fine FD
     // stencil is symmetric (launch_zsweep checks a[4]=a[22], a[10]=a[16], a[12]=a[14]), so four
