@@ -168,8 +168,11 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
     }
 
     double2 px[NLX], pf[NLR];
+    // the chunk stages x planes 2 K0 - 2 .. 2 K1 and f planes 2 K0 - 1 .. 2 K1 - 1: the last step's loads one
+    // plane ahead reload those (never used) instead of fetching the next chunk's planes
+    const int kx_last = 2 * K1, kf_last = 2 * K1 - 1;
     auto issue_x = [&](int k) {
-        const double* base = plane_ptr(a.x, k);
+        const double* base = plane_ptr(a.x, MGMC_CHUNK_CLAMP && k > kx_last ? kx_last : k);
 #pragma unroll
         for (int u = 0; u < NLX; ++u) px[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
     };
@@ -183,7 +186,7 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
             }
     };
     auto issue_f = [&](int k) {
-        const double* base = plane_ptr(a.f, k);
+        const double* base = plane_ptr(a.f, MGMC_CHUNK_CLAMP && k > kf_last ? kf_last : k);
 #pragma unroll
         for (int u = 0; u < NLR; ++u) pf[u] = *reinterpret_cast<const double2*>(base + roff[u]);
     };
