@@ -131,6 +131,10 @@ inline std::string jsweep_grid_check(const Layout& L, const JSweepPlan& p, int j
                 const bool go = (role == 0 ? s < s1 : (s > s0 && s <= s1)) && j >= 1 && j <= L.ny - 1;
                 const bool store = go && (role == 1 || s >= s0);
                 if (store && e.empty() && (j < 1 || j > L.ny - 1 || k < 1 || k > L.nz - 1)) e = bad("store", j, k);
+                // the clamps past the chunk never touch a row that is used: deposited rows (steps
+                // s < s1: ar + 2, ar + 3) stay <= jlast, the f row of a computed row stays <= flast
+                if (e.empty() && s < s1 && ar + 3 > jlast) e = bad("deposit past the chunk's last row", ar + 3, k);
+                if (e.empty() && go && frow(s, role) > flast) e = bad("f row past the chunk's last row", frow(s, role), k);
             }
         }
         if (!e.empty()) return e;
