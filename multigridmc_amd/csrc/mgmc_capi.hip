@@ -108,6 +108,7 @@ enum PathFlag : uint32_t {
     PATH_NO_QRESTRICT = 1u << 14,         // 2D Galerkin levels: last pre-sweep and residual + restriction as two launches
     PATH_NO_TAIL_NOISE = 1u << 15,        // k_tail draws its sweeps' noise itself (not the restriction launch before it)
     PATH_NO_SYM = 1u << 16,               // 27-point kernels read all 27 coefficients even when the stencil is symmetric
+    PATH_NO_PROLONG_Z = 1u << 17,         // big 3D levels: the per-point prolongation instead of the z-marching one
 };
 
 struct PathToken {
@@ -123,7 +124,7 @@ constexpr PathToken kPathTokens[] = {
     {"coarse_precompute", PATH_NO_COARSE_PRECOMPUTE}, {"lr_dense", PATH_NO_LR_DENSE},
     {"chol_dense", PATH_NO_CHOL_DENSE}, {"jsweep", PATH_NO_JSWEEP},
     {"qrestrict", PATH_NO_QRESTRICT}, {"tail_noise", PATH_NO_TAIL_NOISE},
-    {"sym", PATH_NO_SYM},
+    {"sym", PATH_NO_SYM},             {"prolong_z", PATH_NO_PROLONG_Z},
 };
 
 // parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
@@ -922,6 +923,17 @@ void launch_prolongate(const Level& lf, const Level& lc, double* x, const double
     const int zper = lf.spec.dim == 3 ? lf.L.nz - 1 : 1;  // batched chains: blockIdx.z = chain * zper + plane
     dim3 grid = grid3(lf.L.nx / 2, lf.L.ny - 1, zper * nch, block);
     const long long csf = lf.L.nstore, csc = lc.L.nstore;
+#ifndef MGMC_PROLONG_Z  // fine planes per thread of the z-marching prolongation on big 3D levels (0: off)
+#define MGMC_PROLONG_Z 8
+#endif
+    if (MGMC_PROLONG_Z > 0 && lf.spec.dim == 3 && (long long)(lf.L.nx / 2) * (lf.L.ny - 1) * (lf.L.nz - 1) >= (1LL << 16) &&
+        !(lf.paths & PATH_NO_PROLONG_Z)) {
+        constexpr int TZ = MGMC_PROLONG_Z > 0 ? MGMC_PROLONG_Z : 1;
+        const int nzc = (lf.L.nz - 1 + TZ - 1) / TZ;
+        const dim3 gz = grid3(lf.L.nx / 2, lf.L.ny - 1, nzc * nch, block);
+        hipLaunchKernelGGL((k_prolongate_z<TZ>), gz, block, 0, s, lf.L, lc.L, x, xc, alpha, nzc, csf, csc);
+        return;
+    }
     if (lf.spec.dim == 3)
         hipLaunchKernelGGL((k_prolongate_pairs<3>), grid, block, 0, s, lf.L, lc.L, x, xc, alpha, zper, csf, csc);
     else

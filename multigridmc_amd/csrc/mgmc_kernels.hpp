@@ -601,6 +601,96 @@ __global__ void __launch_bounds__(256) k_prolongate_pairs(Layout Lf, Layout Lc, 
     *reinterpret_cast<double2*>(x + p) = v;
 }
 
+// ---- 3D prolongate-add, z-marching: each thread owns one fine x-pair (i odd, i+1) of one fine row j
+// and marches TZ fine planes, keeping the coarse values of the row's parents in registers (a fine
+// plane k reads coarse planes k>>1 and, for odd k, (k>>1)+1; two fine planes share each coarse plane),
+// with the next plane's fine pair loaded one step ahead.  Per fine vertex the terms and their order are
+// k_prolongate_pairs' (coarse planes ascending, rows ascending, then q, q+1): bitwise equal. ----
+template <int TZ>
+__global__ void __launch_bounds__(256) k_prolongate_z(Layout Lf, Layout Lc, double* __restrict__ x,
+                                                      const double* __restrict__ xc, double alpha, int nzc,
+                                                      long long csf, long long csc) {
+    const int ch = (int)blockIdx.z / nzc;  // batched chains: blockIdx.z = chain * nzc + z chunk
+    x += ch * csf;
+    xc += ch * csc;
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = blockIdx.y * blockDim.y + threadIdx.y + 1;
+    const int i = 2 * q + 1;
+    const int k0 = 1 + ((int)blockIdx.z - ch * nzc) * TZ;
+    const int k1 = min(k0 + TZ, Lf.nz);  // one past the last fine plane
+    if (i > Lf.nx - 1 || j > Lf.ny - 1) return;
+    const bool has1 = i + 1 <= Lf.nx - 1;
+    const bool hq0 = q >= 1, hq1 = q + 1 <= Lc.nx - 1;
+    const int j0 = j >> 1, nj = (j & 1) ? 2 : 1;
+    const bool hj[2] = {j0 >= 1 && j0 <= Lc.ny - 1, j0 + 1 >= 1 && j0 + 1 <= Lc.ny - 1};
+    const double wj[2] = {w1(j - 2 * j0), w1(j - 2 * j0 - 2)};
+    // coarse values (rows j0, j0 + 1; columns q, q + 1) of coarse plane K (zero where a parent does
+    // not exist -- never added: the existence tests below are k_prolongate_pairs')
+    auto coarse = [&](int K, double (&c)[2][2]) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int jj = j0 + b;
+            const bool ok = b < nj && hj[b] && K >= 1 && K <= Lc.nz - 1;
+            const double* row = xc + Lc.at(0, ok ? jj : 0, ok ? K : 0);
+            c[b][0] = ok && hq0 ? row[q] : 0.0;
+            c[b][1] = ok && hq1 ? row[q + 1] : 0.0;
+        }
+    };
+    double cA[2][2], cB[2][2];  // coarse planes K, K + 1 around the current fine plane
+    int K = k0 >> 1;
+    coarse(K, cA);
+    coarse(K + 1, cB);
+    double2 vn = *reinterpret_cast<const double2*>(x + Lf.at(i, j, k0));
+    for (int k = k0; k < k1; ++k) {
+        const long long p = Lf.at(i, j, k);
+        double2 v = vn;
+        if (k + 1 < k1) vn = *reinterpret_cast<const double2*>(x + p + Lf.sp);
+        if ((k >> 1) != K) {  // advance the coarse window by one plane
+            K = k >> 1;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                cA[b][0] = cB[b][0];
+                cA[b][1] = cB[b][1];
+            }
+            coarse(K + 1, cB);
+        }
+        const int nk = (k & 1) ? 2 : 1;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            if (a >= nk) break;
+            const int kk = K + a;
+            if (kk < 1 || kk > Lc.nz - 1) continue;
+            const double(&c)[2][2] = a == 0 ? cA : cB;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                if (b >= nj || !hj[b]) continue;
+                if (hq0) {
+                    double w = 1.0;
+                    w *= 0.5;
+                    w *= wj[b];
+                    w *= w1(k - 2 * kk);
+                    v.x += alpha * w * c[b][0];
+                }
+                if (hq1) {
+                    double w = 1.0;
+                    w *= 0.5;
+                    w *= wj[b];
+                    w *= w1(k - 2 * kk);
+                    v.x += alpha * w * c[b][1];
+                    if (has1) {
+                        double w2 = 1.0;
+                        w2 *= 1.0;
+                        w2 *= wj[b];
+                        w2 *= w1(k - 2 * kk);
+                        v.y += alpha * w2 * c[b][1];
+                    }
+                }
+            }
+        }
+        *reinterpret_cast<double2*>(x + p) = v;
+    }
+}
+
 // ---- y = A x (tests, LinearOperator::apply) ----
 template <int DIM, int NPTS>
 __global__ void __launch_bounds__(256) k_operator_apply(Layout L, const double* __restrict__ x, double* __restrict__ y,

@@ -188,7 +188,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
 
     TAIL_STAMP(1);
     const double2* zb = A->zb ? A->zb + ch * A->zbs : nullptr;
-    int stamp_op = 0;  // (MGMC_TAIL_PROF: the op being run)
+    [[maybe_unused]] int stamp_op = 0;  // (MGMC_TAIL_PROF: the op being run)
     // one Gibbs sweep of level t: right hand sides of every vertex, then the colour passes
     auto sweep = [&](const TailLevel& t, int dir, uint32_t tag, int zoff) {
         const Layout& G = t.G;
