@@ -10,7 +10,7 @@ echo "tail prof rc=$rc"; cat $O/tail_prof512.log; [ $rc -eq 0 ] || exit $rc
 # headline and config-3 sizes and their MGMC_DISABLE=sym variants, bitwise against the oracle
 timeout -k 10 600 python -u -m pytest -x -q --timeout 900 --timeout-method thread tests/test_gpu_headline.py tests/test_gpu_config3.py "tests/test_gpu_parity.py::test_variant_cycles_bitwise" -k "headline or config3 or sym or prolong_z or fuse_prolong" > $O/sym_parity.log 2>&1; rc=$?
 echo "sym parity rc=$rc"; tail -3 $O/sym_parity.log; [ $rc -eq 0 ] || exit $rc
-for lib in 0 noclamp o1 o2; do
+for lib in 0 noclamp o1; do
   if [ "$lib" = 0 ]; then unset MGMC_LIBRARY; else export MGMC_LIBRARY=$GRAFT_REPO_ROOT/build/libmgmc_exp$lib.so; fi
   for c in FETCH_SIZE WRITE_SIZE; do
     K=6 timeout -k 10 -s KILL 120 rocprofv3 --kernel-trace --pmc $c -d $O/${lib}_$c -o pmc --output-format csv -- python3 scripts/vcycle_once.py > $O/${lib}_$c.log 2>&1
