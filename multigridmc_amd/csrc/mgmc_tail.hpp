@@ -105,6 +105,77 @@ struct TailArgs {
     } while (0)
 #endif
 
+// Per-op constants pinned in SGPRs.  The tail's arguments sit in global memory behind a pointer; a
+// scalar load the compiler leaves in flight inside a colour pass shares lgkmcnt with the LDS reads and
+// returns out of order, so every wait in the pass became lgkmcnt(0) and the 27 window reads ran one at
+// a time (0.8-1 us per colour pass, round 4).  An empty asm with a "+s" operand makes the value live
+// in an SGPR from here on: the loads complete before the pass, and nothing is re-loaded inside it.
+__device__ __forceinline__ void tail_pin(int& v) { asm volatile("" : "+s"(v)); }
+__device__ __forceinline__ void tail_pin(uint32_t& v) { asm volatile("" : "+s"(v)); }
+__device__ __forceinline__ void tail_pin(long long& v) { asm volatile("" : "+s"(v)); }
+__device__ __forceinline__ void tail_pin(double& v) { asm volatile("" : "+s"(v)); }
+__device__ __forceinline__ void tail_pin(Layout& G) {
+    tail_pin(G.nx);
+    tail_pin(G.ny);
+    tail_pin(G.nz);
+    tail_pin(G.off);
+    tail_pin(G.sx);
+    tail_pin(G.sp);
+}
+template <int NPTS, bool SYM>
+__device__ __forceinline__ void tail_pin(StencilArg& S) {
+#pragma unroll
+    for (int q = 0; q < NPTS; ++q)
+        if (!SYM || sym_rep(q) == q) tail_pin(S.a[q]);
+}
+
+// stencil_fma / stencil_sum of an LDS-resident level with every window read issued before the chain:
+// left to itself the compiler reads one or two values, waits, multiplies, and reads the next, so a
+// colour pass paid the LDS latency 9-14 times in a row.  The empty asm takes all the window values as
+// operands, which orders every read before any use (same values, same arithmetic order).
+template <int NPTS>
+__device__ __forceinline__ void tail_issue_all(double (&v)[NPTS]) {
+    if constexpr (NPTS == 27) {
+        asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                          "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]),
+                          "+v"(v[14]), "+v"(v[15]), "+v"(v[16]), "+v"(v[17]), "+v"(v[18]), "+v"(v[19]),
+                          "+v"(v[20]), "+v"(v[21]), "+v"(v[22]), "+v"(v[23]), "+v"(v[24]), "+v"(v[25]), "+v"(v[26]));
+    } else {
+        static_assert(NPTS == 9, "tail stencils are 27- or 9-point");
+        asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                          "+v"(v[7]), "+v"(v[8]));
+    }
+}
+template <int DIM, int NPTS>
+__device__ __forceinline__ void tail_window(const double* __restrict__ x, int p, const Layout& G, double (&v)[NPTS]) {
+#pragma unroll
+    for (int q = 0; q < NPTS; ++q) {
+        const int dz = DIM == 3 ? q / 9 - 1 : 0, dy = (q / 3) % 3 - 1, dx = q % 3 - 1;
+        v[q] = x[p + dz * (int)G.sp + dy * (int)G.sx + dx];
+    }
+    tail_issue_all<NPTS>(v);
+}
+// a_0 x_0, then fma(a_k, x_k, .) ascending (= stencil_fma)
+template <int DIM, int NPTS, bool SYM>
+__device__ __forceinline__ double tail_fma(const double* __restrict__ x, int p, const Layout& G, const StencilArg& S) {
+    double v[NPTS];
+    tail_window<DIM, NPTS>(x, p, G, v);
+    double res = stencil_coef<SYM && NPTS == 27>(S, 0) * v[0];
+#pragma unroll
+    for (int q = 1; q < NPTS; ++q) res = fma(stencil_coef<SYM && NPTS == 27>(S, q), v[q], res);
+    return res;
+}
+// 0.0 + a_0 x_0 + a_1 x_1 + ... ascending, separate multiply and add (= stencil_sum)
+template <int DIM, int NPTS, bool SYM>
+__device__ __forceinline__ double tail_sum(const double* __restrict__ x, int p, const Layout& G, const StencilArg& S) {
+    double v[NPTS];
+    tail_window<DIM, NPTS>(x, p, G, v);
+    double res = 0.0;
+#pragma unroll
+    for (int q = 0; q < NPTS; ++q) res += stencil_coef<SYM && NPTS == 27>(S, q) * v[q];
+    return res;
+}
+
 // SYM: every 27-point level of the tail has a reflection-symmetric stencil (stencil_coef)
 template <int DIM, bool SYM = false>
 __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
@@ -191,10 +262,21 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
     [[maybe_unused]] int stamp_op = 0;  // (MGMC_TAIL_PROF: the op being run)
     // one Gibbs sweep of level t: right hand sides of every vertex, then the colour passes
     auto sweep = [&](const TailLevel& t, int dir, uint32_t tag, int zoff) {
-        const Layout& G = t.G;
-        double* x = lds + t.ox;
-        double* f = lds + t.of;
-        if (t.m > 0) {  // f += B Sigma^{-1/2} xi' (the sweep's m extra normals)
+        Layout G = t.G;
+        StencilArg S = t.S;
+        double sd = t.sd, wd = t.wd;
+        int ox = t.ox, of = t.of, nc = t.ncolours, lrm = t.m;
+        tail_pin(G);
+        tail_pin<NPTS, SYM>(S);
+        tail_pin(sd);
+        tail_pin(wd);
+        tail_pin(ox);
+        tail_pin(of);
+        tail_pin(nc);
+        tail_pin(lrm);
+        double* x = lds + ox;
+        double* f = lds + of;
+        if (lrm > 0) {  // f += B Sigma^{-1/2} xi' (the sweep's m extra normals)
             if (2 * tid < t.m) {
                 const Philox4 r = philox4x32_10(LR_PAIR0 + (uint32_t)tid, tag, s_lo, s_hi, key.k0, key.k1);
                 double z0, z1;
@@ -223,12 +305,11 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
                 normal_pair(rnd, &z0, &z1);
             }
             const int p = (int)G.at(i0, j, k);
-            scr[p] = fma(t.sd, z0, f[p]);
-            if (i0 + 1 <= G.nx - 1) scr[p + 1] = fma(t.sd, z1, f[p + 1]);
+            scr[p] = fma(sd, z0, f[p]);
+            if (i0 + 1 <= G.nx - 1) scr[p + 1] = fma(sd, z1, f[p + 1]);
         }
         __syncthreads();
         TAIL_STAMP(2 + 2 * stamp_op);
-        const int nc = t.ncolours;
         for (int cc = 0; cc < nc; ++cc) {
             const int c = dir == 1 ? cc : nc - 1 - cc;
             // vertices of colour c: coordinate d = 2 - bit_d(c) + 2 t_d
@@ -247,21 +328,21 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
                 const int tk = DIM == 3 ? (((tid >> 3) & 1) | ((tid >> 7) << 1)) : 0;
                 if (ti < ci && tj < cj && tk < ck) {
                     const int p = (int)G.at(fi + 2 * ti, fj + 2 * tj, DIM == 3 ? fk + 2 * tk : 0);
-                    const double res = stencil_fma<DIM, NPTS, SYM>(x, p, G, t.S);
-                    x[p] = fma(t.wd, scr[p] - res, x[p]);
+                    const double res = tail_fma<DIM, NPTS, SYM>(x, (int)p, G, S);
+                    x[p] = fma(wd, scr[p] - res, x[p]);
                 }
             } else {
                 for (int q = tid; q < ci * cj * ck; q += nt) {
                     const int i = fi + 2 * (q % ci), r = q / ci;
                     const int j = fj + 2 * (r % cj), k = DIM == 3 ? fk + 2 * (r / cj) : 0;
                     const long long p = G.at(i, j, k);
-                    const double res = stencil_fma<DIM, NPTS, SYM>(x, p, G, t.S);
-                    x[p] = fma(t.wd, scr[p] - res, x[p]);
+                    const double res = tail_fma<DIM, NPTS, SYM>(x, (int)p, G, S);
+                    x[p] = fma(wd, scr[p] - res, x[p]);
                 }
             }
             __syncthreads();
         }
-        if (t.m > 0) {  // x -= B_bar (B^T x), f restored
+        if (lrm > 0) {  // x -= B_bar (B^T x), f restored
             lr_dots(t, t.sc_one, x);
             lr_restore_rows(t, f);
             __syncthreads();
@@ -280,7 +361,13 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
     };
 
     for (int o = 0; o < A->nops; ++o) {
-        const TailOp op = A->ops[o];
+        TailOp op = A->ops[o];
+        tail_pin(op.kind);
+        tail_pin(op.level);
+        tail_pin(op.dir);
+        tail_pin(op.tag);
+        tail_pin(op.nsweeps);
+        tail_pin(op.zoff);
         const TailLevel& t = A->lv[op.level];
         stamp_op = o;
         if (op.kind == TAIL_SWEEP) {
@@ -292,11 +379,21 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             }
         } else if (op.kind == TAIL_RESTRICT) {
             const TailLevel& c = A->lv[op.level + 1];
-            const Layout& G = t.G;
-            const double* x = lds + t.ox;
-            double* f = lds + t.of;
+            Layout G = t.G, Gc = c.G;
+            StencilArg S = t.S;
+            int ox = t.ox, of = t.of, cox = c.ox, cof = c.of, lrm = t.m;
+            tail_pin(G);
+            tail_pin(Gc);
+            tail_pin<NPTS, SYM>(S);
+            tail_pin(ox);
+            tail_pin(of);
+            tail_pin(cox);
+            tail_pin(cof);
+            tail_pin(lrm);
+            const double* x = lds + ox;
+            double* f = lds + of;
             const int nd = ndof_of(G);
-            if (t.m > 0) {  // r = (f - B Sigma^{-1} B^T x) - A x
+            if (lrm > 0) {  // r = (f - B Sigma^{-1} B^T x) - A x
                 lr_dots(t, t.sc_inv, x);
                 __syncthreads();
                 lr_patch_rows(t, f, -1);
@@ -306,40 +403,49 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
                 int i, j, k;
                 coords(G, q, i, j, k);
                 const long long p = G.at(i, j, k);
-                scr[p] = f[p] - stencil_sum<DIM, NPTS, SYM>(x, p, G, t.S);
+                scr[p] = f[p] - tail_sum<DIM, NPTS, SYM>(x, (int)p, G, S);
             }
             __syncthreads();
-            const Layout& Gc = c.G;
             const int ndc = ndof_of(Gc);
             for (int q = tid; q < ndc; q += nt) {
                 int I, J, K;
                 coords(Gc, q, I, J, K);
-                const long long pf = G.at(2 * I, 2 * J, 2 * K);
+                const int pf = (int)G.at(2 * I, 2 * J, 2 * K);
+                double rv[NPTS];  // the 3^d residuals, every read issued before the sum (tail_window)
+                tail_window<DIM, NPTS>(scr, pf, G, rv);
                 double result = 0.0;
                 const int zr = DIM == 3 ? 1 : 0;
+#pragma unroll
                 for (int sz = -zr; sz <= zr; ++sz)
+#pragma unroll
                     for (int sy = -1; sy <= 1; ++sy)
+#pragma unroll
                         for (int sx = -1; sx <= 1; ++sx) {
                             double w = 1.0;
                             w *= w1(sx);
                             w *= w1(sy);
                             if (DIM == 3) w *= w1(sz);
-                            result += w * scr[pf + sz * G.sp + sy * G.sx + sx];
+                            result += w * rv[(sz + zr) * 9 + (sy + 1) * 3 + (sx + 1)];
                         }
                 const long long pc = Gc.at(I, J, K);
-                lds[c.of + pc] = result;
-                lds[c.ox + pc] = 0.0;
+                lds[cof + pc] = result;
+                lds[cox + pc] = 0.0;
             }
-            if (t.m > 0) lr_restore_rows(t, f);
+            if (lrm > 0) lr_restore_rows(t, f);
             __syncthreads();
         } else {  // TAIL_PROLONG: x_l += alpha P x_{l+1}
             const TailLevel& c = A->lv[op.level + 1];
-            const Layout& G = t.G;
-            const Layout& Gc = c.G;
-            double* x = lds + t.ox;
-            const double* xc = lds + c.ox;
+            Layout G = t.G, Gc = c.G;
+            int ox = t.ox, cox = c.ox;
+            double alpha = A->alpha;
+            tail_pin(G);
+            tail_pin(Gc);
+            tail_pin(ox);
+            tail_pin(cox);
+            tail_pin(alpha);
+            double* x = lds + ox;
+            const double* xc = lds + cox;
             const int nd = ndof_of(G);
-            const double alpha = A->alpha;
             for (int q = tid; q < nd; q += nt) {
                 int i, j, k;
                 coords(G, q, i, j, k);
