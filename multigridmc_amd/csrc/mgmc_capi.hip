@@ -109,6 +109,7 @@ enum PathFlag : uint32_t {
     PATH_NO_TAIL_NOISE = 1u << 15,        // k_tail draws its sweeps' noise itself (not the restriction launch before it)
     PATH_NO_SYM = 1u << 16,               // 27-point kernels read all 27 coefficients even when the stencil is symmetric
     PATH_NO_PROLONG_Z = 1u << 17,         // big 3D levels: the per-point prolongation instead of the z-marching one
+    PATH_NO_ZPAIRS = 1u << 18,            // fine z-sweep: every z-chunk marches up (no up / down chunk pairs)
 };
 
 struct PathToken {
@@ -125,6 +126,7 @@ constexpr PathToken kPathTokens[] = {
     {"chol_dense", PATH_NO_CHOL_DENSE}, {"jsweep", PATH_NO_JSWEEP},
     {"qrestrict", PATH_NO_QRESTRICT}, {"tail_noise", PATH_NO_TAIL_NOISE},
     {"sym", PATH_NO_SYM},             {"prolong_z", PATH_NO_PROLONG_Z},
+    {"zpairs", PATH_NO_ZPAIRS},
 };
 
 // parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
@@ -470,7 +472,8 @@ void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s,
     a.ntx = (lv.L.nx / 2) / XP;
     a.nty = (lv.L.ny - 1 + TY - 1) / TY;
     a.ntz = (lv.L.nz - 1 + a.tz - 1) / a.tz;
-    const int ntiles = a.ntx * a.nty * a.ntz;
+    // zpairs: tiles in (column, chunk pair) order, an odd chunk count padded by one empty tile per column
+    const int ntiles = a.ntx * a.nty * (a.zpairs ? (a.ntz + 1) / 2 * 2 : a.ntz);
     const int nb = (ntiles + 7) / 8 * 8;
     const size_t lds = zsweep_lds_bytes(XP, TY, prolong);
     // alpha a power of two (coarse_scaling 1): fma prolongation terms, same bits (mgmc_zsweep.hpp)
@@ -500,6 +503,7 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
     a.S = lv.S;
     a.G = g0;
     a.G.colour = (direction == MGMC_FORWARD) ? 0 : 1;
+    a.zpairs = 0;
     const long long txy = (long long)((lv.L.nx / 2) / ZS_XP) * ((lv.L.ny - 1 + ZS_TY - 1) / ZS_TY);
     const long long txyp = (long long)((lv.L.nx / 2) / ZS_XP) * ((lv.L.ny - 1 + ZS_TYP - 1) / ZS_TYP);
     // z-chunk depth: the deepest chunk (fewest prologue steps, 2 per chunk) that still keeps 3/4 of
@@ -516,6 +520,7 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
         return;
     }
     a.tz = depth(txy, ZS_TZ);
+    a.zpairs = (lv.paths & PATH_NO_ZPAIRS) ? 0 : 1;
     launch_zsweep_t<ZS_XP, ZS_TY, ZS_NT, ZS_MINW>(lv, a, false, s, nch);
 }
 
@@ -774,6 +779,22 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
         const long long per_chunk = (long long)a.ntx * a.nty;
         const long long nchunk = std::max(1LL, (2 * slots + per_chunk - 1) / per_chunk);
         a.kz = std::max(8, (int)((lc.L.nz - 1 + nchunk - 1) / nchunk));
+    }
+    if (NPTS == 27 && CX == 64 && work >= 4 * 1024) {
+        // 27-point levels with enough tiles for several rounds (512^3 level 1): the chunk depth that
+        // minimises rounds of resident workgroups x planes staged per chunk (2 kz + 2); 512^3 level 1:
+        // kz 11 = 768 tiles, one round of 3 x 256 slots: 108 -> 101 us (round 4, kernel traces)
+        const long long slots = (long long)(160 * 1024 / zrestrict_lds_bytes(CX, CY)) * lf.num_cu;
+        const long long per_chunk = (long long)a.ntx * a.nty;
+        long long best = -1;
+        for (int kz = 2; kz <= 16; ++kz) {
+            const long long tiles = per_chunk * ((lc.L.nz - 1 + kz - 1) / kz);
+            const long long cost = ((tiles + slots - 1) / slots) * (2 * kz + 2);
+            if (best < 0 || cost < best) {
+                best = cost;
+                a.kz = kz;
+            }
+        }
     }
 #ifdef MGMC_ZR27_KZ  // (timing builds: scripts/build_exp.sh VARIANTS)
     if (NPTS == 27 && CX == 64) a.kz = MGMC_ZR27_KZ;

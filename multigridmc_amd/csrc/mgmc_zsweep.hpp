@@ -50,6 +50,7 @@ struct ZSweepArgs {
     GibbsArg G;                // colour field = first colour (0 forward, 1 backward)
     int tz;                    // planes per z-chunk
     int ntx, nty, ntz;         // tile counts
+    int zpairs;                // plain sweep: z-chunks in pairs marching towards each other (below)
     long long cs, csc;         // batched chains: doubles between chains of the level / coarse level
 };
 
@@ -126,9 +127,23 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     const int tile = (nb & 7) || MGMC_ZS_ORDER == 2 ? b : (b & 7) * per + (b >> 3);
     // x fastest: a workgroup's x neighbours run next to it on the same XCD and share the partial
     // 128-B lines of the x halo through L2 (y fastest: 1.49x algorithmic traffic against 1.21x)
-    const int txi = MGMC_ZS_ORDER == 1 ? (tile / a.nty) % a.ntx : tile % a.ntx;
-    const int tyi = MGMC_ZS_ORDER == 1 ? tile % a.nty : (tile / a.ntx) % a.nty;
-    const int tzi = tile / (a.ntx * a.nty);
+    int txi = MGMC_ZS_ORDER == 1 ? (tile / a.nty) % a.ntx : tile % a.ntx;
+    int tyi = MGMC_ZS_ORDER == 1 ? tile % a.nty : (tile / a.ntx) % a.nty;
+    int tzi = tile / (a.ntx * a.nty);
+    // zpairs (plain sweep): z-chunks 2m and 2m+1 of a column are neighbouring tiles (same XCD, same
+    // round of workgroups); chunk 2m marches up and 2m+1 down, so both reach their shared boundary
+    // planes at the end of their march, and those planes' second read is an L2 hit instead of an HBM
+    // re-read one round later.  The march direction does not change a value: every vertex sees the
+    // same old / new neighbours either way.
+    bool down = false;
+    if (!PROLONG && a.zpairs) {
+        const int nxy = a.ntx * a.nty;
+        const int zp = tile / (2 * nxy), rem = tile - zp * 2 * nxy;
+        txi = (rem >> 1) % a.ntx;
+        tyi = (rem >> 1) / a.ntx;
+        tzi = 2 * zp + (rem & 1);
+        down = (rem & 1) != 0;
+    }
     if (tzi >= a.ntz) return;
     const int q0 = txi * XP;              // first core pair; core positions 2q0+1 .. 2q0+2XP
     const int j0 = 1 + tyi * TY;          // first core row
@@ -186,12 +201,13 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     const int wpar = __builtin_amdgcn_readfirstlane((t.flags >> 3) & 1);
     // element (0 odd position, 1 even) taking the first colour on plane k: wave-uniform.  Chunks
     // start on odd planes, so it is E0 on the steps p = k0-1, k0+1, ... (even p) and 1 - E0 on the
-    // others.  The plain sweep compiles the z march below once per value of E0 and runs the steps in
+    // others (a downward march starts on plane k1: its first step's element is E0d).  The plain sweep compiles the z march below once per value of E0 and runs the steps in
     // pairs, so every element choice in it is a compile-time constant: no selects, and pair loads
     // and stores stay 16-byte accesses (the two copies execute the same sequence of barriers).  The
     // fused-prolongation sweep keeps one copy with wave-uniform selects (its registers are the
     // binding limit: 2 workgroups of 12 waves per CU need <= 80 VGPRs).
     const int E0 = __builtin_amdgcn_readfirstlane(((wpar ^ (k0 - 1)) & 1) == fc ? 0 : 1);
+    const int E0d = __builtin_amdgcn_readfirstlane(((wpar ^ k1) & 1) == fc ? 0 : 1);
     // the odd / even element is an interior vertex (per lane; boundary vertices are never written)
     const bool rowin = (t.flags & 1) != 0;
     const bool in0 = rowin && (t.flags & 2), in1 = rowin && (t.flags & 4);
@@ -305,7 +321,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     // chunk's last steps) are never used: they load plane k1 + 1 again (an L2 hit) instead of the next
     // chunk's planes from HBM; likewise f past k1
     auto issue_x = [&](int k, auto Bc) {
-        const double* base = plane_base(a.xin, MGMC_CHUNK_CLAMP && k > k1 + 1 ? k1 + 1 : k);
+        // (downward march: below k0 - 2)
+        const double* base =
+            plane_base(a.xin, MGMC_CHUNK_CLAMP && k > k1 + 1 ? k1 + 1 : (MGMC_CHUNK_CLAMP && k < k0 - 2 ? k0 - 2 : k));
 #pragma unroll
         for (int u = 0; u < NLX; ++u) ZS_PX(decltype(Bc)::value)[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
     };
@@ -323,7 +341,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     // f of the item on plane k: (first-colour element, other element) -- two 8-byte loads at
     // wave-uniform element offsets instead of a pair load and per-lane selects
     const int foff = PF2 ? (active_wave ? t.goff : L.off + 1) : t.goff;  // (PF2: idle waves load a zero pad pair)
-    auto load_f = [&](int k) { return *reinterpret_cast<const double2*>(plane_base(a.f, MGMC_CHUNK_CLAMP && k > k1 ? k1 : k) + foff); };
+    auto load_f = [&](int k) {
+        return *reinterpret_cast<const double2*>(
+            plane_base(a.f, MGMC_CHUNK_CLAMP && k > k1 ? k1 : (MGMC_CHUNK_CLAMP && k < k0 - 1 ? k0 - 1 : k)) + foff);
+    };
 
     // fma-chain stencil sum (ascending column order) at LDS offset o of plane k.  The fine FD
     // stencil is symmetric (launch_zsweep checks a[4]=a[22], a[10]=a[16], a[12]=a[14]), so four
@@ -343,6 +364,19 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         res = fma(cx, s0[xm + 1], res);
         res = fma(cy, s0[o + RS], res);
         res = fma(cz, sp[o], res);
+        return res;
+    };
+    // the same sum with the value above (i, j, k+1) from a register (second colour of a downward march)
+    auto row_sum_ba = [&](int k, int o, int e, double below, double above) {
+        const double* s0 = xs + slot(k) * PS;
+        const int xm = e ? o - WP : o + WP - 1;
+        double res = cz * below;
+        res = fma(cy, s0[o - RS], res);
+        res = fma(cx, s0[xm], res);
+        res = fma(cc, s0[o], res);
+        res = fma(cx, s0[xm + 1], res);
+        res = fma(cy, s0[o + RS], res);
+        res = fma(cz, above, res);
         return res;
     };
     // the Box-Muller pair of this item on plane k (z.x: odd position i, z.y: even i+1)
@@ -373,8 +407,14 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     double fb = 0.0;  // first-colour value below (plane p-2) at the second-colour position of p-1
     // E0c: std::integral_constant (E0 known at compile time in this copy of the march) or RunE0 (a
     // wave-uniform run-time value: the fused-prolongation sweep, one copy, fewer registers)
-    auto run = [&](auto E0c) __attribute__((always_inline)) {
+    // DNc: a downward march (zpairs, plain sweep only): steps p = k1, k1 - 1, ..., k0 - 1; deposit x(p-1)
+    // into the slot of plane p+3, issue x(p-2) and f(p-1); first colour on p, second colour on p+1, whose
+    // below value (plane p, written by this step's first colour) comes from LDS and whose above value
+    // (plane p+2, whose slot the next step's deposit overwrites) from a register; ring = planes p-1 .. p+2
+    auto run = [&](auto E0c, auto DNc) __attribute__((always_inline)) {
         const int E0c_v = E0c.value;
+        constexpr bool DN = decltype(DNc)::value;
+        constexpr int dz = DN ? -1 : 1;
         auto step = [&](int p, auto ODDc, double2& fcur, double2& fnxt, double pk_in, double& pk_out)
                         __attribute__((always_inline)) {
             constexpr bool odd_step = decltype(ODDc)::value;
@@ -383,7 +423,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
             const bool inf = e ? in1 : in0;  // (compile-time choice)
             // p even on even steps: plane p+1 odd (register set 1), p+3 too
             using Bp = std::integral_constant<int, odd_step ? 0 : 1>;
-            deposit_x(p + 1, std::integral_constant<int, odd_step ? 0 : 1>{}, Bp{});
+            deposit_x(p + dz, std::integral_constant<int, DN ? -1 : (odd_step ? 0 : 1)>{}, Bp{});
             if (PROLONG) {
                 if (odd_step) deposit_c((p + 3) / 2);
                 else issue_c((p + 4) / 2);
@@ -392,8 +432,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
                 issue_x(p + 3, Bp{});  // (past the chunk: clamped planes, loaded and never used)
                 (void)fnxt;
             } else {
-                issue_x(p + 2, Bp{});
-                if (active_wave) fnxt = load_f(p + 1);
+                issue_x(p + 2 * dz, Bp{});
+                if (active_wave) fnxt = load_f(p + dz);
             }
             __syncthreads();
             // first colour on plane p: c = fma(sd, z, f), x = fma(omega/diag, c - S, x); the second
@@ -409,15 +449,20 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
             }
             if constexpr (PF2) fcur = load_f(p + 2);  // this step's f is used up: the registers take f(p+2)
             __syncthreads();
-            // second colour on plane k = p-1 (its element is e: the parity flips with the plane)
-            const int k = p - 1;
+            // second colour on plane k = p-1 (DN: p+1; its element is e: the parity flips with the plane)
+            const int k = p - dz;
             if (core_wave) {
                 const bool own = k >= k0 && k < k1;  // a core plane of this tile (interior)
                 const double* s0 = xs + slot(k) * PS;
                 const double fv = s0[o2];             // final first-colour value
                 if (own && rowin) {
                     double sv = s0[o1];
-                    if (inf) sv = fma(wd, pk_in - row_sum(k, o1, e, fb), sv);
+                    if (inf) {
+                        // DN: below = plane p (this step's first colour, LDS), above = plane p+2 (fb); the
+                        // slot of p+2 takes the next step's deposit, so it is not read here
+                        const double res = DN ? row_sum_ba(k, o1, e, xs[slot(p) * PS + o1], fb) : row_sum(k, o1, e, fb);
+                        sv = fma(wd, pk_in - res, sv);
+                    }
                     double* dst = a.xout + (long long)k * L.sp + t.goff;
                     // (x, y) = (odd, even) element; the second colour is element e here
                     const double2 out = e ? make_double2(fv, sv) : make_double2(sv, fv);
@@ -425,22 +470,30 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
                     __builtin_nontemporal_store(out.x, dst);
                     __builtin_nontemporal_store(out.y, dst + 1);
                 }
-                fb = fv;
+                fb = fv;  // the next step's value below (UP) / above (DN) at its second-colour position
             }
-            if (active_wave && interior_plane(p + 1)) z = noise(p + 1);
+            if (active_wave && interior_plane(p + dz)) z = noise(p + dz);
         };
         double2 fA = make_double2(0.0, 0.0), fB = make_double2(0.0, 0.0);
         double pkA = 0.0, pkB = 0.0;
+        const int pst = DN ? k1 : k0 - 1;  // first step's plane
         if constexpr (PF2) {
             fA = load_f(k0 - 1);
             fB = load_f(k0);
         } else if (active_wave) {
-            fA = load_f(k0 - 1);
+            fA = load_f(pst);
         }
-        if (active_wave && interior_plane(k0 - 1)) z = noise(k0 - 1);
-        for (int p = k0 - 1; p <= k1; p += 2) {
-            step(p, std::integral_constant<bool, false>{}, fA, fB, pkB, pkA);
-            if (p + 1 <= k1) step(p + 1, std::integral_constant<bool, true>{}, fB, fA, pkA, pkB);
+        if (active_wave && interior_plane(pst)) z = noise(pst);
+        if constexpr (DN) {
+            for (int p = k1; p >= k0 - 1; p -= 2) {
+                step(p, std::integral_constant<bool, false>{}, fA, fB, pkB, pkA);
+                if (p - 1 >= k0 - 1) step(p - 1, std::integral_constant<bool, true>{}, fB, fA, pkA, pkB);
+            }
+        } else {
+            for (int p = k0 - 1; p <= k1; p += 2) {
+                step(p, std::integral_constant<bool, false>{}, fA, fB, pkB, pkA);
+                if (p + 1 <= k1) step(p + 1, std::integral_constant<bool, true>{}, fB, fA, pkA, pkB);
+            }
         }
     };
 
@@ -456,6 +509,18 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     // (k0 odd: planes k0-2, k0 take register set 1, k0-1, k0+1 set 0)
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
+    using UP = std::integral_constant<bool, false>;
+    using DOWN = std::integral_constant<bool, true>;
+    if (!PROLONG && down) {  // downward march (zpairs): planes k1 + 1, k1 in LDS, x(k1 - 1) in flight
+        issue_x(k1 + 1, B1{});
+        deposit_x(k1 + 1, std::integral_constant<int, -1>{}, B1{});
+        issue_x(k1, B0{});
+        deposit_x(k1, std::integral_constant<int, -1>{}, B0{});
+        issue_x(k1 - 1, B1{});
+        if (E0d) run(std::integral_constant<int, 1>{}, DOWN{});  // block-uniform branches
+        else run(std::integral_constant<int, 0>{}, DOWN{});
+        return;
+    }
     issue_x(k0 - 2, B1{});
     deposit_x(k0 - 2, std::integral_constant<int, -1>{}, B1{});
     issue_x(k0 - 1, B0{});
@@ -468,9 +533,9 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     }
     issue_x(k0, B1{});
     if constexpr (PF2) issue_x(k0 + 1, B0{});
-    if (PROLONG) run(RunE0{E0});
-    else if (E0) run(std::integral_constant<int, 1>{});  // wave-uniform branch
-    else run(std::integral_constant<int, 0>{});
+    if (PROLONG) run(RunE0{E0}, UP{});
+    else if (E0) run(std::integral_constant<int, 1>{}, UP{});  // wave-uniform branch
+    else run(std::integral_constant<int, 0>{}, UP{});
 }
 
 #undef ZS_PX

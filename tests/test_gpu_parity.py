@@ -189,7 +189,8 @@ VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_
             ("tail,qrestrict", "2d_qr_cj5"), (ALL_PATHS, "2d512_qrestrict"),
             ("tail_noise", "3d16"), ("tail_noise", "3d64_4lvl"), ("tail_noise", "3d32_W_ssor"),
             ("sym", "3d16"), ("sym", "3d64_4lvl"), ("sym", "3d32_W_ssor"),
-            ("prolong_z", "3d128_zsweep"), ("prolong_z", "3d_aniso_zsweep_ssor"), ("prolong_z,fuse_prolong", "3d128_zsweep")]
+            ("prolong_z", "3d128_zsweep"), ("prolong_z", "3d_aniso_zsweep_ssor"), ("prolong_z,fuse_prolong", "3d128_zsweep"),
+            ("zpairs", "3d128_zsweep"), ("zpairs", "3d128_zsweep_odd"), ("zpairs", "3d_aniso_zsweep_ssor")]
 
 
 @pytest.mark.parametrize("paths,name", VARIANTS)
@@ -204,7 +205,8 @@ def test_variant_cycles_bitwise(hip_device, monkeypatch, paths, name):
     instead of one k_quads_restrict2d; tail_noise = k_tail draws its sweeps' Box-Muller pairs itself
     instead of the restriction launch before it; sym = the 27-point kernels read all 27 coefficients
     of a reflection-symmetric stencil instead of one per symmetry class (stencil_coef); prolong_z = the
-    per-point prolongation instead of the z-marching one on 3D levels;
+    per-point prolongation instead of the z-marching one on 3D levels; zpairs = every z-chunk of the plain
+    fine z-sweep marching up (no up / down chunk pairs);
     coarse_precompute = the coarse SSOR sampler's right-hand sides inside its colour passes;
     chol_dense = the coarse Cholesky's blocked banded solves on a small coarsest level (the oracle's
     blocked mode).  Every combination gives the oracle's cycle exactly."""
