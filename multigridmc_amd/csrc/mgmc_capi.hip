@@ -80,6 +80,9 @@ struct Op {
     int lr_coarse_patch = 0;  // OP_RESIDUAL_RESTRICT: ... and the coarse level's first pre-sweep
     uint32_t lr_coarse_tag = 0;
     int tail = -1;           // OP_TAIL: index into mgmc_handle::tail_args
+    int xzero = 0;           // OP_SWEEP: its input x is known zero (the restriction before it zeroed the level, nothing
+                             // wrote it since): the kernel takes zeros instead of loading it (mark_zero_inputs);
+                             // OP_RESIDUAL_RESTRICT: so the coarse x is not written at all
     int zpre = 0;            // OP_SWEEP_RESTRICT: also draws the next OP_COARSE_LDS's noise into mgmc_handle::zbuf;
                              // OP_COARSE_LDS: reads it from there; OP_RESIDUAL_RESTRICT: 1 + the index of
                              // the OP_TAIL after it whose noise its spare workgroups draw
@@ -110,6 +113,7 @@ enum PathFlag : uint32_t {
     PATH_NO_SYM = 1u << 16,               // 27-point kernels read all 27 coefficients even when the stencil is symmetric
     PATH_NO_PROLONG_Z = 1u << 17,         // big 3D levels: the per-point prolongation instead of the z-marching one
     PATH_NO_ZPAIRS = 1u << 18,            // fine z-sweep: every z-chunk marches up (no up / down chunk pairs)
+    PATH_NO_XZERO = 1u << 19,             // the restriction zeroes x_{l+1} and its first pre-sweep loads it
 };
 
 struct PathToken {
@@ -126,7 +130,7 @@ constexpr PathToken kPathTokens[] = {
     {"chol_dense", PATH_NO_CHOL_DENSE}, {"jsweep", PATH_NO_JSWEEP},
     {"qrestrict", PATH_NO_QRESTRICT}, {"tail_noise", PATH_NO_TAIL_NOISE},
     {"sym", PATH_NO_SYM},             {"prolong_z", PATH_NO_PROLONG_Z},
-    {"zpairs", PATH_NO_ZPAIRS},
+    {"zpairs", PATH_NO_ZPAIRS},       {"xzero", PATH_NO_XZERO},
 };
 
 // parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
@@ -572,8 +576,10 @@ bool jsweep_eligible(const LevelSpec& sp, const Layout& L, uint32_t paths) {
 #define MGMC_JS_ROUNDS 1
 #endif
 
+// xzero: xin is known zero (Op::xzero): the first half takes zeros for every x row, the second for its own
+// planes (the neighbouring planes are the first half's new values)
 void launch_jsweep(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
-                   hipStream_t s, int nch) {
+                   hipStream_t s, int nch, bool xzero = false) {
     JSweepArgs a;
     a.cs = lv.L.nstore;
     a.L = lv.L;
@@ -598,10 +604,16 @@ void launch_jsweep(const Level& lv, const double* xin, double* xout, const doubl
         a.nchunk = p.nchunk;
         a.xz = h == 0 ? xin : xout;  // the second half reads the first half's new planes
         const dim3 grid(p.nb, 1, nch), block(2 * np);
-#define MGMC_JS_LAUNCH(NPV, SYMV)                                                                   \
+#define MGMC_JS_LAUNCH_XZ(NPV, SYMV, XZ)                                                            \
     do {                                                                                            \
-        if (fwd) hipLaunchKernelGGL((k_jsweep_half<NPV, false, SYMV>), grid, block, lds, s, a);     \
-        else hipLaunchKernelGGL((k_jsweep_half<NPV, true, SYMV>), grid, block, lds, s, a);          \
+        if (fwd) hipLaunchKernelGGL((k_jsweep_half<NPV, false, SYMV, XZ>), grid, block, lds, s, a); \
+        else hipLaunchKernelGGL((k_jsweep_half<NPV, true, SYMV, XZ>), grid, block, lds, s, a);      \
+    } while (0)
+#define MGMC_JS_LAUNCH(NPV, SYMV)                                 \
+    do {                                                          \
+        if (!xzero) MGMC_JS_LAUNCH_XZ(NPV, SYMV, 0);              \
+        else if (h == 0) MGMC_JS_LAUNCH_XZ(NPV, SYMV, 1);         \
+        else MGMC_JS_LAUNCH_XZ(NPV, SYMV, 2);                     \
     } while (0)
         if (np == 256) {  // FEM prior's 27-point fine level at 512^3 (not symmetric bit for bit)
             MGMC_JS_LAUNCH(256, false);
@@ -611,13 +623,14 @@ void launch_jsweep(const Level& lv, const double* xin, double* xout, const doubl
             MGMC_JS_LAUNCH(128, false);
         }
 #undef MGMC_JS_LAUNCH
+#undef MGMC_JS_LAUNCH_XZ
     }
 }
 
 void launch_quads(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
-                  hipStream_t s, int nch = 1) {
+                  hipStream_t s, int nch = 1, bool xzero = false) {
     if (lv.jsweep) {
-        launch_jsweep(lv, xin, xout, f, g, direction, s, nch);
+        launch_jsweep(lv, xin, xout, f, g, direction, s, nch, xzero);
         return;
     }
     QuadPassArgs a;
@@ -822,8 +835,11 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
 }
 
 // tn: the small z-marching kernel also draws a tail's noise (zr_small_path; ignored elsewhere)
+// skip_xc: the z-marching kernel leaves x_c alone (Op::xzero: the coarse level's first sweep takes it as
+// zeros without loading it)
 void launch_residual_restrict(const Level& lf, const Level& lc, const double* x, const double* f, double* fc,
-                              double* xc, int zero_xc, hipStream_t s, int nch = 1, const TailNoiseLaunch* tn = nullptr) {
+                              double* xc, int zero_xc, hipStream_t s, int nch = 1, const TailNoiseLaunch* tn = nullptr,
+                              bool skip_xc = false) {
     const bool zr = lf.spec.dim == 3 && zero_xc && !lf.field && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8;
     if (nch > 1 && !zr) {  // batched chains on the generic kernels: one launch per chain
         for (int c = 0; c < nch; ++c)
@@ -850,6 +866,7 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
     // most of the chip idle (the 27-point gather kernel took 24 us per launch on the 15^3 / 7^3 levels)
     if (lf.spec.dim == 3 && zero_xc && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8) {
         const bool small = lc.L.nx < 32;
+        if (skip_xc) xc = nullptr;
         if (lf.spec.npoints == 7) {
             if (small) launch_zresrestrict_t<7, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch, tn);
             // 64 x 8 coarse points, 512 threads, 80 KB of LDS (2 workgroups per CU): half the y halo
@@ -1740,9 +1757,37 @@ void fuse_sweep_restrict(mgmc_handle* h) {
     }
 }
 
+// A coarse level's first pre-sweep starts from x_{l+1} = 0 (multigridmc_sampler.cc:122, x_ell.setZero()
+// before the recursive call).  Where that sweep is a j-marching level's out-of-place half-sweep pair and
+// the restriction before it is the z-marching kernel, the sweep takes the zeros as constants instead of
+// loading them (512^3 level 1: the first half moves 2 of its 4 streams, the second 3), and the
+// restriction does not write them (142 MB of the fine residual + restriction's stores).  Nothing else
+// reads that buffer before it is written whole: the sweep writes the other one, and the next sweep out
+// of it (the post-sweep) overwrites every interior vertex; a copy back (OP_COPY) writes it whole too.
+// Only the op right after the restriction is marked (W-cycles: the later visits start from the level's
+// own result, not from zero).  Same values: the restriction's zero is +0.0, so is the constant.
+void mark_zero_inputs(mgmc_handle* h) {
+    for (Op& op : h->ops) op.xzero = 0;
+    if (h->paths & PATH_NO_XZERO) return;
+    for (size_t q = 0; q + 1 < h->ops.size(); ++q) {
+        Op& rr = h->ops[q];
+        Op& sw = h->ops[q + 1];
+        if (rr.kind != OP_RESIDUAL_RESTRICT || sw.kind != OP_SWEEP || sw.level != rr.level + 1 || sw.src != 0 ||
+            rr.zpre != 0)
+            continue;
+        const Level& lf = h->levels[rr.level];
+        const Level& lc = h->levels[sw.level];
+        const bool zr = lf.spec.dim == 3 && !lf.field && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8;
+        if (!zr || !lc.jsweep || lc.field || lf.lr.m > 0 || lc.lr.m > 0) continue;
+        rr.xzero = 1;
+        sw.xzero = 1;
+    }
+}
+
 int build_tails(mgmc_handle* h) {
     const int rc = build_tails_only(h);
     if (rc == MGMC_OK) fuse_sweep_restrict(h);
+    if (rc == MGMC_OK) mark_zero_inputs(h);
     return rc;
 }
 
@@ -1769,7 +1814,7 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                                   h->cfg.coarse_scaling, s, nch);
                 } else if (lv.quads) {
                     xo = lv.buf(1 - op.src);
-                    launch_quads(lv, lv.buf(op.src), xo, fs, g, op.direction, s, nch);
+                    launch_quads(lv, lv.buf(op.src), xo, fs, g, op.direction, s, nch, op.xzero != 0);
                 } else if (lv.rb2d) {
                     xo = lv.buf(1 - op.src);
                     launch_rb2d(lv, lv.buf(op.src), xo, fs, g, op.direction, true, s, nch);
@@ -1822,7 +1867,7 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                                              h->key, (uint32_t)h->chain, (uint32_t)(h->seed >> 32), sample};
                     launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch, &tn);
                 } else {
-                    launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch);
+                    launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch, nullptr, op.xzero != 0);
                 }
                 if (lr && lv.lr.dense_path)
                     ;  // f was never patched; the post-sweep's rhs went to lr.fe2 above

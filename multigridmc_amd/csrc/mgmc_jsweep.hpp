@@ -70,7 +70,10 @@ __device__ __forceinline__ void js_barrier() { asm volatile("s_waitcnt lgkmcnt(0
 constexpr int JS_TAB = 322;  // Box-Muller tables in LDS: log reduction (rc, hi, lo) x 64 + cos/sin 130
 inline size_t jsweep_lds_bytes(int np) { return (size_t)(JS_RING * 3 * (2 * np + 8) + JS_TAB) * sizeof(double); }
 
-template <int NP, bool FIRST_ODD, bool SYM = false>
+// XZ: the sweep's input x is known zero (the level's first pre-sweep, mgmc_capi.hip mark_zero_inputs):
+// 1 = every x row is the constant 0.0 (the first half), 2 = the own planes' rows are (the second half;
+// planes k +- 1 hold the first half's new values) -- those rows are not loaded at all
+template <int NP, bool FIRST_ODD, bool SYM = false, int XZ = 0>
 __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
     constexpr int JS_NP = NP, JS_NT = 2 * NP, JS_RS = 2 * NP + 8, JS_EV = NP + 1;
     {
@@ -113,6 +116,7 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
     // rows, which would be fetched from HBM only to be dropped (their values are never used)
     const int jlast = 2 * s1 + a.jA + 1, flast = 2 * s1 + a.jA;
     auto load_pair = [&](int j, int dz) -> double2 {
+        if (XZ == 1 || (XZ == 2 && dz == 1)) return make_double2(0.0, 0.0);
         j = MGMC_CHUNK_CLAMP && j > jlast ? jlast : j;
         const int jc = j < 0 ? 0 : (j > L.ny ? L.ny : j);
         const double* src = (dz == 1 ? a.xo : a.xz) + L.at(i0, jc, k + dz - 1);

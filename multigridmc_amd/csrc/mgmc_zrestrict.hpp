@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
         for (int u = 0; u < NCP; ++u)
             if (cpin[u]) {
                 a.fc[pk + cpg[u]] = acc[u];
-                a.xc[pk + cpg[u]] = 0.0;
+                if (a.xc) a.xc[pk + cpg[u]] = 0.0;  // (null: the coarse level's first sweep takes x_c = 0 as given)
             }
     };
 

@@ -190,7 +190,8 @@ VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_
             ("tail_noise", "3d16"), ("tail_noise", "3d64_4lvl"), ("tail_noise", "3d32_W_ssor"),
             ("sym", "3d16"), ("sym", "3d64_4lvl"), ("sym", "3d32_W_ssor"),
             ("prolong_z", "3d128_zsweep"), ("prolong_z", "3d_aniso_zsweep_ssor"), ("prolong_z,fuse_prolong", "3d128_zsweep"),
-            ("zpairs", "3d128_zsweep"), ("zpairs", "3d128_zsweep_odd"), ("zpairs", "3d_aniso_zsweep_ssor")]
+            ("zpairs", "3d128_zsweep"), ("zpairs", "3d128_zsweep_odd"), ("zpairs", "3d_aniso_zsweep_ssor"),
+            ("xzero", "3d_zres27"), ("xzero", "3d_jsweep_ssor_W")]
 
 
 @pytest.mark.parametrize("paths,name", VARIANTS)
@@ -206,7 +207,8 @@ def test_variant_cycles_bitwise(hip_device, monkeypatch, paths, name):
     instead of the restriction launch before it; sym = the 27-point kernels read all 27 coefficients
     of a reflection-symmetric stencil instead of one per symmetry class (stencil_coef); prolong_z = the
     per-point prolongation instead of the z-marching one on 3D levels; zpairs = every z-chunk of the plain
-    fine z-sweep marching up (no up / down chunk pairs);
+    fine z-sweep marching up (no up / down chunk pairs); xzero = the restriction zeroes x_{l+1} and the
+    coarse level's first (j-marching) pre-sweep loads it, instead of taking it as zeros;
     coarse_precompute = the coarse SSOR sampler's right-hand sides inside its colour passes;
     chol_dense = the coarse Cholesky's blocked banded solves on a small coarsest level (the oracle's
     blocked mode).  Every combination gives the oracle's cycle exactly."""
