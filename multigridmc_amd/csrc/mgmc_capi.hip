@@ -662,13 +662,22 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
         if (nk == 0) continue;
         const dim3 grid(a.nblk_y * nk, 1, nch);
         if (dim == 3) {
-            if (lv.sym) {
-                if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false, true>), grid, dim3(nt), lds, s, a);
-                else hipLaunchKernelGGL((k_sweep_quads<3, true, true>), grid, dim3(nt), lds, s, a);
-            } else {
-                if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false>), grid, dim3(nt), lds, s, a);
-                else hipLaunchKernelGGL((k_sweep_quads<3, true>), grid, dim3(nt), lds, s, a);
-            }
+            // xzero (3D): the first half takes every x row as 0.0, the second its own planes' rows
+#define MGMC_QD_LAUNCH(SYMV, XZ)                                                                      \
+    do {                                                                                              \
+        if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false, SYMV, XZ>), grid, dim3(nt), lds, s, a);  \
+        else hipLaunchKernelGGL((k_sweep_quads<3, true, SYMV, XZ>), grid, dim3(nt), lds, s, a);       \
+    } while (0)
+#define MGMC_QD_XZ(SYMV)                              \
+    do {                                              \
+        if (!xzero) MGMC_QD_LAUNCH(SYMV, 0);          \
+        else if (h == 0) MGMC_QD_LAUNCH(SYMV, 1);     \
+        else MGMC_QD_LAUNCH(SYMV, 2);                 \
+    } while (0)
+            if (lv.sym) MGMC_QD_XZ(true);
+            else MGMC_QD_XZ(false);
+#undef MGMC_QD_XZ
+#undef MGMC_QD_LAUNCH
         } else {
             if (fwd) hipLaunchKernelGGL((k_sweep_quads<2, false>), grid, dim3(nt), lds, s, a);
             else hipLaunchKernelGGL((k_sweep_quads<2, true>), grid, dim3(nt), lds, s, a);
@@ -1605,6 +1614,9 @@ int build_tails_only(mgmc_handle* h) {
         A.lds_doubles = off;
         // the tail patches level lt's f itself: the restriction before it must not
         if (!out.empty() && out.back().kind == OP_RESIDUAL_RESTRICT) out.back().lr_coarse_patch = 0;
+        // x_lt was just zeroed by that restriction (multigridmc_sampler.cc:122): not loaded
+        A.x_zero = (lt > 0 && !out.empty() && out.back().kind == OP_RESIDUAL_RESTRICT && out.back().level == lt - 1 &&
+                    !(h->paths & PATH_NO_XZERO)) ? 1 : 0;
         A.alpha = h->cfg.coarse_scaling;
         A.key = h->key;
         A.sample = h->ctrl;
@@ -1778,7 +1790,9 @@ void mark_zero_inputs(mgmc_handle* h) {
         const Level& lf = h->levels[rr.level];
         const Level& lc = h->levels[sw.level];
         const bool zr = lf.spec.dim == 3 && !lf.field && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8;
-        if (!zr || !lc.jsweep || lc.field || lf.lr.m > 0 || lc.lr.m > 0) continue;
+        // j-marching levels and 3D quad-pass levels: out of place, x read only as the half-sweeps' input
+        const bool quads3 = lc.quads && lc.spec.dim == 3;
+        if (!zr || !(lc.jsweep || quads3) || lc.field || lf.lr.m > 0 || lc.lr.m > 0) continue;
         rr.xzero = 1;
         sw.xzero = 1;
     }

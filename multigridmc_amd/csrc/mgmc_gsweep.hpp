@@ -159,7 +159,10 @@ struct QuadPassArgs {
     long long cs;       // batched chains: doubles between chains (blockIdx.z = chain)
 };
 
-template <int DIM, bool FIRST_ODD, bool SYM = false>  // SYM: stencil_coef's fold (3D, same bits)
+// SYM: stencil_coef's fold (3D, same bits).  XZ: the input x is known zero (the level's first pre-sweep,
+// mgmc_capi.hip mark_zero_inputs): 1 = every x row is the constant 0.0 (first half), 2 = the own planes'
+// rows are (second half) -- not loaded
+template <int DIM, bool FIRST_ODD, bool SYM = false, int XZ = 0>
 __global__ void __launch_bounds__(1024) k_sweep_quads(QuadPassArgs a) {
     {
         const int ch = batch_chain();
@@ -220,6 +223,10 @@ __global__ void __launch_bounds__(1024) k_sweep_quads(QuadPassArgs a) {
                     w[rr][1] = q[1];
                     w[rr][2] = q[2];
                     w[rr][3] = q[3];
+                    continue;
+                }
+                if (XZ == 1 || (XZ == 2 && dz == 0)) {
+                    w[rr][0] = w[rr][1] = w[rr][2] = w[rr][3] = 0.0;
                     continue;
                 }
                 const double* q = (dz == 0 ? a.x0 : a.xz) + p0 + (long long)dz * L.sp + (long long)dy * L.sx;

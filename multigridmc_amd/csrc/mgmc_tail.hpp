@@ -79,6 +79,8 @@ struct TailLevel {
 
 struct TailArgs {
     int nlev, nops, oscr, lds_doubles;
+    int x_zero;            // level lt's x is known zero on entry (the restriction before the tail zeroed it, lt > 0):
+                           // it is not loaded (the LDS fill already holds the zeros)
     double alpha;          // coarse_scaling
     RngKey key;
     const uint64_t* sample;
@@ -148,10 +150,15 @@ __device__ __forceinline__ void tail_issue_all(double (&v)[NPTS]) {
 }
 template <int DIM, int NPTS>
 __device__ __forceinline__ void tail_window(const double* __restrict__ x, int p, const Layout& G, double (&v)[NPTS]) {
+    // each index hidden behind an empty asm: the compiler cannot pair neighbouring reads into
+    // ds_read2_b64, which moves 8 bytes per lane at half the rate of ds_read_b64 (MI355X_MICROARCH.md,
+    // LDS table) -- the colour passes are bound by LDS throughput
 #pragma unroll
     for (int q = 0; q < NPTS; ++q) {
         const int dz = DIM == 3 ? q / 9 - 1 : 0, dy = (q / 3) % 3 - 1, dx = q % 3 - 1;
-        v[q] = x[p + dz * (int)G.sp + dy * (int)G.sx + dx];
+        int idx = p + dz * (int)G.sp + dy * (int)G.sx + dx;
+        asm volatile("" : "+v"(idx));
+        v[q] = x[idx];
     }
     tail_issue_all<NPTS>(v);
 }
@@ -251,7 +258,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
         for (int q = tid; q < nd; q += nt) {
             int i, j, k;
             coords(t0.G, q, i, j, k);
-            lds[t0.ox + (int)t0.G.at(i, j, k)] = xg[A->Lg.at(i, j, k)];
+            if (!A->x_zero) lds[t0.ox + (int)t0.G.at(i, j, k)] = xg[A->Lg.at(i, j, k)];
             lds[t0.of + (int)t0.G.at(i, j, k)] = fg[A->Lg.at(i, j, k)];
         }
     }

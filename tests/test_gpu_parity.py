@@ -191,7 +191,7 @@ VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_
             ("sym", "3d16"), ("sym", "3d64_4lvl"), ("sym", "3d32_W_ssor"),
             ("prolong_z", "3d128_zsweep"), ("prolong_z", "3d_aniso_zsweep_ssor"), ("prolong_z,fuse_prolong", "3d128_zsweep"),
             ("zpairs", "3d128_zsweep"), ("zpairs", "3d128_zsweep_odd"), ("zpairs", "3d_aniso_zsweep_ssor"),
-            ("xzero", "3d_zres27"), ("xzero", "3d_jsweep_ssor_W")]
+            ("xzero", "3d_zres27"), ("xzero", "3d_jsweep_ssor_W"), ("xzero", "3d64_4lvl"), ("xzero", "3d32_W_ssor")]
 
 
 @pytest.mark.parametrize("paths,name", VARIANTS)
