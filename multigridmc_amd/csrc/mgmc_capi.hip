@@ -567,8 +567,13 @@ void launch_rb2d(const Level& lv, const double* xin, double* xout, const double*
 // With 64-pair rows (512^3 level 2, 256^3 level 1) the kernel is slower than the pair passes (2 x 21 against
 // 4 x 8 us per sweep at 127^3, 256^3 cycle 0.484 -> 0.503 ms): those levels are latency-bound, and the
 // march's chunks are short.
+#ifndef MGMC_JS_NX128  // j-marching half-sweeps also on nx = 128 levels (timing builds: scripts/build_exp.sh)
+#define MGMC_JS_NX128 0
+#endif
+
 bool jsweep_eligible(const LevelSpec& sp, const Layout& L, uint32_t paths) {
-    return sp.dim == 3 && sp.npoints == 27 && (L.nx == 256 || L.nx == 512) && L.ny >= 2 && L.nz >= 2 &&
+    return sp.dim == 3 && sp.npoints == 27 && (L.nx == 256 || L.nx == 512 || (MGMC_JS_NX128 && L.nx == 128)) &&
+           L.ny >= 2 && L.nz >= 2 &&
            !(paths & PATH_NO_JSWEEP);
 }
 
@@ -617,6 +622,11 @@ void launch_jsweep(const Level& lv, const double* xin, double* xout, const doubl
     } while (0)
         if (np == 256) {  // FEM prior's 27-point fine level at 512^3 (not symmetric bit for bit)
             MGMC_JS_LAUNCH(256, false);
+#if MGMC_JS_NX128
+        } else if (np == 64) {
+            if (lv.sym) MGMC_JS_LAUNCH(64, true);
+            else MGMC_JS_LAUNCH(64, false);
+#endif
         } else if (lv.sym) {  // the cubic FD hierarchies' 255^3 level: 8 distinct coefficients
             MGMC_JS_LAUNCH(128, true);
         } else {

@@ -242,25 +242,26 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
         for (int u = tid; u < t.nrows; u += nt) f[t.rows_off[u]] = save[u];
     };
 
-    // interior vertex q of a level -> (i, j, k)
-    auto coords = [](const Layout& G, int q, int& i, int& j, int& k) {
-        const int nxi = G.nx - 1, nyi = G.ny - 1;
-        i = q % nxi + 1;
-        const int r = q / nxi;
-        j = r % nyi + 1;
-        k = DIM == 3 ? r / nyi + 1 : 0;
+    // body(i, j, k) for every interior vertex of a level, threads strided over a power-of-two box: bit
+    // fields instead of integer divisions (each a ~40-instruction sequence on the device), with the
+    // box's vertices outside the interior skipped.  The order is immaterial: vertices are independent.
+    auto bits_of = [](int n) { return 32 - __builtin_clz((unsigned)(n - 1 > 0 ? n - 1 : 1)); };
+    auto for_interior = [&](const Layout& G, auto&& body) __attribute__((always_inline)) {
+        const int bx = bits_of(G.nx), by = bits_of(G.ny), bz = DIM == 3 ? bits_of(G.nz) : 0;
+        const int tot = 1 << (bx + by + bz);
+        for (int q = tid; q < tot; q += nt) {
+            const int i = q & ((1 << bx) - 1), j = (q >> bx) & ((1 << by) - 1), k = DIM == 3 ? q >> (bx + by) : 0;
+            if (i < 1 || i > G.nx - 1 || j < 1 || j > G.ny - 1 || (DIM == 3 && (k < 1 || k > G.nz - 1))) continue;
+            body(i, j, k);
+        }
     };
-    auto ndof_of = [](const Layout& G) { return (G.nx - 1) * (G.ny - 1) * (DIM == 3 ? G.nz - 1 : 1); };
 
     {  // level lt from HBM (boundary entries stay 0)
         const TailLevel& t0 = A->lv[0];
-        const int nd = ndof_of(t0.G);
-        for (int q = tid; q < nd; q += nt) {
-            int i, j, k;
-            coords(t0.G, q, i, j, k);
+        for_interior(t0.G, [&](int i, int j, int k) {
             if (!A->x_zero) lds[t0.ox + (int)t0.G.at(i, j, k)] = xg[A->Lg.at(i, j, k)];
             lds[t0.of + (int)t0.G.at(i, j, k)] = fg[A->Lg.at(i, j, k)];
-        }
+        });
     }
     __syncthreads();
 
@@ -296,10 +297,13 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             __syncthreads();
         }
         const int npair = G.nx / 2;
-        const int nrow = (G.ny - 1) * (DIM == 3 ? G.nz - 1 : 1);
-        for (int q = tid; q < npair * nrow; q += nt) {
-            const int m = q % npair, row = q / npair;
-            const int j = row % (G.ny - 1) + 1, k = DIM == 3 ? row / (G.ny - 1) + 1 : 0;
+        // pairs (i0 = 2m + 1, i0 + 1) over a power-of-two box (bit fields, no divisions); q = the pair's
+        // item index in the pre-drawn noise (row-major over (k, j), m fastest)
+        const int bm = bits_of(npair), by = bits_of(G.ny), bz = DIM == 3 ? bits_of(G.nz) : 0;
+        for (int qq = tid; qq < (1 << (bm + by + bz)); qq += nt) {
+            const int m = qq & ((1 << bm) - 1), j = (qq >> bm) & ((1 << by) - 1), k = DIM == 3 ? qq >> (bm + by) : 0;
+            if (m >= npair || j < 1 || j > G.ny - 1 || (DIM == 3 && (k < 1 || k > G.nz - 1))) continue;
+            const int q = ((DIM == 3 ? k - 1 : 0) * (G.ny - 1) + (j - 1)) * npair + m;
             const int i0 = 2 * m + 1;
             if (i0 > G.nx - 1) continue;
             double z0, z1;
@@ -399,24 +403,18 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             tail_pin(lrm);
             const double* x = lds + ox;
             double* f = lds + of;
-            const int nd = ndof_of(G);
             if (lrm > 0) {  // r = (f - B Sigma^{-1} B^T x) - A x
                 lr_dots(t, t.sc_inv, x);
                 __syncthreads();
                 lr_patch_rows(t, f, -1);
                 __syncthreads();
             }
-            for (int q = tid; q < nd; q += nt) {
-                int i, j, k;
-                coords(G, q, i, j, k);
+            for_interior(G, [&](int i, int j, int k) {
                 const long long p = G.at(i, j, k);
                 scr[p] = f[p] - tail_sum<DIM, NPTS, SYM>(x, (int)p, G, S);
-            }
+            });
             __syncthreads();
-            const int ndc = ndof_of(Gc);
-            for (int q = tid; q < ndc; q += nt) {
-                int I, J, K;
-                coords(Gc, q, I, J, K);
+            for_interior(Gc, [&](int I, int J, int K) {
                 const int pf = (int)G.at(2 * I, 2 * J, 2 * K);
                 double rv[NPTS];  // the 3^d residuals, every read issued before the sum (tail_window)
                 tail_window<DIM, NPTS>(scr, pf, G, rv);
@@ -437,7 +435,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
                 const long long pc = Gc.at(I, J, K);
                 lds[cof + pc] = result;
                 lds[cox + pc] = 0.0;
-            }
+            });
             if (lrm > 0) lr_restore_rows(t, f);
             __syncthreads();
         } else {  // TAIL_PROLONG: x_l += alpha P x_{l+1}
@@ -452,10 +450,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             tail_pin(alpha);
             double* x = lds + ox;
             const double* xc = lds + cox;
-            const int nd = ndof_of(G);
-            for (int q = tid; q < nd; q += nt) {
-                int i, j, k;
-                coords(G, q, i, j, k);
+            for_interior(G, [&](int i, int j, int k) {
                 const long long p = G.at(i, j, k);
                 double v = x[p];
                 const int k0 = k >> 1, nk = (DIM == 3 && (k & 1)) ? 2 : 1;
@@ -479,7 +474,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
                     }
                 }
                 x[p] = v;
-            }
+            });
             __syncthreads();
         }
         TAIL_STAMP(3 + 2 * o);
@@ -487,12 +482,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
 
     {  // level lt back to HBM
         const TailLevel& t0 = A->lv[0];
-        const int nd = ndof_of(t0.G);
-        for (int q = tid; q < nd; q += nt) {
-            int i, j, k;
-            coords(t0.G, q, i, j, k);
-            xg[A->Lg.at(i, j, k)] = lds[t0.ox + (int)t0.G.at(i, j, k)];
-        }
+        for_interior(t0.G, [&](int i, int j, int k) { xg[A->Lg.at(i, j, k)] = lds[t0.ox + (int)t0.G.at(i, j, k)]; });
     }
     TAIL_STAMP(2 + 2 * A->nops);
 }
