@@ -534,14 +534,15 @@ bool pairs_eligible(const LevelSpec& sp, const Layout& L) {
     return (sp.npoints == 27 || sp.npoints == 9) && L.nx / 2 >= 1 && L.nx / 2 <= 256 && L.nx % 2 == 0;
 }
 
-// both colour pairs of a k-parity half per launch (k_sweep_quads): on levels with rows of <= 32
+// both colour pairs of a k-parity half per launch (k_sweep_quads): on levels with rows of <= 64
 // pairs, where each pair pass is launch-latency bound and halving the launches pays (256^3: 63^3
-// level 4 x 5.0 -> 2 x 7.6 us, 31^3 level 4 x 4.8 -> 2 x 6.3 us per sweep), and on every 2D pair-pass
+// level 4 x 5.0 -> 2 x 7.6 us, 31^3 level 4 x 4.8 -> 2 x 6.3 us per sweep; round 4, 127^3 level with
+// the folded stencil and xzero: 8 x 8 -> 61 us per cycle, 256^3 cycle -8 us), and on every 2D pair-pass
 // level (2D 1024^2 FD cycle 0.135 -> 0.129 ms, FEM 0.147 -> 0.139 ms; A/B in one box call).  On the
 // large 3D levels it loses (512^3 level 1: 2 x 105 us against 4 x 41 us per sweep): the
 // second pair's loads wait for the first pair's rows.  Levels that k_tail runs are left to it (caller).
 #ifndef MGMC_QUADS_MAXPAIR  // (timing-experiment builds override it: scripts/build_exp.sh QMAX)
-#define MGMC_QUADS_MAXPAIR 32
+#define MGMC_QUADS_MAXPAIR 64
 #endif
 bool quads_eligible(const LevelSpec& sp, const Layout& L, uint32_t paths) {
     if (!pairs_eligible(sp, L) || (paths & PATH_NO_QUADS)) return false;
@@ -657,7 +658,11 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
 #ifndef MGMC_QUADS_NT  // (timing-experiment builds override it: scripts/build_exp.sh QMAX=<pairs>x<threads>)
 #define MGMC_QUADS_NT 512
 #endif
-    a.T = std::max(1, MGMC_QUADS_NT / npair - 1);
+#ifndef MGMC_QUADS_NT_WIDE  // the same for 3D rows of more than 32 pairs (the 127^3 levels: 256 threads, T = 3,
+                            // 61.6 -> 58.3 us per cycle at 512^3 against 512; 1024: 72.8 us)
+#define MGMC_QUADS_NT_WIDE 256
+#endif
+    a.T = std::max(1, (dim == 3 && npair > 32 ? MGMC_QUADS_NT_WIDE : MGMC_QUADS_NT) / npair - 1);
     a.nblk_y = (lv.L.ny - 1 + 2 * a.T - 1) / (2 * a.T);
     const int nt = npair * (a.T + 1);
     const size_t lds = (size_t)(2 * a.T + 1) * (lv.L.nx + 2) * sizeof(double);
@@ -884,7 +889,10 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
     // coarse n = ZR_SMALL_NX up, 16 x 4 points (one wavefront) below, where the wide tiles would leave
     // most of the chip idle (the 27-point gather kernel took 24 us per launch on the 15^3 / 7^3 levels)
     if (lf.spec.dim == 3 && zero_xc && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8) {
-        const bool small = lc.L.nx < 32;
+#ifndef MGMC_ZR_SMALL_NX  // coarse nx below which the 16 x 4 tiles are used (timing builds: scripts/build_exp.sh)
+#define MGMC_ZR_SMALL_NX 32
+#endif
+        const bool small = lc.L.nx < MGMC_ZR_SMALL_NX;
         if (skip_xc) xc = nullptr;
         if (lf.spec.npoints == 7) {
             if (small) launch_zresrestrict_t<7, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch, tn);
@@ -986,6 +994,16 @@ void launch_prolongate(const Level& lf, const Level& lc, double* x, const double
     if (MGMC_PROLONG_Z > 0 && lf.spec.dim == 3 && (long long)(lf.L.nx / 2) * (lf.L.ny - 1) * (lf.L.nz - 1) >= (1LL << 16) &&
         !(lf.paths & PATH_NO_PROLONG_Z)) {
         constexpr int TZ = MGMC_PROLONG_Z > 0 ? MGMC_PROLONG_Z : 1;
+#ifndef MGMC_PROLONG_Z_SMALL  // planes per thread below 2^21 fine pair items (timing builds: scripts/build_exp.sh)
+#define MGMC_PROLONG_Z_SMALL TZ
+#endif
+        constexpr int TZS = MGMC_PROLONG_Z_SMALL;
+        if (TZS != TZ && (long long)(lf.L.nx / 2) * (lf.L.ny - 1) * (lf.L.nz - 1) < (1LL << 21)) {
+            const int nzc = (lf.L.nz - 1 + TZS - 1) / TZS;
+            const dim3 gz = grid3(lf.L.nx / 2, lf.L.ny - 1, nzc * nch, block);
+            hipLaunchKernelGGL((k_prolongate_z<TZS>), gz, block, 0, s, lf.L, lc.L, x, xc, alpha, nzc, csf, csc);
+            return;
+        }
         const int nzc = (lf.L.nz - 1 + TZ - 1) / TZ;
         const dim3 gz = grid3(lf.L.nx / 2, lf.L.ny - 1, nzc * nch, block);
         hipLaunchKernelGGL((k_prolongate_z<TZ>), gz, block, 0, s, lf.L, lc.L, x, xc, alpha, nzc, csf, csc);

@@ -170,5 +170,5 @@ def test_headline_kernel_instances(headline):
     assert k0["residual_restrict"] == "k_zresrestrict<7,64,8>"
     # the 255^3 Galerkin stencil is reflection-symmetric bit for bit: the folded instance (stencil_coef)
     assert s.level_kernels(1) == {"sweep": "k_jsweep_half<128,sym>", "residual_restrict": "k_zresrestrict<27,64,4>"}
-    assert s.level_kernels(2)["sweep"] == "k_sweep_pairs<3>"  # 64-pair rows: neither j-marching nor quads
+    assert s.level_kernels(2)["sweep"] == "k_sweep_quads<3>"  # 64-pair rows: quad passes
     assert s.level_kernels(NLEVEL - 1)["sweep"] == "k_tail<3>"

@@ -173,7 +173,7 @@ ALL_PATHS = ("tail,fuse_prolong,quads,rb2d,zsweep,pairs,zrestrict,lr_small,lr_me
 VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_ssor"),
             ("fuse_prolong", "3d128_zsweep_odd"), ("fuse_prolong", "3d_zres27"), ("fuse_prolong", "3d_jsweep_ssor_W"),
             ("tail", "3d16"), ("tail", "3d64_4lvl"), ("tail", "2d64_template_W"), ("tail", "3d32_W_ssor"),
-            ("quads", "3d64_4lvl"), ("quads", "3d_zres27"), ("quads", "2d256_global_coarse"),
+            ("quads", "3d64_4lvl"), ("quads", "3d_aniso_zsweep_ssor"), ("quads", "3d_zres27"), ("quads", "2d256_global_coarse"),
             ("quads", "2d_aniso_ssor"),
             ("rb2d", "2d64_template_W"), ("rb2d", "2d_aniso_ssor"),
             ("zsweep", "3d128_zsweep"), ("zsweep", "3d_aniso_zsweep_ssor"), ("zsweep", "3d192_zsweep"),
@@ -259,7 +259,7 @@ def test_nonfinite_state_fails_loudly(hip_device, name, qoi):
 @pytest.mark.parametrize("name,level,sweep", [("2d64_template_W", 0, "k_rb2d"), ("3d128_zsweep", 0, "k_zsweep_rb7<"),
                                               ("3d16", 0, "k_sweep_rb<3>"), ("3d_jsweep_ssor_W", 1, "k_jsweep_half<128>"),
                                               ("3d_zres27", 1, "k_jsweep_half<128>"), ("3d128_zsweep", 1, "k_sweep_quads<3>"),
-                                              ("3d_aniso_zsweep_ssor", 1, "k_sweep_pairs<3>"),
+                                              ("3d_aniso_zsweep_ssor", 1, "k_sweep_quads<3>"),
                                               ("3d64_4lvl", 1, "k_sweep_quads<3>")])
 def test_level_kernels_labels(hip_device, name, level, sweep):
     """mgmc_level_kernels names the sweep each level really runs (bench.py's roofline labels)."""
