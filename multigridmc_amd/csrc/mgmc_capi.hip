@@ -994,8 +994,9 @@ void launch_prolongate(const Level& lf, const Level& lc, double* x, const double
     if (MGMC_PROLONG_Z > 0 && lf.spec.dim == 3 && (long long)(lf.L.nx / 2) * (lf.L.ny - 1) * (lf.L.nz - 1) >= (1LL << 16) &&
         !(lf.paths & PATH_NO_PROLONG_Z)) {
         constexpr int TZ = MGMC_PROLONG_Z > 0 ? MGMC_PROLONG_Z : 1;
-#ifndef MGMC_PROLONG_Z_SMALL  // planes per thread below 2^21 fine pair items (timing builds: scripts/build_exp.sh)
-#define MGMC_PROLONG_Z_SMALL TZ
+#ifndef MGMC_PROLONG_Z_SMALL  // planes per thread below 2^21 fine pair items: twice the threads on the 127^3 /
+                              // 63^3 levels (512^3: 10.7 / 8.9 -> 9.2 / 6.3 us; 2: 9.7 / 6.0 us)
+#define MGMC_PROLONG_Z_SMALL 4
 #endif
         constexpr int TZS = MGMC_PROLONG_Z_SMALL;
         if (TZS != TZ && (long long)(lf.L.nx / 2) * (lf.L.ny - 1) * (lf.L.nz - 1) < (1LL << 21)) {
