@@ -817,7 +817,10 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
         const long long nchunk = std::max(1LL, (2 * slots + per_chunk - 1) / per_chunk);
         a.kz = std::max(8, (int)((lc.L.nz - 1 + nchunk - 1) / nchunk));
     }
-    if (NPTS == 27 && CX == 64 && work >= 4 * 1024) {
+#ifndef MGMC_ZR7_KZ_ROUNDS  // the same depth rule for the 7-point 64 x 4 instance (256^3 fine level; timing builds)
+#define MGMC_ZR7_KZ_ROUNDS 0
+#endif
+    if ((NPTS == 27 || (MGMC_ZR7_KZ_ROUNDS && NPTS == 7 && NT == 256)) && CX == 64 && work >= 4 * 1024) {
         // 27-point levels with enough tiles for several rounds (512^3 level 1): the chunk depth that
         // minimises rounds of resident workgroups x planes staged per chunk (2 kz + 2); 512^3 level 1:
         // kz 11 = 768 tiles, one round of 3 x 256 slots: 108 -> 101 us (round 4, kernel traces)
