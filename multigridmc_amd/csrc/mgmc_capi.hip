@@ -492,6 +492,31 @@ void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s,
         hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 0, MINW>), grid, dim3(NT), lds, s, a);
 }
 
+// z-chunk depth of a z-marching sweep: the deepest chunk (fewest prologue steps, 2 per chunk) that still
+// keeps 3/4 of the 2 x num_cu workgroup slots busy -- 512^3: 32 (plain) / 128 (post) planes, 256^3: 32 / 32.
+// Even: chunks start on odd planes (the first-colour element schedule, the coarse ring)
+static int zsweep_depth(const Level& lv, int ty, int tzmax) {
+    const long long tiles_xy = (long long)((lv.L.nx / 2) / ZS_XP) * ((lv.L.ny - 1 + ty - 1) / ty);
+    int tz = tzmax;
+    while (tz > 8 && 4 * tiles_xy * ((lv.L.nz - 1 + tz - 1) / tz) < 3LL * 2 * lv.num_cu) tz /= 2;
+    return tz;
+}
+
+// rows per tile of the plain z-sweep: a level whose TY-row tiles leave part of the one round of
+// 2 x num_cu slots idle runs the TYP-row tiles if those still fit the round (more, shorter columns;
+// 256^3: 416 -> 512 workgroups, the pre-sweep 100.5 -> 91.9 us; at 512^3, many rounds, the 20-row
+// tiles are faster)
+static int zsweep_plain_rows(const Level& lv, int nch) {
+    const int tz = zsweep_depth(lv, ZS_TY, ZS_TZ);
+    const bool zpairs = !(lv.paths & PATH_NO_ZPAIRS);
+    auto ntiles = [&](int ty) {
+        const long long nz = (lv.L.nz - 1 + tz - 1) / tz;
+        return (long long)((lv.L.nx / 2) / ZS_XP) * ((lv.L.ny - 1 + ty - 1) / ty) * (zpairs ? (nz + 1) / 2 * 2 : nz) * nch;
+    };
+    const long long slots = 2LL * lv.num_cu;
+    return (ZS_TYP != ZS_TY && ZS_NTP == ZS_NT && ntiles(ZS_TY) < slots && ntiles(ZS_TYP) <= slots) ? ZS_TYP : ZS_TY;
+}
+
 void launch_zsweep(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g0,
                    int direction, const Level* coarse, const double* xc, double alpha, hipStream_t s, int nch = 1) {
     ZSweepArgs a;
@@ -508,23 +533,17 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
     a.G = g0;
     a.G.colour = (direction == MGMC_FORWARD) ? 0 : 1;
     a.zpairs = 0;
-    const long long txy = (long long)((lv.L.nx / 2) / ZS_XP) * ((lv.L.ny - 1 + ZS_TY - 1) / ZS_TY);
-    const long long txyp = (long long)((lv.L.nx / 2) / ZS_XP) * ((lv.L.ny - 1 + ZS_TYP - 1) / ZS_TYP);
-    // z-chunk depth: the deepest chunk (fewest prologue steps, 2 per chunk) that still keeps 3/4 of
-    // the 2 x num_cu workgroup slots busy -- 512^3: 32 (plain) / 128 (post) planes, 256^3: 32 / 32.
-    // Even: chunks start on odd planes (the first-colour element schedule, the coarse ring)
-    auto depth = [&](long long tiles_xy, int tzmax) {
-        int tz = tzmax;
-        while (tz > 8 && 4 * tiles_xy * ((lv.L.nz - 1 + tz - 1) / tz) < 3LL * 2 * lv.num_cu) tz /= 2;
-        return tz;
-    };
     if (coarse) {  // fused-prolongation sweep
-        a.tz = depth(txyp, ZS_TZP);
+        a.tz = zsweep_depth(lv, ZS_TYP, ZS_TZP);
         launch_zsweep_t<ZS_XP, ZS_TYP, ZS_NTP, ZS_MINWP>(lv, a, true, s, nch);
         return;
     }
-    a.tz = depth(txy, ZS_TZ);
+    a.tz = zsweep_depth(lv, ZS_TY, ZS_TZ);
     a.zpairs = (lv.paths & PATH_NO_ZPAIRS) ? 0 : 1;
+    if (zsweep_plain_rows(lv, nch) != ZS_TY) {
+        launch_zsweep_t<ZS_XP, ZS_TYP, ZS_NTP, ZS_MINWP>(lv, a, false, s, nch);
+        return;
+    }
     launch_zsweep_t<ZS_XP, ZS_TY, ZS_NT, ZS_MINW>(lv, a, false, s, nch);
 }
 
@@ -817,8 +836,9 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
         const long long nchunk = std::max(1LL, (2 * slots + per_chunk - 1) / per_chunk);
         a.kz = std::max(8, (int)((lc.L.nz - 1 + nchunk - 1) / nchunk));
     }
-#ifndef MGMC_ZR7_KZ_ROUNDS  // the same depth rule for the 7-point 64 x 4 instance (256^3 fine level; timing builds)
-#define MGMC_ZR7_KZ_ROUNDS 0
+#ifndef MGMC_ZR7_KZ_ROUNDS  // the same depth rule for the 7-point 64 x 4 instance (256^3 fine level: kz 4 -> 11, 2,048
+                            // -> 768 workgroups = one round, 64.4 -> 57.7 us)
+#define MGMC_ZR7_KZ_ROUNDS 1
 #endif
     if ((NPTS == 27 || (MGMC_ZR7_KZ_ROUNDS && NPTS == 7 && NT == 256)) && CX == 64 && work >= 4 * 1024) {
         // 27-point levels with enough tiles for several rounds (512^3 level 1): the chunk depth that
@@ -2787,7 +2807,7 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
     } else if (lv.field) {
         sweep = "k_fsweep<" + std::to_string(dim) + ">";
     } else if (lv.zsweep) {
-        sweep = "k_zsweep_rb7<32," + std::to_string(MGMC_ZS_SHAPE_TY) + ",...,0>";
+        sweep = "k_zsweep_rb7<32," + std::to_string(zsweep_plain_rows(lv, h->nchains)) + ",...,0>";
         if (!(h->paths & PATH_NO_FUSE_PROLONG)) post = "k_zsweep_rb7<32," + std::to_string(MGMC_ZS_SHAPE_TYP) + ",...,PROLONG>";
     } else if (lv.jsweep) {
         sweep = "k_jsweep_half<" + std::to_string(lv.L.nx / 2) + (lv.sym && lv.L.nx == 256 ? ",sym" : "") + ">";

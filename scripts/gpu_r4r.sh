@@ -1,0 +1,10 @@
+# Round 4 head: 256^3 fine level with 16-row plain-sweep tiles and the rounds x depth chunk rule of the
+# 7-point residual + restriction -- parity modules (with the kernel-instance tests), 256^3 cycle times,
+# then the round evidence (bench line, rocprofv3 stats of the bench command, PMC FETCH / WRITE passes).
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/r4r && export TMPDIR=/tmp
+O=gpurun_out/r4r
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_headline.py tests/test_gpu_config3.py "tests/test_gpu_parity.py::test_variant_cycles_bitwise" "tests/test_gpu_parity.py::test_mgmc_cycles_bitwise" "tests/test_gpu_parity.py::test_level_kernels_labels" > $O/pytest.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -2 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
+N=256 NLEVEL=6 REPS=3 timeout -k 10 200 python scripts/lib_cycle_bench.py 0 > $O/cycle256.log 2>&1; rc=$?
+echo "cycle256 rc=$rc"; cat $O/cycle256.log; [ $rc -eq 0 ] || exit $rc
+bash scripts/profile_round.sh
