@@ -1,0 +1,22 @@
+# Round 4: the small levels' residual + restriction loading two fine planes ahead (PF2, chunks of <= 2
+# coarse planes; build/libmgmc_expzrpf2.so) against the product -- parity modules, kernel traces at
+# 512^3 and 256^3, cycle times.
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/r4s && export TMPDIR=/tmp
+O=gpurun_out/r4s
+MGMC_LIBRARY=$GRAFT_REPO_ROOT/build/libmgmc_expzrpf2.so timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_headline.py tests/test_gpu_config3.py "tests/test_gpu_parity.py::test_variant_cycles_bitwise" "tests/test_gpu_parity.py::test_mgmc_cycles_bitwise" > $O/pytest_zrpf2.log 2>&1; rc=$?
+echo "pytest zrpf2 rc=$rc"; tail -2 $O/pytest_zrpf2.log; [ $rc -eq 0 ] || exit $rc
+for v in 0 zrpf2; do
+  if [ "$v" = 0 ]; then unset MGMC_LIBRARY; else export MGMC_LIBRARY=$GRAFT_REPO_ROOT/build/libmgmc_exp$v.so; fi
+  K=10 timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $O/kt_$v -o kt -- python3 scripts/vcycle_once.py > $O/kt_$v.log 2>&1
+  rc=$?; echo "$v rc=$rc"; [ $rc -eq 0 ] || exit 3
+  python3 scripts/kstats.py $O/kt_$v/kt_kernel_trace.csv 13 > $O/kstats_$v.txt; echo "== $v"; grep -E "zresrestrict<27|total" $O/kstats_$v.txt
+  N=256 NLEVEL=6 K=10 timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $O/kt256_$v -o kt -- python3 scripts/vcycle_once.py > $O/kt256_$v.log 2>&1
+  rc=$?; echo "$v 256 rc=$rc"; [ $rc -eq 0 ] || exit 3
+  python3 scripts/kstats.py $O/kt256_$v/kt_kernel_trace.csv 13 > $O/kstats256_$v.txt; echo "== 256 $v"; grep -E "zresrestrict<27|total" $O/kstats256_$v.txt
+done
+unset MGMC_LIBRARY
+N=256 NLEVEL=6 REPS=3 timeout -k 10 300 python scripts/lib_cycle_bench.py 0,zrpf2 > $O/cycle256.log 2>&1; rc=$?
+echo "cycle256 rc=$rc"; cat $O/cycle256.log; [ $rc -eq 0 ] || exit $rc
+REPS=2 timeout -k 10 300 python scripts/lib_cycle_bench.py 0,zrpf2 > $O/cycle512.log 2>&1; rc=$?
+echo "cycle512 rc=$rc"; cat $O/cycle512.log
+exit $rc
