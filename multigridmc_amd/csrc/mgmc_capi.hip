@@ -859,12 +859,6 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
 #ifdef MGMC_ZR27_KZ  // (timing builds: scripts/build_exp.sh VARIANTS)
     if (NPTS == 27 && CX == 64) a.kz = MGMC_ZR27_KZ;
 #endif
-    // 27-point levels with chunks of at most 2 coarse planes (the 127^3 level and below): loads two fine
-    // planes ahead (PF2)
-#ifndef MGMC_ZR_PF2  // (timing builds)
-#define MGMC_ZR_PF2 0
-#endif
-    const bool pf2 = MGMC_ZR_PF2 && NPTS == 27 && a.kz <= 2;
     a.ntz = (lc.L.nz - 1 + a.kz - 1) / a.kz;
     const int nt = a.ntx * a.nty * a.ntz;
     const int nb = (nt + 7) / 8 * 8;
@@ -879,23 +873,9 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
         a.seed_hi = tn->seed_hi;
         a.sample = tn->sample;
         const int nextra = (int)std::min<long long>((tn->zbs + NT - 1) / NT, 64);
-        if constexpr (NPTS == 27) {
-            if (pf2) {
-                hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT, true, SYM, true>), dim3(nb + nextra, 1, nch),
-                                   dim3(NT), zrestrict_lds_bytes(CX, CY), s, a);
-                return;
-            }
-        }
         hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT, true, SYM>), dim3(nb + nextra, 1, nch), dim3(NT),
                            zrestrict_lds_bytes(CX, CY), s, a);
         return;
-    }
-    if constexpr (NPTS == 27) {
-        if (pf2) {
-            hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT, false, SYM, true>), dim3(nb, 1, nch), dim3(NT),
-                               zrestrict_lds_bytes(CX, CY), s, a);
-            return;
-        }
     }
     hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT, false, SYM>), dim3(nb, 1, nch), dim3(NT),
                        zrestrict_lds_bytes(CX, CY), s, a);

@@ -19,8 +19,6 @@
 // clamped onto the zero boundary rows / planes, columns past a row end onto the zero pair (nx+1, nx+2).
 // Global traffic: x and f once (16 B per fine vertex) + f_c, x_c (2 B per fine vertex).
 #pragma once
-#include <type_traits>
-
 #include "mgmc_kernels.hpp"
 #include "mgmc_tail.hpp"
 
@@ -48,10 +46,8 @@ struct ZRestrictArgs {
     const uint64_t* sample;
 };
 
-// SYM: a reflection-symmetric 27-point stencil, read by class (stencil_coef; same bits).  PF2: loads two
-// fine planes ahead instead of one (two register buffers for x and f): the small levels' chunks are a
-// few planes deep, and each step would otherwise wait for a load issued one step earlier
-template <int NPTS, int CX, int CY, int NT, bool ZN = false, bool SYM = false, bool PF2 = false>
+// SYM: a reflection-symmetric 27-point stencil, read by class (stencil_coef; same bits)
+template <int NPTS, int CX, int CY, int NT, bool ZN = false, bool SYM = false>
 __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
     if (ZN && (int)blockIdx.x >= a.nblk_main) {  // the tail's noise (see ZRestrictArgs)
         const int ch = batch_chain();
@@ -171,33 +167,28 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
         cpg[u] = cpin[u] ? Lc.at(I0 + cx, J0 + cy, 0) : 0;
     }
 
-    constexpr int NB = PF2 ? 2 : 1;  // register buffers: x(k) in px[k % NB], f(k) in pf[k % NB]
-    double2 px[NB][NLX], pf[NB][NLR];
+    double2 px[NLX], pf[NLR];
     // the chunk stages x planes 2 K0 - 2 .. 2 K1 and f planes 2 K0 - 1 .. 2 K1 - 1: the last step's loads one
     // plane ahead reload those (never used) instead of fetching the next chunk's planes
     const int kx_last = 2 * K1, kf_last = 2 * K1 - 1;
-    // b: the register buffer (static at every call: the parity of k is known there)
-    auto issue_x = [&](int k, auto bc) {
-        constexpr int b = decltype(bc)::value;
+    auto issue_x = [&](int k) {
         const double* base = plane_ptr(a.x, MGMC_CHUNK_CLAMP && k > kx_last ? kx_last : k);
 #pragma unroll
-        for (int u = 0; u < NLX; ++u) px[b][u] = *reinterpret_cast<const double2*>(base + xoff[u]);
+        for (int u = 0; u < NLX; ++u) px[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
     };
-    auto deposit_x = [&](int k, auto bc) {
-        constexpr int b = decltype(bc)::value;
+    auto deposit_x = [&](int k) {
         double* dst = xs + xslot(k) * XPS;
 #pragma unroll
         for (int u = 0; u < NLX; ++u)
             if (xlds[u] >= 0) {
-                dst[xlds[u]] = px[b][u].x;
-                dst[xlds[u] + XPP] = px[b][u].y;
+                dst[xlds[u]] = px[u].x;
+                dst[xlds[u] + XPP] = px[u].y;
             }
     };
-    auto issue_f = [&](int k, auto bc) {
-        constexpr int b = decltype(bc)::value;
+    auto issue_f = [&](int k) {
         const double* base = plane_ptr(a.f, MGMC_CHUNK_CLAMP && k > kf_last ? kf_last : k);
 #pragma unroll
-        for (int u = 0; u < NLR; ++u) pf[b][u] = *reinterpret_cast<const double2*>(base + roff[u]);
+        for (int u = 0; u < NLR; ++u) pf[u] = *reinterpret_cast<const double2*>(base + roff[u]);
     };
     // residual of fine plane k over the residual region (vertices outside the fine interior -> 0).
     // The two vertices of a pair advance together through the stencil terms, so their dependent
@@ -273,46 +264,37 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
             }
     };
 
-    // One fine plane k: deposit x(k+1), issue x(k+2), f(k+1) (PF2: x(k+3), f(k+2)) | barrier |
-    // residual(k) | barrier | accumulate.  The next step's residual writes the residual plane only after
-    // its own first barrier, i.e. after every thread accumulated; x(k+2) overwrites the slot of x(k-1),
-    // last read by residual(k) before the second barrier.  (The loads only target registers.)
+    // One fine plane k: deposit x(k+1), issue x(k+2), f(k+1) | barrier | residual(k) | barrier |
+    // accumulate.  The next step's residual writes the residual plane only after its own first
+    // barrier, i.e. after every thread accumulated; x(k+2) overwrites the slot of x(k-1), last read
+    // by residual(k) before the second barrier.
     double acc[NCP], accn[NCP];
     double2 fcur[NLR];
-    using BufE = std::integral_constant<int, 0>;
-    using BufO = std::integral_constant<int, NB - 1>;  // the odd planes' buffer
-    auto step = [&](int k, auto oddc) __attribute__((always_inline)) {
-        constexpr bool odd = decltype(oddc)::value;  // k odd
-        using Bk = std::conditional_t<odd, BufO, BufE>;  // buffer of planes with k's parity
-        using Bn = std::conditional_t<odd, BufE, BufO>;  // ... and with the other parity
-        deposit_x(k + 1, Bn{});
+    auto step = [&](int k) __attribute__((always_inline)) {
+        deposit_x(k + 1);
 #pragma unroll
-        for (int u = 0; u < NLR; ++u) fcur[u] = pf[Bk::value][u];
-        issue_x(k + 1 + NB, Bn{});
-        issue_f(k + NB, Bk{});
+        for (int u = 0; u < NLR; ++u) fcur[u] = pf[u];
+        issue_x(k + 2);
+        issue_f(k + 1);
         __syncthreads();
         residual(k, fcur);
         __syncthreads();
     };
-    // prologue: x planes 2K0-2, 2K0-1 in LDS; x(2K0) and f(2K0-1) in flight (PF2: also x(2K0+1), f(2K0))
-    issue_x(2 * K0 - 2, BufE{});
-    deposit_x(2 * K0 - 2, BufE{});
-    issue_x(2 * K0 - 1, BufE{});
-    deposit_x(2 * K0 - 1, BufE{});
-    issue_x(2 * K0, BufE{});
-    issue_f(2 * K0 - 1, BufO{});
-    if constexpr (PF2) {
-        issue_x(2 * K0 + 1, BufO{});
-        issue_f(2 * K0, BufE{});
-    }
+    // prologue: x planes 2K0-2, 2K0-1 in LDS, x(2K0) and f(2K0-1) in flight
+    issue_x(2 * K0 - 2);
+    deposit_x(2 * K0 - 2);
+    issue_x(2 * K0 - 1);
+    deposit_x(2 * K0 - 1);
+    issue_x(2 * K0);
+    issue_f(2 * K0 - 1);
 #pragma unroll
     for (int u = 0; u < NCP; ++u) acc[u] = 0.0;
-    step(2 * K0 - 1, std::true_type{});
+    step(2 * K0 - 1);
     accumulate(acc, 0);  // sz = 0 of coarse plane K0
     for (int K = K0; K < K1; ++K) {
-        step(2 * K, std::false_type{});
+        step(2 * K);
         accumulate(acc, 1);
-        step(2 * K + 1, std::true_type{});
+        step(2 * K + 1);
         accumulate(acc, 2);
         finish(acc, K);
 #pragma unroll
