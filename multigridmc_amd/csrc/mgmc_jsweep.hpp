@@ -39,15 +39,7 @@ namespace mgmc {
 
 // NP pairs per row (nx = 2 NP); 2 NP threads (A-row pairs, B-row pairs); ring rows of stride 2 NP + 8: odd pairs [0, NP) and the guard at NP, then
 // the even block from NP + 1: its guard (position 0) first, even pair m at NP + 2 + m
-// rows per plane in the LDS ring.  8: a step deposits the next rows into the slots of rows a-6, a-5
-// (read by no one) before its closing barrier.  6 (timing builds): those slots are rows a-4, a-3, still
-// read by the B-row in this step, so the deposit waits for the closing barrier and the next step opens
-// with one more barrier -- 25% less LDS, 4 instead of 3 workgroups per CU
-#ifndef MGMC_JS_RING
-#define MGMC_JS_RING 8
-#endif
-constexpr int JS_RING = MGMC_JS_RING;
-static_assert(JS_RING == 8 || JS_RING == 6, "JS_RING");
+constexpr int JS_RING = 8;           // rows per plane in the LDS ring
 #ifndef MGMC_JS_D  // (timing builds override it)
 #define MGMC_JS_D 3
 #endif
@@ -82,7 +74,7 @@ inline size_t jsweep_lds_bytes(int np) { return (size_t)(JS_RING * 3 * (2 * np +
 // 1 = every x row is the constant 0.0 (the first half), 2 = the own planes' rows are (the second half;
 // planes k +- 1 hold the first half's new values) -- those rows are not loaded at all
 template <int NP, bool FIRST_ODD, bool SYM = false, int XZ = 0>
-__global__ void __launch_bounds__(2 * NP, JS_RING < 8 && NP == 128 ? 4 : 1) k_jsweep_half(JSweepArgs a) {
+__global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
     constexpr int JS_NP = NP, JS_NT = 2 * NP, JS_RS = 2 * NP + 8, JS_EV = NP + 1;
     {
         const int ch = batch_chain();
@@ -226,7 +218,6 @@ __global__ void __launch_bounds__(2 * NP, JS_RING < 8 && NP == 128 ? 4 : 1) k_js
         const bool odd_in = go;                       // i0 <= nx - 1 always
         const bool even_in = go && i0 + 1 <= L.nx - 1;
         double* own = rowp(j, 1);
-        if constexpr (JS_RING < 8) js_barrier();  // the previous step's deposits (after its closing barrier)
         load_window(j);
         // first colour (a first-colour vertex reads only second-colour positions of its row besides its
         // own, so the new value goes straight into the ring)
@@ -259,9 +250,7 @@ __global__ void __launch_bounds__(2 * NP, JS_RING < 8 && NP == 128 ? 4 : 1) k_js
             __builtin_nontemporal_store(FIRST_ODD ? v1 : v2, dst);
             __builtin_nontemporal_store(FIRST_ODD ? v2 : v1, dst + 1);
         }
-        // the next step's rows (ar + 2, ar + 3) into the slots of rows ar - 6, ar - 5 (read by no one;
-        // ring of 6: rows ar - 4, ar - 3, once every B-row read of this step is past the barrier)
-        if constexpr (JS_RING < 8) js_barrier();
+        // the next step's rows (ar + 2, ar + 3) into the slots of rows ar - 6, ar - 5 (read by no one)
         if (s < s1) {
 #pragma unroll
             for (int q = 0; q < 3; ++q) {
@@ -271,7 +260,7 @@ __global__ void __launch_bounds__(2 * NP, JS_RING < 8 && NP == 128 ? 4 : 1) k_js
             guards(ar + 2);
             guards(ar + 3);
         }
-        if constexpr (JS_RING == 8) js_barrier();
+        js_barrier();
     };
     // steps s0 - 1 .. s1 in groups of JS_D (idle steps at the end), buffers by step index from the chunk
     // start, so the loop carries its registers without copies (a copy of an in-flight load would wait
