@@ -807,6 +807,9 @@ struct TailNoiseLaunch {  // spare workgroups of the launch draw a tail's noise 
     const uint64_t* sample;
 };
 
+#ifndef MGMC_ZR27_CX  // coarse points per tile in x of the symmetric 27-point instance (timing builds)
+#define MGMC_ZR27_CX 64
+#endif
 template <int NPTS, int CX, int CY, int NT, bool SYM = false>
 void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, const double* f, double* fc, double* xc,
                            hipStream_t s, int nch, const TailNoiseLaunch* tn = nullptr) {
@@ -840,11 +843,13 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
                             // -> 768 workgroups = one round, 64.4 -> 57.7 us)
 #define MGMC_ZR7_KZ_ROUNDS 1
 #endif
-    if ((NPTS == 27 || (MGMC_ZR7_KZ_ROUNDS && NPTS == 7 && NT == 256)) && CX == 64 && work >= 4 * 1024) {
+    if ((NPTS == 27 || (MGMC_ZR7_KZ_ROUNDS && NPTS == 7 && NT == 256)) && CX >= 48 && work >= 4 * 1024) {
         // 27-point levels with enough tiles for several rounds (512^3 level 1): the chunk depth that
         // minimises rounds of resident workgroups x planes staged per chunk (2 kz + 2); 512^3 level 1:
         // kz 11 = 768 tiles, one round of 3 x 256 slots: 108 -> 101 us (round 4, kernel traces)
-        const long long slots = (long long)(160 * 1024 / zrestrict_lds_bytes(CX, CY)) * lf.num_cu;
+        // workgroups per CU: LDS-bound, and at most 3 for the 27-point instances (> 128 VGPRs)
+        const long long per_cu = std::min<long long>(160 * 1024 / zrestrict_lds_bytes(CX, CY), NPTS == 27 ? 3 : 4);
+        const long long slots = per_cu * lf.num_cu;
         const long long per_chunk = (long long)a.ntx * a.nty;
         long long best = -1;
         for (int kz = 2; kz <= 16; ++kz) {
@@ -931,7 +936,7 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
 #endif
             if (small && lf.sym) launch_zresrestrict_t<27, 16, 4, 64, true>(lf, lc, x, f, fc, xc, s, nch, tn);
             else if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch, tn);
-            else if (MGMC_ZR27_CY == 4 && lf.sym) launch_zresrestrict_t<27, 64, 4, 256, true>(lf, lc, x, f, fc, xc, s, nch);
+            else if (MGMC_ZR27_CY == 4 && lf.sym) launch_zresrestrict_t<27, MGMC_ZR27_CX, 4, 256, true>(lf, lc, x, f, fc, xc, s, nch);
             else if (MGMC_ZR27_CY == 8 && lc.L.nx >= 128)
                 launch_zresrestrict_t<27, 64, 8, 512>(lf, lc, x, f, fc, xc, s, nch);
             else if (MGMC_ZR27_CY == 3)
@@ -2370,7 +2375,7 @@ static int zrestrict_cx_of(const mgmc_handle* h, int l) {  // launch_residual_re
     const Level& lf = h->levels[l];
     const Level& lc = h->levels[l + 1];
     if (lf.spec.dim != 3 || lf.field || (lf.paths & PATH_NO_ZRESTRICT) || lc.L.nx < 8) return 0;
-    return lc.L.nx < 32 ? 16 : 64;
+    return lc.L.nx < 32 ? 16 : (lf.spec.npoints == 27 && lf.sym ? MGMC_ZR27_CX : 64);
 }
 // both directions and both halves of a j-marching level, with launch_jsweep's plan (short_grid: the plan
 // with its last 8 workgroups dropped -- a negative control for the test, which the replay must reject)
