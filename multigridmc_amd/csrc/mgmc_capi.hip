@@ -681,7 +681,10 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
                             // 61.6 -> 58.3 us per cycle at 512^3 against 512; 1024: 72.8 us)
 #define MGMC_QUADS_NT_WIDE 256
 #endif
-    a.T = std::max(1, (dim == 3 && npair > 32 ? MGMC_QUADS_NT_WIDE : MGMC_QUADS_NT) / npair - 1);
+#ifndef MGMC_QUADS_NT3  // the same for 3D rows of <= 32 pairs (63^3, 31^3; timing builds)
+#define MGMC_QUADS_NT3 MGMC_QUADS_NT
+#endif
+    a.T = std::max(1, (dim == 3 ? (npair > 32 ? MGMC_QUADS_NT_WIDE : MGMC_QUADS_NT3) : MGMC_QUADS_NT) / npair - 1);
     a.nblk_y = (lv.L.ny - 1 + 2 * a.T - 1) / (2 * a.T);
     const int nt = npair * (a.T + 1);
     const size_t lds = (size_t)(2 * a.T + 1) * (lv.L.nx + 2) * sizeof(double);
