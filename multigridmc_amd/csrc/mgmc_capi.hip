@@ -681,8 +681,9 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
                             // 61.6 -> 58.3 us per cycle at 512^3 against 512; 1024: 72.8 us)
 #define MGMC_QUADS_NT_WIDE 256
 #endif
-#ifndef MGMC_QUADS_NT3  // the same for 3D rows of <= 32 pairs (63^3, 31^3; timing builds)
-#define MGMC_QUADS_NT3 MGMC_QUADS_NT
+#ifndef MGMC_QUADS_NT3  // the same for 3D rows of <= 32 pairs (63^3, 31^3): 128 threads, 4x the workgroups of
+                        // 512 (512^3 63^3 launches 7.3-7.8 -> 5.6-6.3 us; 256^3 cycle -7 us; 64 / 256: -6 / -5.5 us)
+#define MGMC_QUADS_NT3 128
 #endif
     a.T = std::max(1, (dim == 3 ? (npair > 32 ? MGMC_QUADS_NT_WIDE : MGMC_QUADS_NT3) : MGMC_QUADS_NT) / npair - 1);
     a.nblk_y = (lv.L.ny - 1 + 2 * a.T - 1) / (2 * a.T);
