@@ -675,8 +675,8 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
     const int npair = lv.L.nx / 2;
     // T+1 thread rows of npair threads
 #ifndef MGMC_QUADS_NT  // 2D levels (timing-experiment builds override it: scripts/build_exp.sh QMAX=<pairs>x<threads>);
-                       // 256: config 2 (2D 1024^2) 10,623 -> 10,775 samples/s against 512, 1024: 10,257
-#define MGMC_QUADS_NT 256
+                       // config 2 (2D 1024^2): 512 10,623, 256 10,775, 128 10,883 samples/s (1024: 10,257)
+#define MGMC_QUADS_NT 128
 #endif
 #ifndef MGMC_QUADS_NT_WIDE  // the same for 3D rows of more than 32 pairs (the 127^3 levels: 256 threads, T = 3,
                             // 61.6 -> 58.3 us per cycle at 512^3 against 512; 1024: 72.8 us)
