@@ -116,6 +116,10 @@ typedef struct mgmc_handle mgmc_handle;
 
 /* ---- host-only helpers (no GPU touched) ---- */
 int mgmc_abi_version(void);
+/* Handles created and not yet destroyed in this process (any mgmc_create* variant).  A host
+ * integration checks with it that its owners release their device state (the reference's
+ * shared_ptr ownership). */
+int mgmc_live_handles(void);
 /* Validate cfg and fill out[0..nlevel-1] with the level hierarchy and Galerkin stencils.
  * Returns the number of levels (> 0) or a negative MGMC_E* code. */
 int mgmc_describe(const mgmc_config* cfg, mgmc_level_desc* out, int max_levels);
@@ -279,7 +283,8 @@ int mgmc_smoother_apply(mgmc_handle* h, int level, int direction, int nsweeps,
                         const double* b, double* x);
 /* The Smoother drop-ins (include/reference_adapter/hip_sor_smoother.hh), noise-free multicolour sweeps:
  * SORSmoother::apply exactly as the reference nests it -- nsmooth x (nsmooth sweeps of apply_sparse,
- * then the B_bar fix once), smoother/sor_smoother.cc:41-53 over :56-78 -- so nsmooth^2 sweeps ... */
+ * then the B_bar fix once), smoother/sor_smoother.cc:41-53 over :56-78 -- so nsmooth^2 sweeps;
+ * 0 <= nsmooth <= 1024, else MGMC_E_INVALID ... */
 int mgmc_sor_smoother_apply(mgmc_handle* h, int level, int direction, int nsmooth, const double* b, double* x);
 /* ... and SSORSmoother::apply (smoother/ssor_smoother.cc:9-15): nsmooth x (forward sweep + fix,
  * backward sweep + fix) */

@@ -25,13 +25,17 @@
 // the CSC form mgmc_set_lowrank takes) and get_Sigma().diagonal().
 //
 // Noise: the reference's sampler draws from the shared std::mt19937_64; the device stream is
-// counter-based (Philox keyed by seed and chain id).  The constructor takes the
-// Philox seed as an explicit argument (default 5418513, the driver's literal seed, driver_mgmc.cc:448)
-// and never draws from the shared engine: the reference's MultigridMCSampler consumes none at
-// construction (multigridmc_sampler.cc:8-100), so the SSOR / Cholesky samplers driver_mgmc builds
-// after it (driver_mgmc.cc:450-501) see the engine state they see in an unmodified reference.  A
-// caller that wants the seed tied to the engine passes rng() itself.  Errors print and exit(-1) like
-// the reference (multigridmc_sampler.cc:47-49).
+// counter-based (Philox keyed by seed and chain id).  By default the Philox seed
+// is the next output of a COPY of the shared engine, so the samples follow the driver's seed
+// (driver_mgmc.cc:448) while the engine itself is never advanced: the reference's
+// MultigridMCSampler consumes none at construction (multigridmc_sampler.cc:8-100), so the SSOR /
+// Cholesky samplers driver_mgmc builds after it (driver_mgmc.cc:450-501) see the engine state they
+// see in an unmodified reference.  Two samplers built on the same (unadvanced) engine therefore get
+// the same seed: give them distinct chain ids, or pass an explicit seed as the last argument.
+// Ownership: like the reference's Sampler, the base class has no virtual destructor, so a sampler is
+// owned as driver_mgmc.cc:450-457 owns it, std::make_shared<HipMultigridMCSampler>(...) (the
+// shared_ptr's deleter destroys the derived object and its device handle).  Errors print and
+// exit(-1) like the reference (multigridmc_sampler.cc:47-49).
 #pragma once
 
 #include <cstdint>
@@ -49,14 +53,25 @@
 class HipMultigridMCSampler : public Sampler {
    public:
     enum class Path { stencil, matrix };
-    static constexpr uint64_t default_seed = 5418513;  // driver_mgmc.cc:448
+    static constexpr uint64_t default_seed = 5418513;  // driver_mgmc.cc:448 (seed of the noise-free smoother handles)
+
+    // Philox seed by default: the next output of a copy of the shared engine (the engine is not advanced)
+    static uint64_t engine_seed(const std::mt19937_64& rng_) {
+        std::mt19937_64 copy = rng_;
+        return copy();
+    }
 
     // The reference's MultigridMCSampler(linear_operator, rng, params, cholesky_params) plus where to
-    // run: the HIP device, the chain id of the Philox key (one chain per rank, nchains per handle) and
-    // the Philox seed.  rng_ is kept as the Sampler base keeps it and is not drawn from.
+    // run: the HIP device and the chain id of the Philox key (one chain per rank, nchains per handle).
+    // rng_ is kept as the Sampler base keeps it and is not drawn from.
     HipMultigridMCSampler(const std::shared_ptr<LinearOperator> linear_operator_, std::mt19937_64& rng_,
-                          const MultigridParameters params_, int device = 0, uint64_t chain_id = 0, int nchains = 1,
-                          uint64_t seed_ = default_seed)
+                          const MultigridParameters params_, int device = 0, uint64_t chain_id = 0, int nchains = 1)
+        : HipMultigridMCSampler(linear_operator_, rng_, params_, device, chain_id, nchains, engine_seed(rng_)) {}
+
+    // ... with an explicit Philox seed
+    HipMultigridMCSampler(const std::shared_ptr<LinearOperator> linear_operator_, std::mt19937_64& rng_,
+                          const MultigridParameters params_, int device, uint64_t chain_id, int nchains,
+                          uint64_t seed_)
         : Sampler(linear_operator_, rng_), seed(seed_) {
         Path path = Path::matrix;
         impl = make_impl(*linear_operator_, params_, device, seed, chain_id, nchains, &path);

@@ -76,6 +76,7 @@ _DP = POINTER(c_double)
 _H = c_void_p
 SIGNATURES = [
     ("mgmc_abi_version", c_int, []),
+    ("mgmc_live_handles", c_int, []),
     ("mgmc_describe", c_int, [POINTER(MgmcConfig), POINTER(MgmcLevelDesc), c_int]),
     ("mgmc_last_error", c_char_p, [_H]),
     ("mgmc_create", c_int, [POINTER(MgmcConfig), c_int, c_uint64, c_uint64, POINTER(c_void_p)]),

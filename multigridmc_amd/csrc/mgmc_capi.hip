@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <mutex>
 #include <string>
@@ -259,7 +260,17 @@ void free_lowrank(LowRankDev& lr) {
 
 }  // namespace
 
+// handles alive in this process (mgmc_live_handles): every mgmc_handle counts itself
+static std::atomic<int> g_live_handles{0};
+struct LiveHandleCount {
+    LiveHandleCount() { g_live_handles.fetch_add(1); }
+    ~LiveHandleCount() { g_live_handles.fetch_sub(1); }
+    LiveHandleCount(const LiveHandleCount&) = delete;
+    LiveHandleCount& operator=(const LiveHandleCount&) = delete;
+};
+
 struct mgmc_handle {
+    LiveHandleCount live;
     mgmc_config cfg;
     int device = 0;
     uint64_t seed = 0, chain = 0;   // chain = the first chain of a batch (mgmc_create_batch)
@@ -321,6 +332,7 @@ struct mgmc_handle {
     double* chol_Li = nullptr;
     int chol_B = 0, chol_nb = 0; // blocked banded (chol_B > 0): Cf, Cb, Df, Db in one allocation
     double* chol_blk = nullptr;
+    bool unusable = false;       // a failed mgmc_set_lowrank could not restore the prior's coarse factor
     bool poison = false;         // MGMC_POISON=1: NaN-filled scratch allocations and LDS (debug, poison_fill)
     unsigned long long* tail_prof = nullptr;  // (timing builds, MGMC_TAIL_PROF: the first tail's phase stamps)
     std::vector<TailOp> tail_prof_ops;
@@ -362,6 +374,15 @@ __global__ void __launch_bounds__(1024) k_lds_poison() {
     __syncthreads();
     // a read the compiler cannot drop keeps the stores alive
     if (lds[(threadIdx.x * 7) % LDS_POISON_DOUBLES] == 0.0) asm volatile("" ::: "memory");
+}
+// NaN into every interior vertex of one level vector (the zero boundary and pad stay zero): in poison
+// mode the coarse x a restriction with Op::xzero leaves unwritten (it holds the previous cycle's
+// values until the post-sweep rewrites it) -- a later op that read it would trip the guard
+__global__ void __launch_bounds__(256) k_poison_interior(Layout L, double* __restrict__ x) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x + 1;
+    const int j = blockIdx.y + 1;
+    const int k = L.dim == 3 ? (int)blockIdx.z + 1 : 0;
+    if (i <= L.nx - 1) x[L.at(i, j, k)] = __builtin_nan("");
 }
 }  // namespace
 
@@ -1944,6 +1965,11 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                     launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch, &tn);
                 } else {
                     launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch, nullptr, op.xzero != 0);
+                    if (op.xzero && h->poison)  // (debug) the skipped x_c write leaves stale values: make them NaN
+                        for (int c = 0; c < nch; ++c)
+                            hipLaunchKernelGGL(k_poison_interior, dim3((lc.L.nx - 1 + 255) / 256, lc.L.ny - 1,
+                                                                       lc.spec.dim == 3 ? lc.L.nz - 1 : 1),
+                                               dim3(256), 0, s, lc.L, chain_ptr(lc.x, lc, c));
                 }
                 if (lr && lv.lr.dense_path)
                     ;  // f was never patched; the post-sweep's rhs went to lr.fe2 above
@@ -2129,8 +2155,15 @@ int download(mgmc_handle* h, int level, const double* pad, double* host) {
     return MGMC_OK;
 }
 
+// a handle whose mgmc_set_lowrank rollback failed refuses all work but mgmc_destroy
+static int refuse_unusable(mgmc_handle* h) {
+    return fail(h, MGMC_E_INVALID, "handle unusable: a failed mgmc_set_lowrank could not restore the prior's coarse "
+                                   "factor (mgmc_destroy it)");
+}
+
 int check_level(mgmc_handle* h, int level, bool need_coarser) {
     if (!h) return fail(nullptr, MGMC_E_INVALID, "null handle");
+    if (h->unusable) return refuse_unusable(h);
     if (level < 0 || level >= (int)h->levels.size()) return fail(h, MGMC_E_INVALID, "level out of range");
     if (need_coarser && level + 1 >= (int)h->levels.size())
         return fail(h, MGMC_E_INVALID, "level has no coarser level");
@@ -2354,6 +2387,8 @@ FieldHost make_field(const CsrHost& A, int dim, const int* n, int level) {
 extern "C" {
 
 int mgmc_abi_version(void) { return MGMC_ABI_VERSION; }
+
+int mgmc_live_handles(void) { return g_live_handles.load(); }
 
 const char* mgmc_last_error(const mgmc_handle* h) {
     if (h) return h->last_error.c_str();
@@ -2939,6 +2974,7 @@ static int set_qoi(mgmc_handle* h, int64_t qoi_index) {
 
 int mgmc_apply(mgmc_handle* h, const double* f, double* x, size_t n) {
     if (!h || !f || !x) return fail(h, MGMC_E_INVALID, "null argument");
+    if (h->unusable) return refuse_unusable(h);
     int rc = mgmc_set_rhs(h, f, n);
     if (rc) return rc;
     if ((rc = mgmc_set_state(h, x, n))) return rc;
@@ -2950,6 +2986,7 @@ int mgmc_apply(mgmc_handle* h, const double* f, double* x, size_t n) {
 
 int mgmc_sample_async(mgmc_handle* h, int nsteps, int64_t qoi_index) {
     if (!h || nsteps < 0) return fail(h, MGMC_E_INVALID, "invalid argument");
+    if (h->unusable) return refuse_unusable(h);
     HIPCHK(h, hipSetDevice(h->device));
     int rc = set_qoi(h, qoi_index);
     if (rc) return rc;
@@ -3158,9 +3195,13 @@ static int smoother_sequence(mgmc_handle* h, int level, const std::vector<std::p
     return download(h, level, lv.scratch[1], x);
 }
 
+// nsmooth bound of the smoother drop-ins: SORSmoother::apply runs nsmooth^2 sweeps, so 1024 is a
+// million sweeps; above it the sweep list (and nsmooth * nsmooth in int) would overflow
+static constexpr int MAX_NSMOOTH = 1024;
+
 int mgmc_sor_smoother_apply(mgmc_handle* h, int level, int direction, int nsmooth, const double* b, double* x) {
     if (direction != MGMC_FORWARD && direction != MGMC_BACKWARD) return fail(h, MGMC_E_INVALID, "invalid direction");
-    if (nsmooth < 0) return fail(h, MGMC_E_INVALID, "nsmooth must be >= 0");
+    if (nsmooth < 0 || nsmooth > MAX_NSMOOTH) return fail(h, MGMC_E_INVALID, "nsmooth must be in [0, 1024]");
     // SORSmoother::apply (sor_smoother.cc:41-53) over apply_sparse (:56-78): both loop nsmooth times
     std::vector<std::pair<int, bool>> seq;
     for (int k = 0; k < nsmooth; ++k)
@@ -3169,7 +3210,7 @@ int mgmc_sor_smoother_apply(mgmc_handle* h, int level, int direction, int nsmoot
 }
 
 int mgmc_ssor_smoother_apply(mgmc_handle* h, int level, int nsmooth, const double* b, double* x) {
-    if (nsmooth < 0) return fail(h, MGMC_E_INVALID, "nsmooth must be >= 0");
+    if (nsmooth < 0 || nsmooth > MAX_NSMOOTH) return fail(h, MGMC_E_INVALID, "nsmooth must be in [0, 1024]");
     // SSORSmoother::apply (ssor_smoother.cc:9-15): its SORSmoothers have nsmooth 1 (ssor_smoother.hh:47-48)
     std::vector<std::pair<int, bool>> seq;
     for (int k = 0; k < nsmooth; ++k) {
@@ -3317,6 +3358,7 @@ int mgmc_sample_timed_stride(mgmc_handle* h, int nsteps, int stride, int64_t qoi
                              double* pre_ms, int* npre, double* post_ms, int* npost) {
     if (!h || nsteps < 1 || stride < 1 || !total_ms || !pre_ms || !npre || !post_ms || !npost)
         return fail(h, MGMC_E_INVALID, "invalid argument");
+    if (h->unusable) return refuse_unusable(h);
     if (h->levels.size() < 2) return fail(h, MGMC_E_UNSUPPORTED, "timed sampling needs nlevel >= 2");
     HIPCHK(h, hipSetDevice(h->device));
     int rc = set_qoi(h, qoi_index);
@@ -3854,14 +3896,21 @@ int mgmc_set_lowrank(mgmc_handle* h, int m, const int64_t* colptr, const int64_t
         for (auto& lv : h->levels) free_lowrank(lv.lr);
         h->lr_cols.clear();
         h->lr_sigma.clear();
-        if (h->chol_n > 0) (void)build_coarse_chol(h, nullptr, nullptr, 0);  // (succeeded at mgmc_create)
         h->last_error = err;
+        if (h->chol_n > 0 && build_coarse_chol(h, nullptr, nullptr, 0) != MGMC_OK) {
+            // the prior's factor built at mgmc_create cannot be rebuilt (e.g. an allocation): no
+            // sample call may run on a half-built coarse factor
+            h->unusable = true;
+            h->last_error = err + "; restoring the prior's coarse Cholesky factor failed too (" + h->last_error +
+                            "): the handle is unusable";
+        }
         set_global_error(err);
     }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     build_ops(h);
     int rc2 = build_tails(h);
     if (!rc2) rc2 = build_graphs(h);
+    if (!rc && !rc2) h->unusable = false;  // a later successful install rebuilt a whole coarse factor
     return rc ? rc : rc2;
 }
 

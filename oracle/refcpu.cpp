@@ -273,7 +273,9 @@ static void vertex_coords(const Lattice& lat, int64_t ell, double* x) {
 // =============================================================================================
 // Fine operator: ShiftedLaplaceFDOperator (shiftedlaplace_fd_operator.cc:9-57)
 // =============================================================================================
-static CSR fd_operator(const Lattice& lat, const KappaModel& kappa) {
+// One row of the FD operator: triplets (shifts in (d, -/+) order, then the diagonal), sorted by
+// column as setFromTriplets leaves them (columns are distinct)
+static int64_t fd_row(const Lattice& lat, const KappaModel& kappa, int64_t ell, int32_t* cols, double* vals) {
     const int dim = lat.dim;
     double hinv2[3] = {0, 0, 0};
     double cell_volume = 1.0;
@@ -282,34 +284,34 @@ static CSR fd_operator(const Lattice& lat, const KappaModel& kappa) {
         hinv2[d] = 1. / (h * h);
         cell_volume *= h;
     }
-    // triplets of one row (shifts in (d, -/+) order, then the diagonal), sorted by column as
-    // setFromTriplets leaves them (columns are distinct)
-    auto row = [&](int64_t ell, int32_t* cols, double* vals) -> int64_t {
-        std::pair<int64_t, double> r[7];
-        int cnt = 0;
-        double xv[3] = {0, 0, 0};
-        vertex_coords(lat, ell, xv);
-        double diagonal = cell_volume * kappa(xv, dim);
-        for (int d = 0; d < dim; ++d) {
-            for (int j = 0; j < 2; ++j) {
-                int s[3] = {0, 0, 0};
-                s[d] = 2 * j - 1;
-                int64_t e;
-                if (lat.shifted(ell, s, e)) r[cnt++] = {e, -cell_volume * hinv2[d]};
-            }
-            diagonal += 2. * cell_volume * hinv2[d];
+    std::pair<int64_t, double> r[7];
+    int cnt = 0;
+    double xv[3] = {0, 0, 0};
+    vertex_coords(lat, ell, xv);
+    double diagonal = cell_volume * kappa(xv, dim);
+    for (int d = 0; d < dim; ++d) {
+        for (int j = 0; j < 2; ++j) {
+            int s[3] = {0, 0, 0};
+            s[d] = 2 * j - 1;
+            int64_t e;
+            if (lat.shifted(ell, s, e)) r[cnt++] = {e, -cell_volume * hinv2[d]};
         }
-        r[cnt++] = {ell, diagonal};
-        std::sort(r, r + cnt, [](const std::pair<int64_t, double>& a, const std::pair<int64_t, double>& b) {
-            return a.first < b.first;
-        });
-        for (int q = 0; q < cnt; ++q) {
-            cols[q] = (int32_t)r[q].first;
-            vals[q] = r[q].second;
-        }
-        return cnt;
-    };
-    return csr_from_rows(lat.nvertex(), row);
+        diagonal += 2. * cell_volume * hinv2[d];
+    }
+    r[cnt++] = {ell, diagonal};
+    std::sort(r, r + cnt, [](const std::pair<int64_t, double>& a, const std::pair<int64_t, double>& b) {
+        return a.first < b.first;
+    });
+    for (int q = 0; q < cnt; ++q) {
+        cols[q] = (int32_t)r[q].first;
+        vals[q] = r[q].second;
+    }
+    return cnt;
+}
+
+static CSR fd_operator(const Lattice& lat, const KappaModel& kappa) {
+    return csr_from_rows(lat.nvertex(),
+                         [&](int64_t ell, int32_t* cols, double* vals) { return fd_row(lat, kappa, ell, cols, vals); });
 }
 
 // ShiftedLaplaceFEMOperator with constant kappa^2 (shiftedlaplace_fem_operator.cc:9-145): sparsity
@@ -1514,6 +1516,42 @@ orc_handle* orc_create_fd(const orc_params* q, int mode, uint64_t seed, uint64_t
     h->f.assign(h->mg->x_ell[0].size(), 0.0);
     h->x.assign(h->mg->x_ell[0].size(), 0.0);
     return h;
+}
+
+// The oracle's own stencil of every level of an FD hierarchy (out: nlevel*27, sidx order) without
+// assembling any level: the fine row is the FD assembly's interior row (2,2[,2]) of the full-size
+// lattice (fd_row, the reference's expression), each coarse stencil the interior row of R*A*R^T
+// evaluated by SpGEMM on an 8^d lattice -- the galerkin == 1 construction of MGMC above, which
+// tests/test_oracle.py pins to the full SpGEMM.  Returns 0, or -1 if the fine lattice has
+// no interior row (2,2[,2]).
+int orc_fd_level_stencils(const orc_params* q, double* out) {
+    Lattice lat = make_lattice(q);
+    for (int d = 0; d < lat.dim; ++d)
+        if (lat.n[d] < 4) return -1;
+    const KappaModel kappa = KappaModel::constant(q->kappa_sq);
+    int idx[3] = {2, 2, 2};
+    int32_t cols[7];
+    double vals[7];
+    const int64_t r = lat.euc2lin(idx);
+    const int64_t cnt = fd_row(lat, kappa, r, cols, vals);
+    double st[27];
+    for (int k = 0; k < 27; ++k) st[k] = 0.0;
+    for (int64_t e = 0; e < cnt; ++e) {
+        int ci[3] = {0, 0, 0};
+        lat.lin2euc(cols[e], ci);
+        st[sidx(lat.dim, ci[0] - 2, lat.dim >= 2 ? ci[1] - 2 : 0, lat.dim == 3 ? ci[2] - 2 : 0)] = vals[e];
+    }
+    Lattice small = lat;
+    for (int d = 0; d < lat.dim; ++d) small.n[d] = 8;
+    for (int level = 0; level < q->nlevel; ++level) {
+        for (int k = 0; k < 27; ++k) out[27 * level + k] = st[k];
+        if (level + 1 == q->nlevel) break;
+        const CSR small_src = stencil_csr(small, st);
+        Intergrid ig(small);
+        const CSR Ac = galerkin_spgemm(small_src, ig);
+        stencil_of_interior_row(Ac, ig.coarse, st);
+    }
+    return 0;
 }
 
 // FEM shifted-Laplace prior (constant kappa^2); override_st as for orc_create_fd

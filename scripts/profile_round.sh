@@ -2,12 +2,23 @@
 # rocprofv3 stats of the bench command, PMC traffic of both fine sweeps inside V-cycles (separate
 # FETCH_SIZE / WRITE_SIZE passes).
 #   RUN_PYTEST=1 bash scripts/profile_round.sh     BENCH_ARGS="--steps 100"
+#   RUN_SMOKE=1: __graft_entry__.smoke();  RUN_POISON=1: the headline cycle / same-seed tests under MGMC_POISON=1
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/round && export TMPDIR=/tmp
 O=gpurun_out/round
 python -c "import os; print('affinity', len(os.sched_getaffinity(0)), 'cpu_count', os.cpu_count(), 'OMP', os.environ.get('OMP_NUM_THREADS'))" > $O/cpu.txt
 if [ -n "$RUN_PYTEST" ]; then
   timeout -k 10 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
   echo "pytest rc=$rc"; tail -3 $O/pytest_gpu.log
+  [ $rc -eq 0 ] || exit $rc
+fi
+if [ -n "$RUN_SMOKE" ]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?
+  echo "smoke rc=$rc"; tail -1 $O/smoke.log
+  [ $rc -eq 0 ] || exit $rc
+fi
+if [ -n "$RUN_POISON" ]; then
+  MGMC_POISON=1 timeout -k 10 600 python -u -m pytest -x -v --timeout 900 --timeout-method thread tests/test_gpu_headline.py -k "same_seed or cycle_and_qoi" > $O/headline_poison.log 2>&1; rc=$?
+  echo "headline poison rc=$rc"; tail -3 $O/headline_poison.log
   [ $rc -eq 0 ] || exit $rc
 fi
 if [ -z "$SKIP_BENCH" ]; then

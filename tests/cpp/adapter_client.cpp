@@ -12,6 +12,11 @@
 //                                            b, x and x after one Smoother::apply(b, x) of the Smoother
 //                                            drop-in (b, x from a fixed mt19937_64 stream); "lowrank" adds two
 //                                            point measurements (MeasuredOperator-like B, Sigma)
+//   adapter_client ownership <rounds>        samplers and smoothers owned the reference's way
+//                                            (std::make_shared<Derived> held as shared_ptr<Base>,
+//                                            driver_mgmc.cc:450-457, multigrid_preconditioner.cc:18-33),
+//                                            used and released; prints mgmc_live_handles() after each
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -147,6 +152,35 @@ int main(int argc, char** argv) {
         std::atexit(report_engine);  // runs on the exit(-1) of a failed device call too
         HipMultigridMCSampler sampler(make_op("fd"), g_rng, params(3), /*device=*/0, /*chain_id=*/0);
         std::printf("seed %llu\n", (unsigned long long)sampler.get_seed());
+        std::mt19937_64 fresh(5418513);
+        std::printf("engine_first %llu\n", (unsigned long long)fresh());
+        return 0;
+    }
+    if (mode == "ownership" && argc > 2) {
+        const int rounds = std::atoi(argv[2]);
+        std::printf("live %d\n", mgmc_live_handles());
+        for (int r = 0; r < rounds; ++r) {
+            const std::shared_ptr<LinearOperator> op = make_op(r % 2 ? "periodic" : "fd");
+            std::shared_ptr<Sampler> sampler = std::make_shared<HipMultigridMCSampler>(op, g_rng, params(3), 0, (uint64_t)r);
+            std::shared_ptr<SmootherFactory> sor = std::make_shared<HipSORSmootherFactory>(1.0, 1, forward);
+            std::shared_ptr<SmootherFactory> ssor = std::make_shared<HipSSORSmootherFactory>(1.0, 1);
+            std::vector<std::shared_ptr<Smoother>> smoothers{sor->get(op), ssor->get(op)};
+            const std::ptrdiff_t ndof = (std::ptrdiff_t)op->get_ndof();
+            Eigen::VectorXd f(ndof), x(ndof);
+            f.setZero();
+            x.setZero();
+            sampler->fix_rhs(f);
+            sampler->apply(f, x);
+            for (const auto& sm : smoothers) sm->apply(f, x);
+            int finite = 1;
+            for (std::ptrdiff_t i = 0; i < ndof; ++i) finite &= std::isfinite(x[i]) ? 1 : 0;
+            const int held = mgmc_live_handles();
+            sampler.reset();  // through the base pointer: the make_shared deleter destroys the derived object
+            smoothers.clear();
+            sor.reset();
+            ssor.reset();
+            std::printf("round %d held %d live %d x %d\n", r, held, mgmc_live_handles(), finite);
+        }
         return 0;
     }
     if (mode == "smoother" && argc > 5) {
@@ -174,6 +208,6 @@ int main(int argc, char** argv) {
         return 0;
     }
     std::fprintf(stderr, "usage: adapter_client describe | sample <n> <fd|fem|periodic> | rngcheck | "
-                         "smoother <fd|fem|periodic> <sor|ssor> <nsmooth> <fwd|bwd> [lowrank]\n");
+                         "smoother <fd|fem|periodic> <sor|ssor> <nsmooth> <fwd|bwd> [lowrank] | ownership <rounds>\n");
     return 2;
 }

@@ -9,7 +9,6 @@
 class Lattice {
    public:
     Lattice(const unsigned int Ncell_, const unsigned int Nvertex_) : Ncell(Ncell_), Nvertex(Nvertex_) {}
-    virtual ~Lattice() = default;
     virtual Eigen::VectorXi shape() const = 0;
     virtual int dim() const { return (int)shape().size(); }
     virtual std::string get_info() const = 0;

@@ -1,6 +1,7 @@
 // Test scaffolding (tests/cpp/refdecl/README.md): the Smoother plugin contract --
 // smoother/smoother.hh:15-44 (ctor :22, apply :29, protected linear_operator :33, SmootherFactory::get
-// :43).  A virtual destructor is added, as in sampler.hh.
+// :43).  No destructor is declared, as in the reference: smoothers are owned through
+// std::make_shared<Derived> (multigrid_preconditioner.cc:18-33).
 #pragma once
 #include <memory>
 
@@ -10,7 +11,6 @@
 class Smoother {
    public:
     Smoother(const std::shared_ptr<LinearOperator> linear_operator_) : linear_operator(linear_operator_) {}
-    virtual ~Smoother() = default;
     virtual void apply(const Eigen::VectorXd& b, Eigen::VectorXd& x) const = 0;
 
    protected:
@@ -19,6 +19,5 @@ class Smoother {
 
 class SmootherFactory {
    public:
-    virtual ~SmootherFactory() = default;
     virtual std::shared_ptr<Smoother> get(std::shared_ptr<LinearOperator> linear_operator) = 0;
 };

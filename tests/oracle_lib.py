@@ -39,6 +39,7 @@ def lib():
         L = ctypes.CDLL(LIB)
         sigs = {
             "orc_create_fd": (c_void_p, [POINTER(OrcParams), c_int, c_uint64, c_uint64, _DP]),
+            "orc_fd_level_stencils": (c_int, [POINTER(OrcParams), _DP]),
             "orc_create_fem": (c_void_p, [POINTER(OrcParams), c_int, c_uint64, c_uint64, _DP]),
             "orc_create_csr": (c_void_p, [POINTER(OrcParams), c_int, c_uint64, c_int64, POINTER(c_int64),
                                           POINTER(c_int32), _DP]),
@@ -140,6 +141,16 @@ class Oracle:
             st = dp(override_stencils)
         h = lib().orc_create_fd(ctypes.byref(p), mode, seed, chain, st)
         return cls(h, p)
+
+    @classmethod
+    def fd_own(cls, shape, mg, kappa_sq, mode=MULTICOLOUR, seed=5418513, chain=0):
+        """FD hierarchy with the oracle's OWN Galerkin levels (no device stencil fed in): the full
+        SpGEMM R*A*R^T (linear_operator.cc:10-23) up to 2^18 fine unknowns, above that the
+        stencil-mode RAP (galerkin=1: SpGEMM on an 8^d lattice from the full-size FD row), which
+        tests/test_oracle.py pins to the full SpGEMM and tests/test_host.py to every level of
+        BASELINE's hierarchies."""
+        big = int(np.prod([n - 1 for n in shape])) > (1 << 18)
+        return cls.fd(shape, mg, kappa_sq, mode=mode, seed=seed, chain=chain, galerkin=1 if big else 0)
 
     @classmethod
     def fem(cls, shape, mg, kappa_sq, mode=FAITHFUL, seed=5418513, chain=0, override_stencils=None):
@@ -301,6 +312,16 @@ class Oracle:
         out = np.empty(self.ndof(level + 1))
         self.L.orc_residual_restrict(self.h, level, dp(f), dp(x), dp(out))
         return out
+
+
+def fd_level_stencils(shape, mg, kappa_sq) -> np.ndarray:
+    """The oracle's own (nlevel, 27) stencils of an FD hierarchy: the reference FD row at full size,
+    then R*A*R^T by SpGEMM per level (the galerkin=1 construction), without assembling any level."""
+    p = params_struct(shape, mg, kappa_sq, 1)
+    out = np.empty((mg.nlevel, 27))
+    if lib().orc_fd_level_stencils(ctypes.byref(p), dp(out)) != 0:
+        raise ValueError(f"lattice {shape} too small")
+    return out
 
 
 def operator_csr(shape, pde, periodic=False, Lambda=0.2, Lambda_min=0.2, Lambda_max=0.4):

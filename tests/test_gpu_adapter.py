@@ -38,3 +38,19 @@ def test_reference_adapter_series_matches_python_host_side(hip_device, tmp_path,
     s.close()
     assert len(z_adapter) == 5 and np.all(np.isfinite(z_adapter))
     assert np.array_equal(z_adapter, z)
+
+
+def test_adapter_ownership_releases_device_handles(hip_device, tmp_path):
+    """Samplers and smoothers owned through std::make_shared<Derived> as shared_ptr<Base> (the
+    reference's ownership, driver_mgmc.cc:450-457, multigrid_preconditioner.cc:18-33; the base classes
+    have no virtual destructor) release every device handle when the base pointers go: after each round
+    mgmc_live_handles() is back to 0."""
+    exe = build_adapter_client(str(tmp_path))
+    r = subprocess.run([exe, "ownership", "4"], capture_output=True, text=True, check=True)
+    lines = r.stdout.splitlines()
+    assert lines[0] == "live 0"
+    rounds = [line.split() for line in lines[1:]]
+    assert len(rounds) == 4
+    for w in rounds:
+        assert w[0] == "round" and w[2] == "held" and int(w[3]) == 3, w
+        assert w[4] == "live" and int(w[5]) == 0 and w[6] == "x" and w[7] == "1", w

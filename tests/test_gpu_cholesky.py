@@ -38,8 +38,7 @@ def _make(shape, kw, kappa_sq=25.0, chain=0, nchains=1):
 
 
 def _oracle(s, p, lat, kappa_sq=25.0, chain=0):
-    st = np.concatenate([s.level_desc(level)["stencil"] for level in range(p.nlevel)])
-    return O.Oracle.fd(lat.shape, p, kappa_sq, mode=O.MULTICOLOUR, seed=SEED, chain=chain, override_stencils=st)
+    return O.Oracle.fd_own(lat.shape, p, kappa_sq, mode=O.MULTICOLOUR, seed=SEED, chain=chain)
 
 
 @pytest.mark.parametrize("name", list(CONFIGS))

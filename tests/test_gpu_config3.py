@@ -6,8 +6,8 @@ z-sweeps run 256-wide rows in shorter z chunks, the fine residual + restriction 
 `k_zresrestrict<7,64,4>` (the coarse level has fewer than 16 K tile planes), level 1 (127^3, 64-pair
 rows) runs colour-pair passes, not j-marching half-sweeps, level 2 (63^3) runs quad passes and
 k_tail takes the 15^3 and 7^3 levels.  One V-cycle from x = 0 plus a 3-sample QoI series are compared
-bit for bit (np.array_equal) with the CPU oracle's MULTICOLOUR replay of the same hierarchy (the
-device's level stencils, Philox key (5418513, 0)); component kernels at this width are compared too.
+bit for bit (np.array_equal) with the CPU oracle's MULTICOLOUR replay (its OWN Galerkin hierarchy:
+the stencil-mode RAP from its FD row, no device stencil fed in; Philox key (5418513, 0)); component kernels at this width are compared too.
 """
 import sys
 import time
@@ -37,9 +37,8 @@ def config3(hip_device):
     p = mg.MultigridParameters(nlevel=NLEVEL, smoother="SOR", coarse_solver="SSOR", npresmooth=1, npostsmooth=1,
                                ncoarsesmooth=1, omega=1.0, cycle=1, coarse_scaling=1.0)
     s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), SEED, p, device=0, chain_id=0)
-    st = np.concatenate([s.level_desc(level)["stencil"] for level in range(NLEVEL)])
     O.set_threads(O.cpu_share())
-    orc = O.Oracle.fd(SHAPE, p, 25.0, mode=O.MULTICOLOUR, seed=SEED, chain=0, override_stencils=st)
+    orc = O.Oracle.fd_own(SHAPE, p, 25.0, mode=O.MULTICOLOUR, seed=SEED, chain=0)
     _log(f"device handle + oracle hierarchy {time.time() - t0:.1f} s")
     yield s, orc, lat, p
     s.close()

@@ -31,8 +31,7 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
 def _mc_oracle(s, p, lat, lowrank=None):
-    st = np.concatenate([s.level_desc(level)["stencil"] for level in range(p.nlevel)])
-    o = O.Oracle.fd(lat.shape, p, 25.0, mode=O.MULTICOLOUR, seed=SEED, chain=0, override_stencils=st)
+    o = O.Oracle.fd_own(lat.shape, p, 25.0, mode=O.MULTICOLOUR, seed=SEED, chain=0)
     if lowrank is not None:
         o.set_lowrank(lowrank)
     return o

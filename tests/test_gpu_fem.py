@@ -3,8 +3,8 @@
 (2^d colours: colour-pair / quad passes, z-marching 27-point residual + restriction, k_tail).
 
 T2 (bitwise, np.array_equal) against the oracle's MULTICOLOUR replay: the oracle assembles the FEM
-matrix cell by cell as the reference does (bitwise the device's fine stencil, test_fem.py) and takes
-the device's Galerkin stencils for the coarse levels.  T3: mean / covariance of the device chain
+matrix cell by cell as the reference does (bitwise the device's fine stencil, test_fem.py) and forms
+its own coarse levels by SpGEMM (linear_operator.cc:10-23); no device stencil is fed in.  T3: mean / covariance of the device chain
 against the exact Q^-1 of the assembled matrix.
 """
 import numpy as np
@@ -34,8 +34,7 @@ def make(name, kappa_sq=25.0, chain=0):
     p = mg.MultigridParameters(**{"nlevel": 3, "smoother": "SOR", "coarse_solver": "SSOR", **kw})
     lat = mg.Lattice(*shape)
     s = mg.MultigridMCSampler(mg.ShiftedLaplaceFEMOperator(lat, kappa_sq), SEED, p, device=0, chain_id=chain)
-    st = np.concatenate([s.level_desc(level)["stencil"] for level in range(p.nlevel)])
-    mc = O.Oracle.fem(shape, p, kappa_sq, mode=O.MULTICOLOUR, seed=SEED, chain=chain, override_stencils=st)
+    mc = O.Oracle.fem(shape, p, kappa_sq, mode=O.MULTICOLOUR, seed=SEED, chain=chain)
     return s, mc, p, lat
 
 

@@ -5,8 +5,9 @@ The kernel instances this configuration selects exist only at this size (mgmc_ca
 residual + restriction `k_zresrestrict<7,64,8,512>` (chosen when the coarse level has >= 16 K tile
 planes), the fused-prolongation post-sweep's 128-plane z chunks, the level-1 j-marching half-sweeps (k_jsweep_half) at
 their full 128-pair row width and the 512^3 `k_tail`.  Every one of them is compared here bit for
-bit (np.array_equal) with the CPU oracle's MULTICOLOUR replay of the same hierarchy (the device's
-level stencils, Philox key (5418513, 0)).  The residual + restriction components are also the
+bit (np.array_equal) with the CPU oracle's MULTICOLOUR replay, which builds its OWN Galerkin
+hierarchy (the stencil-mode RAP from its FD row; no device stencil is fed in) with Philox key
+(5418513, 0).  The residual + restriction components are also the
 FAITHFUL arithmetic: with no low-rank part the oracle's residual is the reference's
 `A_sparse * x` then `f - r` (linear_operator.hh:66-76, multigridmc_sampler.cc:118-120), in CSR order.
 
@@ -42,10 +43,9 @@ def headline(hip_device):
     p = mg.MultigridParameters(nlevel=NLEVEL, smoother="SOR", coarse_solver="SSOR", npresmooth=1, npostsmooth=1,
                                ncoarsesmooth=1, omega=1.0, cycle=1, coarse_scaling=1.0)
     s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), SEED, p, device=0, chain_id=0)
-    st = np.concatenate([s.level_desc(level)["stencil"] for level in range(NLEVEL)])
     _log(f"device handle {time.time() - t0:.1f} s")
     O.set_threads(O.cpu_share())
-    orc = O.Oracle.fd(SHAPE, p, 25.0, mode=O.MULTICOLOUR, seed=SEED, chain=0, override_stencils=st)
+    orc = O.Oracle.fd_own(SHAPE, p, 25.0, mode=O.MULTICOLOUR, seed=SEED, chain=0)
     _log(f"oracle hierarchy ({O.cpu_share()} threads) {time.time() - t0:.1f} s")
     yield s, orc, lat, p
     s.close()
@@ -55,7 +55,7 @@ def headline(hip_device):
 
 def test_headline_fine_stencil_is_the_reference_operator(headline):
     """The device's level-0 stencil is the reference FD row (shiftedlaplace_fd_operator.cc:9-57):
-    the oracle's own assembly of the 512^3 operator (not the override) has it on an interior row."""
+    the oracle's own assembly of the 512^3 operator has it on an interior row."""
     s, orc, lat, p = headline
     st = s.level_desc(0)["stencil"]
     row = lat.Nvertex // 2 + 511 * 5 + 7  # an interior vertex

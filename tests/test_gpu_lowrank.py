@@ -53,8 +53,7 @@ def make(name, kappa_sq=25.0, chain=0):
     p = mg.MultigridParameters(**{"nlevel": 3, "smoother": "SOR", "coarse_solver": "SSOR", **kw})
     op, lat = measured(shape, kappa_sq, radius, nmeas, glob)
     s = mg.MultigridMCSampler(op, SEED, p, device=0, chain_id=chain)
-    st = np.concatenate([s.level_desc(level)["stencil"] for level in range(p.nlevel)])
-    mc = O.Oracle.fd(lat.shape, p, kappa_sq, mode=O.MULTICOLOUR, seed=SEED, chain=chain, override_stencils=st)
+    mc = O.Oracle.fd_own(lat.shape, p, kappa_sq, mode=O.MULTICOLOUR, seed=SEED, chain=chain)
     mc.set_lowrank(op.get_B())
     return s, mc, p, lat, op
 
@@ -132,8 +131,7 @@ def test_set_lowrank_validation_and_reset(hip_device):
     # m = 0 restores the prior: cycles equal the prior oracle
     s.set_lowrank(None)
     assert s.lowrank_info(0, mg.FORWARD) == (0, 0)
-    st = np.concatenate([s.level_desc(level)["stencil"] for level in range(p.nlevel)])
-    prior = O.Oracle.fd(lat.shape, p, 25.0, mode=O.MULTICOLOUR, seed=SEED, override_stencils=st)
+    prior = O.Oracle.fd_own(lat.shape, p, 25.0, mode=O.MULTICOLOUR, seed=SEED)
     f = np.random.default_rng(5).standard_normal(lat.Nvertex)
     xd = np.zeros(lat.Nvertex)
     xo = np.zeros(lat.Nvertex)

@@ -31,8 +31,8 @@ def make(shape, kappa_sq=25.0, chain=0, **kw):
 
 
 def oracle_for(sampler, p, lat, kappa_sq=25.0, mode=O.MULTICOLOUR, chain=0):
-    st = np.concatenate([sampler.level_desc(level)["stencil"] for level in range(p.nlevel)])
-    return O.Oracle.fd(lat.shape, p, kappa_sq, mode=mode, seed=SEED, chain=chain, override_stencils=st)
+    """The oracle with its own Galerkin hierarchy (no device stencil fed in)."""
+    return O.Oracle.fd_own(lat.shape, p, kappa_sq, mode=mode, seed=SEED, chain=chain)
 
 
 CONFIGS = {

@@ -22,8 +22,7 @@ def _pair(shape, nlevel, nchains=1, chain=0):
     p = mg.MultigridParameters(nlevel=nlevel)
     s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), SEED, p, device=0, chain_id=chain,
                               nchains=nchains)
-    st = np.concatenate([s.level_desc(level)["stencil"] for level in range(nlevel)])
-    o = O.Oracle.fd(lat.shape, p, 25.0, mode=O.MULTICOLOUR, seed=SEED, chain=chain, override_stencils=st)
+    o = O.Oracle.fd_own(lat.shape, p, 25.0, mode=O.MULTICOLOUR, seed=SEED, chain=chain)
     return s, o, lat
 
 

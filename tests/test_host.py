@@ -135,6 +135,44 @@ def test_stencils_match_oracle_spgemm_bitwise(shape):
             assert d["stencil"][k] == got.get(k, 0.0), f"level {lev} offset {k}"
 
 
+@pytest.mark.parametrize("shape,nlevel", [
+    ((512, 512, 512), 7),   # BASELINE config 4 (bench.py's hierarchy)
+    ((256, 256, 256), 6),   # configs 3 and 5 (the prior part of the posterior operator)
+    ((1024, 1024), 5),      # config 2
+    ((64, 64), 4),          # config 1's lattice size with the template's nlevel
+    ((128, 128, 128), 5),
+])
+def test_full_size_hierarchy_stencils_match_oracle_rap(shape, nlevel):
+    """Every level of BASELINE's hierarchies, at their real h: the device's stencil-algebra RAP
+    (mgmc_hierarchy.cpp galerkin_stencil) equals the oracle's own R*A*R^T (linear_operator.cc:10-23),
+    formed by SpGEMM from the oracle's FD row (shiftedlaplace_fd_operator.cc:9-57), bit for bit.
+    No device stencil is fed to the oracle."""
+    levels = mg.describe(_cfg(shape, nlevel=nlevel))
+    ref = O.fd_level_stencils(shape, mg.MultigridParameters(nlevel=nlevel), 25.0)
+    assert len(levels) == nlevel
+    for lev, d in enumerate(levels):
+        assert np.array_equal(d["stencil"], ref[lev]), f"level {lev}: {d['stencil']} != {ref[lev]}"
+
+
+def test_oracle_level_stencils_equal_its_assembled_hierarchy():
+    """orc_fd_level_stencils (no level assembled) equals the interior rows of the oracle's full
+    SpGEMM hierarchy (galerkin=0), so it is the same RAP the small-size tests pin."""
+    shape, nlevel = (32, 32, 32), 4
+    p = mg.MultigridParameters(nlevel=nlevel)
+    ref = O.fd_level_stencils(shape, p, 25.0)
+    o = O.Oracle.fd(shape, p, 25.0, galerkin=0)
+    for lev in range(nlevel):
+        n = shape[0] >> lev
+        lat = mg.Lattice(n, n, n)
+        r = lat.vertexidx_euclidean2linear([2, 2, 2])
+        cols, vals = o.csr_row(lev, r)
+        got = np.zeros(27)
+        for c, v in zip(cols, vals):
+            i = lat.vertexidx_linear2euclidean(int(c))
+            got[sum((i[dd] - 2 + 1) * 3 ** dd for dd in range(3))] = v
+        assert np.array_equal(got, ref[lev]), f"level {lev}"
+
+
 def test_parameters_template_parses():
     from multigridmc_amd.parameters import (ConstantCorrelationLengthModelParameters, GeneralParameters,
                                             LatticeParameters, MeasurementParameters, MultigridParameters,
