@@ -23,6 +23,7 @@
 #include "mgmc_hierarchy.hpp"
 #include "mgmc_kernels.hpp"
 #include "mgmc_zsweep.hpp"
+#include "mgmc_tuning.hpp"
 #include "mgmc_layout_check.hpp"
 static_assert(MGMC_LAYOUT_POINT == mgmc::LF_POINT && MGMC_LAYOUT_PAIRS == mgmc::LF_PAIRS &&
                   MGMC_LAYOUT_ZSWEEP == mgmc::LF_ZSWEEP && MGMC_LAYOUT_ZSWEEP_COARSE == mgmc::LF_ZSWEEP_C &&
@@ -164,27 +165,10 @@ bool read_path_flags(uint32_t* flags, std::string* bad) {
 
 // z-marching sweep tile shape (mgmc_zsweep.hpp): 32 x-pairs x TY rows, TY/2 core waves + 2 halo
 // waves rounded up to a multiple of four (768 threads for TY 16); two workgroups per CU need <= 80
-// VGPRs (6 waves per SIMD).  Tuning history in DESIGN.md.
-// (MGMC_ZS_SHAPE_* override the shape in timing-experiment builds only, scripts/build_exp.sh)
-#ifndef MGMC_ZS_SHAPE_TY
-#define MGMC_ZS_SHAPE_TY 20
-#endif
-#ifndef MGMC_ZS_SHAPE_MINW
-#define MGMC_ZS_SHAPE_MINW 6
-#endif
-#ifndef MGMC_ZS_SHAPE_TZ
-#define MGMC_ZS_SHAPE_TZ 32
-#endif
-#ifndef MGMC_ZS_SHAPE_TZP
-#define MGMC_ZS_SHAPE_TZP 128
-#endif
-#ifndef MGMC_ZS_SHAPE_TYP  // the fused-prolongation (post-)sweep
-#define MGMC_ZS_SHAPE_TYP 16
-#define MGMC_ZS_SHAPE_MINWP 6
-#endif
-constexpr int ZS_XP = 32, ZS_TY = MGMC_ZS_SHAPE_TY, ZS_NT = zs_threads(ZS_TY), ZS_MINW = MGMC_ZS_SHAPE_MINW,
-              ZS_TZ = MGMC_ZS_SHAPE_TZ, ZS_TYP = MGMC_ZS_SHAPE_TYP, ZS_NTP = zs_threads(ZS_TYP),
-              ZS_MINWP = MGMC_ZS_SHAPE_MINWP, ZS_TZP = MGMC_ZS_SHAPE_TZP;
+// VGPRs (6 waves per SIMD).  Values in mgmc_tuning.hpp, tuning history in DESIGN.md.
+constexpr int ZS_XP = 32, ZS_TY = tune::ZS_TY, ZS_NT = zs_threads(ZS_TY), ZS_MINW = tune::ZS_MINW,
+              ZS_TZ = tune::ZS_TZ, ZS_TYP = tune::ZS_TYP, ZS_NTP = zs_threads(ZS_TYP),
+              ZS_MINWP = tune::ZS_MINWP, ZS_TZP = tune::ZS_TZP;
 
 // device copy of a level's low-rank part (mgmc_lowrank.hpp); one allocation list, freed together
 struct LowRankDev {
@@ -246,6 +230,7 @@ struct Level {
     bool rb2d = false;     // 2D 5-point level: one-launch red-black sweep, out of place (k_rb2d)
     bool field = false;    // per-vertex coefficients (mgmc_create_csr, mgmc_field.hpp)
     bool sym = false;      // 27-point stencil bitwise reflection-symmetric: kernels fold it (stencil_coef<true>)
+    bool fold = false;     // ... and its residuals take the class-folded sum (fold27; not switched by MGMC_DISABLE)
     FieldArg F;            // ... their device field, pattern and colouring
     double* rbuf = nullptr;  // ... residual scratch (padded layout, zero boundary)
     bool pingpong() const { return zsweep || quads || rb2d; }  // out-of-place sweeps: x <-> x2
@@ -581,12 +566,9 @@ bool pairs_eligible(const LevelSpec& sp, const Layout& L) {
 // level (2D 1024^2 FD cycle 0.135 -> 0.129 ms, FEM 0.147 -> 0.139 ms; A/B in one box call).  On the
 // large 3D levels it loses (512^3 level 1: 2 x 105 us against 4 x 41 us per sweep): the
 // second pair's loads wait for the first pair's rows.  Levels that k_tail runs are left to it (caller).
-#ifndef MGMC_QUADS_MAXPAIR  // (timing-experiment builds override it: scripts/build_exp.sh QMAX)
-#define MGMC_QUADS_MAXPAIR 64
-#endif
 bool quads_eligible(const LevelSpec& sp, const Layout& L, uint32_t paths) {
     if (!pairs_eligible(sp, L) || (paths & PATH_NO_QUADS)) return false;
-    return sp.dim == 2 || L.nx / 2 <= MGMC_QUADS_MAXPAIR;
+    return sp.dim == 2 || L.nx / 2 <= tune::QUADS_MAXPAIR;
 }
 
 // one red-black sweep of a 2D 5-point level, xin -> xout (mgmc_rb2d.hpp)
@@ -608,19 +590,12 @@ void launch_rb2d(const Level& lv, const double* xin, double* xout, const double*
 // With 64-pair rows (512^3 level 2, 256^3 level 1) the kernel is slower than the pair passes (2 x 21 against
 // 4 x 8 us per sweep at 127^3, 256^3 cycle 0.484 -> 0.503 ms): those levels are latency-bound, and the
 // march's chunks are short.
-#ifndef MGMC_JS_NX128  // j-marching half-sweeps also on nx = 128 levels (timing builds: scripts/build_exp.sh)
-#define MGMC_JS_NX128 0
-#endif
-
 bool jsweep_eligible(const LevelSpec& sp, const Layout& L, uint32_t paths) {
-    return sp.dim == 3 && sp.npoints == 27 && (L.nx == 256 || L.nx == 512 || (MGMC_JS_NX128 && L.nx == 128)) &&
+    return sp.dim == 3 && sp.npoints == 27 && (L.nx == 256 || L.nx == 512) &&
            L.ny >= 2 && L.nz >= 2 &&
            !(paths & PATH_NO_JSWEEP);
 }
 
-#ifndef MGMC_JS_ROUNDS  // workgroups per half: this many rounds of the resident slots (timing builds override it)
-#define MGMC_JS_ROUNDS 1
-#endif
 
 // xzero: xin is known zero (Op::xzero): the first half takes zeros for every x row, the second for its own
 // planes (the neighbouring planes are the first half's new values)
@@ -640,7 +615,7 @@ void launch_jsweep(const Level& lv, const double* xin, double* xout, const doubl
     for (int h = 0; h < 2; ++h) {
         // resident workgroups: LDS-bound (160 KB per CU), one round of them per half (jsweep_plan; the
         // host check mgmc_layout_check.hpp jsweep_grid_check replays the same plan)
-        const JSweepPlan p = jsweep_plan(lv.L, fwd, h, lv.num_cu, lds, MGMC_JS_ROUNDS);
+        const JSweepPlan p = jsweep_plan(lv.L, fwd, h, lv.num_cu, lds, tune::JS_ROUNDS);
         if (p.nk == 0) continue;
         a.kp = p.kp;
         a.jA = p.jA;  // first pair of a half: colours (0,1) / (4,5) forward, (7,6) / (3,2) backward
@@ -663,11 +638,6 @@ void launch_jsweep(const Level& lv, const double* xin, double* xout, const doubl
     } while (0)
         if (np == 256) {  // FEM prior's 27-point fine level at 512^3 (not symmetric bit for bit)
             MGMC_JS_LAUNCH(256, false);
-#if MGMC_JS_NX128
-        } else if (np == 64) {
-            if (lv.sym) MGMC_JS_LAUNCH(64, true);
-            else MGMC_JS_LAUNCH(64, false);
-#endif
         } else if (lv.sym) {  // the cubic FD hierarchies' 255^3 level: 8 distinct coefficients
             MGMC_JS_LAUNCH(128, true);
         } else {
@@ -695,19 +665,10 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
     const int dim = lv.spec.dim;
     const int npair = lv.L.nx / 2;
     // T+1 thread rows of npair threads
-#ifndef MGMC_QUADS_NT  // 2D levels (timing-experiment builds override it: scripts/build_exp.sh QMAX=<pairs>x<threads>);
-                       // config 2 (2D 1024^2): 512 10,623, 256 10,775, 128 10,883 samples/s (1024: 10,257)
-#define MGMC_QUADS_NT 128
-#endif
-#ifndef MGMC_QUADS_NT_WIDE  // the same for 3D rows of more than 32 pairs (the 127^3 levels: 256 threads, T = 3,
-                            // 61.6 -> 58.3 us per cycle at 512^3 against 512; 1024: 72.8 us)
-#define MGMC_QUADS_NT_WIDE 256
-#endif
-#ifndef MGMC_QUADS_NT3  // the same for 3D rows of <= 32 pairs (63^3, 31^3): 128 threads, 4x the workgroups of
-                        // 512 (512^3 63^3 launches 7.3-7.8 -> 5.6-6.3 us; 256^3 cycle -7 us; 64 / 256: -6 / -5.5 us)
-#define MGMC_QUADS_NT3 128
-#endif
-    a.T = std::max(1, (dim == 3 ? (npair > 32 ? MGMC_QUADS_NT_WIDE : MGMC_QUADS_NT3) : MGMC_QUADS_NT) / npair - 1);
+    // (threads per workgroup, mgmc_tuning.hpp: 2D config 2 at 1024^2: 512 10,623, 256 10,775, 128 10,883
+    // samples/s; 127^3 rows 256 threads 58.3 us per 512^3 cycle against 61.6 at 512; 63^3 / 31^3 rows 128
+    // threads, 512^3 launches 7.3-7.8 -> 5.6-6.3 us against 512)
+    a.T = std::max(1, (dim == 3 ? (npair > 32 ? tune::QUADS_NT_WIDE : tune::QUADS_NT3) : tune::QUADS_NT) / npair - 1);
     a.nblk_y = (lv.L.ny - 1 + 2 * a.T - 1) / (2 * a.T);
     const int nt = npair * (a.T + 1);
     const size_t lds = (size_t)(2 * a.T + 1) * (lv.L.nx + 2) * sizeof(double);
@@ -833,9 +794,6 @@ struct TailNoiseLaunch {  // spare workgroups of the launch draw a tail's noise 
     const uint64_t* sample;
 };
 
-#ifndef MGMC_ZR27_CX  // coarse points per tile in x of the symmetric 27-point instance (timing builds)
-#define MGMC_ZR27_CX 64
-#endif
 template <int NPTS, int CX, int CY, int NT, bool SYM = false>
 void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, const double* f, double* fc, double* xc,
                            hipStream_t s, int nch, const TailNoiseLaunch* tn = nullptr) {
@@ -865,11 +823,9 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
         const long long nchunk = std::max(1LL, (2 * slots + per_chunk - 1) / per_chunk);
         a.kz = std::max(8, (int)((lc.L.nz - 1 + nchunk - 1) / nchunk));
     }
-#ifndef MGMC_ZR7_KZ_ROUNDS  // the same depth rule for the 7-point 64 x 4 instance (256^3 fine level: kz 4 -> 11, 2,048
-                            // -> 768 workgroups = one round, 64.4 -> 57.7 us)
-#define MGMC_ZR7_KZ_ROUNDS 1
-#endif
-    if ((NPTS == 27 || (MGMC_ZR7_KZ_ROUNDS && NPTS == 7 && NT == 256)) && CX >= 48 && work >= 4 * 1024) {
+    // (the same depth rule for the 7-point 64 x 4 instance: 256^3 fine level kz 4 -> 11, 2,048 -> 768
+    // workgroups = one round, 64.4 -> 57.7 us)
+    if ((NPTS == 27 || (NPTS == 7 && NT == 256)) && CX >= 48 && work >= 4 * 1024) {
         // 27-point levels with enough tiles for several rounds (512^3 level 1): the chunk depth that
         // minimises rounds of resident workgroups x planes staged per chunk (2 kz + 2); 512^3 level 1:
         // kz 11 = 768 tiles, one round of 3 x 256 slots: 108 -> 101 us (round 4, kernel traces)
@@ -887,9 +843,6 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
             }
         }
     }
-#ifdef MGMC_ZR27_KZ  // (timing builds: scripts/build_exp.sh VARIANTS)
-    if (NPTS == 27 && CX == 64) a.kz = MGMC_ZR27_KZ;
-#endif
     a.ntz = (lc.L.nz - 1 + a.kz - 1) / a.kz;
     const int nt = a.ntx * a.nty * a.ntz;
     const int nb = (nt + 7) / 8 * 8;
@@ -943,10 +896,7 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
     // coarse n = ZR_SMALL_NX up, 16 x 4 points (one wavefront) below, where the wide tiles would leave
     // most of the chip idle (the 27-point gather kernel took 24 us per launch on the 15^3 / 7^3 levels)
     if (lf.spec.dim == 3 && zero_xc && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8) {
-#ifndef MGMC_ZR_SMALL_NX  // coarse nx below which the 16 x 4 tiles are used (timing builds: scripts/build_exp.sh)
-#define MGMC_ZR_SMALL_NX 32
-#endif
-        const bool small = lc.L.nx < MGMC_ZR_SMALL_NX;
+        const bool small = lc.L.nx < tune::ZR_SMALL_NX;
         if (skip_xc) xc = nullptr;
         if (lf.spec.npoints == 7) {
             if (small) launch_zresrestrict_t<7, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch, tn);
@@ -957,16 +907,10 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
                 launch_zresrestrict_t<7, 64, 8, 512>(lf, lc, x, f, fc, xc, s, nch);
             else launch_zresrestrict_t<7, 64, 4, 256>(lf, lc, x, f, fc, xc, s, nch);
         } else {
-#ifndef MGMC_ZR27_CY  // (timing builds: scripts/build_exp.sh VARIANTS)
-#define MGMC_ZR27_CY 4
-#endif
-            if (small && lf.sym) launch_zresrestrict_t<27, 16, 4, 64, true>(lf, lc, x, f, fc, xc, s, nch, tn);
+            // (fold levels: the SYM instances, whose residual is fold27's)
+            if (small && lf.fold) launch_zresrestrict_t<27, 16, 4, 64, true>(lf, lc, x, f, fc, xc, s, nch, tn);
             else if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch, tn);
-            else if (MGMC_ZR27_CY == 4 && lf.sym) launch_zresrestrict_t<27, MGMC_ZR27_CX, 4, 256, true>(lf, lc, x, f, fc, xc, s, nch);
-            else if (MGMC_ZR27_CY == 8 && lc.L.nx >= 128)
-                launch_zresrestrict_t<27, 64, 8, 512>(lf, lc, x, f, fc, xc, s, nch);
-            else if (MGMC_ZR27_CY == 3)
-                launch_zresrestrict_t<27, 64, 3, 256>(lf, lc, x, f, fc, xc, s, nch);
+            else if (lf.fold) launch_zresrestrict_t<27, tune::ZR27_CX, 4, 256, true>(lf, lc, x, f, fc, xc, s, nch);
             else launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s, nch);
         }
         return;
@@ -976,6 +920,8 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
     const int dim = lf.spec.dim, np = lf.spec.npoints;
     if (dim == 3 && np == 7)
         hipLaunchKernelGGL((k_residual_restrict<3, 7>), grid, block, 0, s, lf.L, lc.L, x, f, fc, xc, lf.S, zero_xc);
+    else if (dim == 3 && lf.fold)
+        hipLaunchKernelGGL((k_residual_restrict<3, 27, true>), grid, block, 0, s, lf.L, lc.L, x, f, fc, xc, lf.S, zero_xc);
     else if (dim == 3)
         hipLaunchKernelGGL((k_residual_restrict<3, 27>), grid, block, 0, s, lf.L, lc.L, x, f, fc, xc, lf.S, zero_xc);
     else if (np == 5)
@@ -1042,17 +988,13 @@ void launch_prolongate(const Level& lf, const Level& lc, double* x, const double
     const int zper = lf.spec.dim == 3 ? lf.L.nz - 1 : 1;  // batched chains: blockIdx.z = chain * zper + plane
     dim3 grid = grid3(lf.L.nx / 2, lf.L.ny - 1, zper * nch, block);
     const long long csf = lf.L.nstore, csc = lc.L.nstore;
-#ifndef MGMC_PROLONG_Z  // fine planes per thread of the z-marching prolongation on big 3D levels (0: off)
-#define MGMC_PROLONG_Z 8
-#endif
-    if (MGMC_PROLONG_Z > 0 && lf.spec.dim == 3 && (long long)(lf.L.nx / 2) * (lf.L.ny - 1) * (lf.L.nz - 1) >= (1LL << 16) &&
+    // z-marching prolongation on big 3D levels (fine planes per thread: mgmc_tuning.hpp)
+    if (lf.spec.dim == 3 && (long long)(lf.L.nx / 2) * (lf.L.ny - 1) * (lf.L.nz - 1) >= (1LL << 16) &&
         !(lf.paths & PATH_NO_PROLONG_Z)) {
-        constexpr int TZ = MGMC_PROLONG_Z > 0 ? MGMC_PROLONG_Z : 1;
-#ifndef MGMC_PROLONG_Z_SMALL  // planes per thread below 2^21 fine pair items: twice the threads on the 127^3 /
-                              // 63^3 levels (512^3: 10.7 / 8.9 -> 9.2 / 6.3 us; 2: 9.7 / 6.0 us)
-#define MGMC_PROLONG_Z_SMALL 4
-#endif
-        constexpr int TZS = MGMC_PROLONG_Z_SMALL;
+        constexpr int TZ = tune::PROLONG_Z;
+        // fewer planes per thread below 2^21 fine pair items: twice the threads on the 127^3 / 63^3
+        // levels (512^3: 10.7 / 8.9 -> 9.2 / 6.3 us; 2 planes: 9.7 / 6.0 us)
+        constexpr int TZS = tune::PROLONG_Z_SMALL;
         if (TZS != TZ && (long long)(lf.L.nx / 2) * (lf.L.ny - 1) * (lf.L.nz - 1) < (1LL << 21)) {
             const int nzc = (lf.L.nz - 1 + TZS - 1) / TZS;
             const dim3 gz = grid3(lf.L.nx / 2, lf.L.ny - 1, nzc * nch, block);
@@ -1662,6 +1604,7 @@ int build_tails_only(mgmc_handle* h) {
             tl.of = off;
             off += (int)tl.G.nstore;
             tl.ncolours = lv.spec.ncolours;
+            tl.fold = lv.fold ? 1 : 0;
             const GibbsArg g = make_gibbs(h, lv, 0, 0, h->ctrl);
             tl.sd = g.sd;
             tl.wd = g.wd;
@@ -2415,7 +2358,7 @@ static int zrestrict_cx_of(const mgmc_handle* h, int l) {  // launch_residual_re
     const Level& lf = h->levels[l];
     const Level& lc = h->levels[l + 1];
     if (lf.spec.dim != 3 || lf.field || (lf.paths & PATH_NO_ZRESTRICT) || lc.L.nx < 8) return 0;
-    return lc.L.nx < 32 ? 16 : (lf.spec.npoints == 27 && lf.sym ? MGMC_ZR27_CX : 64);
+    return lc.L.nx < 32 ? 16 : (lf.spec.npoints == 27 && lf.fold ? tune::ZR27_CX : 64);
 }
 // both directions and both halves of a j-marching level, with launch_jsweep's plan (short_grid: the plan
 // with its last 8 workgroups dropped -- a negative control for the test, which the replay must reject)
@@ -2423,7 +2366,7 @@ static std::string jsweep_grid_check_level(const Layout& L, int num_cu, bool sho
     const size_t lds = jsweep_lds_bytes(L.nx / 2);
     for (int d = 0; d < 2; ++d)
         for (int half = 0; half < 2; ++half) {
-            JSweepPlan p = jsweep_plan(L, d == 0, half, num_cu, lds, MGMC_JS_ROUNDS);
+            JSweepPlan p = jsweep_plan(L, d == 0, half, num_cu, lds, tune::JS_ROUNDS);
             if (short_grid && p.nb > 8) p.nb -= 8;
             const std::string e = jsweep_grid_check(L, p, JS_D);
             if (!e.empty()) return e;
@@ -2522,7 +2465,8 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
         lv.L = make_layout(cfg->dim, specs[l].n,
                            h->field_mode && (fields[l].scheme == 9 || fields[l].scheme == 27));
         memcpy(lv.S.a, specs[l].st, sizeof(lv.S.a));
-        lv.sym = !h->field_mode && stencil_reflection_symmetric(lv.S.a, lv.spec.npoints) && !(h->paths & PATH_NO_SYM);
+        lv.fold = !h->field_mode && lv.spec.dim == 3 && stencil_reflection_symmetric(lv.S.a, lv.spec.npoints);
+        lv.sym = lv.fold && !(h->paths & PATH_NO_SYM);
         const size_t bytes = lv.L.nstore * sizeof(double);
         const size_t cbytes = bytes * nchains;  // x, x2, f of every chain, L.nstore apart
         if (hipMalloc(&lv.x, cbytes) != hipSuccess || hipMalloc(&lv.f, cbytes) != hipSuccess) {
@@ -2853,7 +2797,7 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
         sweep = "k_fsweep<" + std::to_string(dim) + ">";
     } else if (lv.zsweep) {
         sweep = "k_zsweep_rb7<32," + std::to_string(zsweep_plain_rows(lv, h->nchains)) + ",...,0>";
-        if (!(h->paths & PATH_NO_FUSE_PROLONG)) post = "k_zsweep_rb7<32," + std::to_string(MGMC_ZS_SHAPE_TYP) + ",...,PROLONG>";
+        if (!(h->paths & PATH_NO_FUSE_PROLONG)) post = "k_zsweep_rb7<32," + std::to_string(tune::ZS_TYP) + ",...,PROLONG>";
     } else if (lv.jsweep) {
         sweep = "k_jsweep_half<" + std::to_string(lv.L.nx / 2) + (lv.sym && lv.L.nx == 256 ? ",sym" : "") + ">";
     } else if (lv.quads) {

@@ -34,16 +34,14 @@
 #include <type_traits>
 
 #include "mgmc_kernels.hpp"
+#include "mgmc_tuning.hpp"
 
 namespace mgmc {
 
 // NP pairs per row (nx = 2 NP); 2 NP threads (A-row pairs, B-row pairs); ring rows of stride 2 NP + 8: odd pairs [0, NP) and the guard at NP, then
 // the even block from NP + 1: its guard (position 0) first, even pair m at NP + 2 + m
 constexpr int JS_RING = 8;           // rows per plane in the LDS ring
-#ifndef MGMC_JS_D  // (timing builds override it)
-#define MGMC_JS_D 3
-#endif
-constexpr int JS_D = MGMC_JS_D;      // global loads run this many steps ahead (2 .. 4)
+constexpr int JS_D = tune::JS_D;     // global loads run this many steps ahead (2 .. 4)
 static_assert(JS_D >= 2 && JS_D <= 4, "JS_D");
 
 struct JSweepArgs {
@@ -96,10 +94,7 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
     // 0: A-row, 1: B-row -- uniform across a wavefront (NP is a multiple of 64): readfirstlane lets the
     // compiler keep everything that depends only on the role (rows, ring slots, row offsets, the step's
     // go / store flags) in SGPRs, so the per-lane work is the pair's column arithmetic
-#ifndef MGMC_JS_UNIFORM_ROLE  // (timing builds: 0 = the round-3 per-lane role)
-#define MGMC_JS_UNIFORM_ROLE 1
-#endif
-    const int role = MGMC_JS_UNIFORM_ROLE ? __builtin_amdgcn_readfirstlane(tid / JS_NP) : tid / JS_NP;
+    const int role = __builtin_amdgcn_readfirstlane(tid / JS_NP);
     const int m = tid & (JS_NP - 1);  // pair of the row
     const int i0 = 2 * m + 1;
     const uint64_t sample = *a.G.sample;
@@ -117,7 +112,7 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
     const int jlast = 2 * s1 + a.jA + 1, flast = 2 * s1 + a.jA;
     auto load_pair = [&](int j, int dz) -> double2 {
         if (XZ == 1 || (XZ == 2 && dz == 1)) return make_double2(0.0, 0.0);
-        j = MGMC_CHUNK_CLAMP && j > jlast ? jlast : j;
+        j = j > jlast ? jlast : j;
         const int jc = j < 0 ? 0 : (j > L.ny ? L.ny : j);
         const double* src = (dz == 1 ? a.xo : a.xz) + L.at(i0, jc, k + dz - 1);
         return *reinterpret_cast<const double2*>(src);
@@ -187,7 +182,7 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
     double2 P[JS_D][3], F[JS_D];
     auto frow = [&](int s) { return role == 0 ? 2 * s + a.jA : 2 * s + a.jA - 3; };
     auto load_f = [&](int j) -> double2 {  // (rows outside the lattice or past flast: never used)
-        j = MGMC_CHUNK_CLAMP && j > flast ? flast : j;
+        j = j > flast ? flast : j;
         const int jc = j < 1 ? 1 : (j > L.ny - 1 ? L.ny - 1 : j);
         return *reinterpret_cast<const double2*>(a.f + L.at(i0, jc, k));
     };

@@ -59,11 +59,6 @@ inline Layout make_layout(int dim, const int n[3], bool reach2 = false) {
     return L;
 }
 
-// the sweeps' loads past the end of a workgroup's chunk reload its last needed row / plane instead of
-// fetching the next chunk's (timing builds: 0 = the round-3 loads)
-#ifndef MGMC_CHUNK_CLAMP
-#define MGMC_CHUNK_CLAMP 1
-#endif
 
 struct StencilArg {
     double a[27];
@@ -91,6 +86,33 @@ inline bool stencil_reflection_symmetric(const double* a, int npoints) {
         if (u != v) return false;
     }
     return true;
+}
+
+// Class-folded residual sum of a reflection-symmetric 27-point stencil (the "fold" levels: every
+// 3D Galerkin level of the cubic FD hierarchies).  The 27 window values v[t], t = (dz+1) 9 + (dy+1) 3
+// + (dx+1), fall into 8 coefficient classes c = [dx == 0] + 2 [dy == 0] + 4 [dz == 0] (class
+// representative sym_rep(t), its lowest offset index).  Each class sums its members in ascending t
+// (s_c = v_rep, then s_c + v_t), then y = a_7 s_7 (the centre) and y = fma(a_c, s_c, y) for c = 6 .. 0.
+// 19 adds + 1 multiply + 7 fma instead of 27 multiplies + 27 dependent adds, and a dependency depth
+// of about 9 instead of 27: the 27-point residual + restriction kernels are latency / issue bound on
+// that chain.  It is not the reference's CSR order (linear_operator.hh:66-76), so the
+// fold levels' residuals agree with the FAITHFUL arithmetic to rounding (tests/test_gpu_parity.py,
+// tolerance stated there) and bitwise with the MULTICOLOUR oracle, which folds the same way
+// (oracle/refcpu.cpp folded_row_sum).
+constexpr int fold_class(int t) { return (t % 3 == 1 ? 1 : 0) + ((t / 3) % 3 == 1 ? 2 : 0) + (t / 9 == 1 ? 4 : 0); }
+constexpr int fold_rep(int c) { return (c & 1) + 3 * ((c >> 1) & 1) + 9 * ((c >> 2) & 1); }
+__host__ __device__ __forceinline__ double fold27(const double (&v)[27], const double* a) {
+    double s[8];
+#pragma unroll
+    for (int t = 0; t < 27; ++t) {
+        const int c = fold_class(t);
+        if (fold_rep(c) == t) s[c] = v[t];
+        else s[c] = s[c] + v[t];
+    }
+    double y = a[fold_rep(7)] * s[7];
+#pragma unroll
+    for (int c = 6; c >= 0; --c) y = fma(a[fold_rep(c)], s[c], y);
+    return y;
 }
 
 struct GibbsArg {
@@ -457,7 +479,8 @@ __global__ void __launch_bounds__(1024) k_coarse_ssor_lds(Layout L, double* __re
 // ---- fused residual + restriction: fc = R (f - A x), xc = 0 (multigridmc_sampler.cc:118-122) ----
 __device__ __forceinline__ double w1(int s) { return s == 0 ? 1.0 : 0.5; }
 
-template <int DIM, int NPTS>
+// FOLD: a fold level (27-point, reflection-symmetric): the residual's sum is fold27's
+template <int DIM, int NPTS, bool FOLD = false>
 __global__ void __launch_bounds__(256) k_residual_restrict(Layout Lf, Layout Lc, const double* __restrict__ xf,
                                                            const double* __restrict__ ff, double* __restrict__ fc,
                                                            double* __restrict__ xc, StencilArg S, int zero_xc) {
@@ -475,7 +498,15 @@ __global__ void __launch_bounds__(256) k_residual_restrict(Layout Lf, Layout Lc,
 #pragma unroll
             for (int sx = -1; sx <= 1; ++sx) {
                 const long long q = pf + sz * Lf.sp + sy * Lf.sx + sx;
-                const double y = stencil_sum<DIM, NPTS>(xf, q, Lf, S);
+                double y;
+                if constexpr (FOLD && DIM == 3 && NPTS == 27) {
+                    double v[27];
+#pragma unroll
+                    for (int t = 0; t < 27; ++t) v[t] = xf[q + (t / 9 - 1) * Lf.sp + ((t / 3) % 3 - 1) * Lf.sx + (t % 3 - 1)];
+                    y = fold27(v, S.a);
+                } else {
+                    y = stencil_sum<DIM, NPTS>(xf, q, Lf, S);
+                }
                 const double r = ff[q] - y;
                 double w = 1.0;
                 w *= w1(sx);

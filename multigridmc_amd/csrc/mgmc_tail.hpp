@@ -59,6 +59,7 @@ struct TailLevel {
     Layout G;      // LDS layout (off 0, sx = nx+1, sp = sx (ny+1), 3D padded to 8 mod 16)
     int ox, of;    // LDS offsets (doubles) of x and f
     int ncolours;
+    int fold;      // a fold level (27-point, reflection-symmetric): the residual's sum is fold27's
     double sd, wd; // sqrt(diag (2-omega)/omega), omega/diag
     StencilArg S;
     // low-rank part (m = 0: none); every offset in the LDS layout G
@@ -409,10 +410,19 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
                 lr_patch_rows(t, f, -1);
                 __syncthreads();
             }
-            for_interior(G, [&](int i, int j, int k) {
-                const long long p = G.at(i, j, k);
-                scr[p] = f[p] - tail_sum<DIM, NPTS, SYM>(x, (int)p, G, S);
-            });
+            if (DIM == 3 && NPTS == 27 && t.fold) {
+                for_interior(G, [&](int i, int j, int k) {
+                    const long long p = G.at(i, j, k);
+                    double v[27];
+                    tail_window<3, 27>(x, (int)p, G, v);
+                    scr[p] = f[p] - fold27(v, S.a);
+                });
+            } else {
+                for_interior(G, [&](int i, int j, int k) {
+                    const long long p = G.at(i, j, k);
+                    scr[p] = f[p] - tail_sum<DIM, NPTS, SYM>(x, (int)p, G, S);
+                });
+            }
             __syncthreads();
             for_interior(Gc, [&](int I, int J, int K) {
                 const int pf = (int)G.at(2 * I, 2 * J, 2 * K);

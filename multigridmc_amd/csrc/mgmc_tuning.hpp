@@ -1,0 +1,47 @@
+// mgmc_tuning.hpp -- the library's launch-shape constants, in one place.
+//
+// Every value here is bitwise-neutral: it sets tile shapes, chunk depths, thread counts and launch
+// thresholds, never an arithmetic order, so the results do not depend on it (the -m gpu suite holds at
+// any setting; the layout check of mgmc_layout_check.hpp covers every shape).  The values are the ones
+// measured fastest on MI355X; the losing alternatives and their timings are in docs/HISTORY.md and
+// DESIGN.md 3i.  Timing experiments (scripts/build_exp.sh) build a copy of the sources with edited
+// values here; the product build has no override switches.
+#pragma once
+
+namespace mgmc {
+namespace tune {
+
+// fine 3D 7-point z-sweep (mgmc_zsweep.hpp): 32 x-pairs x ZS_TY rows per tile, z-chunks of ZS_TZ
+// planes, at least ZS_MINW waves per SIMD (2 workgroups of 12 waves per CU, <= 80 VGPRs)
+constexpr int ZS_TY = 20;
+constexpr int ZS_MINW = 6;
+constexpr int ZS_TZ = 32;
+// ... the fused-prolongation post-sweep: 16-row tiles (its registers bind first), 128-plane chunks
+constexpr int ZS_TYP = 16;
+constexpr int ZS_MINWP = 6;
+constexpr int ZS_TZP = 128;
+
+// quad passes (k_sweep_quads) on 3D Galerkin levels with rows of at most QUADS_MAXPAIR pairs;
+// workgroup threads: 2D levels, 3D rows of more than 32 pairs, 3D rows of at most 32 pairs
+constexpr int QUADS_MAXPAIR = 64;
+constexpr int QUADS_NT = 128;
+constexpr int QUADS_NT_WIDE = 256;
+constexpr int QUADS_NT3 = 128;
+
+// j-marching half-sweeps (mgmc_jsweep.hpp): global loads this many steps ahead (2 .. 4), workgroups
+// per half = this many rounds of the resident slots
+constexpr int JS_D = 3;
+constexpr int JS_ROUNDS = 1;
+
+// residual + restriction (mgmc_zrestrict.hpp): coarse points per tile in x of the symmetric 27-point
+// instance; coarse nx below which the one-wavefront 16 x 4 tiles are used
+constexpr int ZR27_CX = 64;
+constexpr int ZR_SMALL_NX = 32;
+
+// z-marching prolongation (k_prolongate_z): fine planes per thread on big 3D levels, and below 2^21
+// fine pair items
+constexpr int PROLONG_Z = 8;
+constexpr int PROLONG_Z_SMALL = 4;
+
+}  // namespace tune
+}  // namespace mgmc

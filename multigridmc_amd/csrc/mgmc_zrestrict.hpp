@@ -9,9 +9,10 @@
 // its 3x3 fine neighbourhood in that plane to a register accumulator.  The restriction sums over
 // (sz, sy, sx) with sz outermost, so plane-by-plane accumulation adds exactly the reference's terms
 // in the reference's order: fine plane 2K-1 is sz = 0 of coarse plane K, 2K is sz = 1, and 2K+1 is
-// sz = 2 of K (which is then final) and sz = 0 of K+1.  Arithmetic is the reference's (A x ascending
-// from 0.0, r = f - Ax, restriction weights multiplied x, y, z), so f_c is bitwise equal to
-// k_residual_restrict and to the CPU oracle.
+// sz = 2 of K (which is then final) and sz = 0 of K+1.  Arithmetic: A x ascending from 0.0 as the
+// reference's (the 7-point fine level and non-symmetric 27-point levels) or class-folded (fold27, the
+// reflection-symmetric 27-point levels); r = f - Ax, restriction weights multiplied x, y, z; f_c is
+// bitwise equal to k_residual_restrict's and to the CPU oracle's.
 //
 // LDS rows are colour-split as in mgmc_zsweep.hpp -- [odd positions | even positions | pad] -- so
 // lanes owning consecutive pairs (residual) or consecutive coarse points (restriction) read
@@ -46,7 +47,7 @@ struct ZRestrictArgs {
     const uint64_t* sample;
 };
 
-// SYM: a reflection-symmetric 27-point stencil, read by class (stencil_coef; same bits)
+// SYM: a fold level (reflection-symmetric 27-point stencil): the residual's sum is fold27's
 template <int NPTS, int CX, int CY, int NT, bool ZN = false, bool SYM = false>
 __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
     if (ZN && (int)blockIdx.x >= a.nblk_main) {  // the tail's noise (see ZRestrictArgs)
@@ -172,7 +173,7 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
     // plane ahead reload those (never used) instead of fetching the next chunk's planes
     const int kx_last = 2 * K1, kf_last = 2 * K1 - 1;
     auto issue_x = [&](int k) {
-        const double* base = plane_ptr(a.x, MGMC_CHUNK_CLAMP && k > kx_last ? kx_last : k);
+        const double* base = plane_ptr(a.x, k > kx_last ? kx_last : k);
 #pragma unroll
         for (int u = 0; u < NLX; ++u) px[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
     };
@@ -186,7 +187,7 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
             }
     };
     auto issue_f = [&](int k) {
-        const double* base = plane_ptr(a.f, MGMC_CHUNK_CLAMP && k > kf_last ? kf_last : k);
+        const double* base = plane_ptr(a.f, k > kf_last ? kf_last : k);
 #pragma unroll
         for (int u = 0; u < NLR; ++u) pf[u] = *reinterpret_cast<const double2*>(base + roff[u]);
     };
@@ -217,6 +218,23 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
                 y1 += a.S.a[16] * pl[1][o1 + XS];
                 y0 += a.S.a[22] * pl[2][o0];
                 y1 += a.S.a[22] * pl[2][o1];
+            } else if constexpr (SYM) {  // a fold level: the class-folded sum (fold27)
+                double v0[27], v1[27];
+#pragma unroll
+                for (int dz = 0; dz < 3; ++dz)
+#pragma unroll
+                    for (int dy = -1; dy <= 1; ++dy) {
+                        const double* rowp = pl[dz] + dy * XS;
+                        const int c = dz * 9 + (dy + 1) * 3;
+                        v0[c] = rowp[m0];
+                        v1[c] = rowp[m1];
+                        v0[c + 1] = rowp[o0];
+                        v1[c + 1] = rowp[o1];
+                        v0[c + 2] = rowp[m0 + 1];
+                        v1[c + 2] = rowp[m1 + 1];
+                    }
+                y0 = fold27(v0, a.S.a);
+                y1 = fold27(v1, a.S.a);
             } else {
 #pragma unroll
                 for (int dz = 0; dz < 3; ++dz)

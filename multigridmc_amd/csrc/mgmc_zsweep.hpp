@@ -121,14 +121,11 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     const int nb = gridDim.x;
     const int b = blockIdx.x;
     const int per = nb >> 3;
-#ifndef MGMC_ZS_ORDER  // (timing builds: 1 = y fastest within the XCD's range, 2 = no XCD remap)
-#define MGMC_ZS_ORDER 0
-#endif
-    const int tile = (nb & 7) || MGMC_ZS_ORDER == 2 ? b : (b & 7) * per + (b >> 3);
+    const int tile = (nb & 7) ? b : (b & 7) * per + (b >> 3);
     // x fastest: a workgroup's x neighbours run next to it on the same XCD and share the partial
     // 128-B lines of the x halo through L2 (y fastest: 1.49x algorithmic traffic against 1.21x)
-    int txi = MGMC_ZS_ORDER == 1 ? (tile / a.nty) % a.ntx : tile % a.ntx;
-    int tyi = MGMC_ZS_ORDER == 1 ? tile % a.nty : (tile / a.ntx) % a.nty;
+    int txi = tile % a.ntx;
+    int tyi = (tile / a.ntx) % a.nty;
     int tzi = tile / (a.ntx * a.nty);
     // zpairs (plain sweep): z-chunks 2m and 2m+1 of a column are neighbouring tiles (same XCD, same
     // round of workgroups); chunk 2m marches up and 2m+1 down, so both reach their shared boundary
@@ -323,7 +320,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     auto issue_x = [&](int k, auto Bc) {
         // (downward march: below k0 - 2)
         const double* base =
-            plane_base(a.xin, MGMC_CHUNK_CLAMP && k > k1 + 1 ? k1 + 1 : (MGMC_CHUNK_CLAMP && k < k0 - 2 ? k0 - 2 : k));
+            plane_base(a.xin, k > k1 + 1 ? k1 + 1 : (k < k0 - 2 ? k0 - 2 : k));
 #pragma unroll
         for (int u = 0; u < NLX; ++u) ZS_PX(decltype(Bc)::value)[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
     };
@@ -343,7 +340,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     const int foff = PF2 ? (active_wave ? t.goff : L.off + 1) : t.goff;  // (PF2: idle waves load a zero pad pair)
     auto load_f = [&](int k) {
         return *reinterpret_cast<const double2*>(
-            plane_base(a.f, MGMC_CHUNK_CLAMP && k > k1 ? k1 : (MGMC_CHUNK_CLAMP && k < k0 - 1 ? k0 - 1 : k)) + foff);
+            plane_base(a.f, k > k1 ? k1 : (k < k0 - 1 ? k0 - 1 : k)) + foff);
     };
 
     // fma-chain stencil sum (ascending column order) at LDS offset o of plane k.  The fine FD

@@ -773,6 +773,7 @@ struct LowRank {
 struct Level {
     Lattice lat;
     CSR A;
+    bool fold = false;  // multicolour: residual by folded_row_sum (a 3D 27-point reflection-symmetric stencil level)
     int ncolours = 2;  // multicolour scheme: 2 (FD level) or 2^d (Galerkin level)
     std::vector<int> colour;  // per row
     std::vector<uint32_t> pair;
@@ -924,20 +925,81 @@ static void posterior_apply(const Level& L, const double* x, double* y, Mode mod
     for (int64_t i = 0; i < L.A.nrow; ++i) y[i] += g[i];
 }
 
+// ---- the device's class-folded residual sum (mgmc_kernels.hpp fold27, restated) ----
+// A level folds when its stencil is 27-point and bitwise reflection-symmetric (each of dx, dy, dz ->
+// -d leaves every coefficient's bits unchanged): every Galerkin level of the cubic FD hierarchies.
+static bool fold_stencil(const Lattice& lat, const CSR& A) {
+    if (lat.dim != 3) return false;
+    for (int d = 0; d < 3; ++d)
+        if (lat.n[d] < 4) return false;  // no interior row (2,2,2): nothing to fold
+    int idx[3] = {2, 2, 2};
+    const int64_t r = lat.euc2lin(idx);
+    if (A.rowptr[r + 1] - A.rowptr[r] != 27) return false;
+    double st[27];
+    stencil_of_interior_row(A, lat, st);
+    for (int dz = 0; dz < 3; ++dz)
+        for (int dy = 0; dy < 3; ++dy)
+            for (int dx = 0; dx < 3; ++dx) {
+                const double a = st[dz * 9 + dy * 3 + dx], b = st[(2 - dz) * 9 + dy * 3 + dx];
+                const double c = st[dz * 9 + (2 - dy) * 3 + dx], e = st[dz * 9 + dy * 3 + (2 - dx)];
+                if (memcmp(&a, &b, 8) || memcmp(&a, &c, 8) || memcmp(&a, &e, 8)) return false;
+            }
+    return true;
+}
+// sum_k a_k x_k of row r by coefficient class: the neighbours with equal (|dx|, |dy|, |dz|) share one
+// coefficient; class c = [dx == 0] + 2 [dy == 0] + 4 [dz == 0] sums its present entries in CSR
+// (= ascending offset) order, then y = a_7 s_7, fma(a_c, s_c, y) for c = 6 .. 0 over the present
+// classes.  Truncated entries are zeros on the device (adding them changes no bits but a zero's sign).
+static double folded_row_sum(const Level& L, int64_t r, const double* x) {
+    double s[8], a[8];
+    bool has[8] = {false, false, false, false, false, false, false, false};
+    int rc[3], cc[3];
+    L.lat.lin2euc(r, rc);
+    for (int64_t q = L.A.rowptr[r]; q < L.A.rowptr[r + 1]; ++q) {
+        L.lat.lin2euc(L.A.col[q], cc);
+        const int c = (cc[0] == rc[0] ? 1 : 0) + (cc[1] == rc[1] ? 2 : 0) + (cc[2] == rc[2] ? 4 : 0);
+        if (!has[c]) {
+            s[c] = x[L.A.col[q]];
+            a[c] = L.A.val[q];
+            has[c] = true;
+        } else {
+            s[c] = s[c] + x[L.A.col[q]];
+        }
+    }
+    double y = 0.0;
+    bool started = false;
+    for (int c = 7; c >= 0; --c) {
+        if (!has[c]) continue;
+        y = started ? fma(a[c], s[c], y) : a[c] * s[c];
+        started = true;
+    }
+    return y;
+}
+static void spmv_level(const Level& L, const double* x, double* y, Mode mode) {
+    if (mode == MULTICOLOUR && L.fold)
+        par_for(L.A.nrow, [&](int64_t r) { y[r] = folded_row_sum(L, r, x); });
+    else
+        spmv(L.A, x, y);
+}
+
 // r = f - (A x + B Sigma^{-1} B^T x).  FAITHFUL: the reference's apply then subtract.  MULTICOLOUR
 // (device order): the low-rank term is folded into f first, r = (f - g) - A x, so the device's
 // residual kernels run unchanged on a patched f.
+// MULTICOLOUR on a fold level: A x by folded_row_sum (the device's residual kernels).
 static void posterior_residual(const Level& L, const double* f, const double* x, double* r, Mode mode) {
     const int64_t n = L.A.nrow;
     if (mode == FAITHFUL || L.lr.m == 0) {
-        posterior_apply(L, x, r, mode);
+        if (mode == MULTICOLOUR && L.fold && L.lr.m == 0)
+            spmv_level(L, x, r, mode);
+        else
+            posterior_apply(L, x, r, mode);
         par_for(n, [&](int64_t q) { r[q] = f[q] - r[q]; });
         return;
     }
     std::vector<double> t(L.lr.m), g(n);
     for (int k = 0; k < L.lr.m; ++k) t[k] = lr_dot(L, k, 1.0 / L.lr.sigma[k], x, mode);
     lr_expand(L, t.data(), g.data());
-    spmv(L.A, x, r);
+    spmv_level(L, x, r, mode);
     for (int64_t q = 0; q < n; ++q) r[q] = (f[q] - g[q]) - r[q];
 }
 
@@ -1379,7 +1441,10 @@ struct MGMC : Sampler {
     std::unique_ptr<Sampler> coarse;
     std::vector<std::vector<double>> x_ell, f_ell, r_ell;
 
-    MGMC(Ctx* c, const Params& p_, const Lattice& lat, CSR A0, const double* override_st /* nlevel*27 or null */)
+    // stencil_hierarchy: the device builds this hierarchy as constant stencils (mgmc_create*: FD / FEM),
+    // so its fold levels take the folded residual; false for a matrix given as CSR (the device's field path)
+    MGMC(Ctx* c, const Params& p_, const Lattice& lat, CSR A0, const double* override_st /* nlevel*27 or null */,
+         bool stencil_hierarchy = true)
         : Sampler(c), p(p_) {
         Lattice lattice = lat;
         CSR A = std::move(A0);
@@ -1391,6 +1456,7 @@ struct MGMC : Sampler {
             std::unique_ptr<Level> L(new Level());
             L->lat = lattice;
             L->A = std::move(A);  // every branch below assigns A before the next level
+            L->fold = stencil_hierarchy && fold_stencil(L->lat, L->A);
             // 2 colours for a 5/7-point fine level (FD), 2^d for 3^d-point levels (FEM, Galerkin)
             if (lattice.dim >= 2) init_colouring(*L, level == 0);
             x_ell.emplace_back(L->A.nrow, 0.0);
@@ -1586,7 +1652,7 @@ orc_handle* orc_create_csr(const orc_params* q, int mode, uint64_t seed, int64_t
     A.val.assign(val, val + rowptr[nrow]);
     Params p = to_params(q);
     p.galerkin = 0;
-    h->mg.reset(new MGMC(&h->ctx, p, make_lattice(q), std::move(A), nullptr));
+    h->mg.reset(new MGMC(&h->ctx, p, make_lattice(q), std::move(A), nullptr, /*stencil_hierarchy=*/false));
     h->f.assign(nrow, 0.0);
     h->x.assign(nrow, 0.0);
     return h;

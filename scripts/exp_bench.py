@@ -1,4 +1,4 @@
-"""Fine-sweep timing of experiment builds (build/libmgmc_exp<N>.so, see scripts/build_exp.sh) against the
+"""Fine-sweep timing of experiment builds (build/libmgmc_<N>.so, see scripts/build_exp.sh) against the
 product library.  python scripts/exp_bench.py [exps, 0 = product]"""
 import os
 import subprocess
@@ -19,7 +19,7 @@ names = {"0": "product", "1": "no-BoxMuller", "2": "no-halo", "3": "no-Philox", 
 for x in exps:
     env = dict(os.environ)
     if x != "0":
-        env["MGMC_LIBRARY"] = os.path.join(ROOT, "build", f"libmgmc_exp{x}.so")  # x = N or s<shape>
+        env["MGMC_LIBRARY"] = os.path.join(ROOT, "build", f"libmgmc_{x}.so")  # x = N or s<shape>
     r = subprocess.run([sys.executable, "-c", CHILD % ROOT], env=env, capture_output=True, text=True, timeout=300)
     out = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else f"FAILED {r.stderr[-300:]}"
     print(f"{names.get(x, x):14s} {out}", flush=True)

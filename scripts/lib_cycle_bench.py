@@ -1,4 +1,4 @@
-"""In-cycle timing of library builds: for each library (product or build/libmgmc_exp<N>.so; "<lib>+VAR=value"
+"""In-cycle timing of library builds: for each library (product or build/libmgmc_<name>.so; "<lib>+VAR=value"
 adds an environment switch, e.g. 0+MGMC_DISABLE=sym), K timed
 N^3 (default 512^3, NLEVEL 7; env N / NLEVEL) V-cycles (mgmc_sample_timed: fine pre / post sweep segments) in a fresh child process, and the
 plain single-graph replay of the same K cycles.  python scripts/lib_cycle_bench.py [exps, 0 = product]"""
@@ -37,6 +37,6 @@ for x in [x for _ in range(int(os.environ.get("REPS", "1"))) for x in libs]:  # 
         k, _, v = extra.partition("=")
         env[k] = v
     if lib != "0":
-        env["MGMC_LIBRARY"] = os.path.join(ROOT, "build", f"libmgmc_exp{lib}.so")
+        env["MGMC_LIBRARY"] = os.path.join(ROOT, "build", f"libmgmc_{lib}.so")
     r = subprocess.run([sys.executable, "-c", CHILD % ROOT], env=env, capture_output=True, text=True, timeout=300)
     print(x, r.stdout.strip().splitlines()[-1] if r.returncode == 0 else f"FAILED {r.stderr[-400:]}", flush=True)

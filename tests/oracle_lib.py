@@ -314,6 +314,24 @@ class Oracle:
         return out
 
 
+def fold_level(desc) -> bool:
+    """A level whose residual the device (and the MULTICOLOUR oracle) sums class-folded (fold27,
+    mgmc_kernels.hpp): 3D, 27-point, bitwise reflection-symmetric stencil (desc = level_desc(l))."""
+    st = np.ascontiguousarray(desc["stencil"], dtype=np.float64)
+    if len(desc["shape"]) != 3 or desc["npoints"] != 27:
+        return False
+    b = st.view(np.uint64).reshape(3, 3, 3)
+    return bool(np.array_equal(b, b[::-1]) and np.array_equal(b, b[:, ::-1]) and np.array_equal(b, b[:, :, ::-1]))
+
+
+def residual_tolerance_ok(got, faithful, A, f, x, R, rtol=1e-14):
+    """|got - faithful| <= rtol * R (|f| + |A| |x|) elementwise: the fold levels' residual (a different
+    summation order from the reference's CSR SpMV) agrees with it to rounding.  R: the restriction as a
+    function of a fine vector (the FAITHFUL oracle's restrict)."""
+    scale = R(np.abs(f) + abs(A) @ np.abs(x))
+    return bool(np.all(np.abs(got - faithful) <= rtol * scale))
+
+
 def fd_level_stencils(shape, mg, kappa_sq) -> np.ndarray:
     """The oracle's own (nlevel, 27) stencils of an FD hierarchy: the reference FD row at full size,
     then R*A*R^T by SpGEMM per level (the galerkin=1 construction), without assembling any level."""

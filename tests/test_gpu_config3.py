@@ -59,7 +59,7 @@ def test_config3_kernel_instances(config3):
 
 @pytest.mark.parametrize("level", [0, 1])
 def test_config3_residual_restrict_bitwise(config3, level):
-    """R (f - A x) at 256^3 and 127^3 against the oracle's CSR SpMV + restriction, bit for bit."""
+    """R (f - A x) at 256^3 (CSR order) and 127^3 (class-folded) against the MULTICOLOUR oracle, bit for bit."""
     s, orc, lat, p = config3
     rng = np.random.default_rng(300 + level)
     n = s.level_desc(level)["ndof"]

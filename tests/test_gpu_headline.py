@@ -7,9 +7,9 @@ planes), the fused-prolongation post-sweep's 128-plane z chunks, the level-1 j-m
 their full 128-pair row width and the 512^3 `k_tail`.  Every one of them is compared here bit for
 bit (np.array_equal) with the CPU oracle's MULTICOLOUR replay, which builds its OWN Galerkin
 hierarchy (the stencil-mode RAP from its FD row; no device stencil is fed in) with Philox key
-(5418513, 0).  The residual + restriction components are also the
-FAITHFUL arithmetic: with no low-rank part the oracle's residual is the reference's
-`A_sparse * x` then `f - r` (linear_operator.hh:66-76, multigridmc_sampler.cc:118-120), in CSR order.
+(5418513, 0).  The level-0 residual + restriction is also the FAITHFUL arithmetic (the reference's
+`A_sparse * x` then `f - r`, linear_operator.hh:66-76, multigridmc_sampler.cc:118-120, in CSR
+order); level 1 and below take the class-folded sum (fold27), which the MULTICOLOUR oracle replays.
 
 The oracle runs its row-parallel loops on the CPU share (tests/oracle_lib.set_threads; bitwise the
 serial oracle's results): setup about 30 s and 4-8 s per cycle on 16 cores.  Progress lines go to
@@ -68,8 +68,8 @@ def test_headline_fine_stencil_is_the_reference_operator(headline):
 
 @pytest.mark.parametrize("level", [0, 1])
 def test_headline_residual_restrict_bitwise(headline, level):
-    """R (f - A x) at 512^3 (level 0: k_zresrestrict<7,64,8,512>) and 255^3 (level 1: the 27-point
-    instance) against the oracle's CSR SpMV + restriction, bit for bit."""
+    """R (f - A x) at 512^3 (level 0: k_zresrestrict<7,64,8,512>, the CSR order) and 255^3 (level 1: the
+    27-point fold instance) against the MULTICOLOUR oracle, bit for bit."""
     s, orc, lat, p = headline
     rng = np.random.default_rng(100 + level)
     n = s.level_desc(level)["ndof"]

@@ -96,7 +96,7 @@ def test_product_reads_only_documented_switches():
     """The only environment the library reads: MGMC_DISABLE (kernel-path switches, each covered by
     tests/test_gpu_parity.py VARIANTS / test_gpu_lowrank.py), MGMC_GRAPH_UNROLL
     (test_unrolled_sample_loop_bitwise) and MGMC_POISON (debug: NaN-filled scratch and LDS,
-    scripts/gpu_r4a.sh runs the headline determinism test with it)."""
+    scripts/profile_round.sh RUN_POISON=1 runs the headline determinism test with it)."""
     src = ""
     csrc = os.path.join(ROOT, "multigridmc_amd", "csrc")
     for fn in os.listdir(csrc):

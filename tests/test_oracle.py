@@ -343,3 +343,31 @@ def test_blocked_cholesky_is_exact_sampler():
     z = o.sample(400, c)
     assert abs(z.mean() - mean) < 5 * np.sqrt(var / 400)
     assert abs(z.var() - var) < 5 * var * np.sqrt(2.0 / 400)
+
+
+# ---------------------------------------------------------------- class-folded residual (fold levels)
+@pytest.mark.parametrize("shape,nlevel,folds", [((16, 16, 16), 3, [False, True]), ((32, 16, 16), 2, [False]),
+                                                 ((64, 64, 64), 4, [False, True, True]),
+                                                 ((512, 16, 24), 3, [False, False]), ((32, 32), 3, [False, False])])
+def test_folded_residual_matches_reference_order_to_rounding(shape, nlevel, folds):
+    """The MULTICOLOUR oracle's residual on a fold level (3D, 27-point, bitwise reflection-symmetric
+    stencil: the device's fold27, mgmc_kernels.hpp) sums by coefficient class.  It equals the reference's
+    CSR order (FAITHFUL, linear_operator.hh:66-76) to 1e-14 of R(|f| + |A||x|) and differs from it in
+    the last bits (the fold is real); on every other level the two are bitwise equal."""
+    import multigridmc_amd as mg
+    p = MultigridParameters(nlevel=nlevel)
+    # the device's decision (host-only mgmc_describe) is the same as the oracle's
+    desc = mg.describe(mg.make_config(mg.ShiftedLaplaceFDOperator(mg.Lattice(*shape), 25.0), p))
+    assert [O.fold_level(d) for d in desc[:len(folds)]] == folds
+    fa = O.Oracle.fd(shape, p, 25.0, mode=O.FAITHFUL)
+    mc = O.Oracle.fd(shape, p, 25.0, mode=O.MULTICOLOUR)
+    rng = np.random.default_rng(5)
+    for level, fold in enumerate(folds):
+        n = fa.ndof(level)
+        x, f = rng.standard_normal(n), rng.standard_normal(n)
+        a, b = fa.residual_restrict(level, f, x), mc.residual_restrict(level, f, x)
+        if fold:
+            assert not np.array_equal(a, b)
+            assert O.residual_tolerance_ok(b, a, fa.csr_matrix(level), f, x, lambda v: fa.restrict(level, v))
+        else:
+            assert np.array_equal(a, b)
