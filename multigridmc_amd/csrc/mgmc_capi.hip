@@ -201,10 +201,18 @@ struct LowRankDev {
     // hold only the local rows; the dense-only rows stream B_g / Y_g, and the patched right-hand
     // side goes to fe (nchains x L.nstore) instead of f
     bool dense_path = false;
+    bool dense_const = false;     // ... its dense column is one number (LRColMeta::cflag): dense_cval
+    double dense_cval = 0.0;
+    int dense_slot = 0;           // ... its value array in dense_val
     int dense_g = -1;
     uint32_t* skip_b = nullptr;                 // bit p: not a dense-only row of the patch
     uint32_t* skip_y[2] = {nullptr, nullptr};   // bit p: not a dense-only row of B_bar (per direction)
     double* yg[2] = {nullptr, nullptr};         // column g of Y (padded, per direction)
+    // ... or, when B_g is one number on a 5 / 7-point level, Y_g as a table: Y_g of a dense-only vertex
+    // is a function of its colour and of which of its 2d neighbours exist (the solve from zero of a
+    // constant right-hand side), so the update reads a 1-byte key per vertex and ytab[d][key]
+    uint8_t* ykey = nullptr;
+    double* ytab[2] = {nullptr, nullptr};
     double* minv_g[2] = {nullptr, nullptr};     // row g of Minv (per direction)
     double* fe = nullptr;
     double* fe2 = nullptr;                      // ... of the first post-sweep, written with the residual's
@@ -1114,7 +1122,9 @@ double* lr_rhs(const mgmc_handle* h, const Level& lv, int mode, double* f, uint3
     a.mask = r.rows_mask;
     a.n = lv.L.nstore;
     a.skip = r.skip_b;
-    a.bg = r.dense_val;  // the only dense column
+    a.bg = r.dense_val + (size_t)r.dense_slot * lv.L.nstore;  // the only dense column
+    a.bgc = r.dense_cval;
+    if (r.dense_const) a.bg = nullptr;  // B_g is one number: not streamed
     const long long nbd = (a.n + LRD_ELEMS - 1) / LRD_ELEMS;
     hipLaunchKernelGGL(k_lr_dense_rhs, dim3((unsigned)(a.nbs + nbd)), dim3(LRD_NT), 0, s, a);
     return a.out;
@@ -1142,6 +1152,8 @@ void lr_fix(const Level& lv, double* x, int direction, double* f_restore, hipStr
         a.n = lv.L.nstore;
         a.skip = r.skip_y[d];
         a.yg = r.yg[d];
+        a.ykey = r.ytab[d] ? r.ykey : nullptr;
+        a.ytab = r.ytab[d];
         a.minv_g = r.minv_g[d];
         const long long nbd = (a.n + LRD_ELEMS - 1) / LRD_ELEMS;
         hipLaunchKernelGGL(k_lr_dense_update, dim3((unsigned)(a.nbs + nbd)), dim3(LRD_NT), 0, s, a);
@@ -3612,7 +3624,8 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
         r.max_col_n = std::max(r.max_col_n, mt.n);
         mt.blk0 = (int)blk_col.size();
         mt.nblk = (int)((mt.n + LR_BLK - 1) / LR_BLK);
-        mt.pad_ = 0;
+        mt.cflag = 0;
+        mt.cval = 0.0;
         for (int b = 0; b < mt.nblk; ++b) blk_col.push_back(k);
         if (dense_here[k]) {
             mt.dense = ndense++;
@@ -3625,6 +3638,24 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
                 t_ent_off.push_back(ref_to_tail(lv, e.first));
                 ent_val.push_back(e.second);
             }
+        }
+    }
+    // a dense column whose every value is one number (bit for bit; the global average on the fine
+    // level, B_g = cell volume: measured_operator.cc:31-45) is read as that constant: no value array is
+    // streamed by the dots and the right-hand-side patches (8 bytes per vertex and launch)
+    for (int k = 0; k < m; ++k) {
+        if (!dense_here[k] || cols[k].ent.empty()) continue;
+        uint64_t b0;
+        memcpy(&b0, &cols[k].ent[0].second, 8);
+        bool same = true;
+        for (long long i = 0; i < N && same; ++i) {
+            uint64_t bi;
+            memcpy(&bi, &cols[k].ent[i].second, 8);
+            same = bi == b0;
+        }
+        if (same) {
+            meta[k].cflag = 1;
+            meta[k].cval = cols[k].ent[0].second;
         }
     }
     r.nblk = (int)blk_col.size();
@@ -3650,6 +3681,9 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
     r.dense_g = -1;
     for (int k = 0; k < m; ++k)
         if (dense_here[k]) r.dense_g = k;
+    r.dense_const = r.dense_g >= 0 && meta[r.dense_g].cflag != 0;
+    r.dense_cval = r.dense_g >= 0 ? meta[r.dense_g].cval : 0.0;
+    r.dense_slot = r.dense_g >= 0 ? meta[r.dense_g].dense : 0;
     const int g = r.dense_path ? r.dense_g : -1;
     // bit p of a skip mask over the padded store: set unless p is an interior vertex of `dense_only`
     auto skip_mask = [&](const std::vector<char>& local, uint32_t** dst) {
@@ -3750,6 +3784,38 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
                 if (!loc && yi[g] != 0.0) ++r.nbar_all[d];
             }
             if ((rc = skip_mask(local, &r.skip_y[d]))) return rc;
+            // the table form of Y_g (see LowRankDev::ykey): key = colour parity | neighbour mask << 1,
+            // every dense-only vertex of one key must hold the same bits, else Y_g is streamed
+            const int dim = lv.spec.dim;
+            if (r.dense_const && lv.spec.npoints == 2 * dim + 1 && !lv.field) {
+                const int n1 = lv.L.nx - 1, n2 = lv.L.ny - 1, n3 = dim == 3 ? lv.L.nz - 1 : 1;
+                std::vector<uint8_t> keys(N);
+                std::vector<double> tab(128, 0.0);
+                std::vector<char> seen(128, 0);
+                bool ok = true;
+                for (long long i = 0; i < N && ok; ++i) {
+                    const int ii = (int)(i % n1) + 1, jj = (int)((i / n1) % n2) + 1, kk = dim == 3 ? (int)(i / ((long long)n1 * n2)) + 1 : 0;
+                    int key = (ii + jj + kk) & 1;
+                    key |= (ii > 1 ? 2 : 0) | (ii < n1 ? 4 : 0) | (jj > 1 ? 8 : 0) | (jj < n2 ? 16 : 0);
+                    if (dim == 3) key |= (kk > 1 ? 32 : 0) | (kk < n3 ? 64 : 0);
+                    keys[i] = (uint8_t)key;
+                    if (local[i]) continue;
+                    if (!seen[key]) {
+                        seen[key] = 1;
+                        tab[key] = col[i];
+                    } else {
+                        ok = memcmp(&tab[key], &col[i], 8) == 0;
+                    }
+                }
+                if (ok) {
+                    if (!r.ykey) {  // keys over the padded store (0 elsewhere: masked by skip_y)
+                        std::vector<uint8_t> kp((size_t)lv.L.nstore + 16, 0);
+                        for (long long i = 0; i < N; ++i) kp[ref_to_padded(lv, i)] = keys[i];
+                        if ((rc = lr_to_device(h, r, &r.ykey, kp))) return rc;
+                    }
+                    if ((rc = lr_to_device(h, r, &r.ytab[d], tab))) return rc;
+                }
+            }
             const size_t yb = (size_t)lv.L.nstore * sizeof(double);
             if (hipMalloc(&r.yg[d], yb) != hipSuccess) return fail(h, MGMC_E_NOMEM, "device allocation failed");
             r.allocs.push_back(r.yg[d]);

@@ -51,7 +51,8 @@ struct LRColMeta {
     long long ent0;  // first entry in the sparse entry arrays (sparse columns)
     int dense;       // index of the column's padded value array, or -1
     int blk0, nblk;  // dot-product blocks
-    int pad_;
+    int cflag;       // dense column whose every value is cval (bit for bit): no value array is read
+    double cval;     // (the global average on the fine level: the cell volume, measured_operator.cc:31-45)
 };
 
 // ---- dot products, stage 1: one wavefront per block of LR_BLK entries ----
@@ -109,7 +110,7 @@ __global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRColMeta* _
 #pragma unroll
             for (int u = 0; u < LRP_U; ++u)
                 if (base + u < cnt) {
-                    a[u] = dv[p[u]];
+                    a[u] = c.cflag ? c.cval : dv[p[u]];
 #pragma unroll
                     for (int q = 0; q < LRP_CH; ++q)
                         if (q < nc) x[q][u] = vc[q * cs + p[u]];
@@ -199,7 +200,7 @@ __global__ void __launch_bounds__(LRS_NT) k_lr_partials_staged(Layout L, const L
 #pragma unroll
         for (int t = 0; t < PER; ++t) {
             const int e = tid + t * LRS_NT;
-            if (e < cnt) prod[e] = (s * dv[p[t]]) * vc[p[t]];
+            if (e < cnt) prod[e] = (s * (c.cflag ? c.cval : dv[p[t]])) * vc[p[t]];
         }
     } else {
 #pragma unroll
@@ -463,7 +464,8 @@ struct LRDenseArgs {
     // dense-only rows (blocks [nbs, ...)): padded range [0, n)
     long long n;
     const uint32_t* skip;
-    const double* bg;
+    const double* bg;         // B_g over the padded store, or null: every B_g entry is bgc
+    double bgc;
 };
 
 // s[ch * m + k] = sq_k xi'_k of sweep `tag` for every chain (only k = g, g's pair, if !all)
@@ -522,7 +524,7 @@ __global__ void __launch_bounds__(LRD_NT) k_lr_dense_rhs(LRDenseArgs a) {
     lrd_pairs(a.skip, a.n, a.nbs, p, ok);
     double2 bv[LRD_PER];
 #pragma unroll
-    for (int r = 0; r < LRD_PER; ++r) bv[r] = *(const double2*)(a.bg + p[r]);
+    for (int r = 0; r < LRD_PER; ++r) bv[r] = a.bg ? *(const double2*)(a.bg + p[r]) : make_double2(a.bgc, a.bgc);
     for (int ch = 0; ch < a.nch; ++ch) {
         const double sg = s[ch * m + a.g];
         const double* fc = a.f + ch * a.cs;
@@ -569,15 +571,20 @@ struct LRDenseUpdateArgs {
     long long n;
     const uint32_t* skip;
     const double* yg;
+    const uint8_t* ykey;      // non-null: Y_g = ytab[ykey[p]] (LowRankDev::ykey), yg is not read
+    const double* ytab;
     const double* minv_g;     // row g of Minv
 };
 
 __global__ void __launch_bounds__(LRD_NT) k_lr_dense_update(LRDenseUpdateArgs a) {
     __shared__ double ws[LR_MAX_CH * LR_MAX_M];
     __shared__ double mg[LR_MAX_M];
+    __shared__ double yt[128];
     const int m = a.m;
     for (int q = threadIdx.x; q < a.nch * m; q += LRD_NT) ws[q] = a.w[q];
     for (int q = threadIdx.x; q < m; q += LRD_NT) mg[q] = a.minv_g[q];
+    if (a.ykey)
+        for (int q = threadIdx.x; q < 128; q += LRD_NT) yt[q] = a.ytab[q];
     __syncthreads();
     if ((int)blockIdx.x < a.nbs) {
         const int u = blockIdx.x * LRD_NT + threadIdx.x;
@@ -596,8 +603,16 @@ __global__ void __launch_bounds__(LRD_NT) k_lr_dense_update(LRDenseUpdateArgs a)
     bool ok[LRD_PER][2];
     lrd_pairs(a.skip, a.n, a.nbs, p, ok);
     double2 yv[LRD_PER];
+    if (a.ykey) {
 #pragma unroll
-    for (int r = 0; r < LRD_PER; ++r) yv[r] = *(const double2*)(a.yg + p[r]);
+        for (int r = 0; r < LRD_PER; ++r) {
+            const uint16_t kk = *(const uint16_t*)(a.ykey + p[r]);  // p even: both keys in one load
+            yv[r] = make_double2(yt[kk & 0xff], yt[kk >> 8]);
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < LRD_PER; ++r) yv[r] = *(const double2*)(a.yg + p[r]);
+    }
     for (int ch = 0; ch < a.nch; ++ch) {
         double* xc = a.x + ch * a.cs;
         double2 xv[LRD_PER];
