@@ -411,12 +411,47 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
                 __syncthreads();
             }
             if (DIM == 3 && NPTS == 27 && t.fold) {
-                for_interior(G, [&](int i, int j, int k) {
-                    const long long p = G.at(i, j, k);
-                    double v[27];
-                    tail_window<3, 27>(x, (int)p, G, v);
-                    scr[p] = f[p] - fold27(v, S.a);
-                });
+                // runs of TSEG vertices along x per thread: each of the 9 window rows is read once over
+                // TSEG + 2 columns (9 (TSEG + 2) LDS reads instead of 27 TSEG) and its values go straight
+                // into the vertices' class sums -- rows ascending, columns ascending: fold27's member
+                // order, so the same bits
+                constexpr int TSEG = 2;
+                const int nseg = (G.nx - 1 + TSEG - 1) / TSEG;
+                const int bs = bits_of(nseg), by = bits_of(G.ny), bz = bits_of(G.nz);
+                for (int q = tid; q < (1 << (bs + by + bz)); q += nt) {
+                    const int sg = q & ((1 << bs) - 1), j = (q >> bs) & ((1 << by) - 1), k = q >> (bs + by);
+                    if (sg >= nseg || j < 1 || j > G.ny - 1 || k < 1 || k > G.nz - 1) continue;
+                    const int i0 = 1 + TSEG * sg;
+                    const int p0 = (int)G.at(i0, j, k);
+                    double cs[TSEG][8];
+#pragma unroll
+                    for (int rr = 0; rr < 9; ++rr) {
+                        double w[TSEG + 2];  // columns i0 - 1 .. i0 + TSEG (past the row end: the next
+                                             // row's zero boundary vertex, used by no interior vertex)
+#pragma unroll
+                        for (int c = 0; c < TSEG + 2; ++c) {
+                            int idx = p0 + (rr / 3 - 1) * (int)G.sp + (rr % 3 - 1) * (int)G.sx + c - 1;
+                            asm volatile("" : "+v"(idx));
+                            w[c] = x[idx];
+                        }
+#pragma unroll
+                        for (int e = 0; e < TSEG; ++e)
+#pragma unroll
+                            for (int dx = 0; dx < 3; ++dx) {
+                                const int t27 = 3 * rr + dx, cl = fold_class(t27);
+                                if (fold_rep(cl) == t27) cs[e][cl] = w[e + dx];
+                                else cs[e][cl] = cs[e][cl] + w[e + dx];
+                            }
+                    }
+#pragma unroll
+                    for (int e = 0; e < TSEG; ++e) {
+                        if (i0 + e > G.nx - 1) break;
+                        double y = S.a[fold_rep(7)] * cs[e][7];
+#pragma unroll
+                        for (int cl = 6; cl >= 0; --cl) y = fma(S.a[fold_rep(cl)], cs[e][cl], y);
+                        scr[p0 + e] = f[p0 + e] - y;
+                    }
+                }
             } else {
                 for_interior(G, [&](int i, int j, int k) {
                     const long long p = G.at(i, j, k);
@@ -460,29 +495,37 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             tail_pin(alpha);
             double* x = lds + ox;
             const double* xc = lds + cox;
+            // every vertex takes the 2^d candidate parents (d >> 1, (d + 1) >> 1) per axis in the
+            // reference's order (kk, jj, ii ascending), with weight 0 where the two coincide (d even):
+            // those terms add an exact 0, and parents on the coarse boundary are zeros of the LDS
+            // layout, so the sum of the present parents' terms is unchanged (only a zero's sign can
+            // differ) -- and no lane diverges on the parent count
             for_interior(G, [&](int i, int j, int k) {
                 const long long p = G.at(i, j, k);
                 double v = x[p];
-                const int k0 = k >> 1, nk = (DIM == 3 && (k & 1)) ? 2 : 1;
-                const int j0 = j >> 1, nj = (j & 1) ? 2 : 1;
-                const int i0 = i >> 1, ni = (i & 1) ? 2 : 1;
-                for (int aa = 0; aa < nk; ++aa) {
-                    const int kk = k0 + aa;
-                    if (DIM == 3 && (kk < 1 || kk > Gc.nz - 1)) continue;
-                    for (int bb = 0; bb < nj; ++bb) {
-                        const int jj = j0 + bb;
-                        if (jj < 1 || jj > Gc.ny - 1) continue;
-                        for (int cc = 0; cc < ni; ++cc) {
-                            const int ii = i0 + cc;
-                            if (ii < 1 || ii > Gc.nx - 1) continue;
+                const int ia = i >> 1, ja = j >> 1, ka = DIM == 3 ? k >> 1 : 0;
+                const double wi[2] = {(i & 1) ? 0.5 : 1.0, (i & 1) ? 0.5 : 0.0};
+                const double wj[2] = {(j & 1) ? 0.5 : 1.0, (j & 1) ? 0.5 : 0.0};
+                const double wk[2] = {(DIM == 3 && (k & 1)) ? 0.5 : 1.0, (DIM == 3 && (k & 1)) ? 0.5 : 0.0};
+                double c[2][2][2];
+#pragma unroll
+                for (int aa = 0; aa < (DIM == 3 ? 2 : 1); ++aa)
+#pragma unroll
+                    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+                        for (int cc = 0; cc < 2; ++cc) c[aa][bb][cc] = xc[Gc.at(ia + cc, ja + bb, DIM == 3 ? ka + aa : 0)];
+#pragma unroll
+                for (int aa = 0; aa < (DIM == 3 ? 2 : 1); ++aa)
+#pragma unroll
+                    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+                        for (int cc = 0; cc < 2; ++cc) {
                             double w = 1.0;
-                            w *= w1(i - 2 * ii);
-                            w *= w1(j - 2 * jj);
-                            if (DIM == 3) w *= w1(k - 2 * kk);
-                            v += alpha * w * xc[Gc.at(ii, jj, DIM == 3 ? kk : 0)];
+                            w *= wi[cc];
+                            w *= wj[bb];
+                            if (DIM == 3) w *= wk[aa];
+                            v += alpha * w * c[aa][bb][cc];
                         }
-                    }
-                }
                 x[p] = v;
             });
             __syncthreads();

@@ -1,4 +1,4 @@
-"""Phase times of k_tail (timing build MGMC_TAIL_PROF: VARIANTS="exptprof=-DMGMC_TAIL_PROF" bash
+"""Phase times of k_tail (timing build MGMC_TAIL_PROF: CXXDEFS=-DMGMC_TAIL_PROF VARIANTS="tprof=-" bash
 scripts/build_exp.sh; MGMC_LIBRARY=build/libmgmc_tprof.so python scripts/tail_prof.py [n] [nlevel]).
 Runs a few prior V-cycles and prints the wall-clock time of every phase of the first tail: the LDS
 fill from HBM, each op's right-hand sides (sweeps) and the rest of the op, the store."""
