@@ -1037,9 +1037,6 @@ void launch_pack(const Level& lv, const double* lex, double* pad, bool pack, hip
 }
 
 // ---- low-rank part (mgmc_lowrank.hpp) ----
-#ifndef LRS_MAX_WAVES  // (timing-experiment builds override it: scripts/build_exp.sh LRSW)
-#define LRS_MAX_WAVES 512
-#endif
 // w = (sc_k B_k)^T v for all columns
 // (batched chains: v cs apart; the partials nblk and w m apart per chain)
 void lr_dots(const Level& lv, const double* v, const double* sc, hipStream_t s, int nch = 1) {
@@ -1047,7 +1044,7 @@ void lr_dots(const Level& lv, const double* v, const double* sc, hipStream_t s, 
     // few wavefronts (coarse levels): the staged kernel (the loads of a block in flight at once);
     // many: one wavefront per block, column values read once per group of chains
     const long long waves = (long long)r.nblk * ((nch + LRP_CH - 1) / LRP_CH);
-    if (r.nblk > 0 && waves < LRS_MAX_WAVES)
+    if (r.nblk > 0 && waves < tune::LR_STAGED_MAX_WAVES)
         hipLaunchKernelGGL(k_lr_partials_staged, dim3(r.nblk, nch), dim3(LRS_NT), 0, s, lv.L, (const LRColMeta*)r.meta,
                            (const int*)r.blk_col, (const long long*)r.ent_off, (const double*)r.ent_val,
                            (const double*)r.dense_val, sc, v, r.part, (long long)lv.L.nstore, r.nblk);

@@ -229,8 +229,19 @@ __global__ void __launch_bounds__(64) k_lr_totals(const LRColMeta* __restrict__ 
     const LRColMeta c = meta[k];
     part += (long long)blockIdx.z * nblk;  // batched chains (blockIdx.z): part nblk, out m apart
     out += (long long)blockIdx.z * m;
+    // lane l adds partials l, l + 64, ... in order; the loads of LRP_U of them are issued together
+    // (the fine level's dense column has ~4000 blocks: 63 dependent round trips per lane otherwise)
+    const double* pc = part + c.blk0;
     double acc = 0.0;
-    for (int b = lane; b < c.nblk; b += 64) acc = acc + part[c.blk0 + b];
+    int b = lane;
+    for (; b + (LRP_U - 1) * 64 < c.nblk; b += LRP_U * 64) {
+        double t[LRP_U];
+#pragma unroll
+        for (int u = 0; u < LRP_U; ++u) t[u] = pc[b + u * 64];
+#pragma unroll
+        for (int u = 0; u < LRP_U; ++u) acc = acc + t[u];
+    }
+    for (; b < c.nblk; b += 64) acc = acc + pc[b];
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
     if (lane == 0) out[k] = acc;

@@ -53,5 +53,10 @@ constexpr int ZR_Y_DESC = 0;
 constexpr int PROLONG_Z = 8;
 constexpr int PROLONG_Z_SMALL = 4;
 
+// ---- low-rank dot products (mgmc_lowrank.hpp) ----
+// levels whose partials need fewer wavefronts than this take the staged kernel (a block's loads
+// spread over a 256-thread workgroup), the others one wavefront per block
+constexpr int LR_STAGED_MAX_WAVES = 512;
+
 }  // namespace tune
 }  // namespace mgmc
