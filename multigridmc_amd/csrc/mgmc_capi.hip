@@ -216,6 +216,12 @@ struct LowRankDev {
     double* minv_g[2] = {nullptr, nullptr};     // row g of Minv (per direction)
     double* fe = nullptr;
     double* fe2 = nullptr;                      // ... of the first post-sweep, written with the residual's
+    // ... or, on a z-sweep level with B_g one number, read in place (LRRhsArg): f is patched in place
+    // on the local rows (saved, restored: the row-list path's k_lr_patch / k_lr_restore_patch), and
+    // the sweep / residual kernels add the dense-only patch e to f on the other rows (e per chain in
+    // rhs_e: [c] the sweep's / residual's, [nchains + c] the first post-sweep's); fe, fe2 unused
+    bool rhs_inplace = false;
+    double* rhs_e = nullptr;
     long long nbar_all[2] = {0, 0};             // B_bar rows in total (local + dense-only with Y_g != 0)
     std::vector<void*> allocs;
 };
@@ -498,10 +504,17 @@ void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s,
     int ex;
     const bool pow2 = std::isnormal(a.alpha) && std::frexp(std::fabs(a.alpha), &ex) == 0.5 && ex > -900 && ex < 900;
     const dim3 grid(nb, 1, nch);  // batched chains: blockIdx.z
-    if (prolong && pow2)
+    const bool lrf = a.lr.skip != nullptr;  // the right-hand side read in place (LRRhsArg)
+    if (prolong && pow2 && lrf)
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 2, MINW, true>), grid, dim3(NT), lds, s, a);
+    else if (prolong && pow2)
         hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 2, MINW>), grid, dim3(NT), lds, s, a);
+    else if (prolong && lrf)
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 1, MINW, true>), grid, dim3(NT), lds, s, a);
     else if (prolong)
         hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 1, MINW>), grid, dim3(NT), lds, s, a);
+    else if (lrf)
+        hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 0, MINW, true>), grid, dim3(NT), lds, s, a);
     else
         hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 0, MINW>), grid, dim3(NT), lds, s, a);
 }
@@ -531,9 +544,12 @@ static int zsweep_plain_rows(const Level& lv, int nch) {
     return (ZS_TYP != ZS_TY && ZS_NTP == ZS_NT && ntiles(ZS_TY) < slots && ntiles(ZS_TYP) <= slots) ? ZS_TYP : ZS_TY;
 }
 
+// lr (non-null): the right-hand side is read in place (LRRhsArg, LowRankDev::rhs_inplace)
 void launch_zsweep(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g0,
-                   int direction, const Level* coarse, const double* xc, double alpha, hipStream_t s, int nch = 1) {
+                   int direction, const Level* coarse, const double* xc, double alpha, hipStream_t s, int nch = 1,
+                   const LRRhsArg* lr = nullptr) {
     ZSweepArgs a;
+    a.lr = lr ? *lr : LRRhsArg{nullptr, nullptr};
     a.cs = lv.L.nstore;
     a.csc = coarse ? coarse->L.nstore : 0;
     a.L = lv.L;
@@ -802,11 +818,12 @@ struct TailNoiseLaunch {  // spare workgroups of the launch draw a tail's noise 
     const uint64_t* sample;
 };
 
-template <int NPTS, int CX, int CY, int NT, bool SYM = false>
+template <int NPTS, int CX, int CY, int NT, bool SYM = false, bool LRF = false>
 void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, const double* f, double* fc, double* xc,
-                           hipStream_t s, int nch, const TailNoiseLaunch* tn = nullptr) {
+                           hipStream_t s, int nch, const TailNoiseLaunch* tn = nullptr, const LRRhsArg* lr = nullptr) {
     ZRestrictArgs a;
     memset(&a, 0, sizeof(a));
+    if (LRF) a.lr = *lr;
     a.csf = lf.L.nstore;
     a.csc = lc.L.nstore;
     a.Lf = lf.L;
@@ -854,7 +871,7 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
     a.ntz = (lc.L.nz - 1 + a.kz - 1) / a.kz;
     const int nt = a.ntx * a.nty * a.ntz;
     const int nb = (nt + 7) / 8 * 8;
-    if (tn) {
+    if (tn && !LRF) {
         a.nblk_main = nb;
         a.jobs = tn->jobs;
         a.njobs = tn->njobs;
@@ -869,16 +886,24 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
                            zrestrict_lds_bytes(CX, CY), s, a);
         return;
     }
-    hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT, false, SYM>), dim3(nb, 1, nch), dim3(NT),
+    hipLaunchKernelGGL((k_zresrestrict<NPTS, CX, CY, NT, false, SYM, LRF>), dim3(nb, 1, nch), dim3(NT),
                        zrestrict_lds_bytes(CX, CY), s, a);
 }
 
 // tn: the small z-marching kernel also draws a tail's noise (zr_small_path; ignored elsewhere)
 // skip_xc: the z-marching kernel leaves x_c alone (Op::xzero: the coarse level's first sweep takes it as
 // zeros without loading it)
+// the levels whose residual + restriction runs a k_zresrestrict instance with an LRF variant (the
+// 7-point z-marching kernels of the non-small coarse levels: launch_residual_restrict below)
+bool zres_lrf_capable(const Level& lf, const Level& lc) {
+    return lf.spec.dim == 3 && lf.spec.npoints == 7 && !lf.field && !(lf.paths & PATH_NO_ZRESTRICT) &&
+           lc.L.nx >= 8 && lc.L.nx >= tune::ZR_SMALL_NX;
+}
+
+// lr (non-null): the level's right-hand side is read in place (LRRhsArg; zres_lrf_capable levels only)
 void launch_residual_restrict(const Level& lf, const Level& lc, const double* x, const double* f, double* fc,
                               double* xc, int zero_xc, hipStream_t s, int nch = 1, const TailNoiseLaunch* tn = nullptr,
-                              bool skip_xc = false) {
+                              bool skip_xc = false, const LRRhsArg* lr = nullptr) {
     const bool zr = lf.spec.dim == 3 && zero_xc && !lf.field && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8;
     if (nch > 1 && !zr) {  // batched chains on the generic kernels: one launch per chain
         for (int c = 0; c < nch; ++c)
@@ -906,7 +931,11 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
     if (lf.spec.dim == 3 && zero_xc && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8) {
         const bool small = lc.L.nx < tune::ZR_SMALL_NX;
         if (skip_xc) xc = nullptr;
-        if (lf.spec.npoints == 7) {
+        if (lr) {  // (zres_lrf_capable)
+            if ((long long)((lc.L.nx + 62) / 64) * ((lc.L.ny + 6) / 8) * (lc.L.nz - 1) >= 16 * 1024)
+                launch_zresrestrict_t<7, 64, 8, 512, false, true>(lf, lc, x, f, fc, xc, s, nch, nullptr, lr);
+            else launch_zresrestrict_t<7, 64, 4, 256, false, true>(lf, lc, x, f, fc, xc, s, nch, nullptr, lr);
+        } else if (lf.spec.npoints == 7) {
             if (small) launch_zresrestrict_t<7, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch, tn);
             // 64 x 8 coarse points, 512 threads, 80 KB of LDS (2 workgroups per CU): half the y halo
             // of 64 x 4 (19 x planes rows per 16 fine rows instead of 11 per 8); 512^3 with kz 32:
@@ -1059,9 +1088,9 @@ void lr_dots(const Level& lv, const double* v, const double* sc, hipStream_t s, 
 
 // patch y on the rows of B (LR_PATCH_NOISE: y += B Sigma^{-1/2} xi'; RESIDUAL: y -= B w; APPLY: y += B w)
 void lr_patch(const mgmc_handle* h, const Level& lv, int mode, double* y, uint32_t tag, const uint64_t* sample,
-              hipStream_t s, int nch = 1) {
+              hipStream_t s, int nch = 1, double* eout = nullptr) {
     const LowRankDev& r = lv.lr;
-    if (r.nrows == 0) return;
+    if (r.nrows == 0 && !eout) return;
     LRPatchArgs a;
     a.m = r.m;
     a.nrows = r.nrows;
@@ -1079,7 +1108,10 @@ void lr_patch(const mgmc_handle* h, const Level& lv, int mode, double* y, uint32
     a.cs = lv.L.nstore;
     a.chain0 = (uint32_t)h->chain;
     a.seed_hi = (uint32_t)(h->seed >> 32);
-    hipLaunchKernelGGL(k_lr_patch, dim3((r.nrows + 255) / 256, 1, nch), dim3(256), 0, s, a);
+    a.eout = eout;  // (the dense-only patch of a level read in place: LRRhsArg)
+    a.g = r.dense_g;
+    a.bgc = r.dense_cval;
+    hipLaunchKernelGGL(k_lr_patch, dim3(std::max((r.nrows + 255) / 256, 1), 1, nch), dim3(256), 0, s, a);
 }
 
 // the right-hand side a low-rank level's sweep (LR_PATCH_NOISE: f + B Sigma^{-1/2} xi') or
@@ -1088,11 +1120,19 @@ void lr_patch(const mgmc_handle* h, const Level& lv, int mode, double* y, uint32
 // LR_PATCH_APPLY: f += B t in place on either path.
 // post_tag >= 0 (dense-column path, LR_PATCH_RESIDUAL): the same launch also writes r.fe2 =
 // f + B Sigma^{-1/2} xi' of the level's first post-sweep (tag post_tag), which then reads r.fe2
+// inplace (non-null, a level with lr.rhs_inplace, LR_PATCH_NOISE / RESIDUAL): f is patched in place on
+// the local rows and the chains' dense-only patch goes to lr.rhs_e; *inplace tells the consumer
+// kernel how to read f (returned; post_tag unused: the first post-sweep's patch is lr_restore_patch's)
 double* lr_rhs(const mgmc_handle* h, const Level& lv, int mode, double* f, uint32_t tag, const uint64_t* sample,
-               hipStream_t s, int nch = 1, int64_t post_tag = -1) {
+               hipStream_t s, int nch = 1, int64_t post_tag = -1, LRRhsArg* inplace = nullptr) {
     const LowRankDev& r = lv.lr;
     if (!r.dense_path) {
         lr_patch(h, lv, mode, f, tag, sample, s, nch);
+        return f;
+    }
+    if (inplace && r.rhs_inplace && mode != LR_PATCH_APPLY) {
+        lr_patch(h, lv, mode, f, tag, sample, s, nch, r.rhs_e);
+        *inplace = LRRhsArg{r.skip_b, r.rhs_e};
         return f;
     }
     LRDenseArgs a;
@@ -1152,6 +1192,11 @@ void lr_fix(const Level& lv, double* x, int direction, double* f_restore, hipStr
         a.ykey = r.ytab[d] ? r.ykey : nullptr;
         a.ytab = r.ytab[d];
         a.minv_g = r.minv_g[d];
+        a.nrest = f_restore ? r.nrows : 0;  // (a right-hand side patched in place: rhs_inplace)
+        a.rest_off = r.rows_off;
+        a.rest_val = r.save;
+        a.f = f_restore;
+        a.nbs = (std::max(a.nbar, a.nrest) + LRD_NT - 1) / LRD_NT;
         const long long nbd = (a.n + LRD_ELEMS - 1) / LRD_ELEMS;
         hipLaunchKernelGGL(k_lr_dense_update, dim3((unsigned)(a.nbs + nbd)), dim3(LRD_NT), 0, s, a);
         return;
@@ -1216,6 +1261,9 @@ LRJob lr_job(const Level& lv, int restore, int noise, uint32_t tag) {
     j.save = r.save;
     j.restore = restore;
     j.noise = noise;
+    j.eout = nullptr;
+    j.g = r.dense_g;
+    j.bgc = r.dense_cval;
     return j;
 }
 
@@ -1227,7 +1275,10 @@ void lr_restore_patch(const mgmc_handle* h, const Op& op, const Level& lv, const
     a.job[0] = lr_job(lv, 1, op.lr_post_patch, op.lr_post_tag);
     a.job[1] = op.lr_coarse_patch ? lr_job(lc, 0, 1, op.lr_coarse_tag) : lr_job(lc, 0, 0, 0);
     if (!op.lr_coarse_patch) a.job[1].nrows = 0;
+    // (a level read in place: the first post-sweep's dense-only patch to rhs_e[nchains + c])
+    if (lv.lr.rhs_inplace && op.lr_post_patch) a.job[0].eout = lv.lr.rhs_e + nch;
     a.nb0 = (a.job[0].nrows + 255) / 256;
+    if (a.job[0].eout) a.nb0 = std::max(a.nb0, 1);
     const int nb = a.nb0 + (a.job[1].nrows + 255) / 256;
     a.key = h->key;
     a.sample = sample;
@@ -1238,9 +1289,10 @@ void lr_restore_patch(const mgmc_handle* h, const Op& op, const Level& lv, const
     if (nb > 0) hipLaunchKernelGGL(k_lr_restore_patch, dim3(nb, 1, nch), dim3(256), 0, s, a);
 }
 
-void lr_restore(const Level& lv, double* f, hipStream_t s, int nch = 1) {
+void lr_restore(const Level& lv, double* f, hipStream_t s, int nch = 1, bool patched = false) {
     const LowRankDev& r = lv.lr;
-    if (r.nrows == 0 || r.dense_path) return;  // dense-column path: f was never patched
+    // dense-column path: f was never patched, unless read in place (patched)
+    if (r.nrows == 0 || (r.dense_path && !patched)) return;
     hipLaunchKernelGGL(k_lr_restore, dim3((r.nrows + 255) / 256, 1, nch), dim3(256), 0, s, r.nrows,
                        (const long long*)r.rows_off, (const double*)r.save, f, (long long)lv.L.nstore);
 }
@@ -1853,14 +1905,21 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 GibbsArg g = make_gibbs(h, lv, op.tag, 0, sample);
                 const bool lr = lv.lr.m > 0;
                 double* fs = lv.f;  // the right-hand side the sweep reads
-                if (lr && !op.lr_skip_patch) fs = lr_rhs(h, lv, LR_PATCH_NOISE, lv.f, op.tag, sample, s, nch);
-                else if (lr && lv.lr.dense_path) fs = lv.lr.fe2;  // written with the level's residual
+                // (rhs_inplace: f itself, patched by the sweep kernel as lrr says)
+                LRRhsArg lrr{nullptr, nullptr};
+                const bool inplace = lr && lv.lr.rhs_inplace;  // (a z-sweep level)
+                if (lr && !op.lr_skip_patch)
+                    fs = lr_rhs(h, lv, LR_PATCH_NOISE, lv.f, op.tag, sample, s, nch, -1, inplace ? &lrr : nullptr);
+                else if (inplace)  // patched (local rows, e) after the level's residual: lr_restore_patch
+                    lrr = LRRhsArg{lv.lr.skip_b, lv.lr.rhs_e + nch};
+                else if (lr && lv.lr.dense_path)
+                    fs = lv.lr.fe2;  // written with the level's residual
                 double* xo = lv.x;
                 if (lv.zsweep) {
                     const Level* lc = op.prolong ? &h->levels[op.level + 1] : nullptr;
                     xo = lv.buf(1 - op.src);
                     launch_zsweep(lv, lv.buf(op.src), xo, fs, g, op.direction, lc, lc ? lc->x : nullptr,
-                                  h->cfg.coarse_scaling, s, nch);
+                                  h->cfg.coarse_scaling, s, nch, lrr.skip ? &lrr : nullptr);
                 } else if (lv.quads) {
                     xo = lv.buf(1 - op.src);
                     launch_quads(lv, lv.buf(op.src), xo, fs, g, op.direction, s, nch, op.xzero != 0);
@@ -1875,7 +1934,7 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 if (lr && lv.lr.small)
                     lr_small(h, lv, xo, op.direction, op.lr_next, op.lr_next_tag, sample, s, nch);
                 else if (lr)
-                    lr_fix(lv, xo, op.direction, lv.lr.dense_path ? nullptr : lv.f, s, nch);
+                    lr_fix(lv, xo, op.direction, lv.lr.dense_path && !inplace ? nullptr : lv.f, s, nch);
                 break;
             }
             case OP_SWEEP_RESTRICT: {  // (2D Galerkin level, no low-rank part: qrestrict_ok)
@@ -1905,10 +1964,12 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 Level& lc = h->levels[op.level + 1];
                 const bool lr = lv.lr.m > 0;
                 double* fr = lv.f;
+                LRRhsArg lrr{nullptr, nullptr};  // (rhs_inplace: f read in place, as lrr says)
                 if (lr && !op.lr_skip_patch) {  // r = (f - B Sigma^{-1} B^T x) - A x
                     lr_dots(lv, lv.buf(op.src), lv.lr.sc_inv, s, nch);
                     fr = lr_rhs(h, lv, LR_PATCH_RESIDUAL, lv.f, 0, sample, s, nch,
-                                lv.lr.dense_path && op.lr_post_patch ? (int64_t)op.lr_post_tag : -1);
+                                lv.lr.dense_path && op.lr_post_patch ? (int64_t)op.lr_post_tag : -1,
+                                lv.lr.rhs_inplace && op.zpre == 0 ? &lrr : nullptr);
                 }
                 if (op.zpre > 0) {  // + the next op's (k_tail's) noise
                     const int ti = op.zpre - 1;
@@ -1916,19 +1977,20 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                                              h->key, (uint32_t)h->chain, (uint32_t)(h->seed >> 32), sample};
                     launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch, &tn);
                 } else {
-                    launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch, nullptr, op.xzero != 0);
+                    launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch, nullptr, op.xzero != 0,
+                                             lrr.skip ? &lrr : nullptr);
                     if (op.xzero && h->poison)  // (debug) the skipped x_c write leaves stale values: make them NaN
                         for (int c = 0; c < nch; ++c)
                             hipLaunchKernelGGL(k_poison_interior, dim3((lc.L.nx - 1 + 255) / 256, lc.L.ny - 1,
                                                                        lc.spec.dim == 3 ? lc.L.nz - 1 : 1),
                                                dim3(256), 0, s, lc.L, chain_ptr(lc.x, lc, c));
                 }
-                if (lr && lv.lr.dense_path)
+                if (lr && lv.lr.dense_path && !lrr.skip)
                     ;  // f was never patched; the post-sweep's rhs went to lr.fe2 above
                 else if (lr && (op.lr_post_patch || op.lr_coarse_patch))
                     lr_restore_patch(h, op, lv, lc, sample, s, nch);
                 else if (lr)
-                    lr_restore(lv, lv.f, s, nch);
+                    lr_restore(lv, lv.f, s, nch, lrr.skip != nullptr);
                 break;
             }
             case OP_PROLONGATE: {
@@ -3707,6 +3769,14 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
             if (hipMalloc(q, fb) != hipSuccess) return fail(h, MGMC_E_NOMEM, "device allocation failed");
             r.allocs.push_back(*q);
             HIPCHK(h, hipMemsetAsync(*q, 0, fb, h->stream));
+        }
+        // the fine z-sweep level's kernels read the patched right-hand side in place (k_zsweep_rb7 /
+        // k_zresrestrict LRF) when B_g is one number
+        r.rhs_inplace = r.dense_path && r.dense_const && lv.zsweep && level + 1 < (int)h->levels.size() &&
+                        zres_lrf_capable(lv, h->levels[level + 1]);
+        if (r.rhs_inplace) {
+            std::vector<double> ez((size_t)2 * h->nchains, 0.0);
+            if ((rc = lr_to_device(h, r, &r.rhs_e, ez))) return rc;
         }
     }
     int nrows = 0;

@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "mgmc_kernels.hpp"
+#include "mgmc_tuning.hpp"
 
 namespace mgmc {
 
@@ -62,7 +63,7 @@ struct LRColMeta {
 // are a handful of wavefronts, each a chain of up to 64 dependent global round trips otherwise).
 // Batched chains: blockIdx.y = a group of LRP_CH chains; the column value of an entry is loaded
 // once for the group (v cs apart, the partials nblk apart per chain).
-constexpr int LRP_U = 8, LRP_CH = 4;
+constexpr int LRP_U = tune::LR_PART_U, LRP_CH = tune::LR_PART_CH;
 __global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRColMeta* __restrict__ meta,
                                                      const int* __restrict__ blk_col,
                                                      const long long* __restrict__ ent_off,
@@ -229,17 +230,18 @@ __global__ void __launch_bounds__(64) k_lr_totals(const LRColMeta* __restrict__ 
     const LRColMeta c = meta[k];
     part += (long long)blockIdx.z * nblk;  // batched chains (blockIdx.z): part nblk, out m apart
     out += (long long)blockIdx.z * m;
-    // lane l adds partials l, l + 64, ... in order; the loads of LRP_U of them are issued together
+    // lane l adds partials l, l + 64, ... in order; the loads of U of them are issued together
     // (the fine level's dense column has ~4000 blocks: 63 dependent round trips per lane otherwise)
     const double* pc = part + c.blk0;
     double acc = 0.0;
     int b = lane;
-    for (; b + (LRP_U - 1) * 64 < c.nblk; b += LRP_U * 64) {
-        double t[LRP_U];
+    constexpr int U = 8;
+    for (; b + (U - 1) * 64 < c.nblk; b += U * 64) {
+        double t[U];
 #pragma unroll
-        for (int u = 0; u < LRP_U; ++u) t[u] = pc[b + u * 64];
+        for (int u = 0; u < U; ++u) t[u] = pc[b + u * 64];
 #pragma unroll
-        for (int u = 0; u < LRP_U; ++u) acc = acc + t[u];
+        for (int u = 0; u < U; ++u) acc = acc + t[u];
     }
     for (; b < c.nblk; b += 64) acc = acc + pc[b];
 #pragma unroll
@@ -268,6 +270,11 @@ struct LRPatchArgs {
     int mode;
     long long cs;               // batched chains (blockIdx.z): y cs, save nrows, t m apart
     uint32_t chain0, seed_hi;   // chain c's Philox key: (key.k0, lo32(chain0 + c) ^ seed_hi)
+    // non-null (a dense-column level read in place, LRRhsArg): eout[c] = the dense-only patch of
+    // chain c, +/-(0.0 + bgc s_g) -- the term k_lr_dense_rhs adds on those rows
+    double* eout;
+    int g;
+    double bgc;
 };
 
 __device__ __forceinline__ RngKey lr_chain_key(RngKey key, uint32_t chain0, uint32_t seed_hi, int ch) {
@@ -299,6 +306,10 @@ __global__ void __launch_bounds__(256) k_lr_patch(LRPatchArgs a) {
         s[threadIdx.x] = a.t[threadIdx.x];
     }
     __syncthreads();
+    if (a.eout && blockIdx.x == 0 && threadIdx.x == 0) {
+        const double e = 0.0 + a.bgc * s[a.g];
+        a.eout[batch_chain()] = a.mode == LR_PATCH_RESIDUAL ? -e : e;  // (y - e == y + (-e))
+    }
     const int u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= a.nrows) return;
     const long long p = a.off[u];
@@ -368,6 +379,9 @@ struct LRJob {
     double* save;
     int restore;  // 1: f = save (+ noise)
     int noise;    // 1: + B Sigma^{-1/2} xi'
+    double* eout;  // non-null (noise, a dense-column level read in place): eout[c] = 0.0 + bgc s_g (k_lr_patch)
+    int g;
+    double bgc;
 };
 
 struct LRRestorePatchArgs {
@@ -401,6 +415,7 @@ __global__ void __launch_bounds__(256) k_lr_restore_patch(LRRestorePatchArgs a) 
             if (2 * t + 1 < j.m) s[2 * t + 1] = j.sq[2 * t + 1] * z1;
         }
         __syncthreads();
+        if (j.eout && u == 0) j.eout[ch] = 0.0 + j.bgc * s[j.g];
     }
     if (u >= j.nrows) return;
     const long long p = j.off[u];
@@ -438,7 +453,7 @@ __global__ void __launch_bounds__(256) k_lr_restore_patch(LRRestorePatchArgs a) 
 // lists are read once for all of them.
 // threads per block, 16-byte pairs of the padded store per thread (L.nstore and every chain / column
 // offset are multiples of 16 doubles), store entries per block
-constexpr int LRD_NT = 256, LRD_PER = 2, LRD_ELEMS = 2 * LRD_PER * LRD_NT;
+constexpr int LRD_NT = 256, LRD_PER = tune::LR_DENSE_PER, LRD_ELEMS = 2 * LRD_PER * LRD_NT;
 
 // the pairs of one thread: p[r] (even) clamped into [0, n), ok[r][h] = a dense-only vertex p + h
 __device__ __forceinline__ void lrd_pairs(const uint32_t* __restrict__ skip, long long n, int nbs, long long p[LRD_PER],
@@ -585,6 +600,12 @@ struct LRDenseUpdateArgs {
     const uint8_t* ykey;      // non-null: Y_g = ytab[ykey[p]] (LowRankDev::ykey), yg is not read
     const double* ytab;
     const double* minv_g;     // row g of Minv
+    // the restore of f on the rows of B (a right-hand side patched in place, LRRhsArg), with the
+    // local blocks: f[rest_off[u]] = rest_val[u] for u < nrest (k_lr_update's)
+    int nrest;
+    const long long* rest_off;
+    const double* rest_val;
+    double* f;
 };
 
 __global__ void __launch_bounds__(LRD_NT) k_lr_dense_update(LRDenseUpdateArgs a) {
@@ -599,15 +620,18 @@ __global__ void __launch_bounds__(LRD_NT) k_lr_dense_update(LRDenseUpdateArgs a)
     __syncthreads();
     if ((int)blockIdx.x < a.nbs) {
         const int u = blockIdx.x * LRD_NT + threadIdx.x;
-        if (u >= a.nbar) return;
-        const double* bv = a.bar_val + (long long)u * m;
-        const long long p = a.bar_off[u];
-        for (int ch = 0; ch < a.nch; ++ch) {
-            double acc = 0.0;
-            for (int k = 0; k < m; ++k) acc = fma(bv[k], ws[ch * m + k], acc);
-            double* xc = a.x + ch * a.cs;
-            xc[p] = xc[p] - acc;
+        if (u < a.nbar) {
+            const double* bv = a.bar_val + (long long)u * m;
+            const long long p = a.bar_off[u];
+            for (int ch = 0; ch < a.nch; ++ch) {
+                double acc = 0.0;
+                for (int k = 0; k < m; ++k) acc = fma(bv[k], ws[ch * m + k], acc);
+                double* xc = a.x + ch * a.cs;
+                xc[p] = xc[p] - acc;
+            }
         }
+        if (u < a.nrest)
+            for (int ch = 0; ch < a.nch; ++ch) a.f[ch * a.cs + a.rest_off[u]] = a.rest_val[(long long)ch * a.nrest + u];
         return;
     }
     long long p[LRD_PER];

@@ -57,6 +57,12 @@ constexpr int PROLONG_Z_SMALL = 4;
 // levels whose partials need fewer wavefronts than this take the staged kernel (a block's loads
 // spread over a 256-thread workgroup), the others one wavefront per block
 constexpr int LR_STAGED_MAX_WAVES = 512;
+// entries per lane whose loads k_lr_partials issues together
+constexpr int LR_PART_U = 8;
+// chains per wavefront of k_lr_partials (batched chains: a column value loaded once for them)
+constexpr int LR_PART_CH = 4;
+// 16-byte pairs per thread of the dense-column kernels (k_lr_dense_rhs / _update)
+constexpr int LR_DENSE_PER = 2;
 
 }  // namespace tune
 }  // namespace mgmc
