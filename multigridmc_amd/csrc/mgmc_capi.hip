@@ -222,6 +222,9 @@ struct LowRankDev {
     // rhs_e: [c] the sweep's / residual's, [nchains + c] the first post-sweep's); fe, fe2 unused
     bool rhs_inplace = false;
     double* rhs_e = nullptr;
+    // the split column of the row patches (mgmc_lowrank.hpp lr_row_patch): the level's one dense
+    // column when every value of it is one number (dense_const), else -1
+    int split_g = -1;
     long long nbar_all[2] = {0, 0};             // B_bar rows in total (local + dense-only with Y_g != 0)
     std::vector<void*> allocs;
 };
@@ -504,7 +507,7 @@ void launch_zsweep_t(const Level& lv, ZSweepArgs a, bool prolong, hipStream_t s,
     int ex;
     const bool pow2 = std::isnormal(a.alpha) && std::frexp(std::fabs(a.alpha), &ex) == 0.5 && ex > -900 && ex < 900;
     const dim3 grid(nb, 1, nch);  // batched chains: blockIdx.z
-    const bool lrf = a.lr.skip != nullptr;  // the right-hand side read in place (LRRhsArg)
+    const bool lrf = a.lr.e != nullptr;  // the right-hand side read in place (LRRhsArg)
     if (prolong && pow2 && lrf)
         hipLaunchKernelGGL((k_zsweep_rb7<XP, TY, NT, 2, MINW, true>), grid, dim3(NT), lds, s, a);
     else if (prolong && pow2)
@@ -549,7 +552,7 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
                    int direction, const Level* coarse, const double* xc, double alpha, hipStream_t s, int nch = 1,
                    const LRRhsArg* lr = nullptr) {
     ZSweepArgs a;
-    a.lr = lr ? *lr : LRRhsArg{nullptr, nullptr};
+    a.lr = lr ? *lr : LRRhsArg{nullptr};
     a.cs = lv.L.nstore;
     a.csc = coarse ? coarse->L.nstore : 0;
     a.L = lv.L;
@@ -1108,8 +1111,8 @@ void lr_patch(const mgmc_handle* h, const Level& lv, int mode, double* y, uint32
     a.cs = lv.L.nstore;
     a.chain0 = (uint32_t)h->chain;
     a.seed_hi = (uint32_t)(h->seed >> 32);
-    a.eout = eout;  // (the dense-only patch of a level read in place: LRRhsArg)
-    a.g = r.dense_g;
+    a.split_g = mode == LR_PATCH_APPLY ? -1 : r.split_g;
+    a.eout = eout;  // (a level read in place: LRRhsArg)
     a.bgc = r.dense_cval;
     hipLaunchKernelGGL(k_lr_patch, dim3(std::max((r.nrows + 255) / 256, 1), 1, nch), dim3(256), 0, s, a);
 }
@@ -1132,7 +1135,7 @@ double* lr_rhs(const mgmc_handle* h, const Level& lv, int mode, double* f, uint3
     }
     if (inplace && r.rhs_inplace && mode != LR_PATCH_APPLY) {
         lr_patch(h, lv, mode, f, tag, sample, s, nch, r.rhs_e);
-        *inplace = LRRhsArg{r.skip_b, r.rhs_e};
+        *inplace = LRRhsArg{r.rhs_e};
         return f;
     }
     LRDenseArgs a;
@@ -1162,6 +1165,7 @@ double* lr_rhs(const mgmc_handle* h, const Level& lv, int mode, double* f, uint3
     a.bg = r.dense_val + (size_t)r.dense_slot * lv.L.nstore;  // the only dense column
     a.bgc = r.dense_cval;
     if (r.dense_const) a.bg = nullptr;  // B_g is one number: not streamed
+    a.split_g = mode == LR_PATCH_APPLY ? -1 : r.split_g;
     const long long nbd = (a.n + LRD_ELEMS - 1) / LRD_ELEMS;
     hipLaunchKernelGGL(k_lr_dense_rhs, dim3((unsigned)(a.nbs + nbd)), dim3(LRD_NT), 0, s, a);
     return a.out;
@@ -1261,8 +1265,8 @@ LRJob lr_job(const Level& lv, int restore, int noise, uint32_t tag) {
     j.save = r.save;
     j.restore = restore;
     j.noise = noise;
+    j.split_g = r.split_g;
     j.eout = nullptr;
-    j.g = r.dense_g;
     j.bgc = r.dense_cval;
     return j;
 }
@@ -1906,12 +1910,12 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 const bool lr = lv.lr.m > 0;
                 double* fs = lv.f;  // the right-hand side the sweep reads
                 // (rhs_inplace: f itself, patched by the sweep kernel as lrr says)
-                LRRhsArg lrr{nullptr, nullptr};
+                LRRhsArg lrr{nullptr};
                 const bool inplace = lr && lv.lr.rhs_inplace;  // (a z-sweep level)
                 if (lr && !op.lr_skip_patch)
                     fs = lr_rhs(h, lv, LR_PATCH_NOISE, lv.f, op.tag, sample, s, nch, -1, inplace ? &lrr : nullptr);
                 else if (inplace)  // patched (local rows, e) after the level's residual: lr_restore_patch
-                    lrr = LRRhsArg{lv.lr.skip_b, lv.lr.rhs_e + nch};
+                    lrr = LRRhsArg{lv.lr.rhs_e + nch};
                 else if (lr && lv.lr.dense_path)
                     fs = lv.lr.fe2;  // written with the level's residual
                 double* xo = lv.x;
@@ -1919,7 +1923,7 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                     const Level* lc = op.prolong ? &h->levels[op.level + 1] : nullptr;
                     xo = lv.buf(1 - op.src);
                     launch_zsweep(lv, lv.buf(op.src), xo, fs, g, op.direction, lc, lc ? lc->x : nullptr,
-                                  h->cfg.coarse_scaling, s, nch, lrr.skip ? &lrr : nullptr);
+                                  h->cfg.coarse_scaling, s, nch, lrr.e ? &lrr : nullptr);
                 } else if (lv.quads) {
                     xo = lv.buf(1 - op.src);
                     launch_quads(lv, lv.buf(op.src), xo, fs, g, op.direction, s, nch, op.xzero != 0);
@@ -1964,7 +1968,7 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 Level& lc = h->levels[op.level + 1];
                 const bool lr = lv.lr.m > 0;
                 double* fr = lv.f;
-                LRRhsArg lrr{nullptr, nullptr};  // (rhs_inplace: f read in place, as lrr says)
+                LRRhsArg lrr{nullptr};  // (rhs_inplace: f read in place, as lrr says)
                 if (lr && !op.lr_skip_patch) {  // r = (f - B Sigma^{-1} B^T x) - A x
                     lr_dots(lv, lv.buf(op.src), lv.lr.sc_inv, s, nch);
                     fr = lr_rhs(h, lv, LR_PATCH_RESIDUAL, lv.f, 0, sample, s, nch,
@@ -1978,19 +1982,19 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                     launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch, &tn);
                 } else {
                     launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch, nullptr, op.xzero != 0,
-                                             lrr.skip ? &lrr : nullptr);
+                                             lrr.e ? &lrr : nullptr);
                     if (op.xzero && h->poison)  // (debug) the skipped x_c write leaves stale values: make them NaN
                         for (int c = 0; c < nch; ++c)
                             hipLaunchKernelGGL(k_poison_interior, dim3((lc.L.nx - 1 + 255) / 256, lc.L.ny - 1,
                                                                        lc.spec.dim == 3 ? lc.L.nz - 1 : 1),
                                                dim3(256), 0, s, lc.L, chain_ptr(lc.x, lc, c));
                 }
-                if (lr && lv.lr.dense_path && !lrr.skip)
+                if (lr && lv.lr.dense_path && !lrr.e)
                     ;  // f was never patched; the post-sweep's rhs went to lr.fe2 above
                 else if (lr && (op.lr_post_patch || op.lr_coarse_patch))
                     lr_restore_patch(h, op, lv, lc, sample, s, nch);
                 else if (lr)
-                    lr_restore(lv, lv.f, s, nch, lrr.skip != nullptr);
+                    lr_restore(lv, lv.f, s, nch, lrr.e != nullptr);
                 break;
             }
             case OP_PROLONGATE: {
@@ -3741,6 +3745,7 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
     for (int k = 0; k < m; ++k)
         if (dense_here[k]) r.dense_g = k;
     r.dense_const = r.dense_g >= 0 && meta[r.dense_g].cflag != 0;
+    r.split_g = ndense == 1 && r.dense_const ? r.dense_g : -1;  // (any path: the row lists too)
     r.dense_cval = r.dense_g >= 0 ? meta[r.dense_g].cval : 0.0;
     r.dense_slot = r.dense_g >= 0 ? meta[r.dense_g].dense : 0;
     const int g = r.dense_path ? r.dense_g : -1;
@@ -3772,7 +3777,7 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
         }
         // the fine z-sweep level's kernels read the patched right-hand side in place (k_zsweep_rb7 /
         // k_zresrestrict LRF) when B_g is one number
-        r.rhs_inplace = r.dense_path && r.dense_const && lv.zsweep && level + 1 < (int)h->levels.size() &&
+        r.rhs_inplace = r.dense_path && r.split_g >= 0 && lv.zsweep && level + 1 < (int)h->levels.size() &&
                         zres_lrf_capable(lv, h->levels[level + 1]);
         if (r.rhs_inplace) {
             std::vector<double> ez((size_t)2 * h->nchains, 0.0);

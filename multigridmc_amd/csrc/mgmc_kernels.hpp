@@ -136,21 +136,16 @@ __device__ __forceinline__ RngKey chain_key(const GibbsArg& G, int c) {
     return k;
 }
 
-// The right-hand side of a dense-column low-rank level read in place (LowRankDev::rhs_inplace): f is
-// patched in place on the local rows only (k_lr_patch / k_lr_restore_patch, the row lists), and the
-// sweep / residual kernel adds the chain's dense-only patch e = +/-(0.0 + B_g s_g) to f where the
-// vertex's bit in skip is clear -- k_lr_dense_rhs's y + e0 / y - e0, the latter as y + (-e0), the
-// same IEEE operation.  Boundary and padding positions carry the bit; their right-hand side is unused.
+// The right-hand side of a low-rank level with a split column g read in place (LowRankDev::
+// rhs_inplace): every interior row carries B_g = one number, so the patch of row i is
+// (f_i +/- e_loc,i) +/- e_g (lr_row_patch).  f is patched in place with the first term on the rows
+// with other columns (k_lr_patch / k_lr_restore_patch, deferring e_g) and the sweep / residual kernel
+// adds the chain's e = +/-(0.0 + B_g s_g) to every f it reads -- y - e_g taken as y + (-e_g), the same
+// IEEE operation.  (Boundary and padding positions get it too; their right-hand side is never used.)
 struct LRRhsArg {
-    const uint32_t* skip;  // null: f itself is the right-hand side
-    const double* e;       // e of chain c at e[c]
+    const double* e;  // e of chain c at e[c]; null: f itself is the right-hand side
 };
-__device__ __forceinline__ uint32_t lr_rhs_bits(const uint32_t* __restrict__ skip, long long p) {
-    return (skip[p >> 5] >> (p & 31)) & 3u;  // p even: the pair's two bits lie in one word
-}
-__device__ __forceinline__ double2 lr_rhs_pair(double2 f, uint32_t bits, double e) {
-    return make_double2((bits & 1) ? f.x : f.x + e, (bits & 2) ? f.y : f.y + e);
-}
+__device__ __forceinline__ double2 lr_rhs_pair(double2 f, double e) { return make_double2(f.x + e, f.y + e); }
 
 // ascending-column-order row sum  sum_k a_k x_k  starting from 0.0 (SYM: stencil_coef's fold)
 template <int DIM, int NPTS, bool SYM = false>

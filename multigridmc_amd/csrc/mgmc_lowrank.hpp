@@ -255,6 +255,31 @@ __global__ void __launch_bounds__(64) k_lr_totals(const LRColMeta* __restrict__ 
 //   mode 2: operator       y = y + B t
 enum { LR_PATCH_NOISE = 0, LR_PATCH_RESIDUAL = 1, LR_PATCH_APPLY = 2 };
 
+// The patch of one row of B: y +/- e, e = 0.0 + sum_k B_ik s_k over the row's columns in ascending k
+// (Eigen's sparse-times-dense order).  On a level with a split column g (LowRankDev::split_g: its one
+// dense column, every value one number -- the fine level's global average) the column is added last
+// and on its own: (y +/- e_loc) +/- e_g, e_loc = 0.0 + sum_{k != g} (applied only on a row with such
+// a k), e_g = 0.0 + B_ig s_g -- the same sum in another order (the oracle's MULTICOLOUR patch follows
+// it).  defer: e_g is left out, the consumer kernel adds it (LRRhsArg).
+__device__ __forceinline__ double lr_row_patch(double y, bool minus, uint64_t msk, const double* cf,
+                                               const double* s, int m, int g, bool defer) {
+    double e = 0.0;
+    bool any = false;
+    for (int k = 0; k < m; ++k)
+        if (k != g && ((msk >> k) & 1)) {
+            e = e + cf[k] * s[k];
+            any = true;
+        }
+    if (g < 0) return minus ? y - e : y + e;
+    double t = y;
+    if (any) t = minus ? t - e : t + e;
+    if (!defer && ((msk >> g) & 1)) {
+        const double eg = 0.0 + cf[g] * s[g];
+        t = minus ? t - eg : t + eg;
+    }
+    return t;
+}
+
 struct LRPatchArgs {
     int m, nrows;
     const long long* off;    // padded offsets of the rows of B
@@ -270,10 +295,10 @@ struct LRPatchArgs {
     int mode;
     long long cs;               // batched chains (blockIdx.z): y cs, save nrows, t m apart
     uint32_t chain0, seed_hi;   // chain c's Philox key: (key.k0, lo32(chain0 + c) ^ seed_hi)
-    // non-null (a dense-column level read in place, LRRhsArg): eout[c] = the dense-only patch of
-    // chain c, +/-(0.0 + bgc s_g) -- the term k_lr_dense_rhs adds on those rows
+    int split_g;                // the level's split column (lr_row_patch), -1: none (and LR_PATCH_APPLY)
+    // non-null (a level read in place, LRRhsArg): the rows defer e_g, and eout[c] = chain c's
+    // +/-(0.0 + bgc s_g), the term every row's consumer adds (bgc = B_g's one number)
     double* eout;
-    int g;
     double bgc;
 };
 
@@ -307,20 +332,16 @@ __global__ void __launch_bounds__(256) k_lr_patch(LRPatchArgs a) {
     }
     __syncthreads();
     if (a.eout && blockIdx.x == 0 && threadIdx.x == 0) {
-        const double e = 0.0 + a.bgc * s[a.g];
+        const double e = 0.0 + a.bgc * s[a.split_g];
         a.eout[batch_chain()] = a.mode == LR_PATCH_RESIDUAL ? -e : e;  // (y - e == y + (-e))
     }
     const int u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= a.nrows) return;
     const long long p = a.off[u];
-    const uint64_t msk = a.mask[u];
-    const double* cf = a.coef + (long long)u * a.m;
-    double e = 0.0;
-    for (int k = 0; k < a.m; ++k)
-        if ((msk >> k) & 1) e = e + cf[k] * s[k];
     const double y = a.y[p];
     if (a.mode != LR_PATCH_APPLY) a.save[u] = y;
-    a.y[p] = a.mode == LR_PATCH_RESIDUAL ? y - e : y + e;
+    a.y[p] = lr_row_patch(y, a.mode == LR_PATCH_RESIDUAL, a.mask[u], a.coef + (long long)u * a.m, s, a.m, a.split_g,
+                          a.eout != nullptr);
 }
 
 // ---- smoother fix x -= B_bar w on B_bar's rows; optionally restore f on the rows of B ----
@@ -379,8 +400,8 @@ struct LRJob {
     double* save;
     int restore;  // 1: f = save (+ noise)
     int noise;    // 1: + B Sigma^{-1/2} xi'
-    double* eout;  // non-null (noise, a dense-column level read in place): eout[c] = 0.0 + bgc s_g (k_lr_patch)
-    int g;
+    int split_g;   // the level's split column (lr_row_patch), -1: none
+    double* eout;  // non-null (noise, a level read in place): rows defer e_g, eout[c] = 0.0 + bgc s_g (k_lr_patch)
     double bgc;
 };
 
@@ -415,7 +436,7 @@ __global__ void __launch_bounds__(256) k_lr_restore_patch(LRRestorePatchArgs a) 
             if (2 * t + 1 < j.m) s[2 * t + 1] = j.sq[2 * t + 1] * z1;
         }
         __syncthreads();
-        if (j.eout && u == 0) j.eout[ch] = 0.0 + j.bgc * s[j.g];
+        if (j.eout && u == 0) j.eout[ch] = 0.0 + j.bgc * s[j.split_g];
     }
     if (u >= j.nrows) return;
     const long long p = j.off[u];
@@ -423,11 +444,6 @@ __global__ void __launch_bounds__(256) k_lr_restore_patch(LRRestorePatchArgs a) 
         j.f[p] = j.save[u];
         return;
     }
-    const uint64_t msk = j.mask[u];
-    const double* cf = j.coef + (long long)u * j.m;
-    double e = 0.0;
-    for (int k = 0; k < j.m; ++k)
-        if ((msk >> k) & 1) e = e + cf[k] * s[k];
     double y;
     if (j.restore) {
         y = j.save[u];
@@ -435,7 +451,7 @@ __global__ void __launch_bounds__(256) k_lr_restore_patch(LRRestorePatchArgs a) 
         y = j.f[p];
         j.save[u] = y;
     }
-    j.f[p] = y + e;
+    j.f[p] = lr_row_patch(y, false, j.mask[u], j.coef + (long long)u * j.m, s, j.m, j.split_g, j.eout != nullptr);
 }
 
 // ---- dense-column path: one dense column g of B (the global average measurement) ----
@@ -492,6 +508,7 @@ struct LRDenseArgs {
     const uint32_t* skip;
     const double* bg;         // B_g over the padded store, or null: every B_g entry is bgc
     double bgc;
+    int split_g;              // local rows: lr_row_patch's split column (-1: none, and LR_PATCH_APPLY)
 };
 
 // s[ch * m + k] = sq_k xi'_k of sweep `tag` for every chain (only k = g, g's pair, if !all)
@@ -532,15 +549,9 @@ __global__ void __launch_bounds__(LRD_NT) k_lr_dense_rhs(LRDenseArgs a) {
         const uint64_t msk = a.mask[u];
         const double* cf = a.coef + (long long)u * m;
         for (int ch = 0; ch < a.nch; ++ch) {
-            double e = 0.0, e2 = 0.0;
-            for (int k = 0; k < m; ++k)
-                if ((msk >> k) & 1) {
-                    e = e + cf[k] * s[ch * m + k];
-                    if (two) e2 = e2 + cf[k] * s2[ch * m + k];
-                }
             const double y = a.f[ch * a.cs + p];
-            a.out[ch * a.cs + p] = minus ? y - e : y + e;
-            if (two) a.out2[ch * a.cs + p] = y + e2;
+            a.out[ch * a.cs + p] = lr_row_patch(y, minus, msk, cf, s + ch * m, m, a.split_g, false);
+            if (two) a.out2[ch * a.cs + p] = lr_row_patch(y, false, msk, cf, s2 + ch * m, m, a.split_g, false);
         }
         return;
     }

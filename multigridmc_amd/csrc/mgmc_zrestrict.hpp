@@ -51,7 +51,7 @@ struct ZRestrictArgs {
 };
 
 // SYM: a fold level (reflection-symmetric 27-point stencil): the residual's sum is fold27's
-// LRF: a dense-column low-rank level whose right-hand side is read in place (a.lr, lr_rhs_pair)
+// LRF: a low-rank level whose right-hand side is read in place (a.lr: f + e, lr_rhs_pair)
 template <int NPTS, int CX, int CY, int NT, bool ZN = false, bool SYM = false, bool LRF = false>
 __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
     if (ZN && (int)blockIdx.x >= a.nblk_main) {  // the tail's noise (see ZRestrictArgs)
@@ -178,7 +178,6 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
     // per plane parity (the set is a compile-time choice: the plane loop runs in pairs)
     constexpr bool XPF2 = NPTS == 7 && tune::ZR7_XPF2 != 0;
     double2 pxb[XPF2 ? 2 : 1][NLX], pf[NLR];
-    uint32_t pfb[NLR];  // LRF: the local-row bits of the f pairs
     // the chunk stages x planes 2 K0 - 2 .. 2 K1 and f planes 2 K0 - 1 .. 2 K1 - 1: the last step's loads one
     // plane ahead reload those (never used) instead of fetching the next chunk's planes
     const int kx_last = 2 * K1, kf_last = 2 * K1 - 1;
@@ -202,16 +201,11 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
         const double* base = plane_ptr(a.f, k > kf_last ? kf_last : k);
 #pragma unroll
         for (int u = 0; u < NLR; ++u) pf[u] = *reinterpret_cast<const double2*>(base + roff[u]);
-        if constexpr (LRF) {
-            const long long pk = (long long)(k > kf_last ? kf_last : k) * Lf.sp;
-#pragma unroll
-            for (int u = 0; u < NLR; ++u) pfb[u] = lr_rhs_bits(a.lr.skip, pk + roff[u]);
-        }
     };
     // residual of fine plane k over the residual region (vertices outside the fine interior -> 0).
     // The two vertices of a pair advance together through the stencil terms, so their dependent
     // adds interleave; each chain still adds its terms in ascending column order from 0.0.
-    auto residual = [&](int k, const double2 (&fv)[NLR], const uint32_t (&fb)[NLR]) {
+    auto residual = [&](int k, const double2 (&fv)[NLR]) {
         const bool kin = k >= 1 && k <= Lf.nz - 1;
         const double* pl[3] = {xs + xslot(k - 1) * XPS, xs + xslot(k) * XPS, xs + xslot(k + 1) * XPS};
 #pragma unroll
@@ -268,7 +262,7 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
                     }
             }
             double2 f = fv[u];
-            if constexpr (LRF) f = lr_rhs_pair(f, fb[u], lre);
+            if constexpr (LRF) f = lr_rhs_pair(f, lre);
             rs[rlds[u]] = (kin && (rflag[u] & 1)) ? f.x - y0 : 0.0;
             rs[rlds[u] + RP] = (kin && (rflag[u] & 2)) ? f.y - y1 : 0.0;
         }
@@ -307,19 +301,15 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
     // by residual(k) before the second barrier.
     double acc[NCP], accn[NCP];
     double2 fcur[NLR];
-    uint32_t fbcur[NLR];
     // Bc: the register set of plane k + 1 (XPF2: (k + 1) & 1), which then takes x(k + 3)
     auto step = [&](int k, auto Bc) __attribute__((always_inline)) {
         deposit_x(k + 1, Bc);
 #pragma unroll
-        for (int u = 0; u < NLR; ++u) {
-            fcur[u] = pf[u];
-            if constexpr (LRF) fbcur[u] = pfb[u];
-        }
+        for (int u = 0; u < NLR; ++u) fcur[u] = pf[u];
         issue_x(XPF2 ? k + 3 : k + 2, Bc);
         issue_f(k + 1);
         __syncthreads();
-        residual(k, fcur, fbcur);
+        residual(k, fcur);
         __syncthreads();
     };
     // prologue: x planes 2K0-2, 2K0-1 in LDS, x(2K0) and f(2K0-1) in flight

@@ -69,7 +69,7 @@ struct ZItem {
 // v = fma(alpha w, x_c, v), selected when alpha is a power of two: alpha w x_c is then exact, so the
 // fma rounds once like the separate add and the bits are the same.
 // MINW: minimum waves per SIMD the register allocation must allow (1 = unconstrained)
-// LRF: a dense-column low-rank level whose right-hand side is read in place (a.lr, lr_rhs_pair)
+// LRF: a low-rank level whose right-hand side is read in place (a.lr: f + e, lr_rhs_pair)
 struct RunE0 {
     int value;
 };
@@ -347,12 +347,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         return *reinterpret_cast<const double2*>(
             plane_base(a.f, k > k1 ? k1 : (k < k0 - 1 ? k0 - 1 : k)) + foff);
     };
-    // LRF: the local-row bits of the same pair (0 otherwise)
-    auto load_fb = [&](int k) -> uint32_t {
-        if constexpr (!LRF) return 0u;
-        const int kc = k > k1 ? k1 : (k < k0 - 1 ? k0 - 1 : k);
-        return lr_rhs_bits(a.lr.skip, (long long)(kc < 0 ? 0 : (kc > L.nz ? L.nz : kc)) * L.sp + foff);
-    };
 
     // fma-chain stencil sum (ascending column order) at LDS offset o of plane k.  The fine FD
     // stencil is symmetric (launch_zsweep checks a[4]=a[22], a[10]=a[16], a[12]=a[14]), so four
@@ -423,8 +417,8 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         const int E0c_v = E0c.value;
         constexpr bool DN = decltype(DNc)::value;
         constexpr int dz = DN ? -1 : 1;
-        auto step = [&](int p, auto ODDc, double2& fcur, double2& fnxt, uint32_t& bcur, uint32_t& bnxt, double pk_in,
-                        double& pk_out) __attribute__((always_inline)) {
+        auto step = [&](int p, auto ODDc, double2& fcur, double2& fnxt, double pk_in, double& pk_out)
+                        __attribute__((always_inline)) {
             constexpr bool odd_step = decltype(ODDc)::value;
             const int e = odd_step ? 1 - E0c_v : E0c_v;  // first-colour element on plane p
             const int o1 = t.lds + e * WP, o2 = t.lds + (1 - e) * WP;
@@ -439,20 +433,16 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
             if constexpr (PF2) {
                 issue_x(p + 3, Bp{});  // (past the chunk: clamped planes, loaded and never used)
                 (void)fnxt;
-                (void)bnxt;
             } else {
                 issue_x(p + 2 * dz, Bp{});
-                if (active_wave) {
-                    fnxt = load_f(p + dz);
-                    if constexpr (LRF) bnxt = load_fb(p + dz);
-                }
+                if (active_wave) fnxt = load_f(p + dz);
             }
             __syncthreads();
             // first colour on plane p: c = fma(sd, z, f), x = fma(omega/diag, c - S, x); the second
             // colour's right-hand side of the pair, c' = fma(sd, z', f')
             if (interior_plane(p) && active_wave) {
                 double2 fv = fcur;
-                if constexpr (LRF) fv = lr_rhs_pair(fv, bcur, lre);
+                if constexpr (LRF) fv = lr_rhs_pair(fv, lre);
                 if (inf) {
                     const double res = row_sum(p, o1, e, xs[slot(p - 1) * PS + o1]);
                     const double crhs = fma(sd, e ? z.y : z.x, e ? fv.y : fv.x);
@@ -461,10 +451,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
                 }
                 pk_out = fma(sd, e ? z.x : z.y, e ? fv.x : fv.y);
             }
-            if constexpr (PF2) {  // this step's f is used up: the registers take f(p+2)
-                fcur = load_f(p + 2);
-                if constexpr (LRF) bcur = load_fb(p + 2);
-            }
+            if constexpr (PF2) fcur = load_f(p + 2);  // this step's f is used up: the registers take f(p+2)
             __syncthreads();
             // second colour on plane k = p-1 (DN: p+1; its element is e: the parity flips with the plane)
             const int k = p - dz;
@@ -496,30 +483,24 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
             if (active_wave && interior_plane(p + dz)) z = noise(p + dz);
         };
         double2 fA = make_double2(0.0, 0.0), fB = make_double2(0.0, 0.0);
-        uint32_t bA = 0, bB = 0;
         double pkA = 0.0, pkB = 0.0;
         const int pst = DN ? k1 : k0 - 1;  // first step's plane
         if constexpr (PF2) {
             fA = load_f(k0 - 1);
             fB = load_f(k0);
-            if constexpr (LRF) {
-                bA = load_fb(k0 - 1);
-                bB = load_fb(k0);
-            }
         } else if (active_wave) {
             fA = load_f(pst);
-            if constexpr (LRF) bA = load_fb(pst);
         }
         if (active_wave && interior_plane(pst)) z = noise(pst);
         if constexpr (DN) {
             for (int p = k1; p >= k0 - 1; p -= 2) {
-                step(p, std::integral_constant<bool, false>{}, fA, fB, bA, bB, pkB, pkA);
-                if (p - 1 >= k0 - 1) step(p - 1, std::integral_constant<bool, true>{}, fB, fA, bB, bA, pkA, pkB);
+                step(p, std::integral_constant<bool, false>{}, fA, fB, pkB, pkA);
+                if (p - 1 >= k0 - 1) step(p - 1, std::integral_constant<bool, true>{}, fB, fA, pkA, pkB);
             }
         } else {
             for (int p = k0 - 1; p <= k1; p += 2) {
-                step(p, std::integral_constant<bool, false>{}, fA, fB, bA, bB, pkB, pkA);
-                if (p + 1 <= k1) step(p + 1, std::integral_constant<bool, true>{}, fB, fA, bB, bA, pkA, pkB);
+                step(p, std::integral_constant<bool, false>{}, fA, fB, pkB, pkA);
+                if (p + 1 <= k1) step(p + 1, std::integral_constant<bool, true>{}, fB, fA, pkA, pkB);
             }
         }
     };

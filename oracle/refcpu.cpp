@@ -768,6 +768,7 @@ struct LowRank {
     std::vector<std::vector<std::pair<int64_t, double>>> cols;
     std::vector<char> dense;
     std::vector<double> sigma;
+    int split = -1;  // MULTICOLOUR patch order: the split column (lr_patch_mc), -1 none
 };
 
 struct Level {
@@ -914,6 +915,35 @@ static void lr_expand(const Level& L, const double* s, double* e) {
     for (int k = 0; k < L.lr.m; ++k)
         for (const auto& en : L.lr.cols[k]) e[en.first] += en.second * s[k];
 }
+// out = f +/- B s in the device's order (mgmc_lowrank.hpp lr_row_patch, MULTICOLOUR): f_i +/- e_i,
+// e_i = 0.0 + sum_k B_ik s_k in ascending k -- or, on a level with a split column g (lr.split), the
+// column added last on its own: (f_i +/- e_loc,i) +/- e_g,i, e_loc summed over k != g and applied on
+// the rows with such a k, e_g,i = 0.0 + B_ig s_g.  The same sum in another order as the reference's
+// c += B xi (sor_sampler.cc:48-56) and its residual (FAITHFUL keeps the reference's).
+static void lr_patch_mc(const Level& L, const double* s, const double* f, double* out, bool minus) {
+    const int64_t n = L.A.nrow;
+    const int g = L.lr.split;
+    std::vector<double> e(n, 0.0);
+    std::vector<char> any(n, 0);
+    for (int k = 0; k < L.lr.m; ++k) {
+        if (k == g) continue;
+        for (const auto& en : L.lr.cols[k]) {
+            e[en.first] += en.second * s[k];
+            any[en.first] = 1;
+        }
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        if (g < 0) {
+            out[i] = minus ? f[i] - e[i] : f[i] + e[i];
+            continue;
+        }
+        double t = f[i];
+        if (any[i]) t = minus ? t - e[i] : t + e[i];
+        const double eg = 0.0 + L.lr.cols[g][i].second * s[g];  // (a dense column lists every row)
+        out[i] = minus ? t - eg : t + eg;
+    }
+}
+
 // y = A x + B (Sigma^{-1} B^T x)  (linear_operator.hh:66-76); t_k in lr_dot order with the
 // Sigma^{-1}-scaled column values of Sigma_inv_BT (measured_operator.cc:48)
 static void posterior_apply(const Level& L, const double* x, double* y, Mode mode) {
@@ -983,8 +1013,8 @@ static void spmv_level(const Level& L, const double* x, double* y, Mode mode) {
 }
 
 // r = f - (A x + B Sigma^{-1} B^T x).  FAITHFUL: the reference's apply then subtract.  MULTICOLOUR
-// (device order): the low-rank term is folded into f first, r = (f - g) - A x, so the device's
-// residual kernels run unchanged on a patched f.
+// (device order): the low-rank term is folded into f first (lr_patch_mc), r = (f - g) - A x, so the
+// device's residual kernels run unchanged on a patched f.
 // MULTICOLOUR on a fold level: A x by folded_row_sum (the device's residual kernels).
 static void posterior_residual(const Level& L, const double* f, const double* x, double* r, Mode mode) {
     const int64_t n = L.A.nrow;
@@ -996,11 +1026,11 @@ static void posterior_residual(const Level& L, const double* f, const double* x,
         par_for(n, [&](int64_t q) { r[q] = f[q] - r[q]; });
         return;
     }
-    std::vector<double> t(L.lr.m), g(n);
+    std::vector<double> t(L.lr.m), fp(n);
     for (int k = 0; k < L.lr.m; ++k) t[k] = lr_dot(L, k, 1.0 / L.lr.sigma[k], x, mode);
-    lr_expand(L, t.data(), g.data());
+    lr_patch_mc(L, t.data(), f, fp.data(), true);
     spmv_level(L, x, r, mode);
-    for (int64_t q = 0; q < n; ++q) r[q] = (f[q] - g[q]) - r[q];
+    for (int64_t q = 0; q < n; ++q) r[q] = fp[q] - r[q];
 }
 
 // inverse of a small dense matrix (row-major m x m): Gauss-Jordan with partial pivoting
@@ -1178,15 +1208,14 @@ struct SORSampler : Sampler {
                 std::vector<double> feff;
                 const double* fe = f;
                 if (L->lr.m > 0) {
-                    feff.assign(f, f + n);
-                    std::vector<double> sv(L->lr.m), e(n);
+                    feff.resize(n);
+                    std::vector<double> sv(L->lr.m);
                     for (int k = 0; k < L->lr.m; ++k) {
                         double z0, z1;
                         philox_normals(ctx->seed, ctx->chain, LR_PAIR0 + (uint32_t)(k >> 1), tag, ctx->sample, z0, z1);
                         sv[k] = sqrt(1.0 / L->lr.sigma[k]) * ((k & 1) ? z1 : z0);
                     }
-                    lr_expand(*L, sv.data(), e.data());
-                    for (int64_t ell = 0; ell < n; ++ell) feff[ell] = f[ell] + e[ell];
+                    lr_patch_mc(*L, sv.data(), f, feff.data(), false);
                     fe = feff.data();
                 }
                 const uint64_t sample = ctx->sample;
@@ -1807,6 +1836,19 @@ void orc_set_lowrank(orc_handle* h, int m, const int64_t* colptr, const int64_t*
                 for (int64_t i = 0; i < n; ++i)
                     if (L.lr.dense[k] || coarse[i] != 0.0) L.lr.cols[k].push_back({i, coarse[i]});
             }
+        }
+        // the split column of the MULTICOLOUR patch (lr_patch_mc; the device's LowRankDev::split_g):
+        // the level's only dense column over more than LR_BLK rows, when its values are one number
+        int ndense = 0, g = -1;
+        for (int k = 0; k < m; ++k)
+            if (L.lr.dense[k] && n > LR_BLK) {
+                ++ndense;
+                g = k;
+            }
+        if (ndense == 1 && !L.lr.cols[g].empty()) {
+            bool same = true;
+            for (const auto& e : L.lr.cols[g]) same = same && memcmp(&e.second, &L.lr.cols[g][0].second, 8) == 0;
+            if (same) L.lr.split = g;
         }
     }
     if (mg.p.coarse_solver == 1) mg.coarse.reset(new DenseCholeskySampler(&h->ctx, mg.levels.back().get()));
