@@ -622,12 +622,21 @@ struct LRDenseUpdateArgs {
 __global__ void __launch_bounds__(LRD_NT) k_lr_dense_update(LRDenseUpdateArgs a) {
     __shared__ double ws[LR_MAX_CH * LR_MAX_M];
     __shared__ double mg[LR_MAX_M];
-    __shared__ double yt[128];
+    __shared__ double dt[LR_MAX_CH * 128];  // ykey: the fix of every key and chain, sum_k B_bar_ik w_k
     const int m = a.m;
     for (int q = threadIdx.x; q < a.nch * m; q += LRD_NT) ws[q] = a.w[q];
     for (int q = threadIdx.x; q < m; q += LRD_NT) mg[q] = a.minv_g[q];
-    if (a.ykey)
-        for (int q = threadIdx.x; q < 128; q += LRD_NT) yt[q] = a.ytab[q];
+    __syncthreads();
+    if (a.ykey && (int)blockIdx.x >= a.nbs)
+        // a dense-only row's fix depends on its Y_g (one of the table's values) and the chain alone:
+        // the per-vertex loop below, computed once per key
+        for (int q = threadIdx.x; q < a.nch * 128; q += LRD_NT) {
+            const int ch = q >> 7;
+            const double y = a.ytab[q & 127];
+            double acc = 0.0;
+            for (int k = 0; k < m; ++k) acc = fma(fma(y, mg[k], 0.0), ws[ch * m + k], acc);
+            dt[q] = acc;
+        }
     __syncthreads();
     if ((int)blockIdx.x < a.nbs) {
         const int u = blockIdx.x * LRD_NT + threadIdx.x;
@@ -648,14 +657,30 @@ __global__ void __launch_bounds__(LRD_NT) k_lr_dense_update(LRDenseUpdateArgs a)
     long long p[LRD_PER];
     bool ok[LRD_PER][2];
     lrd_pairs(a.skip, a.n, a.nbs, p, ok);
-    double2 yv[LRD_PER];
     if (a.ykey) {
+        uint16_t kk[LRD_PER];
 #pragma unroll
-        for (int r = 0; r < LRD_PER; ++r) {
-            const uint16_t kk = *(const uint16_t*)(a.ykey + p[r]);  // p even: both keys in one load
-            yv[r] = make_double2(yt[kk & 0xff], yt[kk >> 8]);
+        for (int r = 0; r < LRD_PER; ++r) kk[r] = *(const uint16_t*)(a.ykey + p[r]);  // p even: both keys in one load
+        for (int ch = 0; ch < a.nch; ++ch) {
+            double* xc = a.x + ch * a.cs;
+            const double* d = dt + ch * 128;
+            double2 xv[LRD_PER];
+#pragma unroll
+            for (int r = 0; r < LRD_PER; ++r) xv[r] = *(const double2*)(xc + p[r]);
+#pragma unroll
+            for (int r = 0; r < LRD_PER; ++r) {
+                double2 o;
+                o.x = xv[r].x - d[kk[r] & 0xff];
+                o.y = xv[r].y - d[kk[r] >> 8];
+                if (ok[r][0] && ok[r][1]) *(double2*)(xc + p[r]) = o;
+                else if (ok[r][0]) xc[p[r]] = o.x;
+                else if (ok[r][1]) xc[p[r] + 1] = o.y;
+            }
         }
-    } else {
+        return;
+    }
+    double2 yv[LRD_PER];
+    {
 #pragma unroll
         for (int r = 0; r < LRD_PER; ++r) yv[r] = *(const double2*)(a.yg + p[r]);
     }

@@ -60,9 +60,9 @@ constexpr int LR_STAGED_MAX_WAVES = 512;
 // entries per lane whose loads k_lr_partials issues together
 constexpr int LR_PART_U = 8;
 // chains per wavefront of k_lr_partials (batched chains: a column value loaded once for them)
-constexpr int LR_PART_CH = 4;
+constexpr int LR_PART_CH = 1;
 // 16-byte pairs per thread of the dense-column kernels (k_lr_dense_rhs / _update)
-constexpr int LR_DENSE_PER = 2;
+constexpr int LR_DENSE_PER = 8;
 
 }  // namespace tune
 }  // namespace mgmc
