@@ -753,8 +753,25 @@ __device__ __forceinline__ void lr_small_chain(LRSmallArgs& a) {
 __device__ __forceinline__ double lr_wave_dot(const LRColMeta& c, const long long* __restrict__ ent_off,
                                               const double* __restrict__ ent_val, double sc,
                                               const double* __restrict__ v, int lane) {
+    // the lane's entries in order, U at a time with their loads issued together (a dense column of
+    // a small level has up to 64 per lane: that many dependent round trips otherwise)
+    constexpr int U = 8;
     double acc = 0.0;
-    for (long long e = lane; e < c.n; e += 64) {
+    long long e = lane;
+    for (; e + (U - 1) * 64 < c.n; e += U * 64) {
+        long long o[U];
+        double bv[U], xv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            o[u] = ent_off[c.ent0 + e + u * 64];
+            bv[u] = ent_val[c.ent0 + e + u * 64];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[u] = v[o[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = acc + (sc * bv[u]) * xv[u];
+    }
+    for (; e < c.n; e += 64) {
         const long long q = c.ent0 + e;
         acc = acc + (sc * ent_val[q]) * v[ent_off[q]];
     }
