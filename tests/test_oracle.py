@@ -371,3 +371,35 @@ def test_folded_residual_matches_reference_order_to_rounding(shape, nlevel, fold
             assert O.residual_tolerance_ok(b, a, fa.csr_matrix(level), f, x, lambda v: fa.restrict(level, v))
         else:
             assert np.array_equal(a, b)
+
+
+# ---------------------------------------------------------------- split column (constant dense column)
+@pytest.mark.parametrize("shape,split", [((24, 24, 24), True), ((128, 128), True), ((12, 12, 12), False)])
+def test_split_column_patch_matches_reference_order_to_rounding(shape, split):
+    """A posterior level whose one dense column is a single number (the fine level's global average,
+    measured_operator.cc:31-45) adds that column's term of B t last and on its own in the MULTICOLOUR
+    oracle (lr_patch_mc, the device's lr_row_patch: mgmc_lowrank.hpp), which lets the device add it
+    inside the sweep / residual kernels.  The posterior residual + restriction still equals the
+    reference's order (FAITHFUL) to rounding -- 1e-14 of R(|f| + |A||x| + |B| |t|) -- and the split is
+    taken only above LR_BLK = 4096 unknowns (12^3 has 1331: the column stays an entry list)."""
+    import multigridmc_amd as mg
+    p = MultigridParameters(nlevel=2)
+    lat = mg.Lattice(*shape)
+    op = mg.synthetic_posterior(mg.ShiftedLaplaceFDOperator(lat, 25.0), 4, 0.0, True)
+    lr = op.get_B()
+    fa = O.Oracle.fd(shape, p, 25.0, mode=O.FAITHFUL)
+    mc = O.Oracle.fd(shape, p, 25.0, mode=O.MULTICOLOUR)
+    fa.set_lowrank(lr)
+    mc.set_lowrank(lr)
+    rng = np.random.default_rng(7)
+    n = fa.ndof(0)
+    assert (n > 4096) == split
+    x, f = rng.standard_normal(n), rng.standard_normal(n)
+    a, b = fa.residual_restrict(0, f, x), mc.residual_restrict(0, f, x)
+    # scale of every term: |f| + |A||x| + |B| |Sigma^-1| |B^T| |x|
+    import scipy.sparse as sp
+    B = sp.csc_matrix((lr.vals, lr.rows, lr.colptr), shape=(n, lr.m))
+    A = fa.csr_matrix(0)
+    scale = np.abs(f) + abs(A) @ np.abs(x) + abs(B) @ ((abs(B).T @ np.abs(x)) / lr.sigma)
+    R = lambda v: fa.restrict(0, v)
+    assert np.all(np.abs(a - b) <= 1e-14 * R(scale) + 1e-300)
