@@ -176,6 +176,7 @@ struct LowRankDev {
     int nblk = 0;                 // dot-product blocks over all columns
     LRColMeta* meta = nullptr;
     int* blk_col = nullptr;
+    LRBlock* blk = nullptr;        // per dot-product block: column, range, value source, scales
     long long* ent_off = nullptr;  // sparse column entries: padded offsets, values
     double* ent_val = nullptr;
     double* dense_val = nullptr;   // dense columns: padded value arrays, L.nstore apart
@@ -1073,17 +1074,18 @@ void launch_pack(const Level& lv, const double* lex, double* pad, bool pack, hip
 // (batched chains: v cs apart; the partials nblk and w m apart per chain)
 void lr_dots(const Level& lv, const double* v, const double* sc, hipStream_t s, int nch = 1) {
     const LowRankDev& r = lv.lr;
+    const int sel = sc == r.sc_one ? 0 : 1;  // (the two scale vectors, LRBlock::sc; callers pass one of them)
     // few wavefronts (coarse levels): the staged kernel (the loads of a block in flight at once);
     // many: one wavefront per block, column values read once per group of chains
     const long long waves = (long long)r.nblk * ((nch + LRP_CH - 1) / LRP_CH);
     if (r.nblk > 0 && waves < tune::LR_STAGED_MAX_WAVES)
-        hipLaunchKernelGGL(k_lr_partials_staged, dim3(r.nblk, nch), dim3(LRS_NT), 0, s, lv.L, (const LRColMeta*)r.meta,
-                           (const int*)r.blk_col, (const long long*)r.ent_off, (const double*)r.ent_val,
-                           (const double*)r.dense_val, sc, v, r.part, (long long)lv.L.nstore, r.nblk);
+        hipLaunchKernelGGL(k_lr_partials_staged, dim3(r.nblk, nch), dim3(LRS_NT), 0, s, lv.L, (const LRBlock*)r.blk, sel,
+                           (const long long*)r.ent_off, (const double*)r.ent_val, (const double*)r.dense_val, v,
+                           r.part, (long long)lv.L.nstore, r.nblk);
     else if (r.nblk > 0)
         hipLaunchKernelGGL(k_lr_partials, dim3(r.nblk, (nch + LRP_CH - 1) / LRP_CH), dim3(64), 0, s, lv.L,
-                           (const LRColMeta*)r.meta, (const int*)r.blk_col, (const long long*)r.ent_off,
-                           (const double*)r.ent_val, (const double*)r.dense_val, sc, v, r.part,
+                           (const LRBlock*)r.blk, sel, (const long long*)r.ent_off,
+                           (const double*)r.ent_val, (const double*)r.dense_val, v, r.part,
                            (long long)lv.L.nstore, r.nblk, nch);
     hipLaunchKernelGGL(k_lr_totals, dim3(r.m, 1, nch), dim3(64), 0, s, (const LRColMeta*)r.meta, (const double*)r.part,
                        r.w, r.nblk, r.m);
@@ -3722,6 +3724,21 @@ int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols,
         }
     }
     r.nblk = (int)blk_col.size();
+    std::vector<LRBlock> blocks(blk_col.size());
+    for (int k = 0; k < m; ++k)
+        for (int b = 0; b < meta[k].nblk; ++b) {
+            LRBlock& B = blocks[(size_t)meta[k].blk0 + b];
+            B.e0 = (long long)b * LR_BLK;
+            B.cnt = (int)std::min<long long>(LR_BLK, meta[k].n - B.e0);
+            B.ent0 = meta[k].dense >= 0 ? 0 : meta[k].ent0 + B.e0;
+            B.k = k;
+            B.dense = meta[k].dense;
+            B.cflag = meta[k].cflag;
+            B.cval = meta[k].cval;
+            B.sc[0] = 1.0;
+            B.sc[1] = 1.0 / sigma[k];  // (the sc_inv values below)
+        }
+    if ((rc = lr_to_device(h, r, &r.blk, blocks))) return rc;
     if ((rc = lr_to_device(h, r, &r.meta, meta)) || (rc = lr_to_device(h, r, &r.blk_col, blk_col)) ||
         (rc = lr_to_device(h, r, &r.ent_off, ent_off)) || (rc = lr_to_device(h, r, &r.ent_val, ent_val)) ||
         (rc = lr_to_device(h, r, &r.t_ent_off, t_ent_off)))

@@ -56,6 +56,44 @@ struct LRColMeta {
     double cval;     // (the global average on the fine level: the cell volume, measured_operator.cc:31-45)
 };
 
+// Everything a dot-product block needs in one load (the kernels used to chase blk_col -> meta -> sc,
+// three dependent round trips before the first entry load; built by lr_setup_level)
+struct LRBlock {
+    long long e0;    // first entry of the block in its column
+    long long ent0;  // entry-list columns: the block's first entry in ent_off / ent_val
+    int k;           // column
+    int cnt;         // entries (<= LR_BLK)
+    int dense;       // value array of a dense column, or -1
+    int cflag;       // dense column whose every value is cval
+    double cval;
+    double sc[2];    // the column's dot scales: 1 (B^T x), 1/Sigma_k (Sigma^{-1} B^T x)
+};
+
+// padded offset of interior vertex e (reference order, x fastest) of a level: e = (k-1) nyi nxi +
+// (j-1) nxi + (i-1) by floating-point reciprocals with one correction step (exact for e < 2^51)
+__device__ __forceinline__ long long lr_entry_pos(const Layout& L, long long e, double rnx, double rny) {
+    const int nxi = L.nx - 1, nyi = L.ny - 1;
+    long long r = (long long)((double)e * rnx);
+    long long i = e - r * nxi;
+    if (i < 0) {
+        --r;
+        i += nxi;
+    } else if (i >= nxi) {
+        ++r;
+        i -= nxi;
+    }
+    long long kk = (long long)((double)r * rny);
+    long long j = r - kk * nyi;
+    if (j < 0) {
+        --kk;
+        j += nyi;
+    } else if (j >= nyi) {
+        ++kk;
+        j -= nyi;
+    }
+    return L.at((int)i + 1, (int)j + 1, L.dim == 3 ? (int)kk + 1 : 0);
+}
+
 // ---- dot products, stage 1: one wavefront per block of LR_BLK entries ----
 // A dense column lists every vertex in reference order: lane l's entries e, e + 64, ... are walked
 // with incremental (i, j, k) (no 64-bit division per entry).  The lane's sum runs in entry order;
@@ -64,33 +102,29 @@ struct LRColMeta {
 // Batched chains: blockIdx.y = a group of LRP_CH chains; the column value of an entry is loaded
 // once for the group (v cs apart, the partials nblk apart per chain).
 constexpr int LRP_U = tune::LR_PART_U, LRP_CH = tune::LR_PART_CH;
-__global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRColMeta* __restrict__ meta,
-                                                     const int* __restrict__ blk_col,
+__global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRBlock* __restrict__ blk, int sel,
                                                      const long long* __restrict__ ent_off,
                                                      const double* __restrict__ ent_val,
                                                      const double* __restrict__ dense_val,
-                                                     const double* __restrict__ sc, const double* __restrict__ v,
+                                                     const double* __restrict__ v,
                                                      double* __restrict__ part, long long cs, int nblk, int nch) {
     const int b = blockIdx.x;
     const int ch0 = blockIdx.y * LRP_CH;
     const int nc = min(LRP_CH, nch - ch0);
     const int lane = threadIdx.x;
-    const int k = blk_col[b];
-    const LRColMeta c = meta[k];
-    const long long e0 = (long long)(b - c.blk0) * LR_BLK;
-    const long long end = min(c.n, e0 + LR_BLK);
-    const double s = sc[k];
+    const LRBlock c = blk[b];
+    const double s = sel ? c.sc[1] : c.sc[0];  // (a static index: no private-memory copy of c)
     const double* vc = v + ch0 * cs;
-    const long long e1 = e0 + lane;
-    const int cnt = e1 < end ? (int)((end - e1 + 63) / 64) : 0;  // entries of this lane
+    const long long e1 = c.e0 + lane;
+    const int cnt = lane < c.cnt ? (c.cnt - lane + 63) / 64 : 0;  // entries of this lane
     double acc[LRP_CH];
 #pragma unroll
     for (int q = 0; q < LRP_CH; ++q) acc[q] = 0.0;
     if (c.dense >= 0) {
         const double* dv = dense_val + (long long)c.dense * L.nstore;
         const int nxi = L.nx - 1, nyi = L.ny - 1;
-        int i = (int)(e1 % nxi) + 1;
         const long long r = e1 / nxi;
+        int i = (int)(e1 - r * nxi) + 1;
         int j = (int)(r % nyi) + 1;
         int kk = L.dim == 3 ? (int)(r / nyi) + 1 : 0;
         for (int base = 0; base < cnt; base += LRP_U) {
@@ -123,7 +157,7 @@ __global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRColMeta* _
                     if (q < nc && base + u < cnt) acc[q] = acc[q] + (s * a[u]) * x[q][u];
         }
     } else {
-        const long long q0 = c.ent0 + e1;
+        const long long q0 = c.ent0 + lane;
         for (int base = 0; base < cnt; base += LRP_U) {
             double a[LRP_U], x[LRP_CH][LRP_U];
 #pragma unroll
@@ -158,45 +192,31 @@ __global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRColMeta* _
 // lane l of the first wavefront adds its entries l, l+64, ... in entry order and the butterfly
 // follows: the single-wavefront kernel's sums, bit for bit.  One chain per blockIdx.y.
 constexpr int LRS_NT = 256;
-__global__ void __launch_bounds__(LRS_NT) k_lr_partials_staged(Layout L, const LRColMeta* __restrict__ meta,
-                                                               const int* __restrict__ blk_col,
+__global__ void __launch_bounds__(LRS_NT) k_lr_partials_staged(Layout L, const LRBlock* __restrict__ blk, int sel,
                                                                const long long* __restrict__ ent_off,
                                                                const double* __restrict__ ent_val,
                                                                const double* __restrict__ dense_val,
-                                                               const double* __restrict__ sc,
                                                                const double* __restrict__ v, double* __restrict__ part,
                                                                long long cs, int nblk) {
     __shared__ double prod[LR_BLK];
     const int b = blockIdx.x;
     const int ch = blockIdx.y;
     const int tid = threadIdx.x;
-    const int k = blk_col[b];
-    const LRColMeta c = meta[k];
-    const long long e0 = (long long)(b - c.blk0) * LR_BLK;
-    const int cnt = (int)min((long long)LR_BLK, c.n - e0);  // entries of this block
-    const double s = sc[k];
+    const LRBlock c = blk[b];
+    const int cnt = c.cnt;  // entries of this block
+    const double s = sel ? c.sc[1] : c.sc[0];  // (a static index: no private-memory copy of c)
     const double* vc = v + ch * cs;
     constexpr int PER = LR_BLK / LRS_NT;
     if (c.dense >= 0) {
         const double* dv = dense_val + (long long)c.dense * L.nstore;
-        const int nxi = L.nx - 1, nyi = L.ny - 1;
-        const long long e1 = e0 + tid;
-        int i = (int)(e1 % nxi) + 1;
-        const long long r = e1 / nxi;
-        int j = (int)(r % nyi) + 1;
-        int kk = L.dim == 3 ? (int)(r / nyi) + 1 : 0;
+        // every entry's vertex directly (the 256-entry carry walked up to 8 rows per step on the small
+        // levels); positions past the column's end are clamped to its first entry, never stored
+        const double rnx = 1.0 / (double)(L.nx - 1), rny = 1.0 / (double)(L.ny - 1);
         long long p[PER];
 #pragma unroll
         for (int t = 0; t < PER; ++t) {
-            p[t] = L.at(i, j, kk);
-            i += LRS_NT;  // advance by 256 entries (carry repeatedly)
-            while (i > nxi) {
-                i -= nxi;
-                if (++j > nyi) {
-                    j = 1;
-                    ++kk;
-                }
-            }
+            const int e = tid + t * LRS_NT;
+            p[t] = lr_entry_pos(L, c.e0 + (e < cnt ? e : 0), rnx, rny);
         }
 #pragma unroll
         for (int t = 0; t < PER; ++t) {
@@ -208,15 +228,24 @@ __global__ void __launch_bounds__(LRS_NT) k_lr_partials_staged(Layout L, const L
         for (int t = 0; t < PER; ++t) {
             const int e = tid + t * LRS_NT;
             if (e < cnt) {
-                const long long q = c.ent0 + e0 + e;
+                const long long q = c.ent0 + e;
                 prod[e] = (s * ent_val[q]) * vc[ent_off[q]];
             }
         }
     }
     __syncthreads();
     if (tid >= 64) return;
+    // lane l: entries l, l + 64, ... in order, their LDS reads issued 8 at a time
     double acc = 0.0;
-    for (int e = tid; e < cnt; e += 64) acc = acc + prod[e];
+    int e = tid;
+    for (; e + 7 * 64 < cnt; e += 8 * 64) {
+        double t8[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t8[u] = prod[e + u * 64];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = acc + t8[u];
+    }
+    for (; e < cnt; e += 64) acc = acc + prod[e];
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
     if (tid == 0) part[(long long)ch * nblk + b] = acc;
