@@ -2903,6 +2903,11 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
     std::string text = "sweep=" + sweep;
     if (!post.empty()) text += ";post_sweep=" + post;
     if (!res.empty()) text += ";residual_restrict=" + res;
+    // the low-rank path of a posterior level (mgmc_lowrank.hpp; rhs_inplace: the sweeps and the
+    // residual above run their LRF instances, f + e read in place)
+    if (lv.lr.m > 0)
+        text += std::string(";lowrank=") + (lv.lr.rhs_inplace ? "dense,rhs_inplace" : lv.lr.dense_path ? "dense"
+                                             : lv.lr.small ? "small" : "rows");
     snprintf(out, n, "%s", text.c_str());
     return MGMC_OK;
 }

@@ -598,7 +598,8 @@ class MultigridMCSampler:
     # -- component operations (reference layout host vectors) --
     def level_kernels(self, level: int) -> dict:
         """The kernels the handle runs on a level (mgmc_level_kernels): {"sweep": ..., "post_sweep": ...,
-        "residual_restrict": ...}"""
+        "residual_restrict": ..., "lowrank": ...} ("lowrank" on posterior levels: "small", "rows",
+        "dense" or "dense,rhs_inplace")"""
         buf = ctypes.create_string_buffer(512)
         self._chk(self.lib.mgmc_level_kernels(self.handle, int(level), buf, 512))
         return dict(kv.split("=", 1) for kv in buf.value.decode().split(";"))

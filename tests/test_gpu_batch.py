@@ -22,7 +22,8 @@ CHAIN0 = 11
 PRIOR = ["3d128_zsweep", "3d_aniso_zsweep_ssor", "3d_zres27", "3d64_4lvl", "2d64_template_W", "2d_aniso_ssor",
          "2d256_global_coarse", "2d64_chol_W", "3d32_chol_ssor", "3d8_1lvl", "2d_qr_aniso_ssor_W"]
 POSTERIOR = ["2d32_point_global", "3d32_ball_global", "3d128_zsweep_points", "3d_aniso_zres_points",
-             "2d32_point_global_chol", "3d32_points_tail_W", "2d128_points_tail", "3d_jsweep_points_ssor"]
+             "2d32_point_global_chol", "3d32_points_tail_W", "2d128_points_tail", "3d_jsweep_points_ssor",
+             "3d128_global_inplace_W"]
 
 
 def _prior(name, nchains=1, chain=0):

@@ -35,6 +35,10 @@ CONFIGS = {
     "2d128_point_global_W": ((128, 128), dict(nlevel=4, cycle=2), (0.0, 4, True)),
     # j-marching half-sweeps on level 1 (128-pair rows) with the low-rank patch / fix around them
     "3d_jsweep_points_ssor": ((512, 24, 20), dict(nlevel=3, smoother="SSOR"), (0.0, 5, False)),
+    # the fine z-sweep level with the constant global column: right-hand side read in place, the
+    # column's term split off (LowRankDev::rhs_inplace, lr_row_patch); two pre- / post-sweeps, W-cycle
+    "3d128_global_inplace_W": ((128, 128, 128), dict(nlevel=3, cycle=2, npresmooth=2, npostsmooth=2),
+                               (0.0, 5, True)),
 }
 TAIL_CONFIGS = ["2d64_ball_ssor_W", "3d32_points_tail_W", "3d48_ball_tail_ssor", "2d128_points_tail"]
 
@@ -83,6 +87,9 @@ def test_lowrank_components_bitwise(hip_device, name):
 @pytest.mark.parametrize("name", list(CONFIGS))
 def test_lowrank_cycles_bitwise(hip_device, name):
     s, mc, p, lat, op = make(name)
+    if name == "3d128_global_inplace_W":  # the path this configuration is here for
+        assert s.level_kernels(0)["lowrank"] == "dense,rhs_inplace"
+        assert s.level_kernels(1)["lowrank"] == "dense"
     rng = np.random.default_rng(11)
     f = rng.standard_normal(lat.Nvertex)
     x_dev = np.zeros(lat.Nvertex)
@@ -179,7 +186,8 @@ def test_posterior_statistics_vs_exact_covariance(hip_device, shape, kw, glob, n
 @pytest.mark.parametrize("name,paths", [(n, "tail") for n in TAIL_CONFIGS] +
                          [(n, q) for n in ("3d32_points_tail_W", "2d32_point_global", "3d_aniso_zres_points")
                           for q in ("lr_small", "lr_merge", "lr_prefetch", "lr_small,lr_merge,tail")] +
-                         [(n, "lr_dense") for n in ("2d128_point_global_W", "3d32_ball_global")])
+                         [(n, "lr_dense") for n in ("2d128_point_global_W", "3d32_ball_global")] +
+                         [("3d128_global_inplace_W", q) for q in ("lr_merge", "lr_dense")])
 def test_lowrank_paths_match(hip_device, name, paths, monkeypatch):
     """Low-rank kernel paths switched off (MGMC_DISABLE): tail = the coarse levels' sub-cycle as
     separate launches instead of k_tail (low-rank patches, fix and residual in LDS); lr_small = the
