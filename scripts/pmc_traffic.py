@@ -14,7 +14,9 @@ import re
 import subprocess
 import sys
 
-KERNEL = re.compile(r"k_zsweep_rb7<\s*(\d+),\s*(\d+),\s*(\d+),\s*(\d+),\s*(\d+)\s*>")
+# <XP, TY, NT, PROLONG, MINW[, LRF]>: the prior's instances (LRF = false, the low-rank posterior's in-place
+# right-hand side: not part of the bench)
+KERNEL = re.compile(r"k_zsweep_rb7<\s*(\d+),\s*(\d+),\s*(\d+),\s*(\d+),\s*(\d+)\s*(?:,\s*false\s*)?>")
 
 
 def per_launch(path, post):
