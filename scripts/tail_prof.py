@@ -1,5 +1,5 @@
 """Phase times of k_tail (timing build MGMC_TAIL_PROF: CXXDEFS=-DMGMC_TAIL_PROF VARIANTS="tprof=-" bash
-scripts/build_exp.sh; MGMC_LIBRARY=build/libmgmc_tprof.so python scripts/tail_prof.py [n] [nlevel]).
+scripts/build_exp.sh; MGMC_LIBRARY=build/libmgmc_tprof.so python scripts/tail_prof.py [n] [nlevel] [npoints]).
 Runs a few prior V-cycles and prints the wall-clock time of every phase of the first tail: the LDS
 fill from HBM, each op's right-hand sides (sweeps) and the rest of the op, the store."""
 import ctypes
@@ -11,8 +11,12 @@ import multigridmc_amd as mg  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 nl = int(sys.argv[2]) if len(sys.argv) > 2 else 7
+npost = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # > 0: config 5's posterior with that many points
 lat = mg.Lattice3d(n, n, n)
-s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), 1, mg.MultigridParameters(nlevel=nl))
+op = mg.ShiftedLaplaceFDOperator(lat, 25.0)
+if npost > 0:
+    op = mg.synthetic_posterior(op, npost, 0.0, False)
+s = mg.MultigridMCSampler(op, 1, mg.MultigridParameters(nlevel=nl))
 lib = mg.load_library()
 f = lib.mgmc_debug_tail_profile
 f.restype = ctypes.c_int
