@@ -936,7 +936,7 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
         const bool small = lc.L.nx < tune::ZR_SMALL_NX;
         if (skip_xc) xc = nullptr;
         if (lr) {  // (zres_lrf_capable)
-            if ((long long)((lc.L.nx + 62) / 64) * ((lc.L.ny + 6) / 8) * (lc.L.nz - 1) >= 16 * 1024)
+            if ((long long)((lc.L.nx + 62) / 64) * ((lc.L.ny + 6) / 8) * (lc.L.nz - 1) >= tune::ZR7_WIDE_MIN_TILES)
                 launch_zresrestrict_t<7, 64, 8, 512, false, true>(lf, lc, x, f, fc, xc, s, nch, nullptr, lr);
             else launch_zresrestrict_t<7, 64, 4, 256, false, true>(lf, lc, x, f, fc, xc, s, nch, nullptr, lr);
         } else if (lf.spec.npoints == 7) {
@@ -944,7 +944,7 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
             // 64 x 8 coarse points, 512 threads, 80 KB of LDS (2 workgroups per CU): half the y halo
             // of 64 x 4 (19 x planes rows per 16 fine rows instead of 11 per 8); 512^3 with kz 32:
             // 505-525 -> 488-502 us (interleaved A/B); at 256^3 too few tiles (73 against 66 us)
-            else if ((long long)((lc.L.nx + 62) / 64) * ((lc.L.ny + 6) / 8) * (lc.L.nz - 1) >= 16 * 1024)
+            else if ((long long)((lc.L.nx + 62) / 64) * ((lc.L.ny + 6) / 8) * (lc.L.nz - 1) >= tune::ZR7_WIDE_MIN_TILES)
                 launch_zresrestrict_t<7, 64, 8, 512>(lf, lc, x, f, fc, xc, s, nch);
             else launch_zresrestrict_t<7, 64, 4, 256>(lf, lc, x, f, fc, xc, s, nch);
         } else {
@@ -2892,7 +2892,7 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
         else if (cx) {
             const Level& lc = h->levels[level + 1];
             const bool wide = np == 7 && cx == 64 &&
-                              (long long)((lc.L.nx + 62) / 64) * ((lc.L.ny + 6) / 8) * (lc.L.nz - 1) >= 16 * 1024;
+                              (long long)((lc.L.nx + 62) / 64) * ((lc.L.ny + 6) / 8) * (lc.L.nz - 1) >= tune::ZR7_WIDE_MIN_TILES;
             res = "k_zresrestrict<" + std::to_string(np) + "," + std::to_string(cx) + "," + (wide ? "8" : "4") + ">";
         } else if (qrestrict_ok(h, level)) {
             sweep = "k_sweep_quads<2> (last pre-sweep: k_quads_restrict2d)";

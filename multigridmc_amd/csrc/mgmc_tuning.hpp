@@ -43,6 +43,9 @@ constexpr int JS_ROUNDS = 1;
 // instance; coarse nx below which the one-wavefront 16 x 4 tiles are used
 constexpr int ZR27_CX = 64;
 constexpr int ZR_SMALL_NX = 32;
+// the 7-point (fine level) instance with 64 x 8 coarse points per 512-thread workgroup (else 64 x 4
+// per 256 threads) from this many 64 x 8 tiles up (512^3: 32,768)
+constexpr int ZR7_WIDE_MIN_TILES = 16 * 1024;
 // the 7-point (fine level) instances load x planes two steps ahead (0: one step)
 constexpr int ZR7_XPF2 = 0;
 // tile rows in descending y order (the fine sweep before it writes its high-y tiles last)
