@@ -39,6 +39,8 @@ CONFIGS = {
     # column's term split off (LowRankDev::rhs_inplace, lr_row_patch); two pre- / post-sweeps, W-cycle
     "3d128_global_inplace_W": ((128, 128, 128), dict(nlevel=3, cycle=2, npresmooth=2, npostsmooth=2),
                                (0.0, 5, True)),
+    # ... the global average alone (m = 1: no local rows, every patch is the kernels' e)
+    "3d128_global_only_inplace": ((128, 128, 128), dict(nlevel=3), (0.0, 0, True)),
 }
 TAIL_CONFIGS = ["2d64_ball_ssor_W", "3d32_points_tail_W", "3d48_ball_tail_ssor", "2d128_points_tail"]
 
@@ -87,7 +89,7 @@ def test_lowrank_components_bitwise(hip_device, name):
 @pytest.mark.parametrize("name", list(CONFIGS))
 def test_lowrank_cycles_bitwise(hip_device, name):
     s, mc, p, lat, op = make(name)
-    if name == "3d128_global_inplace_W":  # the path this configuration is here for
+    if name in ("3d128_global_inplace_W", "3d128_global_only_inplace"):  # the path these configurations are here for
         assert s.level_kernels(0)["lowrank"] == "dense,rhs_inplace"
         assert s.level_kernels(1)["lowrank"] == "dense"
     rng = np.random.default_rng(11)
