@@ -163,15 +163,56 @@ __device__ __forceinline__ void tail_window(const double* __restrict__ x, int p,
     }
     tail_issue_all<NPTS>(v);
 }
-// a_0 x_0, then fma(a_k, x_k, .) ascending (= stencil_fma)
+// LDS byte address of a pointer into the dynamic shared array
+__device__ __forceinline__ uint32_t lds_addr(const double* p) {
+    return (uint32_t)(size_t)(const __attribute__((address_space(3))) double*)p;
+}
+#define TAIL_RD(n, b, o) "ds_read_b64 %" #n ", %" #b " offset:" #o "\n"
+// one vertex of a colour pass: x_p = fma(wd, c_p - S, x_p) with c_p = scr[p] and S = a_0 x_0, then
+// fma(a_k, x_k, .) ascending (= stencil_fma).  The window is read as its 3^(d-1) rows, each from one
+// address with the immediate offsets 0 / 8 / 16 bytes (one address instruction per row instead of two
+// or three per value), c_p with it, all in one asm statement that ends in the wait: one LDS round trip
+// per vertex, and x_p is the window's centre.  Single ds_read_b64: a paired ds_read2_b64 moves 8 bytes
+// per lane at half the rate (MI355X_MICROARCH.md), and reading each row's aligned pair as one
+// ds_read_b128 doubled the 15^3 passes' time (round 5)
 template <int DIM, int NPTS, bool SYM>
-__device__ __forceinline__ double tail_fma(const double* __restrict__ x, int p, const Layout& G, const StencilArg& S) {
-    double v[NPTS];
-    tail_window<DIM, NPTS>(x, p, G, v);
+__device__ __forceinline__ void tail_gibbs(double* __restrict__ x, const double* __restrict__ scr, int p,
+                                           const Layout& G, const StencilArg& S, double wd) {
+    double c, v[NPTS];
+    const uint32_t pc = lds_addr(scr) + 8u * (uint32_t)p, px = lds_addr(x) + 8u * (uint32_t)(p - 1);
+    if constexpr (NPTS == 27) {
+        uint32_t rb[9];
+#pragma unroll
+        for (int rr = 0; rr < 9; ++rr) rb[rr] = px + 8u * (uint32_t)((rr / 3 - 1) * (int)G.sp + (rr % 3 - 1) * (int)G.sx);
+        asm volatile(TAIL_RD(0, 28, 0) TAIL_RD(1, 29, 0) TAIL_RD(2, 29, 8) TAIL_RD(3, 29, 16) TAIL_RD(4, 30, 0)
+                     TAIL_RD(5, 30, 8) TAIL_RD(6, 30, 16) TAIL_RD(7, 31, 0) TAIL_RD(8, 31, 8) TAIL_RD(9, 31, 16)
+                     TAIL_RD(10, 32, 0) TAIL_RD(11, 32, 8) TAIL_RD(12, 32, 16) TAIL_RD(13, 33, 0) TAIL_RD(14, 33, 8)
+                     TAIL_RD(15, 33, 16) TAIL_RD(16, 34, 0) TAIL_RD(17, 34, 8) TAIL_RD(18, 34, 16) TAIL_RD(19, 35, 0)
+                     TAIL_RD(20, 35, 8) TAIL_RD(21, 35, 16) TAIL_RD(22, 36, 0) TAIL_RD(23, 36, 8) TAIL_RD(24, 36, 16)
+                     TAIL_RD(25, 37, 0) TAIL_RD(26, 37, 8) TAIL_RD(27, 37, 16) "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(c), "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]),
+                       "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]),
+                       "=&v"(v[12]), "=&v"(v[13]), "=&v"(v[14]), "=&v"(v[15]), "=&v"(v[16]), "=&v"(v[17]),
+                       "=&v"(v[18]), "=&v"(v[19]), "=&v"(v[20]), "=&v"(v[21]), "=&v"(v[22]), "=&v"(v[23]),
+                       "=&v"(v[24]), "=&v"(v[25]), "=&v"(v[26])
+                     : "v"(pc), "v"(rb[0]), "v"(rb[1]), "v"(rb[2]), "v"(rb[3]), "v"(rb[4]), "v"(rb[5]), "v"(rb[6]),
+                       "v"(rb[7]), "v"(rb[8])
+                     : "memory");
+    } else {
+        static_assert(NPTS == 9, "tail stencils are 27- or 9-point");
+        const uint32_t r0 = px - 8u * (uint32_t)G.sx, r2 = px + 8u * (uint32_t)G.sx;
+        asm volatile(TAIL_RD(0, 10, 0) TAIL_RD(1, 11, 0) TAIL_RD(2, 11, 8) TAIL_RD(3, 11, 16) TAIL_RD(4, 12, 0)
+                     TAIL_RD(5, 12, 8) TAIL_RD(6, 12, 16) TAIL_RD(7, 13, 0) TAIL_RD(8, 13, 8) TAIL_RD(9, 13, 16)
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(c), "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]),
+                       "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8])
+                     : "v"(pc), "v"(r0), "v"(px), "v"(r2)
+                     : "memory");
+    }
     double res = stencil_coef<SYM && NPTS == 27>(S, 0) * v[0];
 #pragma unroll
     for (int q = 1; q < NPTS; ++q) res = fma(stencil_coef<SYM && NPTS == 27>(S, q), v[q], res);
-    return res;
+    x[p] = fma(wd, c - res, v[NPTS / 2]);
 }
 // 0.0 + a_0 x_0 + a_1 x_1 + ... ascending, separate multiply and add (= stencil_sum)
 template <int DIM, int NPTS, bool SYM>
@@ -191,7 +232,13 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int tid = threadIdx.x, nt = blockDim.x;
     const int ntot = A->lds_doubles;
+    // the arguments' cache lines into L2 by vector loads, one line per thread, behind the LDS fill: the
+    // ops' scalar loads of them (each op's fields, then its level's) are otherwise dependent misses to
+    // HBM, the cycle's fine-level sweeps having flushed the caches (44 -> 42 us at 512^3, round 5)
+    uint32_t pre = 0;
+    if (tid * 64 < (int)sizeof(TailArgs)) pre = reinterpret_cast<const uint32_t*>(A)[tid * 16];
     for (int q = tid; q < ntot; q += nt) lds[q] = 0.0;
+    asm volatile("" ::"v"(pre));
     __syncthreads();
     const uint64_t sample = *A->sample;
     const int ch = blockIdx.x;  // batched chains: one workgroup per chain
@@ -322,34 +369,42 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
         }
         __syncthreads();
         TAIL_STAMP(2 + 2 * stamp_op);
+        // vertices of colour c: coordinate d = 2 - bit_d(c) + 2 t_d, t_d < the class size along d.
+        // Small levels (every class <= 8 x 8 x 16, 2D 32 x 32 vertices): thread bits are the class
+        // coordinates.  3D: tid = ti | tk0 << 3 | tj << 4 | (tk >> 1) << 7, so a half-wave holds class
+        // planes tk and tk+1 (vertex planes 2 apart, 16 bank pairs apart with the padded plane stride of
+        // tail_layout): 2-way banks.  Each thread's vertex of every colour (an offset from pb) and the
+        // colours it has (bits of vm) are worked out once per sweep: class sizes and bounds per pass were
+        // ~40 scalar instructions and six branches in every wavefront, half of a pass's time.
+        const int cmi = (G.nx - 2) / 2 + 1, cmj = (G.ny - 2) / 2 + 1, cmk = DIM == 3 ? (G.nz - 2) / 2 + 1 : 1;
+        const bool fast = DIM == 3 ? (cmi <= 8 && cmj <= 8 && cmk * 64 <= nt) : (cmi <= 32 && cmj * 32 <= nt);
+        const int ti = DIM == 3 ? (tid & 7) : (tid & 31);
+        const int tj = DIM == 3 ? ((tid >> 4) & 7) : (tid >> 5);
+        const int tk = DIM == 3 ? (((tid >> 3) & 1) | ((tid >> 7) << 1)) : 0;
+        const int pb = (int)G.at(2 + 2 * ti, 2 + 2 * tj, DIM == 3 ? 2 + 2 * tk : 0);
+        uint32_t vm = 0;
+#pragma unroll
+        for (int c = 0; c < (DIM == 3 ? 8 : 4); ++c) {
+            const bool in = 2 - (c & 1) + 2 * ti <= G.nx - 1 && 2 - ((c >> 1) & 1) + 2 * tj <= G.ny - 1 &&
+                            (DIM == 2 || 2 - ((c >> 2) & 1) + 2 * tk <= G.nz - 1);
+            vm |= (uint32_t)in << c;
+        }
         for (int cc = 0; cc < nc; ++cc) {
             const int c = dir == 1 ? cc : nc - 1 - cc;
-            // vertices of colour c: coordinate d = 2 - bit_d(c) + 2 t_d
-            const int fi = 2 - (c & 1), fj = 2 - ((c >> 1) & 1), fk = DIM == 3 ? 2 - ((c >> 2) & 1) : 0;
-            const int ci = fi > G.nx - 1 ? 0 : (G.nx - 1 - fi) / 2 + 1;
-            const int cj = fj > G.ny - 1 ? 0 : (G.ny - 1 - fj) / 2 + 1;
-            const int ck = DIM == 3 ? (fk > G.nz - 1 ? 0 : (G.nz - 1 - fk) / 2 + 1) : 1;
-            // small classes (<= 8 x 8 x 16, 2D 32 x 32 vertices): thread bits are the class
-            // coordinates, no index division on the pass's critical path.  3D: tid = ti | tk0 << 3 |
-            // tj << 4 | (tk >> 1) << 7, so a half-wave holds class planes tk and tk+1 (vertex planes
-            // 2 apart, 16 bank pairs apart with the padded plane stride of tail_layout): 2-way banks
-            const bool fast = DIM == 3 ? (ci <= 8 && cj <= 8 && ck * 64 <= nt) : (ci <= 32 && cj * 32 <= nt);
             if (fast) {
-                const int ti = DIM == 3 ? (tid & 7) : (tid & 31);
-                const int tj = DIM == 3 ? ((tid >> 4) & 7) : (tid >> 5);
-                const int tk = DIM == 3 ? (((tid >> 3) & 1) | ((tid >> 7) << 1)) : 0;
-                if (ti < ci && tj < cj && tk < ck) {
-                    const int p = (int)G.at(fi + 2 * ti, fj + 2 * tj, DIM == 3 ? fk + 2 * tk : 0);
-                    const double res = tail_fma<DIM, NPTS, SYM>(x, (int)p, G, S);
-                    x[p] = fma(wd, scr[p] - res, x[p]);
+                if ((vm >> c) & 1) {
+                    const int p = pb - (c & 1) - ((c >> 1) & 1) * (int)G.sx - (DIM == 3 ? ((c >> 2) & 1) * (int)G.sp : 0);
+                    tail_gibbs<DIM, NPTS, SYM>(x, scr, p, G, S, wd);
                 }
             } else {
+                const int fi = 2 - (c & 1), fj = 2 - ((c >> 1) & 1), fk = DIM == 3 ? 2 - ((c >> 2) & 1) : 0;
+                const int ci = fi > G.nx - 1 ? 0 : (G.nx - 1 - fi) / 2 + 1;
+                const int cj = fj > G.ny - 1 ? 0 : (G.ny - 1 - fj) / 2 + 1;
+                const int ck = DIM == 3 ? (fk > G.nz - 1 ? 0 : (G.nz - 1 - fk) / 2 + 1) : 1;
                 for (int q = tid; q < ci * cj * ck; q += nt) {
                     const int i = fi + 2 * (q % ci), r = q / ci;
                     const int j = fj + 2 * (r % cj), k = DIM == 3 ? fk + 2 * (r / cj) : 0;
-                    const long long p = G.at(i, j, k);
-                    const double res = tail_fma<DIM, NPTS, SYM>(x, (int)p, G, S);
-                    x[p] = fma(wd, scr[p] - res, x[p]);
+                    tail_gibbs<DIM, NPTS, SYM>(x, scr, (int)G.at(i, j, k), G, S, wd);
                 }
             }
             __syncthreads();
