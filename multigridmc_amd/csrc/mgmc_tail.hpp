@@ -132,83 +132,64 @@ __device__ __forceinline__ void tail_pin(StencilArg& S) {
         if (!SYM || sym_rep(q) == q) tail_pin(S.a[q]);
 }
 
-// stencil_fma / stencil_sum of an LDS-resident level with every window read issued before the chain:
-// left to itself the compiler reads one or two values, waits, multiplies, and reads the next, so a
-// colour pass paid the LDS latency 9-14 times in a row.  The empty asm takes all the window values as
-// operands, which orders every read before any use (same values, same arithmetic order).
-template <int NPTS>
-__device__ __forceinline__ void tail_issue_all(double (&v)[NPTS]) {
-    if constexpr (NPTS == 27) {
-        asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
-                          "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]),
-                          "+v"(v[14]), "+v"(v[15]), "+v"(v[16]), "+v"(v[17]), "+v"(v[18]), "+v"(v[19]),
-                          "+v"(v[20]), "+v"(v[21]), "+v"(v[22]), "+v"(v[23]), "+v"(v[24]), "+v"(v[25]), "+v"(v[26]));
-    } else {
-        static_assert(NPTS == 9, "tail stencils are 27- or 9-point");
-        asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
-                          "+v"(v[7]), "+v"(v[8]));
-    }
-}
-template <int DIM, int NPTS>
-__device__ __forceinline__ void tail_window(const double* __restrict__ x, int p, const Layout& G, double (&v)[NPTS]) {
-    // each index hidden behind an empty asm: the compiler cannot pair neighbouring reads into
-    // ds_read2_b64, which moves 8 bytes per lane at half the rate of ds_read_b64 (MI355X_MICROARCH.md,
-    // LDS table) -- the colour passes are bound by LDS throughput
-#pragma unroll
-    for (int q = 0; q < NPTS; ++q) {
-        const int dz = DIM == 3 ? q / 9 - 1 : 0, dy = (q / 3) % 3 - 1, dx = q % 3 - 1;
-        int idx = p + dz * (int)G.sp + dy * (int)G.sx + dx;
-        asm volatile("" : "+v"(idx));
-        v[q] = x[idx];
-    }
-    tail_issue_all<NPTS>(v);
-}
 // LDS byte address of a pointer into the dynamic shared array
 __device__ __forceinline__ uint32_t lds_addr(const double* p) {
     return (uint32_t)(size_t)(const __attribute__((address_space(3))) double*)p;
 }
 #define TAIL_RD(n, b, o) "ds_read_b64 %" #n ", %" #b " offset:" #o "\n"
-// one vertex of a colour pass: x_p = fma(wd, c_p - S, x_p) with c_p = scr[p] and S = a_0 x_0, then
-// fma(a_k, x_k, .) ascending (= stencil_fma).  The window is read as its 3^(d-1) rows, each from one
-// address with the immediate offsets 0 / 8 / 16 bytes (one address instruction per row instead of two
-// or three per value), c_p with it, all in one asm statement that ends in the wait: one LDS round trip
-// per vertex, and x_p is the window's centre.  Single ds_read_b64: a paired ds_read2_b64 moves 8 bytes
-// per lane at half the rate (MI355X_MICROARCH.md), and reading each row's aligned pair as one
-// ds_read_b128 doubled the 15^3 passes' time (round 5)
-template <int DIM, int NPTS, bool SYM>
-__device__ __forceinline__ void tail_gibbs(double* __restrict__ x, const double* __restrict__ scr, int p,
-                                           const Layout& G, const StencilArg& S, double wd) {
-    double c, v[NPTS];
-    const uint32_t pc = lds_addr(scr) + 8u * (uint32_t)p, px = lds_addr(x) + 8u * (uint32_t)(p - 1);
+// The 3^d window of x around p (v[q], q = 9 (dz+1) + 3 (dy+1) + dx+1) of an LDS-resident level, read
+// as its 3^(d-1) rows, each from one address with the immediate offsets 0 / 8 / 16 bytes, in one asm
+// statement that ends in the wait:
+//  * every read is issued before the first use (left to itself the compiler read one or two values,
+//    waited, multiplied and read the next: the LDS latency 9-14 times per vertex);
+//  * one address instruction per row, not two or three per value (a colour pass's address arithmetic
+//    was as long as its fma chain);
+//  * single ds_read_b64: a paired ds_read2_b64 moves 8 bytes per lane at half the rate
+//    (MI355X_MICROARCH.md, LDS table), and each row's aligned pair as one ds_read_b128 doubled the 15^3
+//    colour passes' time (round 5).
+// The memory clobber keeps the caller's earlier LDS reads (the right-hand side) issued before it.
+template <int DIM, int NPTS>
+__device__ __forceinline__ void tail_window(const double* __restrict__ x, int p, const Layout& G, double (&v)[NPTS]) {
+    const uint32_t px = lds_addr(x) + 8u * (uint32_t)(p - 1);
     if constexpr (NPTS == 27) {
         uint32_t rb[9];
 #pragma unroll
         for (int rr = 0; rr < 9; ++rr) rb[rr] = px + 8u * (uint32_t)((rr / 3 - 1) * (int)G.sp + (rr % 3 - 1) * (int)G.sx);
-        asm volatile(TAIL_RD(0, 28, 0) TAIL_RD(1, 29, 0) TAIL_RD(2, 29, 8) TAIL_RD(3, 29, 16) TAIL_RD(4, 30, 0)
-                     TAIL_RD(5, 30, 8) TAIL_RD(6, 30, 16) TAIL_RD(7, 31, 0) TAIL_RD(8, 31, 8) TAIL_RD(9, 31, 16)
-                     TAIL_RD(10, 32, 0) TAIL_RD(11, 32, 8) TAIL_RD(12, 32, 16) TAIL_RD(13, 33, 0) TAIL_RD(14, 33, 8)
-                     TAIL_RD(15, 33, 16) TAIL_RD(16, 34, 0) TAIL_RD(17, 34, 8) TAIL_RD(18, 34, 16) TAIL_RD(19, 35, 0)
-                     TAIL_RD(20, 35, 8) TAIL_RD(21, 35, 16) TAIL_RD(22, 36, 0) TAIL_RD(23, 36, 8) TAIL_RD(24, 36, 16)
-                     TAIL_RD(25, 37, 0) TAIL_RD(26, 37, 8) TAIL_RD(27, 37, 16) "s_waitcnt lgkmcnt(0)"
-                     : "=&v"(c), "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]),
-                       "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]),
-                       "=&v"(v[12]), "=&v"(v[13]), "=&v"(v[14]), "=&v"(v[15]), "=&v"(v[16]), "=&v"(v[17]),
-                       "=&v"(v[18]), "=&v"(v[19]), "=&v"(v[20]), "=&v"(v[21]), "=&v"(v[22]), "=&v"(v[23]),
-                       "=&v"(v[24]), "=&v"(v[25]), "=&v"(v[26])
-                     : "v"(pc), "v"(rb[0]), "v"(rb[1]), "v"(rb[2]), "v"(rb[3]), "v"(rb[4]), "v"(rb[5]), "v"(rb[6]),
-                       "v"(rb[7]), "v"(rb[8])
+        asm volatile(TAIL_RD(0, 27, 0) TAIL_RD(1, 27, 8) TAIL_RD(2, 27, 16) TAIL_RD(3, 28, 0) TAIL_RD(4, 28, 8)
+                     TAIL_RD(5, 28, 16) TAIL_RD(6, 29, 0) TAIL_RD(7, 29, 8) TAIL_RD(8, 29, 16) TAIL_RD(9, 30, 0)
+                     TAIL_RD(10, 30, 8) TAIL_RD(11, 30, 16) TAIL_RD(12, 31, 0) TAIL_RD(13, 31, 8) TAIL_RD(14, 31, 16)
+                     TAIL_RD(15, 32, 0) TAIL_RD(16, 32, 8) TAIL_RD(17, 32, 16) TAIL_RD(18, 33, 0) TAIL_RD(19, 33, 8)
+                     TAIL_RD(20, 33, 16) TAIL_RD(21, 34, 0) TAIL_RD(22, 34, 8) TAIL_RD(23, 34, 16) TAIL_RD(24, 35, 0)
+                     TAIL_RD(25, 35, 8) TAIL_RD(26, 35, 16) "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+                       "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]), "=&v"(v[12]),
+                       "=&v"(v[13]), "=&v"(v[14]), "=&v"(v[15]), "=&v"(v[16]), "=&v"(v[17]), "=&v"(v[18]),
+                       "=&v"(v[19]), "=&v"(v[20]), "=&v"(v[21]), "=&v"(v[22]), "=&v"(v[23]), "=&v"(v[24]),
+                       "=&v"(v[25]), "=&v"(v[26])
+                     : "v"(rb[0]), "v"(rb[1]), "v"(rb[2]), "v"(rb[3]), "v"(rb[4]), "v"(rb[5]), "v"(rb[6]), "v"(rb[7]),
+                       "v"(rb[8])
                      : "memory");
     } else {
         static_assert(NPTS == 9, "tail stencils are 27- or 9-point");
         const uint32_t r0 = px - 8u * (uint32_t)G.sx, r2 = px + 8u * (uint32_t)G.sx;
-        asm volatile(TAIL_RD(0, 10, 0) TAIL_RD(1, 11, 0) TAIL_RD(2, 11, 8) TAIL_RD(3, 11, 16) TAIL_RD(4, 12, 0)
-                     TAIL_RD(5, 12, 8) TAIL_RD(6, 12, 16) TAIL_RD(7, 13, 0) TAIL_RD(8, 13, 8) TAIL_RD(9, 13, 16)
-                     "s_waitcnt lgkmcnt(0)"
-                     : "=&v"(c), "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]),
-                       "=&v"(v[6]), "=&v"(v[7]), "=&v"(v[8])
-                     : "v"(pc), "v"(r0), "v"(px), "v"(r2)
+        asm volatile(TAIL_RD(0, 9, 0) TAIL_RD(1, 9, 8) TAIL_RD(2, 9, 16) TAIL_RD(3, 10, 0) TAIL_RD(4, 10, 8)
+                     TAIL_RD(5, 10, 16) TAIL_RD(6, 11, 0) TAIL_RD(7, 11, 8) TAIL_RD(8, 11, 16) "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+                       "=&v"(v[7]), "=&v"(v[8])
+                     : "v"(r0), "v"(px), "v"(r2)
                      : "memory");
     }
+}
+#undef TAIL_RD
+// one vertex of a colour pass: x_p = fma(wd, c_p - S, x_p) with c_p = scr[p] and S = a_0 x_0, then
+// fma(a_k, x_k, .) ascending (= stencil_fma); c_p is read just before the window (one LDS round trip
+// per vertex) and x_p is the window's centre
+template <int DIM, int NPTS, bool SYM>
+__device__ __forceinline__ void tail_gibbs(double* __restrict__ x, const double* __restrict__ scr, int p,
+                                           const Layout& G, const StencilArg& S, double wd) {
+    const double c = scr[p];
+    double v[NPTS];
+    tail_window<DIM, NPTS>(x, p, G, v);
     double res = stencil_coef<SYM && NPTS == 27>(S, 0) * v[0];
 #pragma unroll
     for (int q = 1; q < NPTS; ++q) res = fma(stencil_coef<SYM && NPTS == 27>(S, q), v[q], res);
@@ -516,7 +497,7 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
             __syncthreads();
             for_interior(Gc, [&](int I, int J, int K) {
                 const int pf = (int)G.at(2 * I, 2 * J, 2 * K);
-                double rv[NPTS];  // the 3^d residuals, every read issued before the sum (tail_window)
+                double rv[NPTS];  // the 3^d residuals (tail_window)
                 tail_window<DIM, NPTS>(scr, pf, G, rv);
                 double result = 0.0;
                 const int zr = DIM == 3 ? 1 : 0;
@@ -563,12 +544,13 @@ __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
                 const double wj[2] = {(j & 1) ? 0.5 : 1.0, (j & 1) ? 0.5 : 0.0};
                 const double wk[2] = {(DIM == 3 && (k & 1)) ? 0.5 : 1.0, (DIM == 3 && (k & 1)) ? 0.5 : 0.0};
                 double c[2][2][2];
+                const int pc0 = (int)Gc.at(ia, ja, ka);
 #pragma unroll
                 for (int aa = 0; aa < (DIM == 3 ? 2 : 1); ++aa)
 #pragma unroll
                     for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
-                        for (int cc = 0; cc < 2; ++cc) c[aa][bb][cc] = xc[Gc.at(ia + cc, ja + bb, DIM == 3 ? ka + aa : 0)];
+                        for (int cc = 0; cc < 2; ++cc) c[aa][bb][cc] = xc[pc0 + aa * (int)Gc.sp + bb * (int)Gc.sx + cc];
 #pragma unroll
                 for (int aa = 0; aa < (DIM == 3 ? 2 : 1); ++aa)
 #pragma unroll
