@@ -81,6 +81,8 @@ def _iact(z):
 
 def _check_moments(z, mean_exact, var_exact):
     n_eff = len(z) / _iact(z)
+    print(f"T3: n={len(z)} n_eff={n_eff:.0f} mean={z.mean():.6g} (exact {mean_exact:.6g}) "
+          f"var={z.var():.6g} (exact {var_exact:.6g})")
     assert abs(z.mean() - mean_exact) < 5 * np.sqrt(var_exact / n_eff), (z.mean(), mean_exact)
     assert abs(z.var() - var_exact) < 5 * var_exact * np.sqrt(2.0 / n_eff), (z.var(), var_exact)
 
@@ -99,6 +101,30 @@ def test_prior_qoi_variance_at_256_cubed(hip_device):
     var_exact = x[q]
     s.sample(100, q)
     z = s.sample(20000, q)
+    _check_moments(z, 0.0, var_exact)
+    s.close()
+
+
+def test_prior_qoi_variance_at_headline_512_cubed(hip_device):
+    """T3 at the bench's own configuration (BASELINE config 4: 3D 512^3, 7 levels, V-cycle, SOR,
+    SSOR coarse, f = 0) and QoI vertex (the centre, index 66,716,415), as measure_sampling_time does
+    on the timed chain (driver_mgmc.cc:86-104): Var z = (A^-1)_cc from the device MG-CG (a13,
+    linear_operator.hh:153-174 with m = 0), mean 0; 200 warm-up + 20,000 samples within 5 sigma
+    (IACT)."""
+    lat = mg.Lattice(512, 512, 512)
+    p = mg.MultigridParameters(nlevel=7)
+    s = mg.MultigridMCSampler(mg.ShiftedLaplaceFDOperator(lat, 25.0), SEED, p)
+    q = mg.measurement_vector_index(lat, [0.5, 0.5, 0.5])
+    assert q == 66716415
+    e = np.zeros(lat.Nvertex)
+    e[q] = 1.0
+    g, it, rn = s.solve(e, method="cg", rtol=1e-10, maxiter=100)
+    assert it < 100
+    var_exact = g[q]
+    del g, e
+    s.sample(200, q)
+    z = s.sample(20000, q)
+    assert np.all(np.isfinite(z))
     _check_moments(z, 0.0, var_exact)
     s.close()
 
