@@ -234,6 +234,10 @@ int mgmc_set_lowrank(mgmc_handle* h, int m, const int64_t* colptr, const int64_t
 /* m of the current low-rank part (LinearOperator::get_m_lowrank); *nrows_bbar = rows stored for
  * B_bar of (level, direction) */
 int mgmc_lowrank_info(const mgmc_handle* h, int level, int direction, int* m, int64_t* nrows_bbar);
+/* testing hook: the handle's next n builds of the coarse Cholesky factor fail with MGMC_E_NOMEM, so
+ * tests can drive mgmc_set_lowrank's rollback (a failed restore leaves the handle refusing the cycle
+ * and solver calls until a later mgmc_set_lowrank succeeds).  n = 0 clears it. */
+int mgmc_debug_fail_coarse_factor(mgmc_handle* h, int n);
 
 /* ---- Sampler interface (host buffers, reference layout) ---- */
 int mgmc_set_rhs(mgmc_handle* h, const double* f, size_t n);       /* fix_rhs: f stays in HBM */

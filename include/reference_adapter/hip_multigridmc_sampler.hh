@@ -30,8 +30,10 @@
 // (driver_mgmc.cc:448) while the engine itself is never advanced: the reference's
 // MultigridMCSampler consumes none at construction (multigridmc_sampler.cc:8-100), so the SSOR /
 // Cholesky samplers driver_mgmc builds after it (driver_mgmc.cc:450-501) see the engine state they
-// see in an unmodified reference.  Two samplers built on the same (unadvanced) engine therefore get
-// the same seed: give them distinct chain ids, or pass an explicit seed as the last argument.
+// see in an unmodified reference.  The reference's samplers sharing one engine draw different noise,
+// so a second sampler built on the same (unadvanced) engine state in this process does not reuse the
+// seed: every repeat of an engine state mixes a construction counter into it (the first sampler keeps
+// the engine's output itself).  An explicit seed (the last constructor argument) is taken as given.
 // Ownership: like the reference's Sampler, the base class has no virtual destructor, so a sampler is
 // owned as driver_mgmc.cc:450-457 owns it, std::make_shared<HipMultigridMCSampler>(...) (the
 // shared_ptr's deleter destroys the derived object and its device handle).  Errors print and
@@ -41,7 +43,9 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <random>
 #include <string>
 #include <vector>
@@ -55,10 +59,23 @@ class HipMultigridMCSampler : public Sampler {
     enum class Path { stencil, matrix };
     static constexpr uint64_t default_seed = 5418513;  // driver_mgmc.cc:448 (seed of the noise-free smoother handles)
 
-    // Philox seed by default: the next output of a copy of the shared engine (the engine is not advanced)
+    // Philox seed by default: the next output of a copy of the shared engine (the engine is not
+    // advanced); the k-th repeat of that output in this process (k >= 1) is mixed with k (splitmix64)
     static uint64_t engine_seed(const std::mt19937_64& rng_) {
         std::mt19937_64 copy = rng_;
-        return copy();
+        const uint64_t s = copy();
+        static std::mutex mu;
+        static std::map<uint64_t, uint64_t> uses;  // engine output -> samplers seeded from it so far
+        uint64_t k;
+        {
+            std::lock_guard<std::mutex> lock(mu);
+            k = uses[s]++;
+        }
+        if (k == 0) return s;
+        uint64_t z = k + 0x9E3779B97F4A7C15ull;  // splitmix64(k)
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return s ^ (z ^ (z >> 31));
     }
 
     // The reference's MultigridMCSampler(linear_operator, rng, params, cholesky_params) plus where to

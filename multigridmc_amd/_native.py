@@ -100,6 +100,7 @@ SIGNATURES = [
     ("mgmc_level_kernels", c_int, [_H, c_int, ctypes.c_char_p, c_size_t]),
     ("mgmc_set_lowrank", c_int, [_H, c_int, POINTER(c_int64), POINTER(c_int64), _DP, _DP]),
     ("mgmc_lowrank_info", c_int, [_H, c_int, c_int, POINTER(c_int), POINTER(c_int64)]),
+    ("mgmc_debug_fail_coarse_factor", c_int, [_H, c_int]),
     ("mgmc_set_rhs", c_int, [_H, _DP, c_size_t]),
     ("mgmc_set_state", c_int, [_H, _DP, c_size_t]),
     ("mgmc_get_state", c_int, [_H, _DP, c_size_t]),

@@ -6,367 +6,17 @@
 // (sampler/multigridmc_sampler.cc:103-138) = a fixed sequence of kernel launches, captured once
 // into a hipGraph and replayed; the RNG counter (sample index) is read from device memory so
 // the frozen graph produces fresh noise on every replay.
-#include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
-#include <stdio.h>
-#include <stdlib.h>
-#include <string.h>
+#include "mgmc_internal.hpp"
 
-#include <algorithm>
-#include <atomic>
-#include <cmath>
-#include <mutex>
-#include <string>
-#include <vector>
-
-#include "../../include/mgmc.h"
-#include "mgmc_hierarchy.hpp"
-#include "mgmc_kernels.hpp"
-#include "mgmc_zsweep.hpp"
-#include "mgmc_tuning.hpp"
-#include "mgmc_layout_check.hpp"
-static_assert(MGMC_LAYOUT_POINT == mgmc::LF_POINT && MGMC_LAYOUT_PAIRS == mgmc::LF_PAIRS &&
-                  MGMC_LAYOUT_ZSWEEP == mgmc::LF_ZSWEEP && MGMC_LAYOUT_ZSWEEP_COARSE == mgmc::LF_ZSWEEP_C &&
-                  MGMC_LAYOUT_ZRESTRICT == mgmc::LF_ZRESTRICT && MGMC_LAYOUT_RB2D == mgmc::LF_RB2D &&
-                  MGMC_LAYOUT_JSWEEP == mgmc::LF_JSWEEP && MGMC_LAYOUT_QRESTRICT == mgmc::LF_QRESTRICT,
-              "layout family bits");
-#include "mgmc_zrestrict.hpp"
-#include "mgmc_tail.hpp"
-#include "mgmc_gsweep.hpp"
-#include "mgmc_qrestrict.hpp"
-#include "mgmc_jsweep.hpp"
-#include "mgmc_rb2d.hpp"
-#include "mgmc_lowrank.hpp"
-#include "mgmc_solver.hpp"
-#include "mgmc_cholesky.hpp"
-#include "mgmc_field.hpp"
-#include "mgmc_operators.hpp"
-
-using namespace mgmc;
-
-namespace {
-
+namespace mgmc_host {
 std::mutex g_err_mutex;
 std::string g_last_error;
-
+std::atomic<int> g_live_handles{0};
 void set_global_error(const std::string& s) {
     std::lock_guard<std::mutex> lock(g_err_mutex);
     g_last_error = s;
 }
-
-enum OpKind {
-    OP_SWEEP = 0,
-    OP_RESIDUAL_RESTRICT = 1,
-    OP_PROLONGATE = 2,
-    OP_COARSE_LDS = 3,
-    OP_QOI = 4,
-    OP_COPY = 5,
-    OP_COARSE_CHOL = 6,
-    OP_TAIL = 7,     // the sub-cycle of the coarsest levels in one workgroup (mgmc_tail.hpp)
-    OP_SWEEP_RESTRICT = 8   // 2D Galerkin level: last pre-sweep + residual + restriction (mgmc_qrestrict.hpp)
-};
-
-struct Op {
-    OpKind kind;
-    int level;
-    int direction;  // MGMC_FORWARD / MGMC_BACKWARD for sweeps
-    uint32_t tag;   // first sweep tag
-    int nsweeps;    // OP_COARSE_LDS
-    int src = 0;    // buffer index read (x[src]); z-sweeps write x[1-src]
-    int prolong = 0;  // z-sweep with fused prolongate-add of the coarser level's x
-    int lr_next = 0;       // sweep on a small low-rank level: the patch of the next op, fused (LR_NEXT_*)
-    uint32_t lr_next_tag = 0;
-    int lr_skip_patch = 0;  // this op's low-rank patch was done by an earlier op's kernel
-    int lr_post_patch = 0;  // OP_RESIDUAL_RESTRICT: the restore of f also patches the level's first post-sweep
-    uint32_t lr_post_tag = 0;
-    int lr_coarse_patch = 0;  // OP_RESIDUAL_RESTRICT: ... and the coarse level's first pre-sweep
-    uint32_t lr_coarse_tag = 0;
-    int tail = -1;           // OP_TAIL: index into mgmc_handle::tail_args
-    int xzero = 0;           // OP_SWEEP: its input x is known zero (the restriction before it zeroed the level, nothing
-                             // wrote it since): the kernel takes zeros instead of loading it (mark_zero_inputs);
-                             // OP_RESIDUAL_RESTRICT: so the coarse x is not written at all
-    int zpre = 0;            // OP_SWEEP_RESTRICT: also draws the next OP_COARSE_LDS's noise into mgmc_handle::zbuf;
-                             // OP_COARSE_LDS: reads it from there; OP_RESIDUAL_RESTRICT: 1 + the index of
-                             // the OP_TAIL after it whose noise its spare workgroups draw
-};
-
-
-// Kernel-path switches.  Every default fast path has a general fallback (the same arithmetic, bitwise
-// equal); MGMC_DISABLE=<comma list> turns fast paths off at mgmc_create so the variant tests
-// (tests/test_gpu_parity.py test_variant_cycles_bitwise, test_gpu_lowrank.py) can run the fallbacks
-// on shapes where the fast path would be taken.  Read once per handle; unknown tokens are an error.
-enum PathFlag : uint32_t {
-    PATH_NO_TAIL = 1u << 0,               // coarsest levels as separate launches instead of k_tail
-    PATH_NO_FUSE_PROLONG = 1u << 1,       // separate prolongate-add pass before the first post-sweep
-    PATH_NO_QUADS = 1u << 2,              // colour-pair passes instead of two pairs per launch
-    PATH_NO_RB2D = 1u << 3,               // 2D fine level: colour passes instead of k_rb2d
-    PATH_NO_ZSWEEP = 1u << 4,             // 3D fine level: colour passes instead of k_zsweep_rb7
-    PATH_NO_PAIRS = 1u << 5,              // Galerkin levels: per-colour passes instead of pair passes
-    PATH_NO_ZRESTRICT = 1u << 6,          // residual + restriction: per-point gather kernel
-    PATH_NO_LR_SMALL = 1u << 7,           // low-rank fix: generic multi-launch path instead of k_lr_small
-    PATH_NO_LR_MERGE = 1u << 8,           // low-rank: separate restore / patch launches around restriction
-    PATH_NO_LR_PREFETCH = 1u << 9,        // low-rank small fix without the up-front loads
-    PATH_NO_COARSE_PRECOMPUTE = 1u << 10, // coarse SSOR: right-hand sides inside the colour passes
-    PATH_NO_LR_DENSE = 1u << 11,          // dense low-rank column: the row lists over every vertex
-    PATH_NO_CHOL_DENSE = 1u << 12,        // coarse Cholesky: the blocked banded solves at any size
-    PATH_NO_JSWEEP = 1u << 13,            // 3D Galerkin levels of 64 / 128 pairs: colour-pair passes, not j-marching halves
-    PATH_NO_QRESTRICT = 1u << 14,         // 2D Galerkin levels: last pre-sweep and residual + restriction as two launches
-    PATH_NO_TAIL_NOISE = 1u << 15,        // k_tail draws its sweeps' noise itself (not the restriction launch before it)
-    PATH_NO_SYM = 1u << 16,               // 27-point kernels read all 27 coefficients even when the stencil is symmetric
-    PATH_NO_PROLONG_Z = 1u << 17,         // big 3D levels: the per-point prolongation instead of the z-marching one
-    PATH_NO_ZPAIRS = 1u << 18,            // fine z-sweep: every z-chunk marches up (no up / down chunk pairs)
-    PATH_NO_XZERO = 1u << 19,             // the restriction zeroes x_{l+1} and its first pre-sweep loads it
-};
-
-struct PathToken {
-    const char* name;
-    uint32_t flag;
-};
-constexpr PathToken kPathTokens[] = {
-    {"tail", PATH_NO_TAIL},           {"fuse_prolong", PATH_NO_FUSE_PROLONG},
-    {"quads", PATH_NO_QUADS},         {"rb2d", PATH_NO_RB2D},
-    {"zsweep", PATH_NO_ZSWEEP},       {"pairs", PATH_NO_PAIRS},
-    {"zrestrict", PATH_NO_ZRESTRICT}, {"lr_small", PATH_NO_LR_SMALL},
-    {"lr_merge", PATH_NO_LR_MERGE},   {"lr_prefetch", PATH_NO_LR_PREFETCH},
-    {"coarse_precompute", PATH_NO_COARSE_PRECOMPUTE}, {"lr_dense", PATH_NO_LR_DENSE},
-    {"chol_dense", PATH_NO_CHOL_DENSE}, {"jsweep", PATH_NO_JSWEEP},
-    {"qrestrict", PATH_NO_QRESTRICT}, {"tail_noise", PATH_NO_TAIL_NOISE},
-    {"sym", PATH_NO_SYM},             {"prolong_z", PATH_NO_PROLONG_Z},
-    {"zpairs", PATH_NO_ZPAIRS},       {"xzero", PATH_NO_XZERO},
-};
-
-// parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
-bool read_path_flags(uint32_t* flags, std::string* bad) {
-    *flags = 0;
-    const char* e = getenv("MGMC_DISABLE");
-    if (!e) return true;
-    std::string list(e);
-    size_t pos = 0;
-    while (pos <= list.size()) {
-        size_t end = list.find(',', pos);
-        if (end == std::string::npos) end = list.size();
-        const std::string tok = list.substr(pos, end - pos);
-        if (!tok.empty()) {
-            bool found = false;
-            for (const PathToken& t : kPathTokens)
-                if (tok == t.name) {
-                    *flags |= t.flag;
-                    found = true;
-                }
-            if (!found) {
-                *bad = tok;
-                return false;
-            }
-        }
-        pos = end + 1;
-    }
-    return true;
-}
-
-// z-marching sweep tile shape (mgmc_zsweep.hpp): 32 x-pairs x TY rows, TY/2 core waves + 2 halo
-// waves rounded up to a multiple of four (768 threads for TY 16); two workgroups per CU need <= 80
-// VGPRs (6 waves per SIMD).  Values in mgmc_tuning.hpp, tuning history in DESIGN.md.
-constexpr int ZS_XP = 32, ZS_TY = tune::ZS_TY, ZS_NT = zs_threads(ZS_TY), ZS_MINW = tune::ZS_MINW,
-              ZS_TZ = tune::ZS_TZ, ZS_TYP = tune::ZS_TYP, ZS_NTP = zs_threads(ZS_TYP),
-              ZS_MINWP = tune::ZS_MINWP, ZS_TZP = tune::ZS_TZP;
-
-// device copy of a level's low-rank part (mgmc_lowrank.hpp); one allocation list, freed together
-struct LowRankDev {
-    int m = 0;
-    int nblk = 0;                 // dot-product blocks over all columns
-    LRColMeta* meta = nullptr;
-    int* blk_col = nullptr;
-    LRBlock* blk = nullptr;        // per dot-product block: column, range, value source, scales
-    long long* ent_off = nullptr;  // sparse column entries: padded offsets, values
-    double* ent_val = nullptr;
-    double* dense_val = nullptr;   // dense columns: padded value arrays, L.nstore apart
-    int nrows = 0;                 // rows of B: padded offsets, m coefficients, column masks, saved f
-    long long* rows_off = nullptr;
-    double* rows_coef = nullptr;
-    uint64_t* rows_mask = nullptr;
-    double* save = nullptr;
-    int nbar[2] = {0, 0};          // B_bar rows, [0] forward [1] backward
-    long long* bar_off[2] = {nullptr, nullptr};
-    double* bar_val[2] = {nullptr, nullptr};
-    double* sc_one = nullptr;      // dot scales: 1 (B^T x), 1/Sigma_k (Sigma^{-1} B^T x)
-    double* sc_inv = nullptr;
-    double* sq = nullptr;          // sqrt(1/Sigma_k)
-    double* part = nullptr;        // block partials
-    double* w = nullptr;           // m-vector of dots
-    bool small = false;            // k_lr_small path (sparse columns, one block each, few rows)
-    long long max_col_n = 0;       // most entries of one column
-    int* t_ent_off = nullptr;      // the same offsets in k_tail's LDS layout (small levels)
-    int* t_rows_off = nullptr;
-    int* t_bar_off[2] = {nullptr, nullptr};
-    // dense-column path (one dense column g, mgmc_lowrank.hpp k_lr_dense_*): the row lists above
-    // hold only the local rows; the dense-only rows stream B_g / Y_g, and the patched right-hand
-    // side goes to fe (nchains x L.nstore) instead of f
-    bool dense_path = false;
-    bool dense_const = false;     // ... its dense column is one number (LRColMeta::cflag): dense_cval
-    double dense_cval = 0.0;
-    int dense_slot = 0;           // ... its value array in dense_val
-    int dense_g = -1;
-    uint32_t* skip_b = nullptr;                 // bit p: not a dense-only row of the patch
-    uint32_t* skip_y[2] = {nullptr, nullptr};   // bit p: not a dense-only row of B_bar (per direction)
-    double* yg[2] = {nullptr, nullptr};         // column g of Y (padded, per direction)
-    // ... or, when B_g is one number on a 5 / 7-point level, Y_g as a table: Y_g of a dense-only vertex
-    // is a function of its colour and of which of its 2d neighbours exist (the solve from zero of a
-    // constant right-hand side), so the update reads a 1-byte key per vertex and ytab[d][key]
-    uint8_t* ykey = nullptr;
-    double* ytab[2] = {nullptr, nullptr};
-    double* minv_g[2] = {nullptr, nullptr};     // row g of Minv (per direction)
-    double* fe = nullptr;
-    double* fe2 = nullptr;                      // ... of the first post-sweep, written with the residual's
-    // ... or, on a z-sweep level with B_g one number, read in place (LRRhsArg): f is patched in place
-    // on the local rows (saved, restored: the row-list path's k_lr_patch / k_lr_restore_patch), and
-    // the sweep / residual kernels add the dense-only patch e to f on the other rows (e per chain in
-    // rhs_e: [c] the sweep's / residual's, [nchains + c] the first post-sweep's); fe, fe2 unused
-    bool rhs_inplace = false;
-    double* rhs_e = nullptr;
-    // the split column of the row patches (mgmc_lowrank.hpp lr_row_patch): the level's one dense
-    // column when every value of it is one number (dense_const), else -1
-    int split_g = -1;
-    long long nbar_all[2] = {0, 0};             // B_bar rows in total (local + dense-only with Y_g != 0)
-    std::vector<void*> allocs;
-};
-
-struct Level {
-    LevelSpec spec;
-    Layout L;
-    StencilArg S;
-    double* x = nullptr;      // canonical state buffer
-    double* x2 = nullptr;     // ping-pong partner (z-sweep levels only)
-    double* f = nullptr;
-    double* scratch[3] = {nullptr, nullptr, nullptr};
-    size_t lds_bytes = 0;  // >0 if the whole-level LDS kernel can hold x and f
-    int num_cu = 256;      // compute units of the handle's device (grid sizing; MI355X: 256)
-    uint32_t paths = 0;    // PathFlag bits of the handle (MGMC_DISABLE)
-    bool zsweep = false;   // fused z-marching red-black sweep available
-    bool pairs = false;    // Galerkin level swept in colour-pair passes (mgmc_gsweep.hpp)
-    bool quads = false;    // ... two pairs per launch, out of place (k_sweep_quads, or k_jsweep_half:)
-    bool jsweep = false;   // ... j-marching half-sweeps (mgmc_jsweep.hpp)
-    bool rb2d = false;     // 2D 5-point level: one-launch red-black sweep, out of place (k_rb2d)
-    bool field = false;    // per-vertex coefficients (mgmc_create_csr, mgmc_field.hpp)
-    bool sym = false;      // 27-point stencil bitwise reflection-symmetric: kernels fold it (stencil_coef<true>)
-    bool fold = false;     // ... and its residuals take the class-folded sum (fold27; not switched by MGMC_DISABLE)
-    FieldArg F;            // ... their device field, pattern and colouring
-    double* rbuf = nullptr;  // ... residual scratch (padded layout, zero boundary)
-    bool pingpong() const { return zsweep || quads || rb2d; }  // out-of-place sweeps: x <-> x2
-    double* buf(int i) const { return i == 0 ? x : x2; }
-    LowRankDev lr;
-};
-
-void free_lowrank(LowRankDev& lr) {
-    for (void* p : lr.allocs) hipFree(p);
-    lr = LowRankDev();
-}
-
-}  // namespace
-
-// handles alive in this process (mgmc_live_handles): every mgmc_handle counts itself
-static std::atomic<int> g_live_handles{0};
-struct LiveHandleCount {
-    LiveHandleCount() { g_live_handles.fetch_add(1); }
-    ~LiveHandleCount() { g_live_handles.fetch_sub(1); }
-    LiveHandleCount(const LiveHandleCount&) = delete;
-    LiveHandleCount& operator=(const LiveHandleCount&) = delete;
-};
-
-struct mgmc_handle {
-    LiveHandleCount live;
-    mgmc_config cfg;
-    int device = 0;
-    uint64_t seed = 0, chain = 0;   // chain = the first chain of a batch (mgmc_create_batch)
-    int nchains = 1;                // chains of the batch: level vectors, QoI series and moments
-                                    // are nchains copies, L.nstore / capacity / 4 doubles apart
-    RngKey key;
-    std::vector<Level> levels;
-    hipStream_t stream = nullptr;
-    uint64_t* ctrl = nullptr;       // [0] sample index [1] series length [2] qoi index [3] scratch sample
-    double* mom = nullptr;          // running (n, mean, M2, pad) per chain
-    double* series = nullptr;
-    uint64_t series_cap = 0;
-    double* lex_tmp = nullptr;      // staging buffer in reference layout (device)
-    size_t lex_cap = 0;
-    std::vector<Op> ops;            // one sample
-    size_t seg_end_pre = 0, seg_begin_post = 0, seg_end_post = 0;  // fine-sweep segments
-    hipGraphExec_t graph_all = nullptr;
-    hipGraphExec_t graph_unroll = nullptr;  // unroll copies of the cycle in one graph (sample loops)
-    // the cycle with four event-record nodes (before the fine pre-sampler, after it, before the fine
-    // post-sampler, after the QoI record): mgmc_sample_timed points them at per-step events
-    hipGraph_t graph_timed_src = nullptr;
-    hipGraphExec_t graph_timed = nullptr;
-    hipGraphNode_t timed_node[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t timed_ev0[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-    int unroll = 1;
-    int64_t qoi_store_index = -1;   // padded offset of the QoI vertex, -1 none, -2 the QoI vector
-    // QoI vector b (mgmc_set_qoi_vector): padded offsets, values, block partials [nchains][nblk]
-    long long* qv_off = nullptr;
-    double* qv_val = nullptr;
-    double* qv_part = nullptr;
-    long long qv_n = 0;
-    int qv_nblk = 0;
-    std::string last_error;
-    ncclComm_t comm = nullptr;
-    int nranks = 1, rank = 0;
-    double* comm_buf = nullptr;  // device scratch for collectives
-    uint32_t paths = 0;          // PathFlag bits (MGMC_DISABLE)
-    int unroll_override = 0;     // MGMC_GRAPH_UNROLL (cycles per sample-loop graph launch; 0 = by size)
-    double2* zbuf = nullptr;           // the coarse SSOR sampler's pre-drawn Box-Muller pairs [chain][item]
-    long long zbuf_n = 0;              // items per chain
-    std::vector<TailArgs*> tail_args;  // device copies, one per OP_TAIL
-    std::vector<size_t> tail_lds;      // dynamic LDS bytes per OP_TAIL
-    std::vector<char> tail_sym;        // ... every level of it has a symmetric 27-point stencil (k_tail<3, true>)
-    // per OP_TAIL: its sweeps' Box-Muller pairs, drawn by spare workgroups of the restriction launch
-    // before it (nullptr: the tail draws them); the jobs (device) and items per chain
-    std::vector<double2*> tail_zb;
-    std::vector<TailNoiseJob*> tail_jobs;
-    std::vector<int> tail_njobs;
-    std::vector<long long> tail_zn;
-    double* sv[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // solver: b x r z p q (level 0)
-    double* sv_scal = nullptr;   // solver scalars
-    double* sv_part = nullptr;   // reduction partials
-    std::vector<LRColumn> lr_cols;  // low-rank columns of the coarsest level, and Sigma (for the factors)
-    std::vector<double> lr_sigma;
-    bool field_mode = false;     // hierarchy built from a matrix (mgmc_create_csr)
-    CsrHost coarse_csr;          // ... and its coarsest level (dense Cholesky factors)
-    int chol_n = 0;              // Cholesky factors of the coarsest level (mgmc_cholesky.hpp)
-    double* chol_G = nullptr;    // dense: G and L^{-1}
-    double* chol_Li = nullptr;
-    int chol_B = 0, chol_nb = 0; // blocked banded (chol_B > 0): Cf, Cb, Df, Db in one allocation
-    double* chol_blk = nullptr;
-    bool unusable = false;       // a failed mgmc_set_lowrank could not restore the prior's coarse factor
-    bool poison = false;         // MGMC_POISON=1: NaN-filled scratch allocations and LDS (debug, poison_fill)
-    unsigned long long* tail_prof = nullptr;  // (timing builds, MGMC_TAIL_PROF: the first tail's phase stamps)
-    std::vector<TailOp> tail_prof_ops;
-};
-
-#define HIPCHK(h, call)                                                                            \
-    do {                                                                                             \
-        hipError_t e_ = (call);                                                                      \
-        if (e_ != hipSuccess) {                                                                      \
-            std::string m_ = std::string("HIP error ") + hipGetErrorString(e_) + " at " #call;       \
-            if (h) (h)->last_error = m_;                                                             \
-            set_global_error(m_);                                                                    \
-            return MGMC_E_HIP;                                                                       \
-        }                                                                                            \
-    } while (0)
-
-static int fail(mgmc_handle* h, int code, const std::string& msg) {
-    if (h) h->last_error = msg;
-    set_global_error(msg);
-    return code;
-}
-
-// Debug poison (MGMC_POISON=1, read at mgmc_create*): every device buffer the library does not zero
-// or fill completely at allocation (noise buffers, the QoI series, dot partials, staging, solver
-// scratch) is filled with 0xFF bytes (a NaN pattern), and every op of a captured cycle graph is
-// preceded by k_lds_poison, which fills the LDS of every CU with NaN.  A kernel that reads device
-// memory or LDS that no kernel of the cycle wrote -- recycled allocations, the previous kernel's LDS
-// -- then carries a NaN into the chain and the non-finite guard reports it (MGMC_E_NONFINITE).
-static void poison_fill(const mgmc_handle* h, void* p, size_t bytes) {
-    if (h && h->poison && p && bytes) (void)hipMemsetAsync(p, 0xFF, bytes, h->stream);
-}
+}  // namespace mgmc_host
 
 namespace {
 constexpr int LDS_POISON_DOUBLES = 80 * 1024 / 8;  // two 1024-thread workgroups of 80 KB fill a CU's 160 KB
@@ -392,7 +42,7 @@ __global__ void __launch_bounds__(256) k_poison_interior(Layout L, double* __res
 // ------------------------------------------------------------------------------------------
 // launch helpers
 // ------------------------------------------------------------------------------------------
-namespace {
+namespace mgmc_host {
 
 dim3 grid3(int nthreads_x, int nrows_y, int nz_blocks, dim3 block) {
     return dim3((unsigned)((nthreads_x + block.x - 1) / block.x), (unsigned)((nrows_y + block.y - 1) / block.y),
@@ -468,7 +118,7 @@ void launch_fsweep(const Level& lv, double* x, const double* f, const GibbsArg& 
 }
 
 void launch_sweep(const Level& lv, double* x, const double* f, const GibbsArg& g0, int direction, bool noise,
-                  hipStream_t s, int nch = 1) {
+                  hipStream_t s, int nch) {
     if (nch > 1) {  // batched chains on the generic colour-pass kernels: one launch sequence per chain
         for (int c = 0; c < nch; ++c) {
             GibbsArg g = g0;
@@ -539,10 +189,9 @@ static int zsweep_depth(const Level& lv, int ty, int tzmax) {
 // tiles are faster)
 static int zsweep_plain_rows(const Level& lv, int nch) {
     const int tz = zsweep_depth(lv, ZS_TY, ZS_TZ);
-    const bool zpairs = !(lv.paths & PATH_NO_ZPAIRS);
-    auto ntiles = [&](int ty) {
+    auto ntiles = [&](int ty) {  // (z-chunk pairs: an odd chunk count padded by one empty tile per column)
         const long long nz = (lv.L.nz - 1 + tz - 1) / tz;
-        return (long long)((lv.L.nx / 2) / ZS_XP) * ((lv.L.ny - 1 + ty - 1) / ty) * (zpairs ? (nz + 1) / 2 * 2 : nz) * nch;
+        return (long long)((lv.L.nx / 2) / ZS_XP) * ((lv.L.ny - 1 + ty - 1) / ty) * ((nz + 1) / 2 * 2) * nch;
     };
     const long long slots = 2LL * lv.num_cu;
     return (ZS_TYP != ZS_TY && ZS_NTP == ZS_NT && ntiles(ZS_TY) < slots && ntiles(ZS_TYP) <= slots) ? ZS_TYP : ZS_TY;
@@ -573,7 +222,7 @@ void launch_zsweep(const Level& lv, const double* xin, double* xout, const doubl
         return;
     }
     a.tz = zsweep_depth(lv, ZS_TY, ZS_TZ);
-    a.zpairs = (lv.paths & PATH_NO_ZPAIRS) ? 0 : 1;
+    a.zpairs = 1;  // z-chunks in up / down pairs (mgmc_zsweep.hpp)
     if (zsweep_plain_rows(lv, nch) != ZS_TY) {
         launch_zsweep_t<ZS_XP, ZS_TYP, ZS_NTP, ZS_MINWP>(lv, a, false, s, nch);
         return;
@@ -779,8 +428,7 @@ void launch_pairs(const Level& lv, double* x, const double* f, const GibbsArg& g
 // the coarse SSOR sampler's right-hand sides are precomputed when they fit next to x and f
 bool coarse_precompute(const Level& lv, int nsweeps) {
     const long long ndof = (long long)(lv.L.nx - 1) * (lv.L.ny - 1) * (lv.spec.dim == 3 ? lv.L.nz - 1 : 1);
-    return lv.lds_bytes + (size_t)nsweeps * ndof * sizeof(double) <= 150 * 1024 &&
-           !(lv.paths & PATH_NO_COARSE_PRECOMPUTE);
+    return lv.lds_bytes + (size_t)nsweeps * ndof * sizeof(double) <= 150 * 1024;
 }
 
 // zb: its Box-Muller pairs drawn by the launch before (nullptr: drawn here)
@@ -812,15 +460,6 @@ void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStrea
 #undef MGMC_COARSE_LAUNCH
 }
 
-struct TailNoiseLaunch {  // spare workgroups of the launch draw a tail's noise (ZRestrictArgs)
-    const TailNoiseJob* jobs;
-    int njobs;
-    double2* zb;
-    long long zbs;
-    RngKey key;
-    uint32_t chain0, seed_hi;
-    const uint64_t* sample;
-};
 
 template <int NPTS, int CX, int CY, int NT, bool SYM = false, bool LRF = false>
 void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, const double* f, double* fc, double* xc,
@@ -906,8 +545,8 @@ bool zres_lrf_capable(const Level& lf, const Level& lc) {
 
 // lr (non-null): the level's right-hand side is read in place (LRRhsArg; zres_lrf_capable levels only)
 void launch_residual_restrict(const Level& lf, const Level& lc, const double* x, const double* f, double* fc,
-                              double* xc, int zero_xc, hipStream_t s, int nch = 1, const TailNoiseLaunch* tn = nullptr,
-                              bool skip_xc = false, const LRRhsArg* lr = nullptr) {
+                              double* xc, int zero_xc, hipStream_t s, int nch, const TailNoiseLaunch* tn,
+                              bool skip_xc, const LRRhsArg* lr) {
     const bool zr = lf.spec.dim == 3 && zero_xc && !lf.field && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8;
     if (nch > 1 && !zr) {  // batched chains on the generic kernels: one launch per chain
         for (int c = 0; c < nch; ++c)
@@ -1024,7 +663,7 @@ void launch_qrestrict(const Level& lv, const Level& lc, const double* xin, doubl
 }
 
 void launch_prolongate(const Level& lf, const Level& lc, double* x, const double* xc, double alpha, hipStream_t s,
-                       int nch = 1) {
+                       int nch) {
     dim3 block(64, 4, 1);
     const int zper = lf.spec.dim == 3 ? lf.L.nz - 1 : 1;  // batched chains: blockIdx.z = chain * zper + plane
     dim3 grid = grid3(lf.L.nx / 2, lf.L.ny - 1, zper * nch, block);
@@ -1072,9 +711,9 @@ void launch_pack(const Level& lv, const double* lex, double* pad, bool pack, hip
 // ---- low-rank part (mgmc_lowrank.hpp) ----
 // w = (sc_k B_k)^T v for all columns
 // (batched chains: v cs apart; the partials nblk and w m apart per chain)
-void lr_dots(const Level& lv, const double* v, const double* sc, hipStream_t s, int nch = 1) {
+void lr_dots(const Level& lv, const double* v, LRScale scale, hipStream_t s, int nch) {
     const LowRankDev& r = lv.lr;
-    const int sel = sc == r.sc_one ? 0 : 1;  // (the two scale vectors, LRBlock::sc; callers pass one of them)
+    const int sel = (int)scale;
     // few wavefronts (coarse levels): the staged kernel (the loads of a block in flight at once);
     // many: one wavefront per block, column values read once per group of chains
     const long long waves = (long long)r.nblk * ((nch + LRP_CH - 1) / LRP_CH);
@@ -1129,7 +768,7 @@ void lr_patch(const mgmc_handle* h, const Level& lv, int mode, double* y, uint32
 // the local rows and the chains' dense-only patch goes to lr.rhs_e; *inplace tells the consumer
 // kernel how to read f (returned; post_tag unused: the first post-sweep's patch is lr_restore_patch's)
 double* lr_rhs(const mgmc_handle* h, const Level& lv, int mode, double* f, uint32_t tag, const uint64_t* sample,
-               hipStream_t s, int nch = 1, int64_t post_tag = -1, LRRhsArg* inplace = nullptr) {
+               hipStream_t s, int nch, int64_t post_tag, LRRhsArg* inplace) {
     const LowRankDev& r = lv.lr;
     if (!r.dense_path) {
         lr_patch(h, lv, mode, f, tag, sample, s, nch);
@@ -1176,9 +815,9 @@ double* lr_rhs(const mgmc_handle* h, const Level& lv, int mode, double* f, uint3
 // after a sweep in `direction`: x -= B_bar (B^T x) (sor_smoother.cc:47-51); restores f_restore
 // on the rows of B when the sweep ran on a noise-patched f (not on the dense-column path, whose
 // sweeps read r.fe)
-void lr_fix(const Level& lv, double* x, int direction, double* f_restore, hipStream_t s, int nch = 1) {
+void lr_fix(const Level& lv, double* x, int direction, double* f_restore, hipStream_t s, int nch) {
     const LowRankDev& r = lv.lr;
-    lr_dots(lv, x, r.sc_one, s, nch);
+    lr_dots(lv, x, LR_SCALE_ONE, s, nch);
     const int d = direction == MGMC_FORWARD ? 0 : 1;
     if (r.dense_path) {
         LRDenseUpdateArgs a;
@@ -1247,7 +886,7 @@ void lr_small(const mgmc_handle* h, const Level& lv, double* x, int direction, i
     a.chain0 = (uint32_t)h->chain;
     a.seed_hi = (uint32_t)(h->seed >> 32);
     // k_lr_small_pf: one entry per lane, <= 8 columns, <= 2 rows of B_bar and of B per thread
-    if (r.m <= 8 && r.max_col_n <= 64 && a.nbar <= 2048 && a.nrows <= 2048 && !(lv.paths & PATH_NO_LR_PREFETCH))
+    if (r.m <= 8 && r.max_col_n <= 64 && a.nbar <= 2048 && a.nrows <= 2048)
         hipLaunchKernelGGL((k_lr_small_pf<8, 2>), dim3(nch), dim3(1024), 0, s, a);
     else
         hipLaunchKernelGGL(k_lr_small, dim3(nch), dim3(1024), 0, s, a);
@@ -1295,7 +934,7 @@ void lr_restore_patch(const mgmc_handle* h, const Op& op, const Level& lv, const
     if (nb > 0) hipLaunchKernelGGL(k_lr_restore_patch, dim3(nb, 1, nch), dim3(256), 0, s, a);
 }
 
-void lr_restore(const Level& lv, double* f, hipStream_t s, int nch = 1, bool patched = false) {
+void lr_restore(const Level& lv, double* f, hipStream_t s, int nch, bool patched) {
     const LowRankDev& r = lv.lr;
     // dense-column path: f was never patched, unless read in place (patched)
     if (r.nrows == 0 || (r.dense_path && !patched)) return;
@@ -1321,7 +960,7 @@ void launch_operator_apply(const mgmc_handle* h, const Level& lv, const double* 
     else
         hipLaunchKernelGGL((k_operator_apply<2, 9>), grid, block, 0, s, lv.L, xs, ys, lv.S);
     if (lv.lr.m > 0) {  // y += B (Sigma^{-1} B^T x)  (linear_operator.hh:71-75)
-        lr_dots(lv, xs, lv.lr.sc_inv, s);
+        lr_dots(lv, xs, LR_SCALE_INV, s);
         lr_rhs(h, lv, LR_PATCH_APPLY, ys, 0, h->ctrl + 3, s);
     }
 }
@@ -1329,7 +968,7 @@ void launch_operator_apply(const mgmc_handle* h, const Level& lv, const double* 
 // coarsest level: x = G f (+ U xi) with the dense Cholesky factors, or the blocked banded solves
 // (mgmc_cholesky.hpp)
 void launch_coarse_chol(const mgmc_handle* h, const Level& lv, const double* f, double* x, bool noise, uint32_t tag,
-                        const uint64_t* sample, hipStream_t s, int nch = 1) {
+                        const uint64_t* sample, hipStream_t s, int nch) {
     if (h->chol_B > 0) {
         CholBlockArgs b;
         b.L = lv.L;
@@ -1731,7 +1370,7 @@ int build_tails_only(mgmc_handle* h) {
         std::vector<TailNoiseJob> jobs;
         long long zn = 0;
         const bool pre_zr = !out.empty() && out.back().kind == OP_RESIDUAL_RESTRICT && out.back().level == lt - 1 &&
-                            zr_small_path(h, lt - 1) && h->levels[lt - 1].lr.m == 0 && !(h->paths & PATH_NO_TAIL_NOISE);
+                            zr_small_path(h, lt - 1) && h->levels[lt - 1].lr.m == 0;
         for (int o = 0; o < A.nops; ++o) {
             TailOp& t = A.ops[o];
             t.zoff = -1;
@@ -1972,7 +1611,7 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                 double* fr = lv.f;
                 LRRhsArg lrr{nullptr};  // (rhs_inplace: f read in place, as lrr says)
                 if (lr && !op.lr_skip_patch) {  // r = (f - B Sigma^{-1} B^T x) - A x
-                    lr_dots(lv, lv.buf(op.src), lv.lr.sc_inv, s, nch);
+                    lr_dots(lv, lv.buf(op.src), LR_SCALE_INV, s, nch);
                     fr = lr_rhs(h, lv, LR_PATCH_RESIDUAL, lv.f, 0, sample, s, nch,
                                 lv.lr.dense_path && op.lr_post_patch ? (int64_t)op.lr_post_tag : -1,
                                 lv.lr.rhs_inplace && op.zpre == 0 ? &lrr : nullptr);
@@ -2175,8 +1814,11 @@ int download(mgmc_handle* h, int level, const double* pad, double* host) {
     return MGMC_OK;
 }
 
-// a handle whose mgmc_set_lowrank rollback failed refuses all work but mgmc_destroy
-static int refuse_unusable(mgmc_handle* h) {
+// a handle whose mgmc_set_lowrank rollback failed refuses every call that runs the cycle or
+// needs the coarse factor: mgmc_apply, mgmc_sample*, mgmc_sample_timed*, mgmc_solve, and the per-level
+// component calls (check_level); a later successful mgmc_set_lowrank clears it.  State, right-hand side,
+// QoI and RCCL calls do not touch the factor and stay available, as does mgmc_destroy.
+int refuse_unusable(mgmc_handle* h) {
     return fail(h, MGMC_E_INVALID, "handle unusable: a failed mgmc_set_lowrank could not restore the prior's coarse "
                                    "factor (mgmc_destroy it)");
 }
@@ -2187,121 +1829,6 @@ int check_level(mgmc_handle* h, int level, bool need_coarser) {
     if (level < 0 || level >= (int)h->levels.size()) return fail(h, MGMC_E_INVALID, "level out of range");
     if (need_coarser && level + 1 >= (int)h->levels.size())
         return fail(h, MGMC_E_INVALID, "level has no coarser level");
-    return MGMC_OK;
-}
-
-// banded precision of the coarsest level (+ B Sigma^{-1} B^T: cholesky_sampler.cc:30-36, the oracle's
-// order), its Cholesky factor (mgmc_cholesky.hpp, bitwise the dense loop) and either the dense
-// inverses G, L^{-1} (n <= CHOL_MAX_N, O(n^3) on the host) or the blocked banded solve's blocks
-// (above, or MGMC_DISABLE=chol_dense; O(n bw^2)).  The bandwidth is the widest nonzero coupling:
-// matrix / stencil entries and the row span of each low-rank column (the oracle computes the same).
-int build_coarse_chol(mgmc_handle* h, const std::vector<LRColumn>* cols, const double* sigma, int m) {
-    const Level& lv = h->levels.back();
-    const long long n = (long long)lv.spec.ndof;
-    const bool blocked = n > CHOL_MAX_N || (h->paths & PATH_NO_CHOL_DENSE);
-    const int dim = lv.spec.dim;
-    const int nx = lv.spec.n[0], ny = lv.spec.n[1], nz = dim == 3 ? lv.spec.n[2] : 2;
-    // the couplings (row, column, value) of the level's matrix, in the dense assembly's order
-    auto for_each_entry = [&](auto&& fn) {
-        if (h->field_mode) {  // the coarsest Galerkin matrix itself
-            const CsrHost& A = h->coarse_csr;
-            for (long long r = 0; r < n; ++r)
-                for (int64_t q = A.rowptr[r]; q < A.rowptr[r + 1]; ++q) fn(r, (long long)A.col[q], A.val[q]);
-            return;
-        }
-        for (long long r = 0; r < n; ++r) {
-            const int i = (int)(r % (nx - 1)) + 1, j = (int)((r / (nx - 1)) % (ny - 1)) + 1;
-            const int k = dim == 3 ? (int)(r / ((long long)(nx - 1) * (ny - 1))) + 1 : 1;
-            for (int dz = (dim == 3 ? -1 : 0); dz <= (dim == 3 ? 1 : 0); ++dz)
-                for (int dy = -1; dy <= 1; ++dy)
-                    for (int dx = -1; dx <= 1; ++dx) {
-                        const int ii = i + dx, jj = j + dy, kk = k + dz;
-                        if (ii < 1 || ii > nx - 1 || jj < 1 || jj > ny - 1 || (dim == 3 && (kk < 1 || kk > nz - 1)))
-                            continue;
-                        const double v = dim == 3 ? lv.spec.st[(dz + 1) * 9 + (dy + 1) * 3 + (dx + 1)]
-                                                  : lv.spec.st[(dy + 1) * 3 + (dx + 1)];
-                        fn(r, ((long long)(dim == 3 ? kk - 1 : 0) * (ny - 1) + (jj - 1)) * (nx - 1) + (ii - 1), v);
-                    }
-        }
-    };
-    long long bw = 0;
-    for_each_entry([&](long long r, long long c, double v) {
-        if (v != 0.0) bw = std::max(bw, r > c ? r - c : c - r);
-    });
-    for (int k = 0; k < m; ++k) {
-        long long lo = n, hi = -1;
-        for (const auto& e : (*cols)[k].ent)
-            if (e.second != 0.0) {
-                lo = std::min(lo, (long long)e.first);
-                hi = std::max(hi, (long long)e.first);
-            }
-        if (hi > lo) bw = std::max(bw, hi - lo);
-    }
-    const long long B = chol_block_size(bw);
-    if (blocked && B > CHOL_BLOCK_MAX)
-        return fail(h, MGMC_E_UNSUPPORTED,
-                    "coarse Cholesky: " + std::to_string(n) + " unknowns (above " + std::to_string(CHOL_MAX_N) +
-                        ") need a bandwidth of at most " + std::to_string(CHOL_BLOCK_MAX) + ", this level has " +
-                        std::to_string(bw));
-    if (!blocked && n > CHOL_MAX_N)
-        return fail(h, MGMC_E_UNSUPPORTED, "coarse Cholesky: too many unknowns");
-    // the banded host factor costs n bw^2 / 2 multiply-adds: refuse what would take more than a few
-    // minutes on one core (3D 128^3 nlevel 2: 63^3 unknowns, bandwidth 4033 -- a fill-reducing sparse
-    // factorisation, the reference's CHOLMOD, is the tool for such levels)
-    if (blocked && (double)n * (double)bw * (double)bw > CHOL_HOST_WORK_MAX)
-        return fail(h, MGMC_E_UNSUPPORTED,
-                    "coarse Cholesky: " + std::to_string(n) + " unknowns of bandwidth " + std::to_string(bw) +
-                        " exceed the banded factor's host work limit (n bw^2 <= " +
-                        std::to_string((long long)CHOL_HOST_WORK_MAX) + "); use more levels");
-    const long long W = bw + 1;
-    std::vector<double> band((size_t)(n * W), 0.0);
-    for_each_entry([&](long long r, long long c, double v) {
-        if (c <= r && r - c <= bw) band[(size_t)(r * W + (c - r + bw))] = v;
-    });
-    if (m > 0) {
-        std::vector<double> Bd((size_t)n * m, 0.0);
-        for (int k = 0; k < m; ++k)
-            for (const auto& e : (*cols)[k].ent) Bd[(size_t)e.first * m + k] = e.second;
-        for (long long i = 0; i < n; ++i)
-            for (long long j = std::max(0LL, i - bw); j <= i; ++j) {
-                double s = 0.0;
-                for (int k = 0; k < m; ++k) s += Bd[(size_t)i * m + k] / sigma[k] * Bd[(size_t)j * m + k];
-                band[(size_t)(i * W + (j - i + bw))] += s;
-            }
-    }
-    if (!chol_band_factor(band, n, bw)) return fail(h, MGMC_E_INVALID, "coarse precision is not positive definite");
-    if (h->chol_G) hipFree(h->chol_G);
-    if (h->chol_Li) hipFree(h->chol_Li);
-    if (h->chol_blk) hipFree(h->chol_blk);
-    h->chol_G = h->chol_Li = h->chol_blk = nullptr;
-    h->chol_n = h->chol_B = h->chol_nb = 0;
-    if (blocked) {
-        std::vector<double> blk[4];
-        chol_blocks_host(band, n, bw, B, blk[0], blk[1], blk[2], blk[3]);
-        const size_t bytes = blk[0].size() * sizeof(double);
-        if (hipMalloc(&h->chol_blk, 4 * bytes) != hipSuccess) {
-            h->chol_blk = nullptr;
-            return fail(h, MGMC_E_NOMEM, "device allocation failed (blocked coarse Cholesky factors)");
-        }
-        for (int q = 0; q < 4; ++q)
-            HIPCHK(h, hipMemcpy(h->chol_blk + q * blk[0].size(), blk[q].data(), bytes, hipMemcpyHostToDevice));
-        h->chol_B = (int)B;
-        h->chol_nb = (int)((n + B - 1) / B);
-        h->chol_n = (int)n;
-        return MGMC_OK;
-    }
-    std::vector<double> Lm((size_t)n * n, 0.0);
-    for (long long i = 0; i < n; ++i)
-        for (long long c = std::max(0LL, i - bw); c <= i; ++c) Lm[(size_t)i * n + c] = band[(size_t)(i * W + (c - i + bw))];
-    std::vector<double>().swap(band);
-    std::vector<double> Li, G;
-    chol_inverses_host(Lm, n, Li, G);
-    const size_t bytes = (size_t)n * n * sizeof(double);
-    if (hipMalloc(&h->chol_G, bytes) != hipSuccess || hipMalloc(&h->chol_Li, bytes) != hipSuccess)
-        return fail(h, MGMC_E_NOMEM, "device allocation failed (coarse Cholesky factors)");
-    HIPCHK(h, hipMemcpy(h->chol_G, G.data(), bytes, hipMemcpyHostToDevice));
-    HIPCHK(h, hipMemcpy(h->chol_Li, Li.data(), bytes, hipMemcpyHostToDevice));
-    h->chol_n = (int)n;
     return MGMC_OK;
 }
 
@@ -2542,8 +2069,11 @@ static int create_impl(const mgmc_config* cfg, const CsrHost* csr, int device, u
         lv.L = make_layout(cfg->dim, specs[l].n,
                            h->field_mode && (fields[l].scheme == 9 || fields[l].scheme == 27));
         memcpy(lv.S.a, specs[l].st, sizeof(lv.S.a));
-        lv.fold = !h->field_mode && lv.spec.dim == 3 && stencil_reflection_symmetric(lv.S.a, lv.spec.npoints);
-        lv.sym = lv.fold && !(h->paths & PATH_NO_SYM);
+        // (MGMC_DISABLE=fold keeps the reference's CSR summation order in the residuals of these levels;
+        // sym stays: the Gibbs sweeps' arithmetic does not depend on it)
+        const bool refl = !h->field_mode && lv.spec.dim == 3 && stencil_reflection_symmetric(lv.S.a, lv.spec.npoints);
+        lv.fold = refl && !(h->paths & PATH_NO_FOLD);
+        lv.sym = refl;
         const size_t bytes = lv.L.nstore * sizeof(double);
         const size_t cbytes = bytes * nchains;  // x, x2, f of every chain, L.nstore apart
         if (hipMalloc(&lv.x, cbytes) != hipSuccess || hipMalloc(&lv.f, cbytes) != hipSuccess) {
@@ -3299,7 +2829,7 @@ int mgmc_residual_restrict(mgmc_handle* h, int level, const double* f, const dou
     if ((rc = upload(h, level, x, lf.scratch[1]))) return rc;
     double* fr = lf.scratch[0];
     if (lf.lr.m > 0) {  // f - B Sigma^{-1} B^T x, then the residual kernel
-        lr_dots(lf, lf.scratch[1], lf.lr.sc_inv, h->stream);
+        lr_dots(lf, lf.scratch[1], LR_SCALE_INV, h->stream);
         fr = lr_rhs(h, lf, LR_PATCH_RESIDUAL, lf.scratch[0], 0, h->ctrl + 3, h->stream);
     }
     launch_residual_restrict(lf, lc, lf.scratch[1], fr, lc.scratch[0], lc.scratch[1], 1, h->stream);
@@ -3445,684 +2975,6 @@ int mgmc_sample_timed_stride(mgmc_handle* h, int nsteps, int stride, int64_t qoi
     *npost = cpost * nt;
     for (auto& e : ev) hipEventDestroy(e);
     return check_finite(h);
-}
-
-// ---------------- exact-statistics engine: multigrid-preconditioned solvers ----------------
-}  // extern "C"
-
-namespace {
-
-// x = M f: one deterministic multigrid cycle from x = 0 (MultigridPreconditioner::solve,
-// multigrid_preconditioner.cc:74-101) with the hierarchy's noise-free smoothers (B_bar fix
-// included) and ncoarsesmooth SSOR sweeps on the coarsest level.  Levels >= 1 work in their
-// scratch buffers; x of level 0 must be zero on entry.
-void mg_precond(mgmc_handle* h, int level, double* x, double* f, hipStream_t s) {
-    const mgmc_config& c = h->cfg;
-    Level& lv = h->levels[level];
-    auto sweep = [&](int dir) {
-        GibbsArg g = make_gibbs(h, lv, 0, 0, h->ctrl + 3);
-        launch_sweep(lv, x, f, g, dir, false, s);
-        if (lv.lr.m > 0) lr_fix(lv, x, dir, nullptr, s);
-    };
-    if (level == (int)h->levels.size() - 1) {
-        if (h->chol_n > 0) {  // exact coarse solve, as the reference's CholeskySolver
-            launch_coarse_chol(h, lv, f, x, false, 0, h->ctrl + 3, s);
-            return;
-        }
-        for (int t = 0; t < c.ncoarsesmooth; ++t) {
-            sweep(MGMC_FORWARD);
-            sweep(MGMC_BACKWARD);
-        }
-        return;
-    }
-    Level& lc = h->levels[level + 1];
-    const int cycle_ = level > 0 ? c.cycle : 1;
-    for (int j = 0; j < cycle_; ++j) {
-        for (int t = 0; t < c.npresmooth; ++t) {
-            sweep(MGMC_FORWARD);
-            if (c.smoother == MGMC_SMOOTHER_SSOR) sweep(MGMC_BACKWARD);
-        }
-        double* fr = f;
-        if (lv.lr.m > 0) {
-            lr_dots(lv, x, lv.lr.sc_inv, s);
-            fr = lr_rhs(h, lv, LR_PATCH_RESIDUAL, f, 0, h->ctrl + 3, s);
-        }
-        launch_residual_restrict(lv, lc, x, fr, lc.scratch[1], lc.scratch[0], 1, s);  // zeroes x_{l+1}
-        if (lv.lr.m > 0) lr_restore(lv, f, s);
-        mg_precond(h, level + 1, lc.scratch[0], lc.scratch[1], s);
-        launch_prolongate(lv, lc, x, lc.scratch[0], c.coarse_scaling, s);
-        for (int t = 0; t < c.npostsmooth; ++t) {
-            if (c.smoother == MGMC_SMOOTHER_SSOR) sweep(MGMC_FORWARD);
-            sweep(MGMC_BACKWARD);
-        }
-    }
-}
-
-void dev_dot(mgmc_handle* h, const double* a, const double* b, int slot) {
-    const long long n = h->levels[0].L.nstore;
-    hipLaunchKernelGGL(k_dot_partial, dim3(SOLVE_NB), dim3(256), 0, h->stream, n, a, b, h->sv_part);
-    hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, h->stream, (const double*)h->sv_part, SOLVE_NB, h->sv_scal,
-                       slot);
-}
-
-int host_scalar(mgmc_handle* h, int slot, double* v) {
-    HIPCHK(h, hipMemcpyAsync(v, h->sv_scal + slot, sizeof(double), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    return MGMC_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-int mgmc_solve(mgmc_handle* h, int method, const double* b, double* x, double rtol, double atol, int maxiter,
-               int* iters, double* rnorm) {
-    if (!h || !b || !x || !iters || !rnorm) return fail(h, MGMC_E_INVALID, "null argument");
-    if (method != MGMC_SOLVER_LOOP && method != MGMC_SOLVER_CG) return fail(h, MGMC_E_INVALID, "invalid solver method");
-    if (maxiter < 0) return fail(h, MGMC_E_INVALID, "maxiter must be >= 0");
-    HIPCHK(h, hipSetDevice(h->device));
-    int rc;
-    for (size_t l = 1; l < h->levels.size(); ++l)
-        if ((rc = ensure_scratch(h, (int)l))) return rc;
-    Level& l0 = h->levels[0];
-    const long long n = l0.L.nstore;
-    const size_t bytes = (size_t)n * sizeof(double);
-    for (auto& p : h->sv) {
-        if (!p) {
-            if (hipMalloc(&p, bytes) != hipSuccess) {
-                p = nullptr;
-                return fail(h, MGMC_E_NOMEM, "device allocation failed (solver vectors)");
-            }
-            HIPCHK(h, hipMemsetAsync(p, 0, bytes, h->stream));
-        }
-    }
-    // MultigridPreconditioner always solves the coarsest level exactly (Cholesky,
-    // multigrid_preconditioner.cc:41-45): build the dense factors if the level is small enough
-    if (h->chol_n == 0 && h->levels.back().spec.ndof <= 2048) {
-        if ((rc = build_coarse_chol(h, h->lr_cols.empty() ? nullptr : &h->lr_cols, h->lr_sigma.data(),
-                                    (int)h->lr_cols.size())))
-            return rc;
-    }
-    if (!h->sv_scal) {
-        HIPCHK(h, hipMalloc(&h->sv_scal, 16 * sizeof(double)));
-        poison_fill(h, h->sv_scal, 16 * sizeof(double));
-    }
-    if (!h->sv_part) {
-        HIPCHK(h, hipMalloc(&h->sv_part, SOLVE_NB * sizeof(double)));
-        poison_fill(h, h->sv_part, SOLVE_NB * sizeof(double));
-    }
-    double *vb = h->sv[0], *vx = h->sv[1], *vr = h->sv[2], *vz = h->sv[3], *vp = h->sv[4], *vq = h->sv[5];
-    hipStream_t s = h->stream;
-    const dim3 gv(4096), bv(256);
-    if ((rc = upload(h, 0, b, vb))) return rc;
-    HIPCHK(h, hipMemsetAsync(vx, 0, bytes, s));
-    dev_dot(h, vb, vb, 4);
-    double bb = 0.0;
-    if ((rc = host_scalar(h, 4, &bb))) return rc;
-    const double r0 = sqrt(bb);
-    *iters = 0;
-    *rnorm = r0;
-    if (r0 == 0.0) return download(h, 0, vx, x);
-    if (method == MGMC_SOLVER_LOOP) {  // LoopSolver::apply (loop_solver.cc:9-53): x -= M (A x - b)
-        for (int k = 0; k < maxiter; ++k) {
-            launch_operator_apply(h, l0, vx, vq, s);
-            hipLaunchKernelGGL(k_sub, gv, bv, 0, s, n, (const double*)vq, (const double*)vb, vr);
-            dev_dot(h, vr, vr, 2);
-            double rr;
-            if ((rc = host_scalar(h, 2, &rr))) return rc;
-            *rnorm = sqrt(rr);
-            *iters = k;
-            if (*rnorm / r0 < rtol && *rnorm < atol) break;
-            HIPCHK(h, hipMemsetAsync(vz, 0, bytes, s));
-            mg_precond(h, 0, vz, vr, s);
-            hipLaunchKernelGGL(k_sub, gv, bv, 0, s, n, (const double*)vx, (const double*)vz, vx);
-            *iters = k + 1;
-        }
-    } else {  // conjugate gradients preconditioned by the same multigrid cycle
-        HIPCHK(h, hipMemcpyAsync(vr, vb, bytes, hipMemcpyDeviceToDevice, s));
-        HIPCHK(h, hipMemsetAsync(vz, 0, bytes, s));
-        mg_precond(h, 0, vz, vr, s);
-        HIPCHK(h, hipMemcpyAsync(vp, vz, bytes, hipMemcpyDeviceToDevice, s));
-        dev_dot(h, vr, vz, 0);  // rz
-        for (int k = 0; k < maxiter; ++k) {
-            launch_operator_apply(h, l0, vp, vq, s);
-            dev_dot(h, vp, vq, 1);  // pq
-            hipLaunchKernelGGL(k_axpy_ratio, gv, bv, 0, s, n, (const double*)h->sv_scal, (const double*)(h->sv_scal + 1),
-                               1.0, (const double*)vp, vx);
-            hipLaunchKernelGGL(k_axpy_ratio, gv, bv, 0, s, n, (const double*)h->sv_scal, (const double*)(h->sv_scal + 1),
-                               -1.0, (const double*)vq, vr);
-            dev_dot(h, vr, vr, 2);
-            double rr;
-            if ((rc = host_scalar(h, 2, &rr))) return rc;
-            *rnorm = sqrt(rr);
-            *iters = k + 1;
-            if (*rnorm / r0 < rtol && *rnorm < atol) break;
-            HIPCHK(h, hipMemsetAsync(vz, 0, bytes, s));
-            mg_precond(h, 0, vz, vr, s);
-            dev_dot(h, vr, vz, 3);  // rz_new
-            hipLaunchKernelGGL(k_xpby_ratio, gv, bv, 0, s, n, (const double*)vz, (const double*)(h->sv_scal + 3),
-                               (const double*)h->sv_scal, vp);
-            HIPCHK(h, hipMemcpyAsync(h->sv_scal, h->sv_scal + 3, sizeof(double), hipMemcpyDeviceToDevice, s));
-        }
-    }
-    HIPCHK(h, hipGetLastError());
-    return download(h, 0, vx, x);
-}
-
-// ---------------- low-rank posterior part ----------------
-}  // extern "C"
-
-namespace {
-
-long long ref_to_layout(const Level& lv, const Layout& L, long long row) {
-    const long long nxi = lv.L.nx - 1, nyi = lv.L.ny - 1;
-    const int i = (int)(row % nxi) + 1;
-    const long long r = row / nxi;
-    const int j = (int)(r % nyi) + 1;
-    const int k = lv.spec.dim == 3 ? (int)(r / nyi) + 1 : 0;
-    return L.at(i, j, k);
-}
-long long ref_to_padded(const Level& lv, long long row) { return ref_to_layout(lv, lv.L, row); }
-int ref_to_tail(const Level& lv, long long row) { return (int)ref_to_layout(lv, tail_layout(lv.L), row); }
-
-template <class T>
-int lr_to_device(mgmc_handle* h, LowRankDev& r, T** dst, const std::vector<T>& src) {
-    *dst = nullptr;
-    if (src.empty()) return MGMC_OK;
-    if (hipMalloc((void**)dst, src.size() * sizeof(T)) != hipSuccess) {
-        *dst = nullptr;
-        return fail(h, MGMC_E_NOMEM, "device allocation failed (low-rank part)");
-    }
-    r.allocs.push_back(*dst);
-    HIPCHK(h, hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
-    return MGMC_OK;
-}
-
-// B_c = R B, column by column on the device restriction kernel (bitwise the oracle's restrict_)
-int lr_restrict_columns(mgmc_handle* h, int level, std::vector<LRColumn>& cols) {
-    Level& lf = h->levels[level];
-    Level& lc = h->levels[level + 1];
-    int rc;
-    if ((rc = ensure_scratch(h, level)) || (rc = ensure_scratch(h, level + 1))) return rc;
-    std::vector<double> fine(lf.spec.ndof), coarse(lc.spec.ndof);
-    for (auto& col : cols) {
-        std::fill(fine.begin(), fine.end(), 0.0);
-        for (const auto& e : col.ent) fine[e.first] = e.second;
-        if ((rc = upload(h, level, fine.data(), lf.scratch[0]))) return rc;
-        dim3 block(64, 4, 1);
-        dim3 grid = grid3(lc.L.nx - 1, lc.L.ny - 1, lf.spec.dim == 3 ? lc.L.nz - 1 : 1, block);
-        if (lf.spec.dim == 3)
-            hipLaunchKernelGGL((k_restrict<3>), grid, block, 0, h->stream, lf.L, lc.L, (const double*)lf.scratch[0],
-                               lc.scratch[0]);
-        else
-            hipLaunchKernelGGL((k_restrict<2>), grid, block, 0, h->stream, lf.L, lc.L, (const double*)lf.scratch[0],
-                               lc.scratch[0]);
-        HIPCHK(h, hipGetLastError());
-        if ((rc = download(h, level + 1, lc.scratch[0], coarse.data()))) return rc;
-        col.ent.clear();
-        for (long long i = 0; i < (long long)coarse.size(); ++i)
-            if (col.dense || coarse[i] != 0.0) col.ent.push_back({i, coarse[i]});
-    }
-    return MGMC_OK;
-}
-
-// device data of one level: columns, rows of B, and B_bar for both sweep directions
-// (sor_smoother.cc:17-37 with the multicolour splitting: Y = one noise-free multicolour sweep
-// from zero per column, M = Sigma + B^T Y, B_bar = Y M^{-1} on the rows where Y is nonzero)
-int lr_setup_level(mgmc_handle* h, int level, const std::vector<LRColumn>& cols, const double* sigma, int m) {
-    Level& lv = h->levels[level];
-    LowRankDev& r = lv.lr;
-    r.m = m;
-    const long long N = (long long)lv.spec.ndof;
-    int rc;
-    // columns: entry lists (sparse) or padded value arrays (dense), dot-product blocks
-    std::vector<LRColMeta> meta(m);
-    std::vector<int> blk_col;
-    std::vector<long long> ent_off;
-    std::vector<int> t_ent_off;
-    std::vector<double> ent_val;
-    int ndense = 0;
-    // a dense column of a level with at most LR_BLK vertices is one block either way: it is kept as
-    // an entry list (every row, ascending: the dense order), so the level can take the small-level
-    // kernels (k_lr_small, k_tail)
-    std::vector<char> dense_here(m);
-    for (int k = 0; k < m; ++k) dense_here[k] = cols[k].dense && N > LR_BLK;
-    for (int k = 0; k < m; ++k) {
-        const LRColumn& c = cols[k];
-        LRColMeta& mt = meta[k];
-        mt.n = (long long)c.ent.size();
-        r.max_col_n = std::max(r.max_col_n, mt.n);
-        mt.blk0 = (int)blk_col.size();
-        mt.nblk = (int)((mt.n + LR_BLK - 1) / LR_BLK);
-        mt.cflag = 0;
-        mt.cval = 0.0;
-        for (int b = 0; b < mt.nblk; ++b) blk_col.push_back(k);
-        if (dense_here[k]) {
-            mt.dense = ndense++;
-            mt.ent0 = 0;
-        } else {
-            mt.dense = -1;
-            mt.ent0 = (long long)ent_off.size();
-            for (const auto& e : c.ent) {
-                ent_off.push_back(ref_to_padded(lv, e.first));
-                t_ent_off.push_back(ref_to_tail(lv, e.first));
-                ent_val.push_back(e.second);
-            }
-        }
-    }
-    // a dense column whose every value is one number (bit for bit; the global average on the fine
-    // level, B_g = cell volume: measured_operator.cc:31-45) is read as that constant: no value array is
-    // streamed by the dots and the right-hand-side patches (8 bytes per vertex and launch)
-    for (int k = 0; k < m; ++k) {
-        if (!dense_here[k] || cols[k].ent.empty()) continue;
-        uint64_t b0;
-        memcpy(&b0, &cols[k].ent[0].second, 8);
-        bool same = true;
-        for (long long i = 0; i < N && same; ++i) {
-            uint64_t bi;
-            memcpy(&bi, &cols[k].ent[i].second, 8);
-            same = bi == b0;
-        }
-        if (same) {
-            meta[k].cflag = 1;
-            meta[k].cval = cols[k].ent[0].second;
-        }
-    }
-    r.nblk = (int)blk_col.size();
-    std::vector<LRBlock> blocks(blk_col.size());
-    for (int k = 0; k < m; ++k)
-        for (int b = 0; b < meta[k].nblk; ++b) {
-            LRBlock& B = blocks[(size_t)meta[k].blk0 + b];
-            B.e0 = (long long)b * LR_BLK;
-            B.cnt = (int)std::min<long long>(LR_BLK, meta[k].n - B.e0);
-            B.ent0 = meta[k].dense >= 0 ? 0 : meta[k].ent0 + B.e0;
-            B.k = k;
-            B.dense = meta[k].dense;
-            B.cflag = meta[k].cflag;
-            B.cval = meta[k].cval;
-            B.sc[0] = 1.0;
-            B.sc[1] = 1.0 / sigma[k];  // (the sc_inv values below)
-        }
-    if ((rc = lr_to_device(h, r, &r.blk, blocks))) return rc;
-    if ((rc = lr_to_device(h, r, &r.meta, meta)) || (rc = lr_to_device(h, r, &r.blk_col, blk_col)) ||
-        (rc = lr_to_device(h, r, &r.ent_off, ent_off)) || (rc = lr_to_device(h, r, &r.ent_val, ent_val)) ||
-        (rc = lr_to_device(h, r, &r.t_ent_off, t_ent_off)))
-        return rc;
-    if (ndense > 0) {
-        const size_t bytes = (size_t)ndense * lv.L.nstore * sizeof(double);
-        if (hipMalloc(&r.dense_val, bytes) != hipSuccess) return fail(h, MGMC_E_NOMEM, "device allocation failed");
-        r.allocs.push_back(r.dense_val);
-        HIPCHK(h, hipMemsetAsync(r.dense_val, 0, bytes, h->stream));
-        std::vector<double> v(N);
-        for (int k = 0; k < m; ++k) {
-            if (!dense_here[k]) continue;
-            for (long long i = 0; i < N; ++i) v[i] = cols[k].ent[i].second;
-            if ((rc = upload(h, level, v.data(), r.dense_val + (size_t)meta[k].dense * lv.L.nstore))) return rc;
-            HIPCHK(h, hipStreamSynchronize(h->stream));
-        }
-    }
-    // dense-column path: exactly one dense column (mgmc_lowrank.hpp k_lr_dense_*)
-    r.dense_path = ndense == 1 && !(h->paths & PATH_NO_LR_DENSE);
-    r.dense_g = -1;
-    for (int k = 0; k < m; ++k)
-        if (dense_here[k]) r.dense_g = k;
-    r.dense_const = r.dense_g >= 0 && meta[r.dense_g].cflag != 0;
-    r.split_g = ndense == 1 && r.dense_const ? r.dense_g : -1;  // (any path: the row lists too)
-    r.dense_cval = r.dense_g >= 0 ? meta[r.dense_g].cval : 0.0;
-    r.dense_slot = r.dense_g >= 0 ? meta[r.dense_g].dense : 0;
-    const int g = r.dense_path ? r.dense_g : -1;
-    // bit p of a skip mask over the padded store: set unless p is an interior vertex of `dense_only`
-    auto skip_mask = [&](const std::vector<char>& local, uint32_t** dst) {
-        std::vector<uint32_t> words((size_t)(lv.L.nstore + 31) / 32, 0xFFFFFFFFu);
-        for (long long i = 0; i < N; ++i)
-            if (!local[i]) {
-                const long long p = ref_to_padded(lv, i);
-                words[p >> 5] &= ~(1u << (p & 31));
-            }
-        return lr_to_device(h, r, dst, words);
-    };
-    // rows of B (ascending), with the row's coefficients of every column (dense-column path: the
-    // rows with an entry in a column other than g)
-    std::vector<int> slot(N, -1);
-    for (int k = 0; k < m; ++k)
-        if (k != g)
-            for (const auto& e : cols[k].ent) slot[e.first] = 0;
-    if (g >= 0) {
-        std::vector<char> local(N);
-        for (long long i = 0; i < N; ++i) local[i] = slot[i] == 0;
-        if ((rc = skip_mask(local, &r.skip_b))) return rc;
-        const size_t fb = (size_t)lv.L.nstore * h->nchains * sizeof(double);
-        for (double** q : {&r.fe, &r.fe2}) {
-            if (hipMalloc(q, fb) != hipSuccess) return fail(h, MGMC_E_NOMEM, "device allocation failed");
-            r.allocs.push_back(*q);
-            HIPCHK(h, hipMemsetAsync(*q, 0, fb, h->stream));
-        }
-        // the fine z-sweep level's kernels read the patched right-hand side in place (k_zsweep_rb7 /
-        // k_zresrestrict LRF) when B_g is one number
-        r.rhs_inplace = r.dense_path && r.split_g >= 0 && lv.zsweep && level + 1 < (int)h->levels.size() &&
-                        zres_lrf_capable(lv, h->levels[level + 1]);
-        if (r.rhs_inplace) {
-            std::vector<double> ez((size_t)2 * h->nchains, 0.0);
-            if ((rc = lr_to_device(h, r, &r.rhs_e, ez))) return rc;
-        }
-    }
-    int nrows = 0;
-    std::vector<long long> rows_off;
-    std::vector<int> t_rows_off;
-    for (long long i = 0; i < N; ++i)
-        if (slot[i] == 0) {
-            slot[i] = nrows++;
-            rows_off.push_back(ref_to_padded(lv, i));
-            t_rows_off.push_back(ref_to_tail(lv, i));
-        }
-    std::vector<double> coef((size_t)nrows * m, 0.0);
-    std::vector<uint64_t> mask(nrows, 0);
-    for (int k = 0; k < m; ++k)
-        for (const auto& e : cols[k].ent) {
-            const int u = slot[e.first];
-            if (u < 0) continue;  // a dense-only row (dense-column path)
-            coef[(size_t)u * m + k] = e.second;
-            mask[u] |= 1ull << k;
-        }
-    r.nrows = nrows;
-    // per-chain scratch of a batch: saved f (nrows), dot partials (nblk) and dots (m) per chain
-    std::vector<double> sc_one(m, 1.0), sc_inv(m), sq(m), zeros((size_t)std::max(nrows, 1) * h->nchains, 0.0);
-    for (int k = 0; k < m; ++k) {
-        sc_inv[k] = 1.0 / sigma[k];
-        sq[k] = sqrt(1.0 / sigma[k]);  // Sigma^{-1/2} (sor_sampler.cc:30-33)
-    }
-    if ((rc = lr_to_device(h, r, &r.rows_off, rows_off)) || (rc = lr_to_device(h, r, &r.rows_coef, coef)) ||
-        (rc = lr_to_device(h, r, &r.rows_mask, mask)) || (rc = lr_to_device(h, r, &r.save, zeros)) ||
-        (rc = lr_to_device(h, r, &r.sc_one, sc_one)) || (rc = lr_to_device(h, r, &r.sc_inv, sc_inv)) ||
-        (rc = lr_to_device(h, r, &r.sq, sq)) || (rc = lr_to_device(h, r, &r.t_rows_off, t_rows_off)))
-        return rc;
-    std::vector<double> partz((size_t)std::max(r.nblk, 1) * h->nchains, 0.0), wz((size_t)m * h->nchains, 0.0);
-    if ((rc = lr_to_device(h, r, &r.part, partz)) || (rc = lr_to_device(h, r, &r.w, wz))) return rc;
-
-    // B_bar for the forward and backward splittings
-    if ((rc = ensure_scratch(h, level))) return rc;
-    std::vector<double> Y((size_t)N * m), b(N), y(N), col(N);
-    for (int d = 0; d < 2; ++d) {
-        const int direction = d == 0 ? MGMC_FORWARD : MGMC_BACKWARD;
-        for (int l = 0; l < m; ++l) {
-            std::fill(b.begin(), b.end(), 0.0);
-            for (const auto& e : cols[l].ent) b[e.first] = e.second;
-            if ((rc = upload(h, level, b.data(), lv.scratch[0]))) return rc;
-            HIPCHK(h, hipMemsetAsync(lv.scratch[1], 0, lv.L.nstore * sizeof(double), h->stream));
-            GibbsArg g = make_gibbs(h, lv, 0, 0, h->ctrl + 3);
-            launch_sweep(lv, lv.scratch[1], lv.scratch[0], g, direction, false, h->stream);
-            HIPCHK(h, hipGetLastError());
-            if ((rc = download(h, level, lv.scratch[1], y.data()))) return rc;
-            for (long long i = 0; i < N; ++i) Y[(size_t)i * m + l] = y[i];
-        }
-        std::vector<double> M((size_t)m * m), Minv;
-        for (int l = 0; l < m; ++l) {
-            for (long long i = 0; i < N; ++i) col[i] = Y[(size_t)i * m + l];
-            for (int k = 0; k < m; ++k)
-                M[(size_t)k * m + l] = (k == l ? sigma[k] : 0.0) + lr_dot_host(cols[k], 1.0, col.data());
-        }
-        if (!lr_small_inverse(M, m, Minv))
-            return fail(h, MGMC_E_INVALID, "Sigma + B^T (L + D/omega)^{-1} B is singular");
-        std::vector<long long> boff;
-        std::vector<int> t_boff;
-        std::vector<double> bval;
-        r.nbar_all[d] = 0;
-        if (g >= 0) {  // dense-only rows: Y_il = 0 for every l != g; Y_g and row g of Minv on the device
-            std::vector<char> local(N);
-            for (long long i = 0; i < N; ++i) {
-                const double* yi = &Y[(size_t)i * m];
-                bool loc = false;
-                for (int l = 0; l < m; ++l) loc = loc || (l != g && yi[l] != 0.0);
-                local[i] = loc;
-                col[i] = yi[g];
-                if (!loc && yi[g] != 0.0) ++r.nbar_all[d];
-            }
-            if ((rc = skip_mask(local, &r.skip_y[d]))) return rc;
-            // the table form of Y_g (see LowRankDev::ykey): key = colour parity | neighbour mask << 1,
-            // every dense-only vertex of one key must hold the same bits, else Y_g is streamed
-            const int dim = lv.spec.dim;
-            if (r.dense_const && lv.spec.npoints == 2 * dim + 1 && !lv.field) {
-                const int n1 = lv.L.nx - 1, n2 = lv.L.ny - 1, n3 = dim == 3 ? lv.L.nz - 1 : 1;
-                std::vector<uint8_t> keys(N);
-                std::vector<double> tab(128, 0.0);
-                std::vector<char> seen(128, 0);
-                bool ok = true;
-                for (long long i = 0; i < N && ok; ++i) {
-                    const int ii = (int)(i % n1) + 1, jj = (int)((i / n1) % n2) + 1, kk = dim == 3 ? (int)(i / ((long long)n1 * n2)) + 1 : 0;
-                    int key = (ii + jj + kk) & 1;
-                    key |= (ii > 1 ? 2 : 0) | (ii < n1 ? 4 : 0) | (jj > 1 ? 8 : 0) | (jj < n2 ? 16 : 0);
-                    if (dim == 3) key |= (kk > 1 ? 32 : 0) | (kk < n3 ? 64 : 0);
-                    keys[i] = (uint8_t)key;
-                    if (local[i]) continue;
-                    if (!seen[key]) {
-                        seen[key] = 1;
-                        tab[key] = col[i];
-                    } else {
-                        ok = memcmp(&tab[key], &col[i], 8) == 0;
-                    }
-                }
-                if (ok) {
-                    if (!r.ykey) {  // keys over the padded store (0 elsewhere: masked by skip_y)
-                        std::vector<uint8_t> kp((size_t)lv.L.nstore + 16, 0);
-                        for (long long i = 0; i < N; ++i) kp[ref_to_padded(lv, i)] = keys[i];
-                        if ((rc = lr_to_device(h, r, &r.ykey, kp))) return rc;
-                    }
-                    if ((rc = lr_to_device(h, r, &r.ytab[d], tab))) return rc;
-                }
-            }
-            const size_t yb = (size_t)lv.L.nstore * sizeof(double);
-            if (hipMalloc(&r.yg[d], yb) != hipSuccess) return fail(h, MGMC_E_NOMEM, "device allocation failed");
-            r.allocs.push_back(r.yg[d]);
-            HIPCHK(h, hipMemsetAsync(r.yg[d], 0, yb, h->stream));
-            if ((rc = upload(h, level, col.data(), r.yg[d]))) return rc;
-            HIPCHK(h, hipStreamSynchronize(h->stream));
-            std::vector<double> mg(Minv.begin() + (size_t)g * m, Minv.begin() + (size_t)(g + 1) * m);
-            if ((rc = lr_to_device(h, r, &r.minv_g[d], mg))) return rc;
-        }
-        for (long long i = 0; i < N; ++i) {
-            const double* yi = &Y[(size_t)i * m];
-            bool nz = false;
-            for (int l = 0; l < m; ++l) nz = nz || ((g < 0 || l != g) && yi[l] != 0.0);
-            if (!nz) continue;  // B_bar row is exactly zero: x - 0 = x (dense-column path: a dense-only row)
-            boff.push_back(ref_to_padded(lv, i));
-            t_boff.push_back(ref_to_tail(lv, i));
-            for (int k = 0; k < m; ++k) {
-                double u = 0.0;
-                for (int l = 0; l < m; ++l) u = std::fma(yi[l], Minv[(size_t)l * m + k], u);
-                bval.push_back(u);
-            }
-        }
-        r.nbar[d] = (int)boff.size();
-        r.nbar_all[d] += r.nbar[d];
-        if ((rc = lr_to_device(h, r, &r.bar_off[d], boff)) || (rc = lr_to_device(h, r, &r.bar_val[d], bval)) ||
-            (rc = lr_to_device(h, r, &r.t_bar_off[d], t_boff)))
-            return rc;
-    }
-    bool small = !(h->paths & PATH_NO_LR_SMALL) && ndense == 0 && r.nrows <= (1 << 16) &&
-                 r.nbar[0] <= (1 << 16) && r.nbar[1] <= (1 << 16);
-    for (int k = 0; k < m; ++k) small = small && meta[k].nblk <= 1;
-    r.small = small;
-    return MGMC_OK;
-}
-
-}  // namespace
-
-extern "C" {
-
-int mgmc_set_lowrank(mgmc_handle* h, int m, const int64_t* colptr, const int64_t* rows, const double* vals,
-                     const double* sigma) {
-    if (!h) return fail(nullptr, MGMC_E_INVALID, "null handle");
-    if (m < 0 || m > LR_MAX_M) return fail(h, MGMC_E_INVALID, "m_lowrank must be in [0, 64]");
-    const long long N0 = (long long)h->levels[0].spec.ndof;
-    std::vector<LRColumn> cols(m);
-    if (m > 0) {
-        if (!colptr || !sigma) return fail(h, MGMC_E_INVALID, "null argument");
-        if (colptr[0] != 0) return fail(h, MGMC_E_INVALID, "colptr[0] must be 0");
-        if (colptr[m] > 0 && (!rows || !vals)) return fail(h, MGMC_E_INVALID, "null argument");
-        for (int k = 0; k < m; ++k) {
-            if (!(sigma[k] > 0.0) || !std::isfinite(sigma[k])) return fail(h, MGMC_E_INVALID, "Sigma must be positive");
-            if (colptr[k + 1] < colptr[k]) return fail(h, MGMC_E_INVALID, "colptr must be non-decreasing");
-            for (int64_t q = colptr[k]; q < colptr[k + 1]; ++q) {
-                if (rows[q] < 0 || rows[q] >= N0 || (q > colptr[k] && rows[q] <= rows[q - 1]))
-                    return fail(h, MGMC_E_INVALID, "row indices of a column must be strictly ascending in [0, N)");
-                if (!std::isfinite(vals[q])) return fail(h, MGMC_E_INVALID, "non-finite entry of B");
-                cols[k].ent.push_back({rows[q], vals[q]});
-            }
-            cols[k].dense = (long long)cols[k].ent.size() == N0;
-        }
-    }
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    destroy_graphs(h);
-    for (auto& lv : h->levels) free_lowrank(lv.lr);
-    int rc = MGMC_OK;
-    for (size_t l = 0; m > 0 && l < h->levels.size(); ++l) {
-        if (l > 0 && (rc = lr_restrict_columns(h, (int)l - 1, cols))) break;
-        if ((rc = lr_setup_level(h, (int)l, cols, sigma, m))) break;
-    }
-    if (rc) {
-        for (auto& lv : h->levels) free_lowrank(lv.lr);
-    }
-    h->lr_cols.clear();
-    h->lr_sigma.clear();
-    if (!rc && m > 0) {
-        h->lr_cols = cols;
-        h->lr_sigma.assign(sigma, sigma + m);
-    }
-    if (!rc && h->chol_n > 0)  // the coarse factors carry B_c Sigma^{-1} B_c^T
-        rc = build_coarse_chol(h, m > 0 ? &cols : nullptr, sigma, m);
-    if (rc) {
-        // no half-installed posterior: a failure (a coarse band the blocked Cholesky cannot take, the
-        // host work limit, an allocation) leaves the handle with the prior -- no low-rank part on any
-        // level and the prior's coarse factors -- and the error code.  The levels' low-rank parts are
-        // installed before the coarse factor is built, so they are removed again here.
-        const std::string err = h->last_error;
-        for (auto& lv : h->levels) free_lowrank(lv.lr);
-        h->lr_cols.clear();
-        h->lr_sigma.clear();
-        h->last_error = err;
-        if (h->chol_n > 0 && build_coarse_chol(h, nullptr, nullptr, 0) != MGMC_OK) {
-            // the prior's factor built at mgmc_create cannot be rebuilt (e.g. an allocation): no
-            // sample call may run on a half-built coarse factor
-            h->unusable = true;
-            h->last_error = err + "; restoring the prior's coarse Cholesky factor failed too (" + h->last_error +
-                            "): the handle is unusable";
-        }
-        set_global_error(err);
-    }
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    build_ops(h);
-    int rc2 = build_tails(h);
-    if (!rc2) rc2 = build_graphs(h);
-    if (!rc && !rc2) h->unusable = false;  // a later successful install rebuilt a whole coarse factor
-    return rc ? rc : rc2;
-}
-
-int mgmc_lowrank_info(const mgmc_handle* h, int level, int direction, int* m, int64_t* nrows_bbar) {
-    if (!h || !m || !nrows_bbar) return fail(nullptr, MGMC_E_INVALID, "null argument");
-    if (level < 0 || level >= (int)h->levels.size()) return fail(nullptr, MGMC_E_INVALID, "level out of range");
-    if (direction != MGMC_FORWARD && direction != MGMC_BACKWARD) return fail(nullptr, MGMC_E_INVALID, "invalid direction");
-    const LowRankDev& r = h->levels[level].lr;
-    *m = r.m;
-    *nrows_bbar = r.nbar_all[direction == MGMC_FORWARD ? 0 : 1];  // local + dense-only rows
-    return MGMC_OK;
-}
-
-#define NCCLCHK(h, call)                                                                     \
-    do {                                                                                     \
-        ncclResult_t r_ = (call);                                                            \
-        if (r_ != ncclSuccess)                                                               \
-            return fail(h, MGMC_E_HIP, std::string("RCCL error ") + ncclGetErrorString(r_) + " at " #call); \
-    } while (0)
-
-int mgmc_comm_unique_id(unsigned char out[MGMC_UNIQUE_ID_BYTES]) {
-    if (!out) return fail(nullptr, MGMC_E_INVALID, "null argument");
-    ncclUniqueId id;
-    NCCLCHK(nullptr, ncclGetUniqueId(&id));
-    memcpy(out, id.internal, MGMC_UNIQUE_ID_BYTES);
-    return MGMC_OK;
-}
-
-int mgmc_comm_init(mgmc_handle* h, int nranks, int rank, const unsigned char id_bytes[MGMC_UNIQUE_ID_BYTES]) {
-    if (!h || !id_bytes || nranks < 1 || rank < 0 || rank >= nranks) return fail(h, MGMC_E_INVALID, "invalid argument");
-    HIPCHK(h, hipSetDevice(h->device));
-    if (h->comm) {
-        ncclCommDestroy(h->comm);
-        h->comm = nullptr;
-    }
-    ncclUniqueId id;
-    memcpy(id.internal, id_bytes, MGMC_UNIQUE_ID_BYTES);
-    NCCLCHK(h, ncclCommInitRank(&h->comm, nranks, id, rank));
-    h->nranks = nranks;
-    h->rank = rank;
-    if (h->comm_buf) HIPCHK(h, hipFree(h->comm_buf));
-    HIPCHK(h, hipMalloc(&h->comm_buf, (size_t)(4 * nranks + 4) * h->nchains * sizeof(double)));
-    return MGMC_OK;
-}
-
-int mgmc_comm_allgather_moments(mgmc_handle* h, double* out) {
-    if (!h || !out) return fail(h, MGMC_E_INVALID, "null argument");
-    HIPCHK(h, hipSetDevice(h->device));
-    const int nch = h->nchains;
-    if (!h->comm) {  // one rank: this handle's chains
-        for (int c = 0; c < nch; ++c) {
-            int rc = mgmc_qoi_moments_chain(h, c, out + 3 * c);
-            if (rc) return rc;
-        }
-        return MGMC_OK;
-    }
-    // (count, mean, M2) of every chain packed to 3 doubles (the device moments are 4 apart), one
-    // all-gather of 3 * nchains doubles per rank
-    double* send = h->comm_buf + (size_t)4 * h->nranks * nch;
-    HIPCHK(h, hipMemcpy2DAsync(send, 3 * sizeof(double), h->mom, 4 * sizeof(double), 3 * sizeof(double), nch,
-                               hipMemcpyDeviceToDevice, h->stream));
-    NCCLCHK(h, ncclAllGather(send, h->comm_buf, 3 * nch, ncclDouble, h->comm, h->stream));
-    HIPCHK(h, hipMemcpyAsync(out, h->comm_buf, (size_t)3 * h->nranks * nch * sizeof(double), hipMemcpyDeviceToHost,
-                             h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    return MGMC_OK;
-}
-
-int mgmc_comm_allreduce_max(mgmc_handle* h, double* value) {
-    if (!h || !value) return fail(h, MGMC_E_INVALID, "null argument");
-    if (!h->comm) return MGMC_OK;
-    HIPCHK(h, hipSetDevice(h->device));
-    HIPCHK(h, hipMemcpyAsync(h->comm_buf, value, sizeof(double), hipMemcpyHostToDevice, h->stream));
-    NCCLCHK(h, ncclAllReduce(h->comm_buf, h->comm_buf, 1, ncclDouble, ncclMax, h->comm, h->stream));
-    HIPCHK(h, hipMemcpyAsync(value, h->comm_buf, sizeof(double), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    return MGMC_OK;
-}
-
-int mgmc_comm_barrier(mgmc_handle* h) {
-    if (!h) return fail(nullptr, MGMC_E_INVALID, "null handle");
-    HIPCHK(h, hipSetDevice(h->device));
-    if (h->comm) NCCLCHK(h, ncclAllReduce(h->comm_buf, h->comm_buf, 1, ncclDouble, ncclSum, h->comm, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    HIPCHK(h, hipDeviceSynchronize());
-    return MGMC_OK;
-}
-
-int mgmc_comm_info(const mgmc_handle* h, int* rccl_ranks, int* rccl_rank, int* pci_bus_id) {
-    if (!h || !rccl_ranks || !rccl_rank || !pci_bus_id) return fail(nullptr, MGMC_E_INVALID, "null argument");
-    *rccl_ranks = 0;
-    *rccl_rank = -1;
-    if (h->comm) {
-        NCCLCHK(const_cast<mgmc_handle*>(h), ncclCommCount(h->comm, rccl_ranks));
-        NCCLCHK(const_cast<mgmc_handle*>(h), ncclCommUserRank(h->comm, rccl_rank));
-    }
-    if (hipDeviceGetAttribute(pci_bus_id, hipDeviceAttributePciBusId, h->device) != hipSuccess)
-        return fail(const_cast<mgmc_handle*>(h), MGMC_E_HIP, "hipDeviceGetAttribute(PciBusId) failed");
-    return MGMC_OK;
-}
-
-int mgmc_comm_destroy(mgmc_handle* h) {
-    if (!h) return fail(nullptr, MGMC_E_INVALID, "null handle");
-    if (h->comm) ncclCommDestroy(h->comm);
-    h->comm = nullptr;
-    h->nranks = 1;
-    h->rank = 0;
-    return MGMC_OK;
 }
 
 }  // extern "C"

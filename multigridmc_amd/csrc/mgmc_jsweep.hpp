@@ -242,12 +242,8 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
         }
         if (store) {
             double* dst = a.xout + L.at(i0, j, k);
-            if constexpr (tune::JS_NT_STORE != 0) {
-                __builtin_nontemporal_store(FIRST_ODD ? v1 : v2, dst);
-                __builtin_nontemporal_store(FIRST_ODD ? v2 : v1, dst + 1);
-            } else {
-                *reinterpret_cast<double2*>(dst) = FIRST_ODD ? make_double2(v1, v2) : make_double2(v2, v1);
-            }
+            __builtin_nontemporal_store(FIRST_ODD ? v1 : v2, dst);  // streaming stores
+            __builtin_nontemporal_store(FIRST_ODD ? v2 : v1, dst + 1);
         }
         // the next step's rows (ar + 2, ar + 3) into the slots of rows ar - 6, ar - 5 (read by no one)
         if (s < s1) {

@@ -770,7 +770,7 @@ __global__ void __launch_bounds__(256) k_unpack(Layout L, const double* __restri
 // ctrl[0] = sample index, ctrl[1] = series length, ctrl[2] = QoI storage index (int64, <0 = off),
 // ctrl[5] = non-finite guard (0, or 1 + the sample index at which the watched value first was NaN /
 // Inf), ctrl[6] = storage index watched when no QoI is recorded (the lattice centre)
-__global__ void k_qoi_record(const double* __restrict__ x, uint64_t* ctrl, double* series, uint64_t capacity,
+static __global__ void k_qoi_record(const double* __restrict__ x, uint64_t* ctrl, double* series, uint64_t capacity,
                              double* mom, int nchains, long long cs) {
     // thread c records chain c (series and moments chain c * capacity / c * 4 on); the control words
     // are advanced once, after every chain has read them
@@ -813,7 +813,7 @@ __device__ inline double butterfly64(double v) {
     for (int o = 32; o >= 1; o >>= 1) v = v + __shfl_xor(v, o, 64);
     return v;
 }
-__global__ void __launch_bounds__(64) k_qoi_dot(const double* __restrict__ x, const long long* __restrict__ off,
+static __global__ void __launch_bounds__(64) k_qoi_dot(const double* __restrict__ x, const long long* __restrict__ off,
                                                 const double* __restrict__ val, long long n, const uint64_t* ctrl,
                                                 double* __restrict__ part, int nblk, long long cs) {
     if ((long long)ctrl[2] != -2) return;  // not recording the vector in this call (uniform)
@@ -838,7 +838,7 @@ __global__ void __launch_bounds__(64) k_qoi_dot(const double* __restrict__ x, co
 }
 // k_qoi_record with one wavefront per chain: z = x at the QoI vertex (ctrl[2] >= 0), the centre
 // guard (-1), or the combined block partials of k_qoi_dot (-2)
-__global__ void k_qoi_record_vec(const double* __restrict__ x, uint64_t* ctrl, double* series, uint64_t capacity,
+static __global__ void k_qoi_record_vec(const double* __restrict__ x, uint64_t* ctrl, double* series, uint64_t capacity,
                                  double* mom, int nchains, long long cs, const double* __restrict__ part, int nblk) {
     __shared__ int bad;
     const int c = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -878,7 +878,7 @@ __global__ void k_qoi_record_vec(const double* __restrict__ x, uint64_t* ctrl, d
 }
 
 // ---- normals for the RNG parity test ----
-__global__ void k_normals(RngKey key, uint64_t pair0, uint64_t npairs, uint32_t tag, uint64_t sample,
+static __global__ void k_normals(RngKey key, uint64_t pair0, uint64_t npairs, uint32_t tag, uint64_t sample,
                           double* __restrict__ out) {
     const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= npairs) return;

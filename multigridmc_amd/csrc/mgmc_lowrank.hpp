@@ -102,7 +102,7 @@ __device__ __forceinline__ long long lr_entry_pos(const Layout& L, long long e, 
 // Batched chains: blockIdx.y = a group of LRP_CH chains; the column value of an entry is loaded
 // once for the group (v cs apart, the partials nblk apart per chain).
 constexpr int LRP_U = tune::LR_PART_U, LRP_CH = tune::LR_PART_CH;
-__global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRBlock* __restrict__ blk, int sel,
+static __global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRBlock* __restrict__ blk, int sel,
                                                      const long long* __restrict__ ent_off,
                                                      const double* __restrict__ ent_val,
                                                      const double* __restrict__ dense_val,
@@ -192,7 +192,7 @@ __global__ void __launch_bounds__(64) k_lr_partials(Layout L, const LRBlock* __r
 // lane l of the first wavefront adds its entries l, l+64, ... in entry order and the butterfly
 // follows: the single-wavefront kernel's sums, bit for bit.  One chain per blockIdx.y.
 constexpr int LRS_NT = 256;
-__global__ void __launch_bounds__(LRS_NT) k_lr_partials_staged(Layout L, const LRBlock* __restrict__ blk, int sel,
+static __global__ void __launch_bounds__(LRS_NT) k_lr_partials_staged(Layout L, const LRBlock* __restrict__ blk, int sel,
                                                                const long long* __restrict__ ent_off,
                                                                const double* __restrict__ ent_val,
                                                                const double* __restrict__ dense_val,
@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(LRS_NT) k_lr_partials_staged(Layout L, const L
 }
 
 // ---- dot products, stage 2: one wavefront per column ----
-__global__ void __launch_bounds__(64) k_lr_totals(const LRColMeta* __restrict__ meta, const double* __restrict__ part,
+static __global__ void __launch_bounds__(64) k_lr_totals(const LRColMeta* __restrict__ meta, const double* __restrict__ part,
                                                    double* __restrict__ out, int nblk, int m) {
     const int k = blockIdx.x;
     const int lane = threadIdx.x;
@@ -336,7 +336,7 @@ __device__ __forceinline__ RngKey lr_chain_key(RngKey key, uint32_t chain0, uint
     return key;
 }
 
-__global__ void __launch_bounds__(256) k_lr_patch(LRPatchArgs a) {
+static __global__ void __launch_bounds__(256) k_lr_patch(LRPatchArgs a) {
     {
         const int ch = batch_chain();
         a.y += ch * a.cs;
@@ -378,7 +378,7 @@ __global__ void __launch_bounds__(256) k_lr_patch(LRPatchArgs a) {
 // apart, the saved f nrest apart) -- the (N x m) (m x C) product of the chain batch, each chain's
 // entry the single-chain fma chain over k ascending.
 constexpr int LR_MAX_CH = 16;  // chains of one batched handle (w of every chain in LDS)
-__global__ void __launch_bounds__(256) k_lr_update(int m, int nbar, const long long* __restrict__ bar_off,
+static __global__ void __launch_bounds__(256) k_lr_update(int m, int nbar, const long long* __restrict__ bar_off,
                                                     const double* __restrict__ bar_val, const double* __restrict__ w,
                                                     double* __restrict__ x, int nrest,
                                                     const long long* __restrict__ rest_off,
@@ -403,7 +403,7 @@ __global__ void __launch_bounds__(256) k_lr_update(int m, int nbar, const long l
 }
 
 // ---- restore f on the rows of B ----
-__global__ void __launch_bounds__(256) k_lr_restore(int n, const long long* __restrict__ off,
+static __global__ void __launch_bounds__(256) k_lr_restore(int n, const long long* __restrict__ off,
                                                      const double* __restrict__ save, double* __restrict__ f,
                                                      long long cs) {
     save += (long long)blockIdx.z * n;  // batched chains (blockIdx.z)
@@ -443,7 +443,7 @@ struct LRRestorePatchArgs {
     uint32_t chain0, seed_hi;
 };
 
-__global__ void __launch_bounds__(256) k_lr_restore_patch(LRRestorePatchArgs a) {
+static __global__ void __launch_bounds__(256) k_lr_restore_patch(LRRestorePatchArgs a) {
     __shared__ double s[LR_MAX_M];
     const bool second = (int)blockIdx.x >= a.nb0;
     const int ch = batch_chain();
@@ -557,7 +557,7 @@ __device__ __forceinline__ void lrd_noise(const LRDenseArgs& a, uint32_t tag, bo
     }
 }
 
-__global__ void __launch_bounds__(LRD_NT) k_lr_dense_rhs(LRDenseArgs a) {
+static __global__ void __launch_bounds__(LRD_NT) k_lr_dense_rhs(LRDenseArgs a) {
     __shared__ double s[LR_MAX_CH * LR_MAX_M];
     __shared__ double s2[LR_MAX_CH * LR_MAX_M];
     const bool local = (int)blockIdx.x < a.nbs;
@@ -648,7 +648,7 @@ struct LRDenseUpdateArgs {
     double* f;
 };
 
-__global__ void __launch_bounds__(LRD_NT) k_lr_dense_update(LRDenseUpdateArgs a) {
+static __global__ void __launch_bounds__(LRD_NT) k_lr_dense_update(LRDenseUpdateArgs a) {
     __shared__ double ws[LR_MAX_CH * LR_MAX_M];
     __shared__ double mg[LR_MAX_M];
     __shared__ double dt[LR_MAX_CH * 128];  // ykey: the fix of every key and chain, sum_k B_bar_ik w_k
@@ -812,7 +812,7 @@ __device__ __forceinline__ double lr_wave_dot(const LRColMeta& c, const long lon
     return tot;
 }
 
-__global__ void __launch_bounds__(1024) k_lr_small(LRSmallArgs a) {
+static __global__ void __launch_bounds__(1024) k_lr_small(LRSmallArgs a) {
     lr_small_chain(a);
     __shared__ double ws[LR_MAX_M], ts[LR_MAX_M];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;

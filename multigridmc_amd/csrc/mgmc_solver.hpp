@@ -15,7 +15,7 @@ namespace mgmc {
 constexpr int SOLVE_NB = 1024;  // reduction blocks (fixed: deterministic two-stage sums)
 
 // partial[b] = sum over block b's grid-stride range of a_i * b_i  (fixed order per block)
-__global__ void __launch_bounds__(256) k_dot_partial(long long n, const double* __restrict__ a,
+static __global__ void __launch_bounds__(256) k_dot_partial(long long n, const double* __restrict__ a,
                                                       const double* __restrict__ b, double* __restrict__ partial) {
     __shared__ double red[256];
     double acc = 0.0;
@@ -31,7 +31,7 @@ __global__ void __launch_bounds__(256) k_dot_partial(long long n, const double* 
 }
 
 // out[slot] = sum of the partials (one workgroup, fixed tree)
-__global__ void __launch_bounds__(256) k_dot_final(const double* __restrict__ partial, int np, double* __restrict__ out,
+static __global__ void __launch_bounds__(256) k_dot_final(const double* __restrict__ partial, int np, double* __restrict__ out,
                                                     int slot) {
     __shared__ double red[256];
     double acc = 0.0;
@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(256) k_dot_final(const double* __restrict__ pa
 }
 
 // y = a x + y  (alpha read from device scalars: alpha = num[0] / den[0] * sign)
-__global__ void __launch_bounds__(256) k_axpy_ratio(long long n, const double* __restrict__ num,
+static __global__ void __launch_bounds__(256) k_axpy_ratio(long long n, const double* __restrict__ num,
                                                      const double* __restrict__ den, double sign,
                                                      const double* __restrict__ x, double* __restrict__ y) {
     const double alpha = sign * (num[0] / den[0]);
@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(256) k_axpy_ratio(long long n, const double* _
 }
 
 // p = z + beta p, beta = num[0] / den[0]
-__global__ void __launch_bounds__(256) k_xpby_ratio(long long n, const double* __restrict__ z,
+static __global__ void __launch_bounds__(256) k_xpby_ratio(long long n, const double* __restrict__ z,
                                                      const double* __restrict__ num, const double* __restrict__ den,
                                                      double* __restrict__ p) {
     const double beta = num[0] / den[0];
@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(256) k_xpby_ratio(long long n, const double* _
 }
 
 // y = a - b
-__global__ void __launch_bounds__(256) k_sub(long long n, const double* __restrict__ a, const double* __restrict__ b,
+static __global__ void __launch_bounds__(256) k_sub(long long n, const double* __restrict__ a, const double* __restrict__ b,
                                               double* __restrict__ y) {
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
         y[i] = a[i] - b[i];

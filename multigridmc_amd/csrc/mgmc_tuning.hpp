@@ -20,12 +20,6 @@ constexpr int ZS_TZ = 32;
 constexpr int ZS_TYP = 16;
 constexpr int ZS_MINWP = 6;
 constexpr int ZS_TZP = 128;
-// ... which loads its x planes two steps ahead (one register set per plane parity; 0: one step ahead,
-// as the plain sweep)
-constexpr int ZS_PF2 = 1;
-// non-temporal (streaming) stores of the new x: the z-sweeps, the j-marching half-sweeps
-constexpr int ZS_NT_STORE = 1;
-constexpr int JS_NT_STORE = 1;
 
 // quad passes (k_sweep_quads) on 3D Galerkin levels with rows of at most QUADS_MAXPAIR pairs;
 // workgroup threads: 2D levels, 3D rows of more than 32 pairs, 3D rows of at most 32 pairs
@@ -46,10 +40,6 @@ constexpr int ZR_SMALL_NX = 32;
 // the 7-point (fine level) instance with 64 x 8 coarse points per 512-thread workgroup (else 64 x 4
 // per 256 threads) from this many 64 x 8 tiles up (512^3: 32,768)
 constexpr int ZR7_WIDE_MIN_TILES = 16 * 1024;
-// the 7-point (fine level) instances load x planes two steps ahead (0: one step)
-constexpr int ZR7_XPF2 = 0;
-// tile rows in descending y order (the fine sweep before it writes its high-y tiles last)
-constexpr int ZR_Y_DESC = 0;
 
 // z-marching prolongation (k_prolongate_z): fine planes per thread on big 3D levels, and below 2^21
 // fine pair items

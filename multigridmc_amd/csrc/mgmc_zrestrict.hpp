@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
     const int nb = ZN ? a.nblk_main : (int)gridDim.x, b = blockIdx.x, per = nb >> 3;
     const int tile = (nb & 7) ? b : (b & 7) * per + (b >> 3);
     const int txi = tile % a.ntx;
-    const int tyi = tune::ZR_Y_DESC ? a.nty - 1 - (tile / a.ntx) % a.nty : (tile / a.ntx) % a.nty;
+    const int tyi = (tile / a.ntx) % a.nty;
     const int tzi = tile / (a.ntx * a.nty);
     if (tzi >= a.ntz) return;
     const int I0 = 1 + txi * CX, J0 = 1 + tyi * CY;
@@ -174,21 +174,16 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
         cpg[u] = cpin[u] ? Lc.at(I0 + cx, J0 + cy, 0) : 0;
     }
 
-    // XPF2 (the 7-point fine level, tune::ZR7_XPF2): x planes are loaded two steps ahead, one register set
-    // per plane parity (the set is a compile-time choice: the plane loop runs in pairs)
-    constexpr bool XPF2 = NPTS == 7 && tune::ZR7_XPF2 != 0;
-    double2 pxb[XPF2 ? 2 : 1][NLX], pf[NLR];
+    double2 px[NLX], pf[NLR];
     // the chunk stages x planes 2 K0 - 2 .. 2 K1 and f planes 2 K0 - 1 .. 2 K1 - 1: the last step's loads one
     // plane ahead reload those (never used) instead of fetching the next chunk's planes
     const int kx_last = 2 * K1, kf_last = 2 * K1 - 1;
-    auto issue_x = [&](int k, auto Bc) {
-        double2 (&px)[NLX] = pxb[XPF2 ? decltype(Bc)::value : 0];
+    auto issue_x = [&](int k) {
         const double* base = plane_ptr(a.x, k > kx_last ? kx_last : k);
 #pragma unroll
         for (int u = 0; u < NLX; ++u) px[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
     };
-    auto deposit_x = [&](int k, auto Bc) {
-        const double2 (&px)[NLX] = pxb[XPF2 ? decltype(Bc)::value : 0];
+    auto deposit_x = [&](int k) {
         double* dst = xs + xslot(k) * XPS;
 #pragma unroll
         for (int u = 0; u < NLX; ++u)
@@ -301,35 +296,31 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
     // by residual(k) before the second barrier.
     double acc[NCP], accn[NCP];
     double2 fcur[NLR];
-    // Bc: the register set of plane k + 1 (XPF2: (k + 1) & 1), which then takes x(k + 3)
-    auto step = [&](int k, auto Bc) __attribute__((always_inline)) {
-        deposit_x(k + 1, Bc);
+    auto step = [&](int k) __attribute__((always_inline)) {
+        deposit_x(k + 1);
 #pragma unroll
         for (int u = 0; u < NLR; ++u) fcur[u] = pf[u];
-        issue_x(XPF2 ? k + 3 : k + 2, Bc);
+        issue_x(k + 2);
         issue_f(k + 1);
         __syncthreads();
         residual(k, fcur);
         __syncthreads();
     };
     // prologue: x planes 2K0-2, 2K0-1 in LDS, x(2K0) and f(2K0-1) in flight
-    using S0 = std::integral_constant<int, 0>;  // even planes
-    using S1 = std::integral_constant<int, 1>;  // odd planes
-    issue_x(2 * K0 - 2, S0{});
-    deposit_x(2 * K0 - 2, S0{});
-    issue_x(2 * K0 - 1, S1{});
-    deposit_x(2 * K0 - 1, S1{});
-    issue_x(2 * K0, S0{});
-    if constexpr (XPF2) issue_x(2 * K0 + 1, S1{});
+    issue_x(2 * K0 - 2);
+    deposit_x(2 * K0 - 2);
+    issue_x(2 * K0 - 1);
+    deposit_x(2 * K0 - 1);
+    issue_x(2 * K0);
     issue_f(2 * K0 - 1);
 #pragma unroll
     for (int u = 0; u < NCP; ++u) acc[u] = 0.0;
-    step(2 * K0 - 1, S0{});
+    step(2 * K0 - 1);
     accumulate(acc, 0);  // sz = 0 of coarse plane K0
     for (int K = K0; K < K1; ++K) {
-        step(2 * K, S1{});
+        step(2 * K);
         accumulate(acc, 1);
-        step(2 * K + 1, S0{});
+        step(2 * K + 1);
         accumulate(acc, 2);
         finish(acc, K);
 #pragma unroll

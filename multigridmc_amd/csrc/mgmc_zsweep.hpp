@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
     // parity, chosen at compile time from the step's parity) and f unconditionally (idle waves load a
     // zero pad pair): its 0.686 -> 0.677 ms (round 3, interleaved A/B).  The plain sweep has no
     // registers to spare for the second set (it spills at its 80-VGPR budget).
-    constexpr bool PF2 = PROLONG != 0 && tune::ZS_PF2 != 0;
+    constexpr bool PF2 = PROLONG != 0;
     double2 pxb[PF2 ? 2 : 1][NLX];
 #define ZS_PX(B) pxb[PF2 ? (B) : 0]
     // planes past the chunk's last deposited plane k1 + 1 (the loads issued one / two steps ahead in the
@@ -470,13 +470,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
                     double* dst = a.xout + (long long)k * L.sp + t.goff;
                     // (x, y) = (odd, even) element; the second colour is element e here
                     const double2 out = e ? make_double2(fv, sv) : make_double2(sv, fv);
-                    // streaming store: keep the write stream out of L2
-                    if constexpr (tune::ZS_NT_STORE != 0) {
-                        __builtin_nontemporal_store(out.x, dst);
-                        __builtin_nontemporal_store(out.y, dst + 1);
-                    } else {
-                        *reinterpret_cast<double2*>(dst) = out;
-                    }
+                    // streaming store: keep the write stream out of L2 (plain stores: pre-sweep 0.641 ->
+                    // 0.673 ms)
+                    __builtin_nontemporal_store(out.x, dst);
+                    __builtin_nontemporal_store(out.y, dst + 1);
                 }
                 fb = fv;  // the next step's value below (UP) / above (DN) at its second-colour position
             }

@@ -1277,6 +1277,9 @@ static void dense_factor_inverses(const std::vector<double>& L, int64_t n, std::
 //   t = f_k - C_k y_{k-1}, y_k = L_kk^{-1} t;   y' = y + xi;   t = y'_k - C_{k+1}^T x_{k+1}, x_k = L_kk^{-T} t
 // with every row an fma chain in ascending column order.
 static int g_chol_blocked = 0;
+// g_no_fold: hierarchies built while it is set take no fold levels (the device's MGMC_DISABLE=fold: the
+// residuals of the reflection-symmetric 27-point levels in the reference's CSR order)
+static int g_no_fold = 0;
 static const int64_t kCholDenseMax = 8192;
 
 struct DenseCholeskySampler : Sampler {
@@ -1485,7 +1488,7 @@ struct MGMC : Sampler {
             std::unique_ptr<Level> L(new Level());
             L->lat = lattice;
             L->A = std::move(A);  // every branch below assigns A before the next level
-            L->fold = stencil_hierarchy && fold_stencil(L->lat, L->A);
+            L->fold = stencil_hierarchy && !g_no_fold && fold_stencil(L->lat, L->A);
             // 2 colours for a 5/7-point fine level (FD), 2^d for 3^d-point levels (FEM, Galerkin)
             if (lattice.dim >= 2) init_colouring(*L, level == 0);
             x_ell.emplace_back(L->A.nrow, 0.0);
@@ -1693,6 +1696,7 @@ void orc_destroy(orc_handle* h) { delete h; }
 void orc_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
 // coarse Cholesky: the blocked banded solves at any size (read when a sampler is built)
 void orc_set_chol_blocked(int on) { g_chol_blocked = on ? 1 : 0; }
+void orc_set_no_fold(int on) { g_no_fold = on ? 1 : 0; }
 int orc_get_threads(void) { return g_threads; }
 
 // the reference's fine operators (any correlation-length model) as CSR: pde 0 FD, 1 FEM, 2 squared

@@ -11,8 +11,10 @@ ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 mkdir -p "$ROOT/build"
 HIPX="/opt/rocm/bin/hipcc -O3 -std=c++17 -ffp-contract=off -fPIC -w --offload-arch=gfx950 -shared ${CXXDEFS:-}"
 LIBS="-L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib"
+pids=""
 for v in ${VARIANTS:-}; do
   name=${v%%=*}; edits=${v#*=}
+  rm -f "$ROOT/build/libmgmc_$name.so"  # a failed compile must not leave an older build to be A/B'd
   src="$ROOT/build/exp_$name"
   rm -rf "$src" && mkdir -p "$src/multigridmc_amd" "$src/include"
   cp -r "$ROOT/multigridmc_amd/csrc" "$src/multigridmc_amd/"
@@ -24,7 +26,7 @@ for v in ${VARIANTS:-}; do
     grep -q "constexpr int $key = " "$tun" || { echo "build_exp: no constant $key in mgmc_tuning.hpp" >&2; exit 2; }
     sed -i "s/constexpr int $key = [^;]*;/constexpr int $key = $val;/" "$tun"
   done
-  (cd "$src/multigridmc_amd/csrc" && $HIPX -o "$ROOT/build/libmgmc_$name.so" mgmc_capi.hip mgmc_hierarchy.cpp \
-     mgmc_operators.cpp $LIBS) &
+  (cd "$src/multigridmc_amd/csrc" && $HIPX -o "$ROOT/build/libmgmc_$name.so" *.hip *.cpp $LIBS) &
+  pids="$pids $!"
 done
-wait
+for p in $pids; do wait "$p" || { echo "build_exp: a variant failed to compile" >&2; exit 1; }; done

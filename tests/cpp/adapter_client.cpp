@@ -8,6 +8,8 @@
 //   adapter_client rngcheck                  constructs a sampler on the driver's shared engine and
 //                                            reports (also from an atexit handler, so a failed device
 //                                            call's exit(-1) reports too) whether the engine moved
+//   adapter_client seedrepeat                three default seeds drawn from the unadvanced shared engine
+//                                            (no device): the engine's own output first, then distinct ones
 //   adapter_client smoother <fd|fem|periodic> <sor|ssor> <nsmooth> <fwd|bwd> [lowrank]
 //                                            b, x and x after one Smoother::apply(b, x) of the Smoother
 //                                            drop-in (b, x from a fixed mt19937_64 stream); "lowrank" adds two
@@ -154,6 +156,15 @@ int main(int argc, char** argv) {
         std::printf("seed %llu\n", (unsigned long long)sampler.get_seed());
         std::mt19937_64 fresh(5418513);
         std::printf("engine_first %llu\n", (unsigned long long)fresh());
+        return 0;
+    }
+    if (mode == "seedrepeat") {
+        g_rng_before = g_rng;
+        for (int q = 0; q < 3; ++q)
+            std::printf("seed%d %llu\n", q, (unsigned long long)HipMultigridMCSampler::engine_seed(g_rng));
+        std::mt19937_64 fresh(5418513);
+        std::printf("engine_first %llu\n", (unsigned long long)fresh());
+        report_engine();
         return 0;
     }
     if (mode == "ownership" && argc > 2) {

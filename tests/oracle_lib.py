@@ -46,6 +46,7 @@ def lib():
             "orc_destroy": (None, [c_void_p]),
             "orc_set_threads": (None, [c_int]),
             "orc_set_chol_blocked": (None, [c_int]),
+            "orc_set_no_fold": (None, [c_int]),
             "orc_get_threads": (c_int, []),
             "orc_ndof": (c_int64, [c_void_p, c_int]),
             "orc_nlevel": (c_int, [c_void_p]),
@@ -366,6 +367,12 @@ def set_chol_blocked(on: bool) -> None:
     """Coarse Cholesky: the blocked banded solves at any size (the device's MGMC_DISABLE=chol_dense);
     read when an oracle is built."""
     lib().orc_set_chol_blocked(1 if on else 0)
+
+
+def set_no_fold(on: bool) -> None:
+    """No fold levels: residuals of reflection-symmetric 27-point levels in the reference's CSR order
+    (the device's MGMC_DISABLE=fold); read when an oracle is built."""
+    lib().orc_set_no_fold(1 if on else 0)
 
 
 def cpu_share() -> int:

@@ -123,6 +123,19 @@ def test_adapter_construction_leaves_the_shared_engine_alone(tmp_path):
         assert vals["seed"] == vals["engine_first"]
 
 
+def test_adapter_default_seeds_differ_on_one_engine(tmp_path):
+    """samplers sharing the reference's engine draw different noise; adapters built on the
+    same unadvanced engine state get distinct Philox seeds (the first one the engine's own next
+    output, driver_mgmc.cc:448), and the engine is still never advanced."""
+    exe = build_adapter_client(str(tmp_path))
+    r = subprocess.run([exe, "seedrepeat"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    vals = dict(line.split() for line in r.stdout.splitlines() if line.startswith(("seed", "engine_first")))
+    assert vals["seed0"] == vals["engine_first"]
+    assert len({vals["seed0"], vals["seed1"], vals["seed2"]}) == 3
+    assert "engine unchanged" in r.stdout
+
+
 def test_adapter_ownership_through_base_pointers_compiles(tmp_path):
     """the restated Sampler / Smoother / SmootherFactory / Lattice declare no
     destructor, exactly as the reference's (sampler/sampler.hh:23-72, smoother/smoother.hh:15-44), and

@@ -187,15 +187,14 @@ def test_posterior_statistics_vs_exact_covariance(hip_device, shape, kw, glob, n
 
 @pytest.mark.parametrize("name,paths", [(n, "tail") for n in TAIL_CONFIGS] +
                          [(n, q) for n in ("3d32_points_tail_W", "2d32_point_global", "3d_aniso_zres_points")
-                          for q in ("lr_small", "lr_merge", "lr_prefetch", "lr_small,lr_merge,tail")] +
+                          for q in ("lr_small", "lr_merge", "lr_small,lr_merge,tail")] +
                          [(n, "lr_dense") for n in ("2d128_point_global_W", "3d32_ball_global")] +
                          [("3d128_global_inplace_W", q) for q in ("lr_merge", "lr_dense")])
 def test_lowrank_paths_match(hip_device, name, paths, monkeypatch):
     """Low-rank kernel paths switched off (MGMC_DISABLE): tail = the coarse levels' sub-cycle as
     separate launches instead of k_tail (low-rank patches, fix and residual in LDS); lr_small = the
     generic fix / patch / restore launches instead of the single-workgroup k_lr_small; lr_merge =
-    separate restore and patch launches around the residual + restriction; lr_prefetch = k_lr_small
-    without its up-front loads; lr_dense = the row lists over every vertex for a dense column (the
+    separate restore and patch launches around the residual + restriction; lr_dense = the row lists over every vertex for a dense column (the
     global average measurement) instead of streaming B_g / Y_g with the patched right-hand side in
     a separate vector.  QoI series and state bitwise against the oracle, on and off."""
     out = []
@@ -212,3 +211,43 @@ def test_lowrank_paths_match(hip_device, name, paths, monkeypatch):
         assert np.array_equal(out[-1], mc.get_state())
         s.close()
     assert np.array_equal(out[0], out[1])
+
+
+def test_failed_rollback_refuses_cycle_until_reinstall(hip_device):
+    """mgmc_set_lowrank's failure path: a coarse Cholesky factor that cannot be built
+    after the argument checks leaves the prior operator; if restoring the prior's factor fails as
+    well, the handle refuses every call that runs the cycle or needs the factor (sample, apply,
+    solve, per-level calls) with the reason, keeps the state / QoI calls, and a later successful
+    mgmc_set_lowrank clears it -- after which the chain equals a fresh posterior handle's."""
+    s, mc, p, lat, op = make("2d32_point_global_chol")
+    q = mg.measurement_vector_index(lat, [0.5, 0.5])
+    B = op.get_B()
+    s.sample(2, q)
+    # one injected failure: the posterior factor fails, the prior's is rebuilt -> usable prior handle
+    assert s.lib.mgmc_debug_fail_coarse_factor(s.handle, 1) == 0
+    with pytest.raises(mg.MgmcError, match="injected failure"):
+        s.set_lowrank(B)
+    assert s.lowrank_info(0, mg.FORWARD)[0] == 0
+    s.sample(2, q)
+    # two: the restore fails too -> unusable
+    assert s.lib.mgmc_debug_fail_coarse_factor(s.handle, 2) == 0
+    with pytest.raises(mg.MgmcError, match="unusable"):
+        s.set_lowrank(B)
+    for call in (lambda: s.sample(1, q), lambda: s.apply(np.zeros(lat.Nvertex), np.zeros(lat.Nvertex)),
+                 lambda: s.solve(np.ones(lat.Nvertex), method="cg"), lambda: s.operator_apply(0, np.zeros(lat.Nvertex))):
+        with pytest.raises(mg.MgmcError, match="unusable"):
+            call()
+    x = s.get_state()  # state calls stay available
+    s.set_state(x)
+    # a successful install clears it; the chain then equals a fresh posterior handle's
+    s.set_lowrank(B)
+    ref, _, _, _, _ = make("2d32_point_global_chol")
+    f = np.random.default_rng(5).standard_normal(lat.Nvertex)
+    for h in (s, ref):
+        h.fix_rhs(f)
+        h.set_state(x)
+        h.set_sample_index(40)
+    assert np.array_equal(s.sample(3, q), ref.sample(3, q))
+    assert np.array_equal(s.get_state(), ref.get_state())
+    s.close()
+    ref.close()

@@ -129,6 +129,28 @@ def test_component_kernels_bitwise(hip_device, name):
     s.close()
 
 
+@pytest.mark.parametrize("name", ["3d16", "3d_aniso", "3d_zres27", "3d_zres_lasttile", "3d128_zsweep", "3d64_4lvl"])
+def test_fold_levels_reference_order_bitwise(hip_device, monkeypatch, name):
+    """MGMC_DISABLE=fold: the residual + restriction of every 3D reflection-symmetric 27-point level
+    keeps the reference's CSR summation order (A x ascending from 0.0, then f - Ax:
+    linear_operator.hh:66-76, multigridmc_sampler.cc:118-120), so it equals the FAITHFUL oracle's CSR
+    SpMV + restriction bit for bit on the levels where the default path sums class-folded."""
+    monkeypatch.setenv("MGMC_DISABLE", "fold")
+    shape, kw = CONFIGS[name]
+    s, p, lat = make(shape, **kw)
+    faithful = O.Oracle.fd(lat.shape, p, 25.0, mode=O.FAITHFUL, seed=SEED)
+    rng = np.random.default_rng(43)
+    folds = 0
+    for level in range(p.nlevel - 1):
+        desc = s.level_desc(level)
+        x = rng.standard_normal(desc["ndof"])
+        f = rng.standard_normal(desc["ndof"])
+        folds += O.fold_level(desc)
+        assert np.array_equal(s.residual_restrict(level, f, x), faithful.residual_restrict(level, f, x)), level
+    assert folds >= 1
+    s.close()
+
+
 @pytest.mark.parametrize("name", ["2d64_template_W", "3d16", "3d_aniso", "2d_aniso_ssor", "3d64_4lvl",
                                   "3d128_zsweep", "3d_aniso_zsweep_ssor"])
 def test_multicolour_sweeps_bitwise(hip_device, name):
@@ -183,8 +205,7 @@ def test_mgmc_cycles_bitwise(hip_device, name):
 
 # every MGMC_DISABLE token of mgmc_capi.hip (PathFlag), alone and all together, on configurations
 # where the fast path it turns off would run
-ALL_PATHS = ("tail,fuse_prolong,quads,rb2d,zsweep,pairs,zrestrict,lr_small,lr_merge,lr_prefetch,coarse_precompute,jsweep,"
-             "qrestrict,tail_noise")
+ALL_PATHS = "tail,fuse_prolong,quads,rb2d,zsweep,pairs,zrestrict,lr_small,lr_merge,jsweep,qrestrict,fold"
 VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_ssor"),
             ("fuse_prolong", "3d128_zsweep_odd"), ("fuse_prolong", "3d_zres27"), ("fuse_prolong", "3d_jsweep_ssor_W"),
             ("tail", "3d16"), ("tail", "3d64_4lvl"), ("tail", "2d64_template_W"), ("tail", "3d32_W_ssor"),
@@ -194,19 +215,16 @@ VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_
             ("zsweep", "3d128_zsweep"), ("zsweep", "3d_aniso_zsweep_ssor"), ("zsweep", "3d192_zsweep"),
             ("pairs", "3d64_4lvl"), ("pairs", "2d64_template_W"), ("pairs,quads", "3d32_W_ssor"),
             ("zrestrict", "3d_zres7"), ("zrestrict", "3d_zres27"), ("zrestrict", "3d128_zsweep"),
-            ("coarse_precompute", "3d16"), ("coarse_precompute", "2d64_template_W"),
-            ("coarse_precompute", "3d32_W_ssor"), ("coarse_precompute,tail", "3d64_4lvl"),
             (ALL_PATHS, "3d128_zsweep"), (ALL_PATHS, "3d_aniso_zsweep_ssor"), (ALL_PATHS, "2d64_template_W"),
             (ALL_PATHS, "2d_aniso_ssor"), (ALL_PATHS, "3d_zres27"),
             ("chol_dense", "2d64_chol_W"), ("chol_dense", "3d32_chol_ssor"), ("chol_dense", "3d128_zsweep_chol"),
             ("jsweep", "3d_zres27"), ("jsweep", "3d_jsweep_ssor_W"),
             ("qrestrict", "2d512_qrestrict"), ("qrestrict", "2d_qr_aniso_ssor_W"), ("tail", "2d_qr_cj5"),
             ("tail,qrestrict", "2d_qr_cj5"), (ALL_PATHS, "2d512_qrestrict"),
-            ("tail_noise", "3d16"), ("tail_noise", "3d64_4lvl"), ("tail_noise", "3d32_W_ssor"),
-            ("sym", "3d16"), ("sym", "3d64_4lvl"), ("sym", "3d32_W_ssor"),
             ("prolong_z", "3d128_zsweep"), ("prolong_z", "3d_aniso_zsweep_ssor"), ("prolong_z,fuse_prolong", "3d128_zsweep"),
-            ("zpairs", "3d128_zsweep"), ("zpairs", "3d128_zsweep_odd"), ("zpairs", "3d_aniso_zsweep_ssor"),
-            ("xzero", "3d_zres27"), ("xzero", "3d_jsweep_ssor_W"), ("xzero", "3d64_4lvl"), ("xzero", "3d32_W_ssor")]
+            ("xzero", "3d_zres27"), ("xzero", "3d_jsweep_ssor_W"), ("xzero", "3d64_4lvl"), ("xzero", "3d32_W_ssor"),
+            ("fold", "3d16"), ("fold", "3d64_4lvl"), ("fold", "3d_zres27"), ("fold,tail", "3d64_4lvl"),
+            ("fold,zrestrict", "3d32_W_ssor")]
 
 
 @pytest.mark.parametrize("paths,name", VARIANTS)
@@ -218,23 +236,22 @@ def test_variant_cycles_bitwise(hip_device, monkeypatch, paths, name):
     colour per pass on Galerkin levels; jsweep = colour-pair passes instead of the j-marching half-sweeps
     on 3D Galerkin levels of 64 / 128 pairs per row; zrestrict = the per-point residual + restriction;
     qrestrict = a 2D Galerkin level's last pre-sweep and its residual + restriction as two launches
-    instead of one k_quads_restrict2d; tail_noise = k_tail draws its sweeps' Box-Muller pairs itself
-    instead of the restriction launch before it; sym = the 27-point kernels read all 27 coefficients
-    of a reflection-symmetric stencil instead of one per symmetry class (stencil_coef); prolong_z = the
-    per-point prolongation instead of the z-marching one on 3D levels; zpairs = every z-chunk of the plain
-    fine z-sweep marching up (no up / down chunk pairs); xzero = the restriction zeroes x_{l+1} and the
-    coarse level's first (j-marching) pre-sweep loads it, instead of taking it as zeros;
-    coarse_precompute = the coarse SSOR sampler's right-hand sides inside its colour passes;
+    instead of one k_quads_restrict2d; prolong_z = the per-point prolongation instead of the z-marching
+    one on 3D levels; xzero = the restriction zeroes x_{l+1} and the coarse level's first (j-marching)
+    pre-sweep loads it, instead of taking it as zeros; fold = the residuals of reflection-symmetric
+    27-point levels in the reference's CSR order instead of fold27's;
     chol_dense = the coarse Cholesky's blocked banded solves on a small coarsest level (the oracle's
     blocked mode).  Every combination gives the oracle's cycle exactly."""
     monkeypatch.setenv("MGMC_DISABLE", paths)
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)
     O.set_chol_blocked("chol_dense" in paths.split(","))
+    O.set_no_fold("fold" in paths.split(","))
     try:
         mc = oracle_for(s, p, lat)
     finally:
         O.set_chol_blocked(False)
+        O.set_no_fold(False)
     f = np.random.default_rng(7).standard_normal(lat.Nvertex)
     x_dev, x_orc = np.zeros(lat.Nvertex), np.zeros(lat.Nvertex)
     for _ in range(2):
