@@ -350,6 +350,7 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
     const int nt = npair * (a.T + 1);
     const size_t lds = (size_t)(2 * a.T + 1) * (lv.L.nx + 2) * sizeof(double);
     const bool fwd = direction == MGMC_FORWARD;
+    const bool lanes = dim == 3 && 64 % npair == 0 && tune::QUADS_LANES != 0;
     a.jp1 = fwd ? 0 : 1;  // first pair: colours (0,1) / (4,5) forward, (7,6) / (3,2) backward
     const int nhalf = dim == 3 ? 2 : 1;
     for (int h = 0; h < nhalf; ++h) {
@@ -361,10 +362,15 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
         const dim3 grid(a.nblk_y * nk, 1, nch);
         if (dim == 3) {
             // xzero (3D): the first half takes every x row as 0.0, the second its own planes' rows
-#define MGMC_QD_LAUNCH(SYMV, XZ)                                                                      \
-    do {                                                                                              \
-        if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false, SYMV, XZ>), grid, dim3(nt), lds, s, a);  \
-        else hipLaunchKernelGGL((k_sweep_quads<3, true, SYMV, XZ>), grid, dim3(nt), lds, s, a);       \
+            // rows of npair dividing 64 (127^3 / 63^3 / 31^3 ...): whole rows per wavefront, the window's
+            // outer columns by lane shifts (k_sweep_quads LANES)
+#define MGMC_QD_LAUNCH(SYMV, XZ)                                                                            \
+    do {                                                                                                    \
+        if (lanes) {                                                                                        \
+            if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false, SYMV, XZ, true>), grid, dim3(nt), lds, s, a); \
+            else hipLaunchKernelGGL((k_sweep_quads<3, true, SYMV, XZ, true>), grid, dim3(nt), lds, s, a);      \
+        } else if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false, SYMV, XZ>), grid, dim3(nt), lds, s, a);  \
+        else hipLaunchKernelGGL((k_sweep_quads<3, true, SYMV, XZ>), grid, dim3(nt), lds, s, a);             \
     } while (0)
 #define MGMC_QD_XZ(SYMV)                              \
     do {                                              \
@@ -498,7 +504,8 @@ void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, co
         // minimises rounds of resident workgroups x planes staged per chunk (2 kz + 2); 512^3 level 1:
         // kz 11 = 768 tiles, one round of 3 x 256 slots: 108 -> 101 us (round 4, kernel traces)
         // workgroups per CU: LDS-bound, and at most 3 for the 27-point instances (> 128 VGPRs)
-        const long long per_cu = std::min<long long>(160 * 1024 / zrestrict_lds_bytes(CX, CY), NPTS == 27 ? 3 : 4);
+        const long long per_cu = std::min<long long>(160 * 1024 / zrestrict_lds_bytes(CX, CY),
+                                                     NPTS == 27 ? std::max(3, tune::ZR27_MINW) : 4);
         const long long slots = per_cu * lf.num_cu;
         const long long per_chunk = (long long)a.ntx * a.nty;
         long long best = -1;
@@ -590,7 +597,7 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
             // (fold levels: the SYM instances, whose residual is fold27's)
             if (small && lf.fold) launch_zresrestrict_t<27, 16, 4, 64, true>(lf, lc, x, f, fc, xc, s, nch, tn);
             else if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch, tn);
-            else if (lf.fold) launch_zresrestrict_t<27, tune::ZR27_CX, 4, 256, true>(lf, lc, x, f, fc, xc, s, nch);
+            else if (lf.fold) launch_zresrestrict_t<27, tune::ZR27_CX, tune::ZR27_CY, 256, true>(lf, lc, x, f, fc, xc, s, nch);
             else launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s, nch);
         }
         return;

@@ -159,11 +159,30 @@ struct QuadPassArgs {
     long long cs;       // batched chains: doubles between chains (blockIdx.z = chain)
 };
 
+// 64-bit value of the neighbouring lane (wave_shr:1: lane l - 1's, wave_shl:1: lane l + 1's; 0 past the
+// wavefront's ends), two 32-bit DPP moves
+__device__ __forceinline__ double lane_prev(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xF, 0xF, true);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double lane_next(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xF, 0xF, true);
+    return __hiloint2double(hi, lo);
+}
+
 // SYM: stencil_coef's fold (3D, same bits).  XZ: the input x is known zero (the level's first pre-sweep,
 // mgmc_capi.hip mark_zero_inputs): 1 = every x row is the constant 0.0 (first half), 2 = the own planes'
-// rows are (second half) -- not loaded
-template <int DIM, bool FIRST_ODD, bool SYM = false, int XZ = 0>
+// rows are (second half) -- not loaded.
+// LANES (3D, npair dividing 64: every wavefront holds whole rows, thread = row * npair + pair): each
+// lane loads only its own pair (2m+1, 2m+2) of a window row; the outer columns 2m and 2m+3 are the
+// neighbouring lanes' pairs (lane_prev / lane_next), or the zero guards at positions 0 and nx+1 for the
+// row's first / last pair -- one 16-byte load per row instead of three (the passes are bound by the
+// vector-memory instructions' address / L1 throughput, not by HBM: the window's 27 loads mostly hit)
+template <int DIM, bool FIRST_ODD, bool SYM = false, int XZ = 0, bool LANES = false>
 __global__ void __launch_bounds__(1024) k_sweep_quads(QuadPassArgs a) {
+    static_assert(!LANES || DIM == 3, "LANES: 3D levels");
     {
         const int ch = batch_chain();
         a.x0 += ch * a.cs;
@@ -213,7 +232,38 @@ __global__ void __launch_bounds__(1024) k_sweep_quads(QuadPassArgs a) {
         const bool own = inrow && ((lr & 1) ? true : (a.jp1 == 0 ? lr > 0 : lr < 2 * a.T));
         const long long p0 = inrow ? L.at(i0, j, k) : 0;
         double2 fv = make_double2(0.0, 0.0);
-        if (inrow) {
+        if constexpr (LANES) {
+            // own pairs of the window rows (the whole wavefront takes part in the lane shifts below:
+            // lanes of rows outside the pass hold zeros, and a row's first / last lane never uses a
+            // neighbouring row's value)
+            double2 mid[NR];
+#pragma unroll
+            for (int rr = 0; rr < NR; ++rr) {
+                const int dz = rr / 3 - 1, dy = rr % 3 - 1;
+                mid[rr] = make_double2(0.0, 0.0);
+                if (!inrow || (from_lds && dz == 0 && dy != 0) || XZ == 1 || (XZ == 2 && dz == 0)) continue;
+                mid[rr] = *reinterpret_cast<const double2*>((dz == 0 ? a.x0 : a.xz) + p0 + (long long)dz * L.sp +
+                                                            (long long)dy * L.sx);
+            }
+            if (inrow) fv = *reinterpret_cast<const double2*>(a.f + p0);
+#pragma unroll
+            for (int rr = 0; rr < NR; ++rr) {
+                const int dz = rr / 3 - 1, dy = rr % 3 - 1;
+                if (from_lds && dz == 0 && dy != 0) {  // the new first-pair rows of this plane
+                    const double* q = rowbuf + (lr + dy) * RW + 2 * m;
+                    w[rr][0] = q[0];
+                    w[rr][1] = q[1];
+                    w[rr][2] = q[2];
+                    w[rr][3] = q[3];
+                    continue;
+                }
+                const double l = lane_prev(mid[rr].y), r = lane_next(mid[rr].x);
+                w[rr][0] = m == 0 ? 0.0 : l;
+                w[rr][1] = mid[rr].x;
+                w[rr][2] = mid[rr].y;
+                w[rr][3] = m == npair - 1 ? 0.0 : r;
+            }
+        } else if (inrow) {
 #pragma unroll
             for (int rr = 0; rr < NR; ++rr) {
                 const int dz = DIM == 3 ? rr / 3 - 1 : 0, dy = rr % 3 - 1;

@@ -114,6 +114,19 @@ __host__ __device__ __forceinline__ double fold27(const double (&v)[27], const d
     for (int c = 6; c >= 0; --c) y = fma(a[fold_rep(c)], s[c], y);
     return y;
 }
+// fold27 one value at a time, in ascending t (the same operations in the same order): a caller that
+// walks the window row by row keeps 8 class sums live instead of 27 values
+__device__ __forceinline__ void fold27_acc(double (&s)[8], int t, double v) {
+    const int c = fold_class(t);
+    if (fold_rep(c) == t) s[c] = v;
+    else s[c] = s[c] + v;
+}
+__device__ __forceinline__ double fold27_finish(const double (&s)[8], const double* a) {
+    double y = a[fold_rep(7)] * s[7];
+#pragma unroll
+    for (int c = 6; c >= 0; --c) y = fma(a[fold_rep(c)], s[c], y);
+    return y;
+}
 
 struct GibbsArg {
     double omega;

@@ -27,6 +27,9 @@ constexpr int QUADS_MAXPAIR = 64;
 constexpr int QUADS_NT = 128;
 constexpr int QUADS_NT_WIDE = 256;
 constexpr int QUADS_NT3 = 128;
+// 3D quad passes on rows of npair dividing 64 read one pair per window row and shift the outer columns
+// in from the neighbouring lanes (k_sweep_quads LANES); 0: three pair loads per row
+constexpr int QUADS_LANES = 1;
 
 // j-marching half-sweeps (mgmc_jsweep.hpp): global loads this many steps ahead (2 .. 4), workgroups
 // per half = this many rounds of the resident slots
@@ -36,6 +39,9 @@ constexpr int JS_ROUNDS = 1;
 // residual + restriction (mgmc_zrestrict.hpp): coarse points per tile in x of the symmetric 27-point
 // instance; coarse nx below which the one-wavefront 16 x 4 tiles are used
 constexpr int ZR27_CX = 64;
+// ... its coarse rows per tile and minimum waves per SIMD (register budget: 4 = <= 128 VGPRs)
+constexpr int ZR27_CY = 4;
+constexpr int ZR27_MINW = 1;
 constexpr int ZR_SMALL_NX = 32;
 // the 7-point (fine level) instance with 64 x 8 coarse points per 512-thread workgroup (else 64 x 4
 // per 256 threads) from this many 64 x 8 tiles up (512^3: 32,768)

@@ -53,7 +53,8 @@ struct ZRestrictArgs {
 // SYM: a fold level (reflection-symmetric 27-point stencil): the residual's sum is fold27's
 // LRF: a low-rank level whose right-hand side is read in place (a.lr: f + e, lr_rhs_pair)
 template <int NPTS, int CX, int CY, int NT, bool ZN = false, bool SYM = false, bool LRF = false>
-__global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NPTS == 27 && SYM && CX >= 48 ? tune::ZR27_MINW : 1)))
+k_zresrestrict(ZRestrictArgs a) {
     if (ZN && (int)blockIdx.x >= a.nblk_main) {  // the tail's noise (see ZRestrictArgs)
         const int ch = batch_chain();
         RngKey key = a.key;
@@ -224,23 +225,23 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
                 y1 += a.S.a[16] * pl[1][o1 + XS];
                 y0 += a.S.a[22] * pl[2][o0];
                 y1 += a.S.a[22] * pl[2][o1];
-            } else if constexpr (SYM) {  // a fold level: the class-folded sum (fold27)
-                double v0[27], v1[27];
+            } else if constexpr (SYM) {  // a fold level: the class-folded sum (fold27), row by row
+                double s0[8], s1[8];
 #pragma unroll
                 for (int dz = 0; dz < 3; ++dz)
 #pragma unroll
                     for (int dy = -1; dy <= 1; ++dy) {
                         const double* rowp = pl[dz] + dy * XS;
                         const int c = dz * 9 + (dy + 1) * 3;
-                        v0[c] = rowp[m0];
-                        v1[c] = rowp[m1];
-                        v0[c + 1] = rowp[o0];
-                        v1[c + 1] = rowp[o1];
-                        v0[c + 2] = rowp[m0 + 1];
-                        v1[c + 2] = rowp[m1 + 1];
+                        fold27_acc(s0, c, rowp[m0]);
+                        fold27_acc(s1, c, rowp[m1]);
+                        fold27_acc(s0, c + 1, rowp[o0]);
+                        fold27_acc(s1, c + 1, rowp[o1]);
+                        fold27_acc(s0, c + 2, rowp[m0 + 1]);
+                        fold27_acc(s1, c + 2, rowp[m1 + 1]);
                     }
-                y0 = fold27(v0, a.S.a);
-                y1 = fold27(v1, a.S.a);
+                y0 = fold27_finish(s0, a.S.a);
+                y1 = fold27_finish(s1, a.S.a);
             } else {
 #pragma unroll
                 for (int dz = 0; dz < 3; ++dz)
@@ -290,20 +291,18 @@ __global__ void __launch_bounds__(NT) k_zresrestrict(ZRestrictArgs a) {
             }
     };
 
-    // One fine plane k: deposit x(k+1), issue x(k+2), f(k+1) | barrier | residual(k) | barrier |
+    // One fine plane k: deposit x(k+1), issue x(k+2) | barrier | residual(k), issue f(k+1) | barrier |
     // accumulate.  The next step's residual writes the residual plane only after its own first
     // barrier, i.e. after every thread accumulated; x(k+2) overwrites the slot of x(k-1), last read
     // by residual(k) before the second barrier.
     double acc[NCP], accn[NCP];
-    double2 fcur[NLR];
+    // f(k) is in pf when residual(k) runs; f(k+1) is issued once it has used it (one register set)
     auto step = [&](int k) __attribute__((always_inline)) {
         deposit_x(k + 1);
-#pragma unroll
-        for (int u = 0; u < NLR; ++u) fcur[u] = pf[u];
         issue_x(k + 2);
-        issue_f(k + 1);
         __syncthreads();
-        residual(k, fcur);
+        residual(k, pf);
+        issue_f(k + 1);
         __syncthreads();
     };
     // prologue: x planes 2K0-2, 2K0-1 in LDS, x(2K0) and f(2K0-1) in flight
