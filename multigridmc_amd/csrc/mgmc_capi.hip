@@ -325,13 +325,16 @@ void launch_jsweep(const Level& lv, const double* xin, double* xout, const doubl
     }
 }
 
+// zb: the sweep's Box-Muller pairs drawn by a tail launch (Op::pnz; 3D quad-pass levels, one chain, input x
+// not known zero)
 void launch_quads(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
-                  hipStream_t s, int nch = 1, bool xzero = false) {
+                  hipStream_t s, int nch = 1, bool xzero = false, const double2* zb = nullptr) {
     if (lv.jsweep) {
         launch_jsweep(lv, xin, xout, f, g, direction, s, nch, xzero);
         return;
     }
     QuadPassArgs a;
+    a.zb = zb;
     a.cs = lv.L.nstore;
     a.L = lv.L;
     a.x0 = xin;
@@ -372,15 +375,23 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
         } else if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false, SYMV, XZ>), grid, dim3(nt), lds, s, a);  \
         else hipLaunchKernelGGL((k_sweep_quads<3, true, SYMV, XZ>), grid, dim3(nt), lds, s, a);             \
     } while (0)
+#define MGMC_QD_PZ(SYMV, LANESV)                                                                                  \
+    do {                                                                                                          \
+        if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false, SYMV, 0, LANESV, true>), grid, dim3(nt), lds, s, a); \
+        else hipLaunchKernelGGL((k_sweep_quads<3, true, SYMV, 0, LANESV, true>), grid, dim3(nt), lds, s, a);      \
+    } while (0)
 #define MGMC_QD_XZ(SYMV)                              \
     do {                                              \
-        if (!xzero) MGMC_QD_LAUNCH(SYMV, 0);          \
+        if (zb && lanes) MGMC_QD_PZ(SYMV, true);      \
+        else if (zb) MGMC_QD_PZ(SYMV, false);         \
+        else if (!xzero) MGMC_QD_LAUNCH(SYMV, 0);     \
         else if (h == 0) MGMC_QD_LAUNCH(SYMV, 1);     \
         else MGMC_QD_LAUNCH(SYMV, 2);                 \
     } while (0)
             if (lv.sym) MGMC_QD_XZ(true);
             else MGMC_QD_XZ(false);
 #undef MGMC_QD_XZ
+#undef MGMC_QD_PZ
 #undef MGMC_QD_LAUNCH
         } else {
             if (fwd) hipLaunchKernelGGL((k_sweep_quads<2, false>), grid, dim3(nt), lds, s, a);
@@ -1250,6 +1261,10 @@ void free_tails(mgmc_handle* h) {
         if (p) hipFree(p);
     for (auto p : h->tail_jobs)
         if (p) hipFree(p);
+    for (auto p : h->pn_bufs)
+        if (p) hipFree(p);
+    h->pn_bufs.clear();
+    h->tail_pn_wg.clear();
     h->tail_args.clear();
     h->tail_lds.clear();
     h->tail_sym.clear();
@@ -1365,6 +1380,8 @@ int build_tails_only(mgmc_handle* h) {
         A.cs = h->levels[lt].L.nstore;  // batched chains: one workgroup per chain
         A.chain0 = (uint32_t)h->chain;
         A.seed_hi = (uint32_t)(h->seed >> 32);
+        A.nwg = h->nchains;  // (post-sweep noise jobs: plan_post_noise)
+        A.npn = 0;
 #ifdef MGMC_TAIL_PROF
         if (h->tail_args.empty()) {
             if (!h->tail_prof) HIPCHK(h, hipMalloc(&h->tail_prof, 256 * sizeof(unsigned long long)));
@@ -1413,6 +1430,7 @@ int build_tails_only(mgmc_handle* h) {
         h->tail_jobs.push_back(dj);
         h->tail_njobs.push_back(zb ? (int)jobs.size() : 0);
         h->tail_zn.push_back(zb ? zn : 0);
+        h->tail_pn_wg.push_back(0);
         TailArgs* d = nullptr;
         HIPCHK(h, hipMalloc(&d, sizeof(TailArgs)));
         HIPCHK(h, hipMemcpy(d, &A, sizeof(TailArgs), hipMemcpyHostToDevice));
@@ -1537,10 +1555,66 @@ void mark_zero_inputs(mgmc_handle* h) {
     }
 }
 
+// A tail launch runs one workgroup on one CU (512^3: 40-43 us); the rest of the chip is idle meanwhile.
+// Its spare workgroups draw the Box-Muller pairs of the sweeps that follow it instead: for every 3D
+// Galerkin level swept by quad passes (no low-rank part, not a field level), the first sweep on that
+// level after the tail and before the next tail (in a V-cycle its post-sweep) whose input x is not known
+// zero.  The pairs are those the sweep would draw (same Philox counter: pair id, the sweep's tag, the
+// sample index at run time; same arithmetic), so the chain is bitwise unchanged.  512^3 (round 6): the
+// 127^3 post quad passes 16.5 -> 13.9 us each.  Not the j-marching levels: their post half-sweeps,
+// reading the pairs (16 B per pair) instead of drawing them, stayed at 72 us, and the 8.3 M pairs of
+// the 255^3 level took the tail launch from 43 to 60 us.  One chain per handle (batched handles' tails
+// run one workgroup per chain; their draws stay in the sweeps), and at most PN_MAX_PAIRS pairs per
+// tail, well inside what the spare workgroups draw within the tail's own time.
+constexpr long long PN_MAX_PAIRS = 2LL << 20;
+
+int plan_post_noise(mgmc_handle* h) {
+    for (Op& op : h->ops) op.pnz = nullptr;
+    if ((h->paths & PATH_NO_POST_NOISE) || h->nchains != 1) return MGMC_OK;
+    std::vector<double2*> buf(h->levels.size(), nullptr);
+    for (size_t t = 0; t < h->ops.size(); ++t) {
+        if (h->ops[t].kind != OP_TAIL) continue;
+        const int ti = h->ops[t].tail;
+        std::vector<PostNoiseJob> jobs;
+        std::vector<char> used(h->levels.size(), 0);
+        long long total = 0;
+        for (size_t q = t + 1; q < h->ops.size() && h->ops[q].kind != OP_TAIL; ++q) {
+            Op& op = h->ops[q];
+            if (op.kind != OP_SWEEP || op.xzero || op.level < 1 || used[op.level]) continue;
+            const Level& lv = h->levels[op.level];
+            if (lv.spec.dim != 3 || lv.field || lv.lr.m > 0 || !lv.quads || lv.jsweep || !lv.pingpong()) continue;
+            used[op.level] = 1;
+            const long long n = (long long)(lv.L.nx / 2) * (lv.L.ny - 1) * (lv.L.nz - 1);
+            if (total + n > PN_MAX_PAIRS || (int)jobs.size() >= TAIL_MAX_PN_JOBS) continue;
+            if (!buf[op.level]) {
+                if (hipMalloc(&buf[op.level], (size_t)n * sizeof(double2)) != hipSuccess) {
+                    buf[op.level] = nullptr;
+                    (void)hipGetLastError();
+                    continue;  // (this sweep draws its own)
+                }
+                poison_fill(h, buf[op.level], (size_t)n * sizeof(double2));
+                h->pn_bufs.push_back(buf[op.level]);
+            }
+            total += n;
+            jobs.push_back(PostNoiseJob{lv.L.nx, lv.L.ny, lv.L.nz, op.tag, buf[op.level]});
+            op.pnz = buf[op.level];
+        }
+        if (jobs.empty()) continue;
+        TailArgs* d = h->tail_args[ti];
+        const int npn = (int)jobs.size();
+        HIPCHK(h, hipMemcpy(d->pn, jobs.data(), jobs.size() * sizeof(PostNoiseJob), hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(&d->npn, &npn, sizeof(int), hipMemcpyHostToDevice));
+        // one workgroup per other CU (the tail's LDS admits one per CU)
+        h->tail_pn_wg[ti] = std::max(1, h->levels[0].num_cu - h->nchains);
+    }
+    return MGMC_OK;
+}
+
 int build_tails(mgmc_handle* h) {
-    const int rc = build_tails_only(h);
+    int rc = build_tails_only(h);
     if (rc == MGMC_OK) fuse_sweep_restrict(h);
     if (rc == MGMC_OK) mark_zero_inputs(h);
+    if (rc == MGMC_OK) rc = plan_post_noise(h);
     return rc;
 }
 
@@ -1574,7 +1648,7 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                                   h->cfg.coarse_scaling, s, nch, lrr.e ? &lrr : nullptr);
                 } else if (lv.quads) {
                     xo = lv.buf(1 - op.src);
-                    launch_quads(lv, lv.buf(op.src), xo, fs, g, op.direction, s, nch, op.xzero != 0);
+                    launch_quads(lv, lv.buf(op.src), xo, fs, g, op.direction, s, nch, op.xzero != 0, op.pnz);
                 } else if (lv.rb2d) {
                     xo = lv.buf(1 - op.src);
                     launch_rb2d(lv, lv.buf(op.src), xo, fs, g, op.direction, true, s, nch);
@@ -1655,15 +1729,16 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                                hipMemcpyDeviceToDevice, s);
                 break;
             }
-            case OP_TAIL: {  // one workgroup per chain
+            case OP_TAIL: {  // one workgroup per chain (+ spare workgroups drawing post-sweep noise)
                 const size_t lds = h->tail_lds[op.tail];
+                const dim3 grid(nch + h->tail_pn_wg[op.tail]);
                 if (lv.spec.dim == 3 && h->tail_sym[op.tail])
-                    hipLaunchKernelGGL((k_tail<3, true>), dim3(nch), dim3(TAIL_NT), lds, s,
+                    hipLaunchKernelGGL((k_tail<3, true>), grid, dim3(TAIL_NT), lds, s,
                                        (const TailArgs*)h->tail_args[op.tail]);
                 else if (lv.spec.dim == 3)
-                    hipLaunchKernelGGL(k_tail<3>, dim3(nch), dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
+                    hipLaunchKernelGGL(k_tail<3>, grid, dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
                 else
-                    hipLaunchKernelGGL(k_tail<2>, dim3(nch), dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
+                    hipLaunchKernelGGL(k_tail<2>, grid, dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
                 break;
             }
             case OP_QOI: {
@@ -2439,6 +2514,12 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
     }
     std::string text = "sweep=" + sweep;
     if (!post.empty()) text += ";post_sweep=" + post;
+    // a sweep of this level reads its Box-Muller pairs from a tail launch's spare workgroups (plan_post_noise)
+    for (const Op& op : h->ops)
+        if (op.kind == OP_SWEEP && op.level == level && op.pnz) {
+            text += ";noise=tail";
+            break;
+        }
     if (!res.empty()) text += ";residual_restrict=" + res;
     // the low-rank path of a posterior level (mgmc_lowrank.hpp; rhs_inplace: the sweeps and the
     // residual above run their LRF instances, f + e read in place)

@@ -157,6 +157,7 @@ struct QuadPassArgs {
     int T;              // rows of parity jp2 per workgroup (2T+1 rows in all)
     int nblk_y;         // workgroups along j
     long long cs;       // batched chains: doubles between chains (blockIdx.z = chain)
+    const double2* zb;  // PZ: the sweep's Box-Muller pairs, drawn earlier (pair id order; one chain)
 };
 
 // 64-bit value of the neighbouring lane (wave_shr:1: lane l - 1's, wave_shl:1: lane l + 1's; 0 past the
@@ -180,7 +181,8 @@ __device__ __forceinline__ double lane_next(double v) {
 // neighbouring lanes' pairs (lane_prev / lane_next), or the zero guards at positions 0 and nx+1 for the
 // row's first / last pair -- one 16-byte load per row instead of three (the passes are bound by the
 // vector-memory instructions' address / L1 throughput, not by HBM: the window's 27 loads mostly hit)
-template <int DIM, bool FIRST_ODD, bool SYM = false, int XZ = 0, bool LANES = false>
+// PZ: the Box-Muller pairs come from a.zb (k_tail's spare workgroups, mgmc_tail.hpp tail_post_noise)
+template <int DIM, bool FIRST_ODD, bool SYM = false, int XZ = 0, bool LANES = false, bool PZ = false>
 __global__ void __launch_bounds__(1024) k_sweep_quads(QuadPassArgs a) {
     static_assert(!LANES || DIM == 3, "LANES: 3D levels");
     {
@@ -232,6 +234,7 @@ __global__ void __launch_bounds__(1024) k_sweep_quads(QuadPassArgs a) {
         const bool own = inrow && ((lr & 1) ? true : (a.jp1 == 0 ? lr > 0 : lr < 2 * a.T));
         const long long p0 = inrow ? L.at(i0, j, k) : 0;
         double2 fv = make_double2(0.0, 0.0);
+        double2 zzv = make_double2(0.0, 0.0);  // PZ: the pair's noise, loaded with f
         if constexpr (LANES) {
             // own pairs of the window rows (the whole wavefront takes part in the lane shifts below:
             // lanes of rows outside the pass hold zeros, and a row's first / last lane never uses a
@@ -246,6 +249,7 @@ __global__ void __launch_bounds__(1024) k_sweep_quads(QuadPassArgs a) {
                                                             (long long)dy * L.sx);
             }
             if (inrow) fv = *reinterpret_cast<const double2*>(a.f + p0);
+            if (PZ && inrow) zzv = a.zb[pair_id<DIM>(L, i0, j, k)];
 #pragma unroll
             for (int rr = 0; rr < NR; ++rr) {
                 const int dz = rr / 3 - 1, dy = rr % 3 - 1;
@@ -289,6 +293,7 @@ __global__ void __launch_bounds__(1024) k_sweep_quads(QuadPassArgs a) {
                 w[rr][3] = hi.x;
             }
             fv = *reinterpret_cast<const double2*>(a.f + p0);
+            if (PZ) zzv = a.zb[pair_id<DIM>(L, i0, j, k)];
         } else {
 #pragma unroll
             for (int rr = 0; rr < NR; ++rr) w[rr][0] = w[rr][1] = w[rr][2] = w[rr][3] = 0.0;
@@ -296,7 +301,10 @@ __global__ void __launch_bounds__(1024) k_sweep_quads(QuadPassArgs a) {
         double z0 = 0.0, z1 = 0.0;
         const bool odd_in = inrow && i0 <= L.nx - 1;
         const bool even_in = inrow && i0 + 1 <= L.nx - 1;
-        if (odd_in) {
+        if (PZ) {
+            z0 = zzv.x;
+            z1 = zzv.y;
+        } else if (odd_in) {
             const uint32_t pair = pair_id<DIM>(L, i0, j, k);
             const Philox4 rnd = philox4x32_10(pair, a.G.tag, (uint32_t)*a.G.sample, (uint32_t)(*a.G.sample >> 32),
                                               a.G.key.k0, a.G.key.k1);

@@ -86,6 +86,7 @@ struct Op {
     int zpre = 0;            // OP_SWEEP_RESTRICT: also draws the next OP_COARSE_LDS's noise into mgmc_handle::zbuf;
                              // OP_COARSE_LDS: reads it from there; OP_RESIDUAL_RESTRICT: 1 + the index of
                              // the OP_TAIL after it whose noise its spare workgroups draw
+    const double2* pnz = nullptr;  // OP_SWEEP: its Box-Muller pairs, drawn by an earlier tail launch (plan_post_noise)
 };
 
 
@@ -110,6 +111,7 @@ enum PathFlag : uint32_t {
     PATH_NO_PROLONG_Z = 1u << 13,         // big 3D levels: the per-point prolongation instead of the z-marching one
     PATH_NO_XZERO = 1u << 14,             // the restriction zeroes x_{l+1} and its first pre-sweep loads it
     PATH_NO_FOLD = 1u << 15,              // 3D fold levels: residuals in the reference's CSR order, not fold27's
+    PATH_NO_POST_NOISE = 1u << 16,        // sweeps after a tail draw their own noise (not the tail launch's spare workgroups)
 };
 
 struct PathToken {
@@ -125,6 +127,7 @@ constexpr PathToken kPathTokens[] = {
     {"chol_dense", PATH_NO_CHOL_DENSE}, {"jsweep", PATH_NO_JSWEEP},
     {"qrestrict", PATH_NO_QRESTRICT}, {"prolong_z", PATH_NO_PROLONG_Z},
     {"xzero", PATH_NO_XZERO},         {"fold", PATH_NO_FOLD},
+    {"post_noise", PATH_NO_POST_NOISE},
 };
 
 // parse MGMC_DISABLE; returns false (and the offending token in *bad) for an unknown token
@@ -317,6 +320,10 @@ struct mgmc_handle {
     std::vector<TailNoiseJob*> tail_jobs;
     std::vector<int> tail_njobs;
     std::vector<long long> tail_zn;
+    // per OP_TAIL: spare workgroups of its launch drawing the post-sweep noise jobs (plan_post_noise), and
+    // the noise buffers of those jobs (one per level, freed with the tails)
+    std::vector<int> tail_pn_wg;
+    std::vector<double2*> pn_bufs;
     double* sv[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // solver: b x r z p q (level 0)
     double* sv_scal = nullptr;   // solver scalars
     double* sv_part = nullptr;   // reduction partials

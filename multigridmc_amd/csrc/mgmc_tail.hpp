@@ -55,6 +55,17 @@ struct TailNoiseJob {
 };
 constexpr int TAIL_MAX_NOISE_JOBS = 24;
 
+// one job of the noise the tail launch draws for a sweep after it (the first post-sweep of each 3D
+// Galerkin level between the tail and the fine level, plan_post_noise in mgmc_capi.hip): every pair of
+// the level's sweep with tag `tag`, pair id q -> dst[q] (pair_id<3> order), drawn by the launch's spare
+// workgroups while the tail's one workgroup runs on one CU
+struct PostNoiseJob {
+    int nx, ny, nz;
+    uint32_t tag;
+    double2* dst;
+};
+constexpr int TAIL_MAX_PN_JOBS = 8;
+
 struct TailLevel {
     Layout G;      // LDS layout (off 0, sx = nx+1, sp = sx (ny+1), 3D padded to 8 mod 16)
     int ox, of;    // LDS offsets (doubles) of x and f
@@ -92,6 +103,9 @@ struct TailArgs {
     uint32_t chain0, seed_hi;  // chain c's Philox key: (key.k0, lo32(chain0 + c) ^ seed_hi)
     const double2* zb;     // pre-drawn Box-Muller pairs of the sweeps (nullptr: drawn here), zbs per chain
     long long zbs;
+    int nwg;               // workgroups running the tail (one per chain); the launch's blocks from nwg on draw pn
+    int npn;               // post-sweep noise jobs (one chain only)
+    PostNoiseJob pn[TAIL_MAX_PN_JOBS];
     TailLevel lv[TAIL_MAX_LEVELS];
     TailOp ops[TAIL_MAX_OPS];
     unsigned long long* prof;  // (timing builds, MGMC_TAIL_PROF: wall-clock stamps per phase; else null)
@@ -206,11 +220,45 @@ __device__ __forceinline__ double tail_sum(const double* __restrict__ x, int p, 
     return res;
 }
 
+// The spare workgroups of a tail launch (blocks nwg ..): the Box-Muller pairs of the post-sweep noise
+// jobs (PostNoiseJob), pair q of a job -> dst[q], the same Philox counter and arithmetic as the sweep
+// kernel would use (normal_pair_t with the tables in LDS), chain 0's key.  Items are dealt round-robin
+// over every spare thread, so consecutive lanes store consecutive 16-byte pairs.
+__device__ __forceinline__ void tail_post_noise(const TailArgs* __restrict__ A, double* tab) {
+    for (int q = threadIdx.x; q < 64; q += blockDim.x) {
+        tab[q] = LOGTAB_RC[q];
+        tab[64 + q] = LOGTAB_HI[q];
+        tab[128 + q] = LOGTAB_LO[q];
+    }
+    for (int q = threadIdx.x; q < 130; q += blockDim.x) tab[192 + q] = SINCOS_TAB[q];
+    __syncthreads();
+    const uint64_t sample = *A->sample;
+    const uint32_t s_lo = (uint32_t)sample, s_hi = (uint32_t)(sample >> 32);
+    const RngKey key = A->key;
+    const uint32_t nw = (gridDim.x - (uint32_t)A->nwg) * blockDim.x;
+    const uint32_t w0 = (blockIdx.x - (uint32_t)A->nwg) * blockDim.x + threadIdx.x;
+    const int npn = A->npn;
+    for (int jb = 0; jb < npn; ++jb) {
+        const PostNoiseJob J = A->pn[jb];
+        const uint32_t n = (uint32_t)(J.nx / 2) * (uint32_t)(J.ny - 1) * (uint32_t)(J.nz - 1);
+        for (uint32_t q = w0; q < n; q += nw) {
+            const Philox4 r = philox4x32_10(q, J.tag, s_lo, s_hi, key.k0, key.k1);
+            double z0, z1;
+            normal_pair_t(r, &z0, &z1, tab, tab + 64, tab + 128, tab + 192);
+            J.dst[q] = make_double2(z0, z1);
+        }
+    }
+}
+
 // SYM: every 27-point level of the tail has a reflection-symmetric stencil (stencil_coef)
 template <int DIM, bool SYM = false>
 __global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
     constexpr int NPTS = DIM == 3 ? 27 : 9;
     extern __shared__ __attribute__((aligned(16))) double lds[];
+    if ((int)blockIdx.x >= A->nwg) {  // a spare workgroup: post-sweep noise only
+        tail_post_noise(A, lds);
+        return;
+    }
     const int tid = threadIdx.x, nt = blockDim.x;
     const int ntot = A->lds_doubles;
     // the arguments' cache lines into L2 by vector loads, one line per thread, behind the LDS fill: the

@@ -50,6 +50,27 @@ struct ZRestrictArgs {
     LRRhsArg lr;               // LRF: the right-hand side is f patched in place (mgmc_kernels.hpp)
 };
 
+// One plane's 3 x 4 window of a residual pair item (rows dy = -1, 0, 1 at byte offsets 0, RB, 2 RB from
+// `base`, the LDS byte address of row dy = -1's odd element i): per row x(i), x(i+2), x(i-1), x(i+1) at
+// byte offsets 0, 8, EV - 8, EV (EV = the even block's offset).  Twelve single ds_read_b64 with immediate
+// offsets in one statement that ends in the wait: the compiler otherwise pairs them into ds_read2_b64,
+// which moves 8 bytes per lane at half the LDS rate (MI355X_MICROARCH.md, LDS table) -- the level-1
+// residual + restriction reads 36 values per pair item from LDS and was bound by those reads.
+#define ZR_RD(n, o) "ds_read_b64 %" #n ", %12 offset:" #o "\n"
+template <int RB, int EV>
+__device__ __forceinline__ void zr_plane12(uint32_t base, double (&v)[12]) {
+    static_assert(2 * RB + EV < 65536 && EV >= 8, "ds offsets");
+    asm volatile(ZR_RD(0, 0) ZR_RD(1, 8) ZR_RD(2, %c13) ZR_RD(3, %c14)
+                 ZR_RD(4, %c15) ZR_RD(5, %c16) ZR_RD(6, %c17) ZR_RD(7, %c18)
+                 ZR_RD(8, %c19) ZR_RD(9, %c20) ZR_RD(10, %c21) ZR_RD(11, %c22) "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
+                   "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11])
+                 : "v"(base), "i"(EV - 8), "i"(EV), "i"(RB), "i"(RB + 8), "i"(RB + EV - 8), "i"(RB + EV),
+                   "i"(2 * RB), "i"(2 * RB + 8), "i"(2 * RB + EV - 8), "i"(2 * RB + EV)
+                 : "memory");
+}
+#undef ZR_RD
+
 // SYM: a fold level (reflection-symmetric 27-point stencil): the residual's sum is fold27's
 // LRF: a low-rank level whose right-hand side is read in place (a.lr: f + e, lr_rhs_pair)
 template <int NPTS, int CX, int CY, int NT, bool ZN = false, bool SYM = false, bool LRF = false>
@@ -208,7 +229,7 @@ k_zresrestrict(ZRestrictArgs a) {
         for (int u = 0; u < NLR; ++u) {
             if (rlds[u] < 0) continue;
             const int o0 = rxo[u], o1 = rxo[u] + XPP;  // odd / even vertex
-            const int m0 = o0 + XPP - 1, m1 = o1 - XPP;   // their x-1 neighbours (x+1 = m + 1)
+            const int m0 = o0 + XPP - 1, m1 = o1 - XPP;   // their x-1 neighbours (x+1 = m + 1; 7-point)
             double y0 = 0.0, y1 = 0.0;
             if (NPTS == 7) {
                 y0 += a.S.a[4] * pl[0][o0];
@@ -225,37 +246,43 @@ k_zresrestrict(ZRestrictArgs a) {
                 y1 += a.S.a[16] * pl[1][o1 + XS];
                 y0 += a.S.a[22] * pl[2][o0];
                 y1 += a.S.a[22] * pl[2][o1];
-            } else if constexpr (SYM) {  // a fold level: the class-folded sum (fold27), row by row
+            } else if constexpr (SYM) {  // a fold level: the class-folded sum (fold27), each plane's window by
+                                         // zr_plane12 (512^3 level 1: 96 -> 81 us against the compiler's read2 pairs)
                 double s0[8], s1[8];
 #pragma unroll
-                for (int dz = 0; dz < 3; ++dz)
+                for (int dz = 0; dz < 3; ++dz) {
+                    double v[12];
+                    zr_plane12<XS * 8, XPP * 8>(lds_addr(pl[dz] - XS + o0), v);
 #pragma unroll
-                    for (int dy = -1; dy <= 1; ++dy) {
-                        const double* rowp = pl[dz] + dy * XS;
-                        const int c = dz * 9 + (dy + 1) * 3;
-                        fold27_acc(s0, c, rowp[m0]);
-                        fold27_acc(s1, c, rowp[m1]);
-                        fold27_acc(s0, c + 1, rowp[o0]);
-                        fold27_acc(s1, c + 1, rowp[o1]);
-                        fold27_acc(s0, c + 2, rowp[m0 + 1]);
-                        fold27_acc(s1, c + 2, rowp[m1 + 1]);
+                    for (int r = 0; r < 3; ++r) {
+                        const int c = dz * 9 + r * 3;
+                        // row by row, (i-1, i, i+1) for the odd vertex and (i, i+1, i+2) for the even one
+                        fold27_acc(s0, c, v[4 * r + 2]);
+                        fold27_acc(s1, c, v[4 * r + 0]);
+                        fold27_acc(s0, c + 1, v[4 * r + 0]);
+                        fold27_acc(s1, c + 1, v[4 * r + 3]);
+                        fold27_acc(s0, c + 2, v[4 * r + 3]);
+                        fold27_acc(s1, c + 2, v[4 * r + 1]);
                     }
+                }
                 y0 = fold27_finish(s0, a.S.a);
                 y1 = fold27_finish(s1, a.S.a);
-            } else {
+            } else {  // the reference's CSR order: ascending columns from 0.0, separate multiply and add
 #pragma unroll
-                for (int dz = 0; dz < 3; ++dz)
+                for (int dz = 0; dz < 3; ++dz) {
+                    double v[12];
+                    zr_plane12<XS * 8, XPP * 8>(lds_addr(pl[dz] - XS + o0), v);
 #pragma unroll
-                    for (int dy = -1; dy <= 1; ++dy) {
-                        const double* rowp = pl[dz] + dy * XS;
-                        const int c = dz * 9 + (dy + 1) * 3;
-                        y0 += stencil_coef<SYM>(a.S, c) * rowp[m0];
-                        y1 += stencil_coef<SYM>(a.S, c) * rowp[m1];
-                        y0 += stencil_coef<SYM>(a.S, c + 1) * rowp[o0];
-                        y1 += stencil_coef<SYM>(a.S, c + 1) * rowp[o1];
-                        y0 += stencil_coef<SYM>(a.S, c + 2) * rowp[m0 + 1];
-                        y1 += stencil_coef<SYM>(a.S, c + 2) * rowp[m1 + 1];
+                    for (int r = 0; r < 3; ++r) {
+                        const int c = dz * 9 + r * 3;
+                        y0 += a.S.a[c] * v[4 * r + 2];
+                        y1 += a.S.a[c] * v[4 * r + 0];
+                        y0 += a.S.a[c + 1] * v[4 * r + 0];
+                        y1 += a.S.a[c + 1] * v[4 * r + 3];
+                        y0 += a.S.a[c + 2] * v[4 * r + 3];
+                        y1 += a.S.a[c + 2] * v[4 * r + 1];
                     }
+                }
             }
             double2 f = fv[u];
             if constexpr (LRF) f = lr_rhs_pair(f, lre);

@@ -67,6 +67,9 @@ CONFIGS = {
     "3d_zsr_ssor_W": ((128, 64, 64), dict(nlevel=3, cycle=2, smoother="SSOR", npresmooth=2, omega=0.9)),
     # j-marching half-sweeps (k_jsweep_half) on a short level 1 of 128-pair rows, SSOR, W-cycle
     "3d_jsweep_ssor_W": ((512, 44, 60), dict(nlevel=3, cycle=2, smoother="SSOR", npresmooth=2, omega=1.1)),
+    # a tail (levels 3-4) followed by a 127 x 7 x 7 quad-pass level whose post-sweep reads the Box-Muller pairs
+    # the tail launch's spare workgroups drew (plan_post_noise), and a 255 x 15 x 15 j-marching level
+    "3d_jsweep_tail": ((512, 32, 32), dict(nlevel=5)),
     # dense Cholesky coarse sampler (CholeskySampler, x = G f + U xi on the coarsest level)
     "2d64_chol_W": ((64, 64), dict(nlevel=4, cycle=2, coarse_solver="Cholesky")),
     "3d32_chol_ssor": ((32, 32, 32), dict(nlevel=3, smoother="SSOR", coarse_solver="Cholesky")),
@@ -204,9 +207,31 @@ def test_mgmc_cycles_bitwise(hip_device, name):
     s.close()
 
 
+def test_tail_drawn_post_noise_path(hip_device, monkeypatch):
+    """The quad-pass levels between a tail and the fine level read their first post-sweep's Box-Muller
+    pairs from the tail launch's spare workgroups (not the j-marching level 1, not the fine level), and
+    the cycle is bitwise the same with the sweeps drawing them themselves (MGMC_DISABLE=post_noise)."""
+    shape, kw = CONFIGS["3d_jsweep_tail"]
+    s, p, lat = make(shape, **kw)
+    assert s.level_kernels(1)["sweep"].startswith("k_jsweep_half<128")
+    assert s.level_kernels(2)["sweep"] == "k_sweep_quads<3>" and s.level_kernels(2).get("noise") == "tail"
+    assert "noise" not in s.level_kernels(0) and "noise" not in s.level_kernels(1)
+    monkeypatch.setenv("MGMC_DISABLE", "post_noise")
+    s2, _, _ = make(shape, **kw)
+    assert "noise" not in s2.level_kernels(2)
+    f = np.random.default_rng(3).standard_normal(lat.Nvertex)
+    q = mg.measurement_vector_index(lat, [0.5] * lat.dim)
+    out = []
+    for h in (s, s2):
+        h.fix_rhs(f)
+        out.append((h.sample(4, q), h.get_state()))
+        h.close()
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+
+
 # every MGMC_DISABLE token of mgmc_capi.hip (PathFlag), alone and all together, on configurations
 # where the fast path it turns off would run
-ALL_PATHS = "tail,fuse_prolong,quads,rb2d,zsweep,pairs,zrestrict,lr_small,lr_merge,jsweep,qrestrict,fold"
+ALL_PATHS = "tail,fuse_prolong,quads,rb2d,zsweep,pairs,zrestrict,lr_small,lr_merge,jsweep,qrestrict,fold,post_noise"
 VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_ssor"),
             ("fuse_prolong", "3d128_zsweep_odd"), ("fuse_prolong", "3d_zres27"), ("fuse_prolong", "3d_jsweep_ssor_W"),
             ("tail", "3d16"), ("tail", "3d64_4lvl"), ("tail", "2d64_template_W"), ("tail", "3d32_W_ssor"),
@@ -225,7 +250,9 @@ VARIANTS = [("fuse_prolong", "3d128_zsweep"), ("fuse_prolong", "3d_aniso_zsweep_
             ("prolong_z", "3d128_zsweep"), ("prolong_z", "3d_aniso_zsweep_ssor"), ("prolong_z,fuse_prolong", "3d128_zsweep"),
             ("xzero", "3d_zres27"), ("xzero", "3d_jsweep_ssor_W"), ("xzero", "3d64_4lvl"), ("xzero", "3d32_W_ssor"),
             ("fold", "3d16"), ("fold", "3d64_4lvl"), ("fold", "3d_zres27"), ("fold,tail", "3d64_4lvl"),
-            ("fold,zrestrict", "3d32_W_ssor")]
+            ("fold,zrestrict", "3d32_W_ssor"),
+            ("post_noise", "3d64_4lvl"), ("post_noise", "3d32_W_ssor"), ("post_noise", "3d_jsweep_tail"),
+            ("jsweep", "3d_jsweep_tail")]
 
 
 @pytest.mark.parametrize("paths,name", VARIANTS)
@@ -242,7 +269,9 @@ def test_variant_cycles_bitwise(hip_device, monkeypatch, paths, name):
     pre-sweep loads it, instead of taking it as zeros; fold = the residuals of reflection-symmetric
     27-point levels in the reference's CSR order instead of fold27's;
     chol_dense = the coarse Cholesky's blocked banded solves on a small coarsest level (the oracle's
-    blocked mode).  Every combination gives the oracle's cycle exactly."""
+    blocked mode); post_noise = the sweeps after a tail draw their own Box-Muller pairs instead of
+    reading those the tail launch's spare workgroups drew.  Every combination gives the oracle's cycle
+    exactly."""
     monkeypatch.setenv("MGMC_DISABLE", paths)
     shape, kw = CONFIGS[name]
     s, p, lat = make(shape, **kw)

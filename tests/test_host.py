@@ -104,7 +104,7 @@ def test_product_reads_only_documented_switches():
             src += open(os.path.join(csrc, fn)).read()
     assert sorted(set(re.findall(r'getenv\("([A-Z_0-9]+)"\)', src))) == ["MGMC_DISABLE", "MGMC_GRAPH_UNROLL", "MGMC_POISON"]
     tokens = re.findall(r'\{"([a-z_0-9]+)", PATH_NO_', src)
-    assert len(tokens) == 16
+    assert len(tokens) == 17
     tested = open(os.path.join(ROOT, "tests", "test_gpu_parity.py")).read() + \
         open(os.path.join(ROOT, "tests", "test_gpu_lowrank.py")).read()
     for t in tokens:
