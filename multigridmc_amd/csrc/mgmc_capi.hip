@@ -1380,8 +1380,7 @@ int build_tails_only(mgmc_handle* h) {
         A.cs = h->levels[lt].L.nstore;  // batched chains: one workgroup per chain
         A.chain0 = (uint32_t)h->chain;
         A.seed_hi = (uint32_t)(h->seed >> 32);
-        A.nwg = h->nchains;  // (post-sweep noise jobs: plan_post_noise)
-        A.npn = 0;
+        A.npn = 0;  // (post-sweep noise jobs: plan_post_noise)
 #ifdef MGMC_TAIL_PROF
         if (h->tail_args.empty()) {
             if (!h->tail_prof) HIPCHK(h, hipMalloc(&h->tail_prof, 256 * sizeof(unsigned long long)));
@@ -1732,13 +1731,13 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
             case OP_TAIL: {  // one workgroup per chain (+ spare workgroups drawing post-sweep noise)
                 const size_t lds = h->tail_lds[op.tail];
                 const dim3 grid(nch + h->tail_pn_wg[op.tail]);
+                const TailArgs* ta = h->tail_args[op.tail];
                 if (lv.spec.dim == 3 && h->tail_sym[op.tail])
-                    hipLaunchKernelGGL((k_tail<3, true>), grid, dim3(TAIL_NT), lds, s,
-                                       (const TailArgs*)h->tail_args[op.tail]);
+                    hipLaunchKernelGGL((k_tail<3, true>), grid, dim3(TAIL_NT), lds, s, ta, nch);
                 else if (lv.spec.dim == 3)
-                    hipLaunchKernelGGL(k_tail<3>, grid, dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
+                    hipLaunchKernelGGL(k_tail<3>, grid, dim3(TAIL_NT), lds, s, ta, nch);
                 else
-                    hipLaunchKernelGGL(k_tail<2>, grid, dim3(TAIL_NT), lds, s, (const TailArgs*)h->tail_args[op.tail]);
+                    hipLaunchKernelGGL(k_tail<2>, grid, dim3(TAIL_NT), lds, s, ta, nch);
                 break;
             }
             case OP_QOI: {

@@ -103,8 +103,7 @@ struct TailArgs {
     uint32_t chain0, seed_hi;  // chain c's Philox key: (key.k0, lo32(chain0 + c) ^ seed_hi)
     const double2* zb;     // pre-drawn Box-Muller pairs of the sweeps (nullptr: drawn here), zbs per chain
     long long zbs;
-    int nwg;               // workgroups running the tail (one per chain); the launch's blocks from nwg on draw pn
-    int npn;               // post-sweep noise jobs (one chain only)
+    int npn;               // post-sweep noise jobs (one chain only): drawn by the launch's blocks from nwg on
     PostNoiseJob pn[TAIL_MAX_PN_JOBS];
     TailLevel lv[TAIL_MAX_LEVELS];
     TailOp ops[TAIL_MAX_OPS];
@@ -224,7 +223,7 @@ __device__ __forceinline__ double tail_sum(const double* __restrict__ x, int p, 
 // jobs (PostNoiseJob), pair q of a job -> dst[q], the same Philox counter and arithmetic as the sweep
 // kernel would use (normal_pair_t with the tables in LDS), chain 0's key.  Items are dealt round-robin
 // over every spare thread, so consecutive lanes store consecutive 16-byte pairs.
-__device__ __forceinline__ void tail_post_noise(const TailArgs* __restrict__ A, double* tab) {
+__device__ __forceinline__ void tail_post_noise(const TailArgs* __restrict__ A, int nwg, double* tab) {
     for (int q = threadIdx.x; q < 64; q += blockDim.x) {
         tab[q] = LOGTAB_RC[q];
         tab[64 + q] = LOGTAB_HI[q];
@@ -235,8 +234,8 @@ __device__ __forceinline__ void tail_post_noise(const TailArgs* __restrict__ A, 
     const uint64_t sample = *A->sample;
     const uint32_t s_lo = (uint32_t)sample, s_hi = (uint32_t)(sample >> 32);
     const RngKey key = A->key;
-    const uint32_t nw = (gridDim.x - (uint32_t)A->nwg) * blockDim.x;
-    const uint32_t w0 = (blockIdx.x - (uint32_t)A->nwg) * blockDim.x + threadIdx.x;
+    const uint32_t nw = (gridDim.x - (uint32_t)nwg) * blockDim.x;
+    const uint32_t w0 = (blockIdx.x - (uint32_t)nwg) * blockDim.x + threadIdx.x;
     const int npn = A->npn;
     for (int jb = 0; jb < npn; ++jb) {
         const PostNoiseJob J = A->pn[jb];
@@ -251,12 +250,14 @@ __device__ __forceinline__ void tail_post_noise(const TailArgs* __restrict__ A, 
 }
 
 // SYM: every 27-point level of the tail has a reflection-symmetric stencil (stencil_coef)
+// nwg: workgroups running the tail (one per chain; a kernel argument, not a field of *A: the tail's first
+// read of its arguments would be a dependent miss); blocks from nwg on draw the post-sweep noise
 template <int DIM, bool SYM = false>
-__global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A) {
+__global__ void __launch_bounds__(1024) k_tail(const TailArgs* __restrict__ A, int nwg) {
     constexpr int NPTS = DIM == 3 ? 27 : 9;
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    if ((int)blockIdx.x >= A->nwg) {  // a spare workgroup: post-sweep noise only
-        tail_post_noise(A, lds);
+    if ((int)blockIdx.x >= nwg) {  // a spare workgroup: post-sweep noise only
+        tail_post_noise(A, nwg, lds);
         return;
     }
     const int tid = threadIdx.x, nt = blockDim.x;
