@@ -46,10 +46,6 @@ constexpr int ZR_SMALL_NX = 32;
 // the 7-point (fine level) instance with 64 x 8 coarse points per 512-thread workgroup (else 64 x 4
 // per 256 threads) from this many 64 x 8 tiles up (512^3: 32,768)
 constexpr int ZR7_WIDE_MIN_TILES = 16 * 1024;
-// ... its residual windows read by single ds_read_b64 in one asm statement (zr_window7)
-constexpr int ZR7_LDSREAD = 0;
-// ... and every instance's restriction windows (zr_window9)
-constexpr int ZR_ACC_LDSREAD = 0;
 
 // z-marching prolongation (k_prolongate_z): fine planes per thread on big 3D levels, and below 2^21
 // fine pair items

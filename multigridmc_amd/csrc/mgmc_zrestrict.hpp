@@ -69,36 +69,6 @@ __device__ __forceinline__ void zr_plane12(uint32_t base, double (&v)[12]) {
                    "i"(2 * RB), "i"(2 * RB + 8), "i"(2 * RB + EV - 8), "i"(2 * RB + EV)
                  : "memory");
 }
-// The 7-point window of a residual pair item (odd vertex i, even i+1) in one statement: plane k-1 at b0
-// (x(i), x(i+1): offsets 0, EV), plane k at b1 = row j-1's x(i) (row j-1: 0, EV; row j: x(i-1), x(i),
-// x(i+1), x(i+2) at RB + EV - 8, RB, RB + EV, RB + 8; row j+1: 2 RB, 2 RB + EV), plane k+1 at b2 (0, EV)
-#define ZR_RDB(n, b, o) "ds_read_b64 %" #n ", %" #b " offset:" #o "\n"
-template <int RB, int EV>
-__device__ __forceinline__ void zr_window7(uint32_t b0, uint32_t b1, uint32_t b2, double (&v)[12]) {
-    static_assert(2 * RB + EV < 65536 && EV >= 8, "ds offsets");
-    asm volatile(ZR_RDB(0, 12, 0) ZR_RDB(1, 12, %c15) ZR_RDB(2, 13, 0) ZR_RDB(3, 13, %c15)
-                 ZR_RDB(4, 13, %c16) ZR_RDB(5, 13, %c17) ZR_RDB(6, 13, %c18) ZR_RDB(7, 13, %c19)
-                 ZR_RDB(8, 13, %c20) ZR_RDB(9, 13, %c21) ZR_RDB(10, 14, 0) ZR_RDB(11, 14, %c15) "s_waitcnt lgkmcnt(0)"
-                 : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
-                   "=&v"(v[7]), "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11])
-                 : "v"(b0), "v"(b1), "v"(b2), "i"(EV), "i"(RB + EV - 8), "i"(RB), "i"(RB + EV), "i"(RB + 8),
-                   "i"(2 * RB), "i"(2 * RB + EV)
-                 : "memory");
-}
-// The 3 x 3 residuals of a coarse point's fine neighbourhood in one plane: rows sy = -1, 0, 1 at byte
-// offsets 0, RB, 2 RB from b (row sy = -1's odd element left of the centre), per row sx = -1, 0, 1 at 0,
-// EV, 8
-template <int RB, int EV>
-__device__ __forceinline__ void zr_window9(uint32_t b, double (&v)[9]) {
-    static_assert(2 * RB + EV < 65536 && EV >= 8, "ds offsets");
-    asm volatile(ZR_RDB(0, 9, 0) ZR_RDB(1, 9, %c10) ZR_RDB(2, 9, 8) ZR_RDB(3, 9, %c11) ZR_RDB(4, 9, %c12)
-                 ZR_RDB(5, 9, %c13) ZR_RDB(6, 9, %c14) ZR_RDB(7, 9, %c15) ZR_RDB(8, 9, %c16) "s_waitcnt lgkmcnt(0)"
-                 : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]),
-                   "=&v"(v[7]), "=&v"(v[8])
-                 : "v"(b), "i"(EV), "i"(RB), "i"(RB + EV), "i"(RB + 8), "i"(2 * RB), "i"(2 * RB + EV), "i"(2 * RB + 8)
-                 : "memory");
-}
-#undef ZR_RDB
 #undef ZR_RD
 
 // SYM: a fold level (reflection-symmetric 27-point stencil): the residual's sum is fold27's
@@ -261,24 +231,7 @@ k_zresrestrict(ZRestrictArgs a) {
             const int o0 = rxo[u], o1 = rxo[u] + XPP;  // odd / even vertex
             const int m0 = o0 + XPP - 1, m1 = o1 - XPP;   // their x-1 neighbours (x+1 = m + 1; 7-point)
             double y0 = 0.0, y1 = 0.0;
-            if (NPTS == 7 && tune::ZR7_LDSREAD) {  // the same terms in the same order as below
-                double v[12];
-                zr_window7<XS * 8, XPP * 8>(lds_addr(pl[0] + o0), lds_addr(pl[1] + o0 - XS), lds_addr(pl[2] + o0), v);
-                y0 += a.S.a[4] * v[0];
-                y1 += a.S.a[4] * v[1];
-                y0 += a.S.a[10] * v[2];
-                y1 += a.S.a[10] * v[3];
-                y0 += a.S.a[12] * v[4];
-                y1 += a.S.a[12] * v[5];
-                y0 += a.S.a[13] * v[5];
-                y1 += a.S.a[13] * v[6];
-                y0 += a.S.a[14] * v[6];
-                y1 += a.S.a[14] * v[7];
-                y0 += a.S.a[16] * v[8];
-                y1 += a.S.a[16] * v[9];
-                y0 += a.S.a[22] * v[10];
-                y1 += a.S.a[22] * v[11];
-            } else if (NPTS == 7) {
+            if (NPTS == 7) {
                 y0 += a.S.a[4] * pl[0][o0];
                 y1 += a.S.a[4] * pl[0][o1];
                 y0 += a.S.a[10] * pl[1][o0 - XS];
@@ -342,22 +295,6 @@ k_zresrestrict(ZRestrictArgs a) {
 #pragma unroll
         for (int u = 0; u < NCP; ++u) {
             double result = acc[u];
-            if constexpr (tune::ZR_ACC_LDSREAD != 0) {  // the same terms in the same order as below
-                double v[9];
-                zr_window9<RSr * 8, RP * 8>(lds_addr(rs + cpo[u] - RSr), v);
-#pragma unroll
-                for (int sy = -1; sy <= 1; ++sy)
-#pragma unroll
-                    for (int sx = -1; sx <= 1; ++sx) {
-                        double w = 1.0;
-                        w *= w1(sx);
-                        w *= w1(sy);
-                        w *= w1(sz - 1);
-                        result += w * v[3 * (sy + 1) + sx + 1];
-                    }
-                acc[u] = result;
-                continue;
-            }
 #pragma unroll
             for (int sy = -1; sy <= 1; ++sy)
 #pragma unroll
