@@ -1548,7 +1548,9 @@ void mark_zero_inputs(mgmc_handle* h) {
         const bool zr = lf.spec.dim == 3 && !lf.field && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8;
         // j-marching levels and 3D quad-pass levels: out of place, x read only as the half-sweeps' input
         const bool quads3 = lc.quads && lc.spec.dim == 3;
-        if (!zr || !(lc.jsweep || quads3) || lc.field || lf.lr.m > 0 || lc.lr.m > 0) continue;
+        // (low-rank levels too: the patches before a sweep change f only, the fix after it reads the
+        // sweep's output, and the residual's dots read the fine level's x)
+        if (!zr || !(lc.jsweep || quads3) || lc.field) continue;
         rr.xzero = 1;
         sw.xzero = 1;
     }
@@ -1556,7 +1558,7 @@ void mark_zero_inputs(mgmc_handle* h) {
 
 // A tail launch runs one workgroup on one CU (512^3: 40-43 us); the rest of the chip is idle meanwhile.
 // Its spare workgroups draw the Box-Muller pairs of the sweeps that follow it instead: for every 3D
-// Galerkin level swept by quad passes (no low-rank part, not a field level), the first sweep on that
+// Galerkin level swept by quad passes (not a field level; with or without a low-rank part), the first sweep on that
 // level after the tail and before the next tail (in a V-cycle its post-sweep) whose input x is not known
 // zero.  The pairs are those the sweep would draw (same Philox counter: pair id, the sweep's tag, the
 // sample index at run time; same arithmetic), so the chain is bitwise unchanged.  512^3 (round 6): the
@@ -1581,7 +1583,8 @@ int plan_post_noise(mgmc_handle* h) {
             Op& op = h->ops[q];
             if (op.kind != OP_SWEEP || op.xzero || op.level < 1 || used[op.level]) continue;
             const Level& lv = h->levels[op.level];
-            if (lv.spec.dim != 3 || lv.field || lv.lr.m > 0 || !lv.quads || lv.jsweep || !lv.pingpong()) continue;
+            // (a low-rank level's sweep draws the same pairs: its patch of f and its fix are separate ops)
+            if (lv.spec.dim != 3 || lv.field || !lv.quads || lv.jsweep || !lv.pingpong()) continue;
             used[op.level] = 1;
             const long long n = (long long)(lv.L.nx / 2) * (lv.L.ny - 1) * (lv.L.nz - 1);
             if (total + n > PN_MAX_PAIRS || (int)jobs.size() >= TAIL_MAX_PN_JOBS) continue;
