@@ -1606,8 +1606,8 @@ int plan_post_noise(mgmc_handle* h) {
         const int npn = (int)jobs.size();
         HIPCHK(h, hipMemcpy(d->pn, jobs.data(), jobs.size() * sizeof(PostNoiseJob), hipMemcpyHostToDevice));
         HIPCHK(h, hipMemcpy(&d->npn, &npn, sizeof(int), hipMemcpyHostToDevice));
-        // one workgroup per other CU (the tail's LDS admits one per CU)
-        h->tail_pn_wg[ti] = std::max(1, h->levels[0].num_cu - h->nchains);
+        // one workgroup per other CU (the tail's LDS admits one per CU), or tune::TAIL_PN_WG
+        h->tail_pn_wg[ti] = tune::TAIL_PN_WG > 0 ? tune::TAIL_PN_WG : std::max(1, h->levels[0].num_cu - h->nchains);
     }
     return MGMC_OK;
 }
