@@ -1562,7 +1562,8 @@ void mark_zero_inputs(mgmc_handle* h) {
 // level after the tail and before the next tail (in a V-cycle its post-sweep) whose input x is not known
 // zero.  The pairs are those the sweep would draw (same Philox counter: pair id, the sweep's tag, the
 // sample index at run time; same arithmetic), so the chain is bitwise unchanged.  512^3 (round 6): the
-// 127^3 post quad passes 16.5 -> 13.9 us each.  Not the j-marching levels: their post half-sweeps,
+// 127^3 post quad passes 16.5 -> 13.9 us each, the tail launch +0.8 us with tune::TAIL_PN_WG = 32 spare
+// workgroups (+4 us with one per CU).  Not the j-marching levels: their post half-sweeps,
 // reading the pairs (16 B per pair) instead of drawing them, stayed at 72 us, and the 8.3 M pairs of
 // the 255^3 level took the tail launch from 43 to 60 us.  One chain per handle (batched handles' tails
 // run one workgroup per chain; their draws stay in the sweeps), and at most PN_MAX_PAIRS pairs per

@@ -42,8 +42,6 @@ constexpr int ZR27_CX = 64;
 // ... its coarse rows per tile and minimum waves per SIMD (register budget: 4 = <= 128 VGPRs)
 constexpr int ZR27_CY = 4;
 constexpr int ZR27_MINW = 1;
-// ... x planes loaded two planes ahead (one more register set)
-constexpr int ZR27_XPF2 = 0;
 constexpr int ZR_SMALL_NX = 32;
 // the 7-point (fine level) instance with 64 x 8 coarse points per 512-thread workgroup (else 64 x 4
 // per 256 threads) from this many 64 x 8 tiles up (512^3: 32,768)
@@ -54,8 +52,10 @@ constexpr int ZR7_WIDE_MIN_TILES = 16 * 1024;
 constexpr int PROLONG_Z = 8;
 constexpr int PROLONG_Z_SMALL = 4;
 
-// spare workgroups of a tail launch drawing the post-sweep noise (plan_post_noise); 0: one per other CU
-constexpr int TAIL_PN_WG = 0;
+// spare workgroups of a tail launch drawing the post-sweep noise (plan_post_noise; 0: one per other CU).
+// Each adds to the launch: 512^3 tail 43.5 us alone, 44.3 / 46.9 / 47.4 us with 32 / 64 / 255 of them; 32
+// draw the 1.15 M pairs of the 127^3-31^3 post-sweeps inside the tail's own time
+constexpr int TAIL_PN_WG = 32;
 
 // ---- low-rank dot products (mgmc_lowrank.hpp) ----
 // levels whose partials need fewer wavefronts than this take the staged kernel (a block's loads

@@ -196,21 +196,16 @@ k_zresrestrict(ZRestrictArgs a) {
         cpg[u] = cpin[u] ? Lc.at(I0 + cx, J0 + cy, 0) : 0;
     }
 
-    // XPF2: x planes loaded two planes ahead, one register set per plane parity (the fold levels' wide
-    // tiles: their registers leave room for the second set at 3 workgroups per CU)
-    constexpr bool XPF2 = NPTS == 27 && SYM && CX >= 48 && tune::ZR27_XPF2;
-    double2 pxb[XPF2 ? 2 : 1][NLX], pf[NLR];
+    double2 px[NLX], pf[NLR];
     // the chunk stages x planes 2 K0 - 2 .. 2 K1 and f planes 2 K0 - 1 .. 2 K1 - 1: the last step's loads one
-    // (two) plane(s) ahead reload those (never used) instead of fetching the next chunk's planes
+    // plane ahead reload those (never used) instead of fetching the next chunk's planes
     const int kx_last = 2 * K1, kf_last = 2 * K1 - 1;
     auto issue_x = [&](int k) {
-        double2(&px)[NLX] = pxb[XPF2 ? (k & 1) : 0];
         const double* base = plane_ptr(a.x, k > kx_last ? kx_last : k);
 #pragma unroll
         for (int u = 0; u < NLX; ++u) px[u] = *reinterpret_cast<const double2*>(base + xoff[u]);
     };
     auto deposit_x = [&](int k) {
-        const double2(&px)[NLX] = pxb[XPF2 ? (k & 1) : 0];
         double* dst = xs + xslot(k) * XPS;
 #pragma unroll
         for (int u = 0; u < NLX; ++u)
@@ -331,7 +326,7 @@ k_zresrestrict(ZRestrictArgs a) {
     // f(k) is in pf when residual(k) runs; f(k+1) is issued once it has used it (one register set)
     auto step = [&](int k) __attribute__((always_inline)) {
         deposit_x(k + 1);
-        issue_x(XPF2 ? k + 3 : k + 2);  // (XPF2: into the register set deposit_x just emptied)
+        issue_x(k + 2);
         __syncthreads();
         residual(k, pf);
         issue_f(k + 1);
@@ -343,7 +338,6 @@ k_zresrestrict(ZRestrictArgs a) {
     issue_x(2 * K0 - 1);
     deposit_x(2 * K0 - 1);
     issue_x(2 * K0);
-    if (XPF2) issue_x(2 * K0 + 1);
     issue_f(2 * K0 - 1);
 #pragma unroll
     for (int u = 0; u < NCP; ++u) acc[u] = 0.0;
