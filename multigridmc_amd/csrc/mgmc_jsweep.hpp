@@ -193,15 +193,6 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
             dst[q] = load_pair(j0 + item / 3, item % 3);
         }
     };
-    // JS_PA: the Philox block of a step's row is drawn at the end of the previous step's second phase
-    // (the first phase keeps the Box-Muller arithmetic, the window reads and the first colour; the
-    // second the second colour, the stores, the deposits and the next step's Philox rounds)
-    constexpr bool JS_PA = tune::JS_PHILOX_AHEAD != 0;
-    Philox4 rq;
-    auto philox_row = [&](int j) {
-        return philox4x32_10(pair_id<3>(L, i0, j, k), a.G.tag, (uint32_t)sample, (uint32_t)(sample >> 32), a.G.key.k0,
-                             a.G.key.k1);
-    };
     auto step = [&](auto par_c, int s) __attribute__((always_inline)) {
         constexpr int par = decltype(par_c)::value;  // (s - s0 + 1) % JS_D
         const int ar = 2 * s + a.jA;
@@ -214,10 +205,9 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
         const bool go = (role == 0 ? s < s1 : (s > s0 && s <= s1)) && j >= 1 && j <= L.ny - 1;
         const bool store = go && (role == 1 || s >= s0);
         double z0 = 0.0, z1 = 0.0;
-        if (JS_PA && go) {
-            normal_pair_t(rq, &z0, &z1, tab, tab + 64, tab + 128, tab + 192);
-        } else if (go) {
-            const Philox4 rnd = philox_row(j);
+        if (go) {
+            const Philox4 rnd = philox4x32_10(pair_id<3>(L, i0, j, k), a.G.tag, (uint32_t)sample,
+                                              (uint32_t)(sample >> 32), a.G.key.k0, a.G.key.k1);
             normal_pair_t(rnd, &z0, &z1, tab, tab + 64, tab + 128, tab + 192);
         }
         const bool odd_in = go;                       // i0 <= nx - 1 always
@@ -265,7 +255,6 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
             guards(ar + 2);
             guards(ar + 3);
         }
-        if (JS_PA) rq = philox_row(j + 2);  // the next step's row (rows past the lattice: drawn, never used)
         js_barrier();
     };
     // steps s0 - 1 .. s1 in groups of JS_D (idle steps at the end), buffers by step index from the chunk
@@ -275,7 +264,6 @@ __global__ void __launch_bounds__(2 * NP) k_jsweep_half(JSweepArgs a) {
     for (int t = 0; t + 1 < JS_D; ++t) load_rows(P[t], a0 + 2 + 2 * t);
 #pragma unroll
     for (int t = 0; t < JS_D; ++t) F[t] = load_f(frow(s0 - 1 + t));
-    if (JS_PA) rq = philox_row(frow(s0 - 1));
     for (int s = s0 - 1; s <= s1; s += JS_D) {
         step(std::integral_constant<int, 0>{}, s);
         step(std::integral_constant<int, 1>{}, s + 1);

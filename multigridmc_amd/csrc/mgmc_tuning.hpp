@@ -35,8 +35,6 @@ constexpr int QUADS_LANES = 1;
 // per half = this many rounds of the resident slots
 constexpr int JS_D = 3;
 constexpr int JS_ROUNDS = 1;
-// ... the Philox rounds of a step's noise drawn in the previous step's second phase
-constexpr int JS_PHILOX_AHEAD = 0;
 
 // residual + restriction (mgmc_zrestrict.hpp): coarse points per tile in x of the symmetric 27-point
 // instance; coarse nx below which the one-wavefront 16 x 4 tiles are used
