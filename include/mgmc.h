@@ -212,8 +212,9 @@ int mgmc_nchains(const mgmc_handle* h);
 int mgmc_destroy(mgmc_handle* h);
 int mgmc_level_desc_get(const mgmc_handle* h, int level, mgmc_level_desc* out);
 /* The kernels this handle runs on a level (ABI 5), as text "sweep=<kernel>[;post_sweep=<kernel>]
- * [;residual_restrict=<kernel>][;noise=tail][;lowrank=<path>]" -- for labels (bench.py) and profiles;
- * noise=tail: a sweep of the level reads Box-Muller pairs drawn by a tail launch's spare workgroups;
+ * [;residual_restrict=<kernel>][;noise=<source>][;lowrank=<path>]" -- for labels (bench.py) and profiles;
+ * <source>: restriction | tail | restriction+tail -- sweeps of the level read Box-Muller pairs drawn by the
+ * restriction launch before the first pre-sweep and / or a tail launch's spare workgroups;
  * <path> on a posterior level: small | rows | dense | dense,rhs_inplace */
 int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n);
 

@@ -325,8 +325,8 @@ void launch_jsweep(const Level& lv, const double* xin, double* xout, const doubl
     }
 }
 
-// zb: the sweep's Box-Muller pairs drawn by a tail launch (Op::pnz; 3D quad-pass levels, one chain, input x
-// not known zero)
+// zb: the sweep's Box-Muller pairs, drawn by an earlier launch (Op::pnz, plan_drawn_noise; 3D quad-pass
+// levels, one chain; with xzero forward sweeps only)
 void launch_quads(const Level& lv, const double* xin, double* xout, const double* f, const GibbsArg& g, int direction,
                   hipStream_t s, int nch = 1, bool xzero = false, const double2* zb = nullptr) {
     if (lv.jsweep) {
@@ -375,10 +375,13 @@ void launch_quads(const Level& lv, const double* xin, double* xout, const double
         } else if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false, SYMV, XZ>), grid, dim3(nt), lds, s, a);  \
         else hipLaunchKernelGGL((k_sweep_quads<3, true, SYMV, XZ>), grid, dim3(nt), lds, s, a);             \
     } while (0)
-#define MGMC_QD_PZ(SYMV, LANESV)                                                                                  \
-    do {                                                                                                          \
-        if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false, SYMV, 0, LANESV, true>), grid, dim3(nt), lds, s, a); \
-        else hipLaunchKernelGGL((k_sweep_quads<3, true, SYMV, 0, LANESV, true>), grid, dim3(nt), lds, s, a);      \
+// (drawn noise with a known-zero input: forward sweeps only, plan_drawn_noise)
+#define MGMC_QD_PZ(SYMV, LANESV)                                                                                   \
+    do {                                                                                                           \
+        if (xzero && h == 0) hipLaunchKernelGGL((k_sweep_quads<3, false, SYMV, 1, LANESV, true>), grid, dim3(nt), lds, s, a); \
+        else if (xzero) hipLaunchKernelGGL((k_sweep_quads<3, false, SYMV, 2, LANESV, true>), grid, dim3(nt), lds, s, a);      \
+        else if (fwd) hipLaunchKernelGGL((k_sweep_quads<3, false, SYMV, 0, LANESV, true>), grid, dim3(nt), lds, s, a);       \
+        else hipLaunchKernelGGL((k_sweep_quads<3, true, SYMV, 0, LANESV, true>), grid, dim3(nt), lds, s, a);                  \
     } while (0)
 #define MGMC_QD_XZ(SYMV)                              \
     do {                                              \
@@ -480,10 +483,16 @@ void launch_coarse_lds(const Level& lv, const GibbsArg& g, int nsweeps, hipStrea
 
 template <int NPTS, int CX, int CY, int NT, bool SYM = false, bool LRF = false>
 void launch_zresrestrict_t(const Level& lf, const Level& lc, const double* x, const double* f, double* fc, double* xc,
-                           hipStream_t s, int nch, const TailNoiseLaunch* tn = nullptr, const LRRhsArg* lr = nullptr) {
+                           hipStream_t s, int nch, const TailNoiseLaunch* tn = nullptr, const LRRhsArg* lr = nullptr,
+                           const PreNoiseLaunch* pn = nullptr) {
     ZRestrictArgs a;
     memset(&a, 0, sizeof(a));
     if (LRF) a.lr = *lr;
+    if (pn) {  // (one chain: nch == 1)
+        a.pn = pn->job;
+        a.key = pn->key;
+        a.sample = pn->sample;
+    }
     a.csf = lf.L.nstore;
     a.csc = lc.L.nstore;
     a.Lf = lf.L;
@@ -562,9 +571,16 @@ bool zres_lrf_capable(const Level& lf, const Level& lc) {
 }
 
 // lr (non-null): the level's right-hand side is read in place (LRRhsArg; zres_lrf_capable levels only)
+// the z-marching 27-point residual + restriction of a non-small coarse level: launch_residual_restrict's path
+// for zero_xc = 1 that can also draw the coarse level's first pre-sweep's noise (pn)
+bool zres_draws_noise(const Level& lf, const Level& lc) {
+    return lf.spec.dim == 3 && lf.spec.npoints == 27 && !lf.field && !(lf.paths & PATH_NO_ZRESTRICT) &&
+           lc.L.nx >= tune::ZR_SMALL_NX;
+}
+
 void launch_residual_restrict(const Level& lf, const Level& lc, const double* x, const double* f, double* fc,
                               double* xc, int zero_xc, hipStream_t s, int nch, const TailNoiseLaunch* tn,
-                              bool skip_xc, const LRRhsArg* lr) {
+                              bool skip_xc, const LRRhsArg* lr, const PreNoiseLaunch* pn) {
     const bool zr = lf.spec.dim == 3 && zero_xc && !lf.field && !(lf.paths & PATH_NO_ZRESTRICT) && lc.L.nx >= 8;
     if (nch > 1 && !zr) {  // batched chains on the generic kernels: one launch per chain
         for (int c = 0; c < nch; ++c)
@@ -608,8 +624,10 @@ void launch_residual_restrict(const Level& lf, const Level& lc, const double* x,
             // (fold levels: the SYM instances, whose residual is fold27's)
             if (small && lf.fold) launch_zresrestrict_t<27, 16, 4, 64, true>(lf, lc, x, f, fc, xc, s, nch, tn);
             else if (small) launch_zresrestrict_t<27, 16, 4, 64>(lf, lc, x, f, fc, xc, s, nch, tn);
-            else if (lf.fold) launch_zresrestrict_t<27, tune::ZR27_CX, tune::ZR27_CY, 256, true>(lf, lc, x, f, fc, xc, s, nch);
-            else launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s, nch);
+            else if (lf.fold)
+                launch_zresrestrict_t<27, tune::ZR27_CX, tune::ZR27_CY, 256, true>(lf, lc, x, f, fc, xc, s, nch, nullptr,
+                                                                                   nullptr, pn);
+            else launch_zresrestrict_t<27, 64, 4, 256>(lf, lc, x, f, fc, xc, s, nch, nullptr, nullptr, pn);
         }
         return;
     }
@@ -1380,7 +1398,7 @@ int build_tails_only(mgmc_handle* h) {
         A.cs = h->levels[lt].L.nstore;  // batched chains: one workgroup per chain
         A.chain0 = (uint32_t)h->chain;
         A.seed_hi = (uint32_t)(h->seed >> 32);
-        A.npn = 0;  // (post-sweep noise jobs: plan_post_noise)
+        A.npn = 0;  // (post-sweep noise jobs: plan_drawn_noise)
 #ifdef MGMC_TAIL_PROF
         if (h->tail_args.empty()) {
             if (!h->tail_prof) HIPCHK(h, hipMalloc(&h->tail_prof, 256 * sizeof(unsigned long long)));
@@ -1570,10 +1588,49 @@ void mark_zero_inputs(mgmc_handle* h) {
 // tail, well inside what the spare workgroups draw within the tail's own time.
 constexpr long long PN_MAX_PAIRS = 2LL << 20;
 
-int plan_post_noise(mgmc_handle* h) {
-    for (Op& op : h->ops) op.pnz = nullptr;
+//
+// The same for the first pre-sweep of a 3D quad-pass level after a 27-point z-marching residual +
+// restriction (zres_draws_noise): every workgroup of that launch draws its share of the coarse level's
+// pairs after its own march (ZRestrictArgs::pn; the sweep then loads them, with xzero its known-zero
+// x too).  One buffer per level serves both: the pre-sweep reads it before the tail rewrites it.
+int plan_drawn_noise(mgmc_handle* h) {
+    for (Op& op : h->ops) {
+        op.pnz = nullptr;
+        op.pn_dst = nullptr;
+        op.pn_tag = 0;
+    }
     if ((h->paths & PATH_NO_POST_NOISE) || h->nchains != 1) return MGMC_OK;
     std::vector<double2*> buf(h->levels.size(), nullptr);
+    auto level_buf = [&](int l) -> double2* {
+        if (!buf[l]) {
+            const Level& lv = h->levels[l];
+            const long long n = (long long)(lv.L.nx / 2) * (lv.L.ny - 1) * (lv.L.nz - 1);
+            if (hipMalloc(&buf[l], (size_t)n * sizeof(double2)) != hipSuccess) {
+                buf[l] = nullptr;
+                (void)hipGetLastError();
+                return nullptr;
+            }
+            poison_fill(h, buf[l], (size_t)n * sizeof(double2));
+            h->pn_bufs.push_back(buf[l]);
+        }
+        return buf[l];
+    };
+    auto quad_consumer = [&](const Level& lv) {
+        return lv.spec.dim == 3 && !lv.field && lv.quads && !lv.jsweep && lv.pingpong();
+    };
+    for (size_t q = 0; q + 1 < h->ops.size(); ++q) {  // pre-sweeps: drawn by the restriction before them
+        Op& rr = h->ops[q];
+        Op& sw = h->ops[q + 1];
+        if (rr.kind != OP_RESIDUAL_RESTRICT || rr.zpre != 0 || sw.kind != OP_SWEEP || sw.level != rr.level + 1) continue;
+        const Level& lf = h->levels[rr.level];
+        const Level& lc = h->levels[sw.level];
+        if (!zres_draws_noise(lf, lc) || !quad_consumer(lc) || (sw.xzero && sw.direction != MGMC_FORWARD)) continue;
+        double2* b = level_buf(sw.level);
+        if (!b) continue;
+        rr.pn_dst = b;
+        rr.pn_tag = sw.tag;
+        sw.pnz = b;
+    }
     for (size_t t = 0; t < h->ops.size(); ++t) {
         if (h->ops[t].kind != OP_TAIL) continue;
         const int ti = h->ops[t].tail;
@@ -1582,25 +1639,20 @@ int plan_post_noise(mgmc_handle* h) {
         long long total = 0;
         for (size_t q = t + 1; q < h->ops.size() && h->ops[q].kind != OP_TAIL; ++q) {
             Op& op = h->ops[q];
+            // (W-cycles: a restriction in the window that rewrites a level's buffer ends the tail's use of it)
+            if (op.kind == OP_RESIDUAL_RESTRICT && op.pn_dst) used[op.level + 1] = 1;
             if (op.kind != OP_SWEEP || op.xzero || op.level < 1 || used[op.level]) continue;
             const Level& lv = h->levels[op.level];
             // (a low-rank level's sweep draws the same pairs: its patch of f and its fix are separate ops)
-            if (lv.spec.dim != 3 || lv.field || !lv.quads || lv.jsweep || !lv.pingpong()) continue;
+            if (!quad_consumer(lv) || op.pnz) continue;
             used[op.level] = 1;
             const long long n = (long long)(lv.L.nx / 2) * (lv.L.ny - 1) * (lv.L.nz - 1);
             if (total + n > PN_MAX_PAIRS || (int)jobs.size() >= TAIL_MAX_PN_JOBS) continue;
-            if (!buf[op.level]) {
-                if (hipMalloc(&buf[op.level], (size_t)n * sizeof(double2)) != hipSuccess) {
-                    buf[op.level] = nullptr;
-                    (void)hipGetLastError();
-                    continue;  // (this sweep draws its own)
-                }
-                poison_fill(h, buf[op.level], (size_t)n * sizeof(double2));
-                h->pn_bufs.push_back(buf[op.level]);
-            }
+            double2* b = level_buf(op.level);
+            if (!b) continue;  // (this sweep draws its own)
             total += n;
-            jobs.push_back(PostNoiseJob{lv.L.nx, lv.L.ny, lv.L.nz, op.tag, buf[op.level]});
-            op.pnz = buf[op.level];
+            jobs.push_back(PostNoiseJob{lv.L.nx, lv.L.ny, lv.L.nz, op.tag, b});
+            op.pnz = b;
         }
         if (jobs.empty()) continue;
         TailArgs* d = h->tail_args[ti];
@@ -1617,7 +1669,7 @@ int build_tails(mgmc_handle* h) {
     int rc = build_tails_only(h);
     if (rc == MGMC_OK) fuse_sweep_restrict(h);
     if (rc == MGMC_OK) mark_zero_inputs(h);
-    if (rc == MGMC_OK) rc = plan_post_noise(h);
+    if (rc == MGMC_OK) rc = plan_drawn_noise(h);
     return rc;
 }
 
@@ -1706,8 +1758,14 @@ void enqueue_ops(mgmc_handle* h, size_t begin, size_t end, hipStream_t s) {
                                              h->key, (uint32_t)h->chain, (uint32_t)(h->seed >> 32), sample};
                     launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch, &tn);
                 } else {
+                    PreNoiseLaunch pnl;
+                    if (op.pn_dst) {
+                        pnl.job = PostNoiseJob{lc.L.nx, lc.L.ny, lc.L.nz, op.pn_tag, op.pn_dst};
+                        pnl.key = h->key;
+                        pnl.sample = sample;
+                    }
                     launch_residual_restrict(lv, lc, lv.buf(op.src), fr, lc.f, lc.x, 1, s, nch, nullptr, op.xzero != 0,
-                                             lrr.e ? &lrr : nullptr);
+                                             lrr.e ? &lrr : nullptr, op.pn_dst ? &pnl : nullptr);
                     if (op.xzero && h->poison)  // (debug) the skipped x_c write leaves stale values: make them NaN
                         for (int c = 0; c < nch; ++c)
                             hipLaunchKernelGGL(k_poison_interior, dim3((lc.L.nx - 1 + 255) / 256, lc.L.ny - 1,
@@ -2517,12 +2575,17 @@ int mgmc_level_kernels(const mgmc_handle* h, int level, char* out, size_t n) {
     }
     std::string text = "sweep=" + sweep;
     if (!post.empty()) text += ";post_sweep=" + post;
-    // a sweep of this level reads its Box-Muller pairs from a tail launch's spare workgroups (plan_post_noise)
-    for (const Op& op : h->ops)
-        if (op.kind == OP_SWEEP && op.level == level && op.pnz) {
-            text += ";noise=tail";
-            break;
-        }
+    // sweeps of this level read Box-Muller pairs drawn by an earlier launch (plan_drawn_noise): the
+    // restriction before the first pre-sweep and / or a tail launch
+    bool by_rr = false, by_tail = false;
+    for (size_t q = 0; q < h->ops.size(); ++q) {
+        const Op& op = h->ops[q];
+        if (op.kind != OP_SWEEP || op.level != level || !op.pnz) continue;
+        if (q > 0 && h->ops[q - 1].kind == OP_RESIDUAL_RESTRICT && h->ops[q - 1].pn_dst == op.pnz) by_rr = true;
+        else by_tail = true;
+    }
+    if (by_rr || by_tail)
+        text += std::string(";noise=") + (by_rr && by_tail ? "restriction+tail" : by_rr ? "restriction" : "tail");
     if (!res.empty()) text += ";residual_restrict=" + res;
     // the low-rank path of a posterior level (mgmc_lowrank.hpp; rhs_inplace: the sweeps and the
     // residual above run their LRF instances, f + e read in place)

@@ -86,7 +86,9 @@ struct Op {
     int zpre = 0;            // OP_SWEEP_RESTRICT: also draws the next OP_COARSE_LDS's noise into mgmc_handle::zbuf;
                              // OP_COARSE_LDS: reads it from there; OP_RESIDUAL_RESTRICT: 1 + the index of
                              // the OP_TAIL after it whose noise its spare workgroups draw
-    const double2* pnz = nullptr;  // OP_SWEEP: its Box-Muller pairs, drawn by an earlier tail launch (plan_post_noise)
+    const double2* pnz = nullptr;  // OP_SWEEP: its Box-Muller pairs, drawn by an earlier launch (plan_drawn_noise)
+    double2* pn_dst = nullptr;     // OP_RESIDUAL_RESTRICT: also draws the next op's (the coarse level's first
+    uint32_t pn_tag = 0;           // pre-sweep's) pairs, tag pn_tag, into pn_dst
 };
 
 
@@ -111,7 +113,7 @@ enum PathFlag : uint32_t {
     PATH_NO_PROLONG_Z = 1u << 13,         // big 3D levels: the per-point prolongation instead of the z-marching one
     PATH_NO_XZERO = 1u << 14,             // the restriction zeroes x_{l+1} and its first pre-sweep loads it
     PATH_NO_FOLD = 1u << 15,              // 3D fold levels: residuals in the reference's CSR order, not fold27's
-    PATH_NO_POST_NOISE = 1u << 16,        // sweeps after a tail draw their own noise (not the tail launch's spare workgroups)
+    PATH_NO_POST_NOISE = 1u << 16,        // every sweep draws its own noise (none drawn by a restriction / tail launch)
 };
 
 struct PathToken {
@@ -320,7 +322,7 @@ struct mgmc_handle {
     std::vector<TailNoiseJob*> tail_jobs;
     std::vector<int> tail_njobs;
     std::vector<long long> tail_zn;
-    // per OP_TAIL: spare workgroups of its launch drawing the post-sweep noise jobs (plan_post_noise), and
+    // per OP_TAIL: spare workgroups of its launch drawing the post-sweep noise jobs (plan_drawn_noise), and
     // the noise buffers of those jobs (one per level, freed with the tails)
     std::vector<int> tail_pn_wg;
     std::vector<double2*> pn_bufs;
@@ -381,6 +383,13 @@ struct TailNoiseLaunch {  // spare workgroups of the launch draw a tail's noise 
     uint32_t chain0, seed_hi;
     const uint64_t* sample;
 };
+// the workgroups of a 27-point residual + restriction also draw the coarse level's first pre-sweep's
+// Box-Muller pairs (ZRestrictArgs::pn; plan_drawn_noise)
+struct PreNoiseLaunch {
+    PostNoiseJob job;
+    RngKey key;
+    const uint64_t* sample;
+};
 // the scale of the low-rank dots: LR_SCALE_ONE (B^T v) or LR_SCALE_INV (Sigma^{-1} B^T v) -- LRBlock::sc[sel]
 enum LRScale { LR_SCALE_ONE = 0, LR_SCALE_INV = 1 };
 
@@ -392,7 +401,8 @@ void launch_sweep(const Level& lv, double* x, const double* f, const GibbsArg& g
 bool zres_lrf_capable(const Level& lf, const Level& lc);
 void launch_residual_restrict(const Level& lf, const Level& lc, const double* x, const double* f, double* fc,
                               double* xc, int zero_xc, hipStream_t s, int nch = 1, const TailNoiseLaunch* tn = nullptr,
-                              bool skip_xc = false, const LRRhsArg* lr = nullptr);
+                              bool skip_xc = false, const LRRhsArg* lr = nullptr, const PreNoiseLaunch* pn = nullptr);
+bool zres_draws_noise(const Level& lf, const Level& lc);
 void launch_prolongate(const Level& lf, const Level& lc, double* x, const double* xc, double alpha, hipStream_t s,
                        int nch = 1);
 void lr_dots(const Level& lv, const double* v, LRScale scale, hipStream_t s, int nch = 1);

@@ -56,7 +56,7 @@ struct TailNoiseJob {
 constexpr int TAIL_MAX_NOISE_JOBS = 24;
 
 // one job of the noise the tail launch draws for a sweep after it (the first post-sweep of each 3D
-// Galerkin level between the tail and the fine level, plan_post_noise in mgmc_capi.hip): every pair of
+// Galerkin level between the tail and the fine level, plan_drawn_noise in mgmc_capi.hip): every pair of
 // the level's sweep with tag `tag`, pair id q -> dst[q] (pair_id<3> order), drawn by the launch's spare
 // workgroups while the tail's one workgroup runs on one CU
 struct PostNoiseJob {

@@ -52,7 +52,7 @@ constexpr int ZR7_WIDE_MIN_TILES = 16 * 1024;
 constexpr int PROLONG_Z = 8;
 constexpr int PROLONG_Z_SMALL = 4;
 
-// spare workgroups of a tail launch drawing the post-sweep noise (plan_post_noise; 0: one per other CU).
+// spare workgroups of a tail launch drawing the post-sweep noise (plan_drawn_noise; 0: one per other CU).
 // Each adds to the launch: 512^3 tail 43.5 us alone, 44.3 / 46.9 / 47.4 us with 32 / 64 / 255 of them; 32
 // draw the 1.15 M pairs of the 127^3-31^3 post-sweeps inside the tail's own time
 constexpr int TAIL_PN_WG = 32;

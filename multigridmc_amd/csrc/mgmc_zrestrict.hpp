@@ -48,6 +48,9 @@ struct ZRestrictArgs {
     uint32_t chain0, seed_hi;
     const uint64_t* sample;
     LRRhsArg lr;               // LRF: the right-hand side is f patched in place (mgmc_kernels.hpp)
+    // pn.dst (non-null): every workgroup also draws its share of the Box-Muller pairs of the coarse level's
+    // first pre-sweep (pair q -> pn.dst[q], chain 0's key: one chain), after its own march
+    PostNoiseJob pn;
 };
 
 // One plane's 3 x 4 window of a residual pair item (rows dy = -1, 0, 1 at byte offsets 0, RB, 2 RB from
@@ -135,7 +138,23 @@ k_zresrestrict(ZRestrictArgs a) {
     const int txi = tile % a.ntx;
     const int tyi = (tile / a.ntx) % a.nty;
     const int tzi = tile / (a.ntx * a.nty);
-    if (tzi >= a.ntz) return;
+    // the coarse level's first pre-sweep's pairs (a.pn): workgroup b draws q = b NT + tid + r nb NT
+    auto draw_pn = [&]() {
+        if (!a.pn.dst) return;
+        const uint64_t sample = *a.sample;
+        const uint32_t n = (uint32_t)(a.pn.nx / 2) * (uint32_t)(a.pn.ny - 1) * (uint32_t)(a.pn.nz - 1);
+        const uint32_t nw = (uint32_t)nb * NT;
+        for (uint32_t q = (uint32_t)b * NT + threadIdx.x; q < n; q += nw) {
+            const Philox4 r = philox4x32_10(q, a.pn.tag, (uint32_t)sample, (uint32_t)(sample >> 32), a.key.k0, a.key.k1);
+            double z0, z1;
+            normal_pair(r, &z0, &z1);
+            a.pn.dst[q] = make_double2(z0, z1);
+        }
+    };
+    if (tzi >= a.ntz) {
+        draw_pn();
+        return;
+    }
     const int I0 = 1 + txi * CX, J0 = 1 + tyi * CY;
     const int K0 = 1 + tzi * a.kz, K1 = min(K0 + a.kz, Lc.nz);  // coarse planes [K0, K1)
     const int xi0 = 2 * I0 - 3;  // fine position of x pair column 0 (odd)
@@ -355,6 +374,7 @@ k_zresrestrict(ZRestrictArgs a) {
 #pragma unroll
         for (int u = 0; u < NCP; ++u) acc[u] = accn[u];
     }
+    draw_pn();
 }
 
 inline size_t zrestrict_lds_bytes(int CX, int CY) {

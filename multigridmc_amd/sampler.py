@@ -599,8 +599,8 @@ class MultigridMCSampler:
     def level_kernels(self, level: int) -> dict:
         """The kernels the handle runs on a level (mgmc_level_kernels): {"sweep": ..., "post_sweep": ...,
         "residual_restrict": ..., "lowrank": ..., "noise": ...} ("lowrank" on posterior levels: "small",
-        "rows", "dense" or "dense,rhs_inplace"; "noise": "tail" when a sweep of the level reads Box-Muller
-        pairs drawn by a tail launch's spare workgroups)"""
+        "rows", "dense" or "dense,rhs_inplace"; "noise": "restriction", "tail" or "restriction+tail" when sweeps
+        of the level read Box-Muller pairs drawn by the restriction launch before them / a tail launch)"""
         buf = ctypes.create_string_buffer(512)
         self._chk(self.lib.mgmc_level_kernels(self.handle, int(level), buf, 512))
         return dict(kv.split("=", 1) for kv in buf.value.decode().split(";"))

@@ -52,10 +52,11 @@ def test_config3_kernel_instances(config3):
     k0 = s.level_kernels(0)
     assert k0["sweep"].startswith("k_zsweep_rb7<") and k0["post_sweep"].endswith("PROLONG>")
     assert k0["residual_restrict"] == "k_zresrestrict<7,64,4>"
-    # levels 1-3 (quad passes after the tail): post-sweep noise drawn by the tail launch's spare workgroups
+    # levels 1-3 (quad passes): pre-sweep noise drawn by the restriction launch before them (level 1: the
+    # fine 7-point residual, which does not), post-sweep noise by the tail launch's spare workgroups
     assert s.level_kernels(1) == {"sweep": "k_sweep_quads<3>", "residual_restrict": "k_zresrestrict<27,64,4>",
                                   "noise": "tail"}
-    assert s.level_kernels(2)["sweep"] == "k_sweep_quads<3>" and s.level_kernels(2)["noise"] == "tail"
+    assert s.level_kernels(2)["sweep"] == "k_sweep_quads<3>" and s.level_kernels(2)["noise"] == "restriction+tail"
     assert s.level_kernels(NLEVEL - 1)["sweep"] == "k_tail<3>"
 
 

@@ -171,6 +171,7 @@ def test_headline_kernel_instances(headline):
     # the 255^3 Galerkin stencil is reflection-symmetric bit for bit: the folded instance (stencil_coef)
     assert s.level_kernels(1) == {"sweep": "k_jsweep_half<128,sym>", "residual_restrict": "k_zresrestrict<27,64,4>"}
     assert s.level_kernels(2)["sweep"] == "k_sweep_quads<3>"  # 64-pair rows: quad passes
-    # levels 2-4: the post-sweeps read the Box-Muller pairs the tail launch's spare workgroups drew
-    assert all(s.level_kernels(l).get("noise") == "tail" for l in range(2, NLEVEL - 2))
+    # levels 2-4: the first pre-sweep reads the Box-Muller pairs the restriction launch drew, the post-sweep
+    # those the tail launch's spare workgroups drew
+    assert all(s.level_kernels(l).get("noise") == "restriction+tail" for l in range(2, NLEVEL - 2))
     assert s.level_kernels(NLEVEL - 1)["sweep"] == "k_tail<3>"

@@ -209,12 +209,13 @@ def test_mgmc_cycles_bitwise(hip_device, name):
 
 def test_tail_drawn_post_noise_path(hip_device, monkeypatch):
     """The quad-pass levels between a tail and the fine level read their first post-sweep's Box-Muller
-    pairs from the tail launch's spare workgroups (not the j-marching level 1, not the fine level), and
-    the cycle is bitwise the same with the sweeps drawing them themselves (MGMC_DISABLE=post_noise)."""
+    pairs from the tail launch's spare workgroups and their first pre-sweep's from the 27-point residual +
+    restriction launch before it (not the j-marching level 1, not the fine level), and the cycle is
+    bitwise the same with the sweeps drawing them themselves (MGMC_DISABLE=post_noise)."""
     shape, kw = CONFIGS["3d_jsweep_tail"]
     s, p, lat = make(shape, **kw)
     assert s.level_kernels(1)["sweep"].startswith("k_jsweep_half<128")
-    assert s.level_kernels(2)["sweep"] == "k_sweep_quads<3>" and s.level_kernels(2).get("noise") == "tail"
+    assert s.level_kernels(2)["sweep"] == "k_sweep_quads<3>" and s.level_kernels(2).get("noise") == "restriction+tail"
     assert "noise" not in s.level_kernels(0) and "noise" not in s.level_kernels(1)
     monkeypatch.setenv("MGMC_DISABLE", "post_noise")
     s2, _, _ = make(shape, **kw)
@@ -269,8 +270,8 @@ def test_variant_cycles_bitwise(hip_device, monkeypatch, paths, name):
     pre-sweep loads it, instead of taking it as zeros; fold = the residuals of reflection-symmetric
     27-point levels in the reference's CSR order instead of fold27's;
     chol_dense = the coarse Cholesky's blocked banded solves on a small coarsest level (the oracle's
-    blocked mode); post_noise = the sweeps after a tail draw their own Box-Muller pairs instead of
-    reading those the tail launch's spare workgroups drew.  Every combination gives the oracle's cycle
+    blocked mode); post_noise = every sweep draws its own Box-Muller pairs instead of reading those a
+    restriction launch or a tail launch's spare workgroups drew.  Every combination gives the oracle's cycle
     exactly."""
     monkeypatch.setenv("MGMC_DISABLE", paths)
     shape, kw = CONFIGS[name]
