@@ -1654,7 +1654,14 @@ int plan_drawn_noise(mgmc_handle* h) {
             jobs.push_back(PostNoiseJob{lv.L.nx, lv.L.ny, lv.L.nz, op.tag, b});
             op.pnz = b;
         }
-        if (jobs.empty()) continue;
+        // (the spare workgroups keep the Box-Muller tables in the launch's LDS: 322 doubles)
+        if (jobs.empty() || h->tail_lds[ti] < 322 * sizeof(double)) {
+            for (size_t u = t + 1; u < h->ops.size() && h->ops[u].kind != OP_TAIL; ++u)
+                if (h->ops[u].kind == OP_SWEEP && !(u > 0 && h->ops[u - 1].kind == OP_RESIDUAL_RESTRICT &&
+                                                    h->ops[u - 1].pn_dst == h->ops[u].pnz))
+                    h->ops[u].pnz = nullptr;  // (no jobs: the window's sweeps draw their own)
+            continue;
+        }
         TailArgs* d = h->tail_args[ti];
         const int npn = (int)jobs.size();
         HIPCHK(h, hipMemcpy(d->pn, jobs.data(), jobs.size() * sizeof(PostNoiseJob), hipMemcpyHostToDevice));
