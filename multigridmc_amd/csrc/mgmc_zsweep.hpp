@@ -104,6 +104,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MINW)))
         tab[128 + q] = LOGTAB_LO[q];
     }
     for (int q = threadIdx.x; q < 130; q += NT) tab[192 + q] = SINCOS_TAB[q];
+    // waves 0-2 write the tables, every wave reads them in its first noise draw, which the plain sweep
+    // makes before the march's first barrier (the fused-prolongation sweep has a prologue barrier
+    // first): without this barrier a wave dispatched ahead of waves 0-2 reads whatever the CU's LDS held
+    if (!PROLONG) __syncthreads();
     // PROLONG: ring of two coarse planes (slot K & 1) over the tile's coarse footprint, coarse
     // columns [q0-3, q0+XP+4] (starting on an even storage index: 16-byte pair loads) x rows
     // [(j0-3)/2, (j0+TY+1)/2]
