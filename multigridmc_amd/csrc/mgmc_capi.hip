@@ -2867,6 +2867,9 @@ static int sweep_component(mgmc_handle* h, int level, int direction, int nsweeps
         GibbsArg g = make_gibbs(h, lv, tag + (uint32_t)s, 0, h->ctrl + 3);
         double* fb = lv.scratch[0];
         if (lr && noise) fb = lr_rhs(h, lv, LR_PATCH_NOISE, lv.scratch[0], tag + (uint32_t)s, h->ctrl + 3, h->stream);
+        if (h->poison)  // (debug: as enqueue_ops) the sweep starts on NaN-filled LDS
+            hipLaunchKernelGGL(k_lds_poison, dim3(8 * lv.num_cu), dim3(1024), LDS_POISON_DOUBLES * sizeof(double),
+                               h->stream);
         if (noise && lv.zsweep) {  // the fused z-marching kernel of the V-cycle (out of place)
             launch_zsweep(lv, lv.scratch[cur], lv.scratch[3 - cur], fb, g, direction, nullptr, nullptr, 0.0, h->stream);
             cur = 3 - cur;
